@@ -1,0 +1,273 @@
+/*
+ * mgs_gpu.h — C-ABI of libmgs_gpu.so, the MI355X batched grasp-evaluation engine.
+ *
+ * The reference (freiberg-roman/mj-grasp-sim) has no FFI of its own: its hot
+ * path calls the MuJoCo 3.2.2 C library through the `mujoco` Python bindings,
+ * one candidate at a time.  Each entry point below replaces a group of those
+ * binding calls for a whole batch of grasp candidates:
+ *
+ *   mgs_model_create      <- mujoco.MjModel.from_xml_string + mujoco.MjData
+ *                            (mgs/env/gravityless_object_grasping.py:67-71);
+ *                            the MJCF is compiled host-side by mgs.core.mjcf
+ *                            into the flat model described by mgs_model_desc.
+ *   mgs_collision_free    <- per-candidate mj_resetData / set_qpos / set_pose /
+ *                            mj_forward / `data.ncon != 0`
+ *                            (mgs/env/gravityless_object_grasping.py:90-125,
+ *                             mgs/core/simualtion.py:45-49, mgs/gripper/base.py:48-59)
+ *   mgs_rollout           <- per-candidate close_gripper_at + lift + shake loop of
+ *                            grasp_stability_evaluation_from_joints
+ *                            (mgs/env/gravityless_object_grasping.py:127-295,
+ *                             mgs/gripper/robotiq2f85.py:240-244), each step one
+ *                            mujoco.mj_step, each check check_contact_with_object
+ *                            (:309-320).
+ *
+ * Conventions: all pointers are host pointers to C-contiguous arrays owned by
+ * the caller (the library copies in/out).  Functions return 0 on success and a
+ * negative MGS_E* code on failure; mgs_last_error() returns a thread-local
+ * message.  One mgs_batch is used by one host thread at a time; a batch is bound
+ * to one HIP device (one process per GPU for multi-GPU runs).
+ *
+ * The compiled model is two flat buffers (int32 and float64).  mgs_model_desc
+ * holds the sizes, the physics options and, for every array, its offset into
+ * the int buffer (fields named i_*) or the double buffer (fields named d_*).
+ * The Python side builds this struct by parsing this header, so the field list
+ * below is the single source of truth.
+ */
+#ifndef MGS_GPU_H_
+#define MGS_GPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGS_ABI_VERSION 1
+
+/* error codes */
+#define MGS_OK 0
+#define MGS_EINVAL (-1)
+#define MGS_EHIP (-2)
+#define MGS_ECAPACITY (-3)
+#define MGS_ENOMEM (-4)
+
+/* joint types (MuJoCo mjtJoint numbering) */
+#define MGS_JNT_FREE 0
+#define MGS_JNT_BALL 1
+#define MGS_JNT_SLIDE 2
+#define MGS_JNT_HINGE 3
+
+/* equality types (MuJoCo mjtEq numbering) */
+#define MGS_EQ_CONNECT 0
+#define MGS_EQ_WELD 1
+#define MGS_EQ_JOINT 2
+
+/* actuator transmission / gain / bias types (MuJoCo numbering) */
+#define MGS_TRN_JOINT 0
+#define MGS_TRN_TENDON 3
+#define MGS_GAIN_FIXED 0
+#define MGS_GAIN_AFFINE 1
+#define MGS_BIAS_NONE 0
+#define MGS_BIAS_AFFINE 1
+
+/* constraint row kinds (efc) */
+#define MGS_EFC_EQUALITY 0
+#define MGS_EFC_FRICTION 1
+#define MGS_EFC_LIMIT 2
+#define MGS_EFC_CONTACT 3
+
+/* predicate for the collision pre-filter */
+#define MGS_PRED_ANY_CONTACT 0     /* data.ncon != 0            (gravityless :306-307) */
+#define MGS_PRED_PARTITION 1       /* gripper geom vs geom past the partition (clutter) */
+
+typedef struct mgs_model_desc {
+  /* sizes */
+  int32_t nq;
+  int32_t nv;
+  int32_t nbody;
+  int32_t njnt;
+  int32_t ngeom;      /* collision geoms only, in MuJoCo geom order */
+  int32_t nhull;
+  int32_t nhullvert;
+  int32_t npair;      /* statically admissible collision pairs */
+  int32_t neq;
+  int32_t ntendon;
+  int32_t nwrap;
+  int32_t nu;
+  int32_t nmocap;
+  int32_t ncon_max;   /* contact capacity per candidate (set by host) */
+  int32_t nefc_max;   /* constraint-row capacity per candidate (set by host) */
+  int32_t maxhullvert;
+  /* options (MuJoCo <option>) */
+  int32_t iterations;
+  int32_t noslip_iterations;
+  int32_t cone;       /* 1 = elliptic (the only cone supported) */
+  int32_t integrator; /* 2 = implicitfast (the only integrator supported) */
+  double timestep;
+  double impratio;
+  double tolerance;
+  double noslip_tolerance;
+  double mpr_tolerance;
+  double gravity[3];
+  /* body arrays: int */
+  int32_t i_body_parentid;
+  int32_t i_body_rootid;
+  int32_t i_body_mocapid;
+  int32_t i_body_jntnum;
+  int32_t i_body_jntadr;
+  int32_t i_body_dofnum;
+  int32_t i_body_dofadr;
+  int32_t i_body_lastdof;   /* last dof in the body's kinematic chain, -1 if none */
+  /* body arrays: double */
+  int32_t d_body_pos;       /* 3 */
+  int32_t d_body_quat;      /* 4 */
+  int32_t d_body_ipos;      /* 3 */
+  int32_t d_body_iquat;     /* 4 */
+  int32_t d_body_mass;      /* 1 */
+  int32_t d_body_inertia;   /* 3 */
+  /* joints */
+  int32_t i_jnt_type;
+  int32_t i_jnt_qposadr;
+  int32_t i_jnt_dofadr;
+  int32_t i_jnt_bodyid;
+  int32_t i_jnt_limited;
+  int32_t d_jnt_pos;        /* 3 */
+  int32_t d_jnt_axis;       /* 3 */
+  int32_t d_jnt_range;      /* 2 */
+  int32_t d_jnt_solref;     /* 2 */
+  int32_t d_jnt_solimp;     /* 5 */
+  int32_t d_jnt_margin;     /* 1 */
+  int32_t d_jnt_stiffness;  /* 1 */
+  /* dofs */
+  int32_t i_dof_bodyid;
+  int32_t i_dof_jntid;
+  int32_t i_dof_parentid;
+  int32_t d_dof_armature;
+  int32_t d_dof_damping;
+  int32_t d_dof_frictionloss;
+  int32_t d_dof_solref;     /* 2 */
+  int32_t d_dof_solimp;     /* 5 */
+  int32_t d_qpos0;          /* nq */
+  int32_t d_qpos_spring;    /* nq */
+  /* collision geoms */
+  int32_t i_geom_bodyid;
+  int32_t i_geom_hullid;
+  int32_t i_geom_side;      /* -1 before the partition geom, 0 the partition geom, +1 after */
+  int32_t d_geom_pos;       /* 3 */
+  int32_t d_geom_quat;      /* 4 */
+  int32_t d_geom_aabb;      /* 6: local box center (3), half sizes (3) */
+  /* convex hulls */
+  int32_t i_hull_vertadr;
+  int32_t i_hull_vertnum;
+  int32_t d_hull_vert;      /* 3 * nhullvert, in geom frame */
+  int32_t d_hull_center;    /* 3 * nhull, interior point (vertex centroid) */
+  /* admissible pairs with mixed contact parameters */
+  int32_t i_pair_geom1;
+  int32_t i_pair_geom2;
+  int32_t i_pair_condim;
+  int32_t d_pair_friction;  /* 5 */
+  int32_t d_pair_solref;    /* 2 */
+  int32_t d_pair_solimp;    /* 5 */
+  int32_t d_pair_margin;    /* 1 */
+  /* equality constraints */
+  int32_t i_eq_type;
+  int32_t i_eq_obj1id;
+  int32_t i_eq_obj2id;
+  int32_t d_eq_data;        /* 11 */
+  int32_t d_eq_solref;      /* 2 */
+  int32_t d_eq_solimp;      /* 5 */
+  /* fixed tendons */
+  int32_t i_tendon_adr;
+  int32_t i_tendon_num;
+  int32_t i_wrap_dofid;
+  int32_t i_wrap_qposadr;
+  int32_t d_wrap_coef;
+  /* actuators */
+  int32_t i_actuator_trntype;
+  int32_t i_actuator_trnid;
+  int32_t i_actuator_gaintype;
+  int32_t i_actuator_biastype;
+  int32_t i_actuator_ctrllimited;
+  int32_t i_actuator_forcelimited;
+  int32_t d_actuator_gainprm;   /* 3 */
+  int32_t d_actuator_biasprm;   /* 3 */
+  int32_t d_actuator_ctrlrange; /* 2 */
+  int32_t d_actuator_forcerange;/* 2 */
+  int32_t d_actuator_gear;      /* 1 */
+  /* buffer lengths (elements) */
+  int32_t isize;
+  int32_t dsize;
+} mgs_model_desc;
+
+/* Rollout schedule: a sequence of phases (close, lift, back, right, left ...).
+ * During phase p, step t (0-based) the mocap position is
+ *     start + (target - start) * (t / nsteps)          (per component, fp64)
+ * with per-candidate start/target given to mgs_rollout; ctrl is held at
+ * ctrl[p*32 .. p*32+nu).  After step t, if check_every > 0 and t > 0 and
+ * t % check_every == 0, the gripper-object contact predicate is evaluated on
+ * the contacts of that step; if check_at_end, it is evaluated after the last
+ * step.  The first failed check ends the candidate with label 0.            */
+#define MGS_MAX_PHASES 8
+typedef struct mgs_schedule {
+  int32_t nphase;
+  int32_t obj_qposadr;   /* qpos address of the object free joint reported in obj_qpos (-1: none) */
+  int32_t nsteps[MGS_MAX_PHASES];
+  int32_t check_every[MGS_MAX_PHASES];
+  int32_t check_at_end[MGS_MAX_PHASES];
+  double ctrl[MGS_MAX_PHASES * 32];
+} mgs_schedule;
+
+/* per-candidate rollout outputs */
+typedef struct mgs_rollout_out {
+  uint8_t* label;          /* n: 1 = every check passed */
+  int32_t* fail_step;      /* n: global step index of the failed check, -1 if none */
+  double* obj_qpos;        /* n * 7: object free-joint qpos when the candidate stopped (may be NULL) */
+  int32_t* stats;          /* n * 4: max ncon, max nefc, overflow flags, total solver iterations (may be NULL) */
+} mgs_rollout_out;
+
+typedef struct mgs_model mgs_model;
+typedef struct mgs_batch mgs_batch;
+
+int mgs_abi_version(void);
+const char* mgs_last_error(void);
+
+/* Upload a compiled model; ibuf/dbuf hold desc->isize int32 and desc->dsize doubles. */
+int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const double* dbuf,
+                     int device, mgs_model** out);
+void mgs_model_free(mgs_model* model);
+
+/* Device buffers for up to `capacity` candidates. */
+int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out);
+void mgs_batch_close(mgs_batch* batch);
+
+/* Collision pre-filter (grasp_collision_mask).  qpos_init: n * nq initial qpos of
+ * every candidate (host applies set_qpos / set_pose semantics); mocap_pos n*3,
+ * mocap_quat n*4 (wxyz).  out_free[i] = 1 if the candidate is collision free. */
+int mgs_collision_free(mgs_batch* batch, int n, const double* qpos_init,
+                       const double* mocap_pos, const double* mocap_quat,
+                       int predicate, uint8_t* out_free);
+
+/* Close -> lift -> shake rollout.  phase_start / phase_target: n * nphase * 3
+ * mocap endpoints per candidate and phase. */
+int mgs_rollout(mgs_batch* batch, const mgs_schedule* sched, int n,
+                const double* qpos_init, const double* mocap_quat,
+                const double* phase_start, const double* phase_target,
+                mgs_rollout_out* out);
+
+/* Same as mgs_rollout but with inputs already resident on the device (device
+ * pointers, same layouts); outputs stay on the device.  Used to time the
+ * kernel with inputs in HBM.  stream may be NULL (default stream). */
+int mgs_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n,
+                       const double* d_qpos_init, const double* d_mocap_quat,
+                       const double* d_phase_start, const double* d_phase_target,
+                       uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
+                       int32_t* d_stats, void* stream);
+
+/* Average duration (ms) of the last timed rollout kernel launch, measured
+ * with HIP events on the launch stream. */
+double mgs_last_kernel_ms(mgs_batch* batch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGS_GPU_H_ */

@@ -1,0 +1,269 @@
+// mgs_capi.hip -- host side of libmgs_gpu.so: the C-ABI declared in
+// include/mgs_gpu.h (model upload, batch buffers, kernel launches, timing).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mgs_kernels.hip"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, const char* what = "") {
+  char buf[512];
+  snprintf(buf, sizeof(buf), fmt, what);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) return fail(MGS_EHIP, "HIP error: %s", hipGetErrorString(_e)); \
+  } while (0)
+
+// LDS carve-up of one candidate's working set (doubles, then int counters/arrays)
+Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
+  Lay l;
+  memset(&l, 0, sizeof(l));
+  int nq = m.nq, nv = m.nv, nb = m.nbody, ng = m.ngeom, nu = m.nu > 0 ? m.nu : 1;
+  int nj = m.njnt > 0 ? m.njnt : 1, nc = m.ncon_max, ne = m.nefc_max;
+  int sizes[L_COUNT];
+  sizes[L_qpos] = nq; sizes[L_qvel] = nv; sizes[L_qacc_ws] = nv; sizes[L_ctrl] = nu;
+  sizes[L_mocap_pos] = 3 * m.nmocap + 3; sizes[L_mocap_quat] = 4 * m.nmocap + 4; sizes[L_time] = 1;
+  sizes[L_xpos] = 3 * nb; sizes[L_xquat] = 4 * nb; sizes[L_xmat] = 9 * nb; sizes[L_xipos] = 3 * nb;
+  sizes[L_ximat] = 9 * nb; sizes[L_xanchor] = 3 * nj; sizes[L_xaxis] = 3 * nj;
+  sizes[L_subtree_com] = 3 * nb; sizes[L_subtree_mass] = nb; sizes[L_cinert] = 10 * nb; sizes[L_crb] = 10 * nb;
+  sizes[L_cdof] = 6 * nv; sizes[L_cdof_dot] = 6 * nv; sizes[L_cvel] = 6 * nb; sizes[L_cacc] = 6 * nb;
+  sizes[L_cfrc] = 6 * nb; sizes[L_geom_xpos] = 3 * ng; sizes[L_geom_xmat] = 9 * ng;
+  sizes[L_M] = nv * nv; sizes[L_L] = nv * nv; sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_qDeriv] = nv * nv;
+  sizes[L_qfrc_bias] = nv; sizes[L_qfrc_passive] = nv; sizes[L_qfrc_actuator] = nv; sizes[L_qfrc_smooth] = nv;
+  sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv; sizes[L_qacc] = nv;
+  sizes[L_act_force] = nu; sizes[L_act_moment] = nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
+  sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc;
+  sizes[L_J] = ne * nv; sizes[L_K] = ne * nv; sizes[L_efc_pos] = ne; sizes[L_efc_margin] = ne;
+  sizes[L_efc_vel] = ne; sizes[L_efc_aref] = ne; sizes[L_efc_R] = ne; sizes[L_efc_A] = ne; sizes[L_efc_b] = ne;
+  sizes[L_efc_f] = ne; sizes[L_efc_mu] = 5 * ne; sizes[L_efc_blk] = 36 * ne; sizes[L_efc_floss] = ne;
+  sizes[L_w] = nv; sizes[L_jac] = 12 * nv; sizes[L_scratch] = ne > 64 ? ne : 64;
+  sizes[L_poly] = 3 * 3 * K_MAXPOLY;
+  sizes[L_ints] = (16 + 3 * nc + 3 * ne + 1) / 2;
+  int off = 0;
+  for (int k = 0; k < L_COUNT; k++) {
+    l.o[k] = off;
+    off += sizes[k];
+  }
+  l.ncon_max = nc;
+  l.nefc_max = ne;
+  l.total_doubles = off;
+  *bytes = (size_t)off * sizeof(double);
+  return l;
+}
+}  // namespace
+
+struct mgs_model {
+  mgs_model_desc desc;
+  int device;
+  int32_t* dI;
+  double* dD;
+  Lay lay;
+  size_t lds_bytes;
+};
+
+struct mgs_batch {
+  mgs_model* m;
+  int cap;
+  double *d_qpos, *d_mpos, *d_mquat, *d_ps, *d_pt, *d_objq;
+  uint8_t *d_label, *d_free;
+  int32_t *d_fail, *d_stats;
+  hipEvent_t e0, e1;
+  double last_ms;
+};
+
+extern "C" {
+
+int mgs_abi_version(void) { return MGS_ABI_VERSION; }
+const char* mgs_last_error(void) { return g_err.c_str(); }
+
+int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const double* dbuf, int device,
+                     mgs_model** out) {
+  if (!desc || !ibuf || !dbuf || !out) return fail(MGS_EINVAL, "mgs_model_create: null argument%s");
+  if (desc->nv > 64 || desc->nv < 1) return fail(MGS_EINVAL, "nv must be in [1, 64]%s");
+  if (desc->cone != 1 || desc->integrator != 2)
+    return fail(MGS_EINVAL, "only elliptic cones and implicitfast are supported%s");
+  if (desc->nu > 32) return fail(MGS_EINVAL, "at most 32 actuators%s");
+  if (desc->nmocap > 1) return fail(MGS_EINVAL, "at most one mocap body%s");
+  HIPCHK(hipSetDevice(device));
+  mgs_model* m = new mgs_model();
+  m->desc = *desc;
+  m->device = device;
+  size_t ib = sizeof(int32_t) * (desc->isize > 0 ? desc->isize : 1);
+  size_t db = sizeof(double) * (desc->dsize > 0 ? desc->dsize : 1);
+  if (hipMalloc(&m->dI, ib) != hipSuccess || hipMalloc(&m->dD, db) != hipSuccess) {
+    delete m;
+    return fail(MGS_ENOMEM, "device allocation failed%s");
+  }
+  HIPCHK(hipMemcpy(m->dI, ibuf, sizeof(int32_t) * desc->isize, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(m->dD, dbuf, sizeof(double) * desc->dsize, hipMemcpyHostToDevice));
+  m->lay = make_layout(*desc, &m->lds_bytes);
+  if (m->lds_bytes > 160 * 1024) {
+    size_t need = m->lds_bytes;
+    mgs_model_free(m);
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%zu", need);
+    return fail(MGS_ECAPACITY, "per-candidate working set %s B exceeds 160 KiB LDS; lower ncon_max", buf);
+  }
+  HIPCHK(hipFuncSetAttribute((const void*)mgs_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)m->lds_bytes));
+  HIPCHK(hipFuncSetAttribute((const void*)mgs_collision_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)m->lds_bytes));
+  *out = m;
+  return MGS_OK;
+}
+
+void mgs_model_free(mgs_model* m) {
+  if (!m) return;
+  hipFree(m->dI);
+  hipFree(m->dD);
+  delete m;
+}
+
+int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out) {
+  if (!model || capacity <= 0 || !out) return fail(MGS_EINVAL, "mgs_batch_open: bad argument%s");
+  HIPCHK(hipSetDevice(model->device));
+  mgs_batch* b = new mgs_batch();
+  memset(b, 0, sizeof(*b));
+  b->m = model;
+  b->cap = capacity;
+  const mgs_model_desc& d = model->desc;
+  size_t n = (size_t)capacity;
+  bool ok = hipMalloc(&b->d_qpos, sizeof(double) * n * d.nq) == hipSuccess &&
+            hipMalloc(&b->d_mpos, sizeof(double) * n * 3) == hipSuccess &&
+            hipMalloc(&b->d_mquat, sizeof(double) * n * 4) == hipSuccess &&
+            hipMalloc(&b->d_ps, sizeof(double) * n * 3 * MGS_MAX_PHASES) == hipSuccess &&
+            hipMalloc(&b->d_pt, sizeof(double) * n * 3 * MGS_MAX_PHASES) == hipSuccess &&
+            hipMalloc(&b->d_objq, sizeof(double) * n * 7) == hipSuccess &&
+            hipMalloc(&b->d_label, n) == hipSuccess && hipMalloc(&b->d_free, n) == hipSuccess &&
+            hipMalloc(&b->d_fail, sizeof(int32_t) * n) == hipSuccess &&
+            hipMalloc(&b->d_stats, sizeof(int32_t) * n * 4) == hipSuccess;
+  if (!ok) {
+    mgs_batch_close(b);
+    return fail(MGS_ENOMEM, "device allocation failed%s");
+  }
+  HIPCHK(hipEventCreate(&b->e0));
+  HIPCHK(hipEventCreate(&b->e1));
+  *out = b;
+  return MGS_OK;
+}
+
+void mgs_batch_close(mgs_batch* b) {
+  if (!b) return;
+  hipFree(b->d_qpos); hipFree(b->d_mpos); hipFree(b->d_mquat); hipFree(b->d_ps); hipFree(b->d_pt);
+  hipFree(b->d_objq); hipFree(b->d_label); hipFree(b->d_free); hipFree(b->d_fail); hipFree(b->d_stats);
+  if (b->e0) hipEventDestroy(b->e0);
+  if (b->e1) hipEventDestroy(b->e1);
+  delete b;
+}
+
+static Mdl device_model(const mgs_model* m) {
+  Mdl md;
+  md.m = m->desc;
+  md.I = m->dI;
+  md.D = m->dD;
+  return md;
+}
+
+int mgs_collision_free(mgs_batch* b, int n, const double* qpos_init, const double* mocap_pos,
+                       const double* mocap_quat, int predicate, uint8_t* out_free) {
+  if (!b || n < 0 || n > b->cap) return fail(MGS_EINVAL, "mgs_collision_free: n exceeds batch capacity%s");
+  if (n == 0) return MGS_OK;
+  if (!qpos_init || !mocap_pos || !mocap_quat || !out_free) return fail(MGS_EINVAL, "null argument%s");
+  const mgs_model_desc& d = b->m->desc;
+  HIPCHK(hipSetDevice(b->m->device));
+  HIPCHK(hipMemcpy(b->d_qpos, qpos_init, sizeof(double) * n * d.nq, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b->d_mpos, mocap_pos, sizeof(double) * n * 3, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b->d_mquat, mocap_quat, sizeof(double) * n * 4, hipMemcpyHostToDevice));
+  Mdl md = device_model(b->m);
+  hipLaunchKernelGGL(mgs_collision_kernel, dim3(n), dim3(64), b->m->lds_bytes, 0, md, b->m->lay, n, b->d_qpos,
+                     b->d_mpos, b->d_mquat, predicate, b->d_free);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out_free, b->d_free, n, hipMemcpyDeviceToHost));
+  return MGS_OK;
+}
+
+int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                       const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
+                       uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats,
+                       void* stream) {
+  if (!b || !sched || n < 0) return fail(MGS_EINVAL, "mgs_rollout_device: bad argument%s");
+  if (sched->nphase < 1 || sched->nphase > MGS_MAX_PHASES) return fail(MGS_EINVAL, "bad phase count%s");
+  if (n == 0) return MGS_OK;
+  HIPCHK(hipSetDevice(b->m->device));
+  hipStream_t st = (hipStream_t)stream;
+  Mdl md = device_model(b->m);
+  HIPCHK(hipEventRecord(b->e0, st));
+  hipLaunchKernelGGL(mgs_rollout_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, b->m->lay, *sched, n,
+                     d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_label, d_fail_step, d_obj_qpos,
+                     d_stats);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(b->e1, st));
+  return MGS_OK;
+}
+
+double mgs_last_kernel_ms(mgs_batch* b) {
+  if (!b) return -1.0;
+  float ms = 0.f;
+  if (hipEventSynchronize(b->e1) != hipSuccess) return -1.0;
+  if (hipEventElapsedTime(&ms, b->e0, b->e1) != hipSuccess) return -1.0;
+  b->last_ms = ms;
+  return ms;
+}
+
+int mgs_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* qpos_init,
+                const double* mocap_quat, const double* phase_start, const double* phase_target,
+                mgs_rollout_out* out) {
+  if (!b || !sched || !out || n < 0 || n > b->cap) return fail(MGS_EINVAL, "mgs_rollout: bad argument%s");
+  if (n == 0) return MGS_OK;
+  if (!qpos_init || !mocap_quat || !phase_start || !phase_target || !out->label)
+    return fail(MGS_EINVAL, "mgs_rollout: null argument%s");
+  const mgs_model_desc& d = b->m->desc;
+  int np = sched->nphase;
+  HIPCHK(hipSetDevice(b->m->device));
+  HIPCHK(hipMemcpy(b->d_qpos, qpos_init, sizeof(double) * n * d.nq, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b->d_mquat, mocap_quat, sizeof(double) * n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b->d_ps, phase_start, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b->d_pt, phase_target, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
+  int rc = mgs_rollout_device(b, sched, n, b->d_qpos, b->d_mquat, b->d_ps, b->d_pt, b->d_label, b->d_fail,
+                              b->d_objq, b->d_stats, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(out->label, b->d_label, n, hipMemcpyDeviceToHost));
+  if (out->fail_step) HIPCHK(hipMemcpy(out->fail_step, b->d_fail, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (out->obj_qpos) HIPCHK(hipMemcpy(out->obj_qpos, b->d_objq, sizeof(double) * n * 7, hipMemcpyDeviceToHost));
+  if (out->stats) HIPCHK(hipMemcpy(out->stats, b->d_stats, sizeof(int32_t) * n * 4, hipMemcpyDeviceToHost));
+  return MGS_OK;
+}
+
+// test hook: device arithmetic on n inputs (out: n*4 = sqrt|x|, x/y, sin, cos)
+int mgs_arith_probe(const double* x, const double* y, int n, double* out) {
+  double *dx, *dy, *dout;
+  HIPCHK(hipMalloc(&dx, sizeof(double) * n));
+  HIPCHK(hipMalloc(&dy, sizeof(double) * n));
+  HIPCHK(hipMalloc(&dout, sizeof(double) * n * 4));
+  HIPCHK(hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy, y, sizeof(double) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(mgs_arith_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, dx, dy, n, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, sizeof(double) * n * 4, hipMemcpyDeviceToHost));
+  hipFree(dx); hipFree(dy); hipFree(dout);
+  return MGS_OK;
+}
+
+int mgs_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,153 @@
+"""ctypes binding of libmgs_gpu.so (the MI355X engine).
+
+There is deliberately no CPU fallback: if the HIP library is missing or no
+GPU is visible, every entry point raises.  (The CPU restatement under oracle/
+is test infrastructure and is never imported from here.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from mgs.core import abi
+from mgs.core.abi import ptr
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libmgs_gpu.so")
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise EngineError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    c_i, c_d, c_u8, vp = ctypes.c_int32, ctypes.c_double, ctypes.c_uint8, ctypes.c_void_p
+    L.mgs_abi_version.restype = ctypes.c_int
+    L.mgs_last_error.restype = ctypes.c_char_p
+    L.mgs_model_create.argtypes = [P(abi.ModelDesc), P(c_i), P(c_d), ctypes.c_int, P(vp)]
+    L.mgs_model_free.argtypes = [vp]
+    L.mgs_batch_open.argtypes = [vp, ctypes.c_int, P(vp)]
+    L.mgs_batch_close.argtypes = [vp]
+    L.mgs_collision_free.argtypes = [vp, ctypes.c_int, P(c_d), P(c_d), P(c_d), ctypes.c_int, P(c_u8)]
+    L.mgs_rollout.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d),
+                              P(abi.RolloutOut)]
+    L.mgs_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mgs_last_kernel_ms.argtypes = [vp]
+    L.mgs_last_kernel_ms.restype = ctypes.c_double
+    L.mgs_arith_probe.argtypes = [P(c_d), P(c_d), ctypes.c_int, P(c_d)]
+    L.mgs_device_count.restype = ctypes.c_int
+    if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
+        raise EngineError("libmgs_gpu.so ABI version mismatch with include/mgs_gpu.h")
+    _lib = L
+    return L
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = load_library().mgs_last_error().decode(errors="replace")
+        raise EngineError(f"{what} failed ({rc}): {msg}")
+
+
+class Engine:
+    """One compiled model resident on one GPU plus a reusable batch."""
+
+    def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None):
+        self.lib = load_library()
+        if self.lib.mgs_device_count() <= device:
+            raise EngineError("no HIP device visible for the MI355X engine")
+        fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
+        self.desc = abi.make_desc(fields)
+        self.cm = cm
+        self.device = device
+        self._model = ctypes.c_void_p()
+        _check(self.lib.mgs_model_create(ctypes.byref(self.desc), ptr(self._ib, ctypes.c_int32),
+                                         ptr(self._db, ctypes.c_double), device, ctypes.byref(self._model)),
+               "mgs_model_create")
+        self._batch = ctypes.c_void_p()
+        self._cap = 0
+
+    def close(self):
+        if self._batch:
+            self.lib.mgs_batch_close(self._batch)
+            self._batch = ctypes.c_void_p()
+        if self._model:
+            self.lib.mgs_model_free(self._model)
+            self._model = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch(self, n):
+        if n > self._cap:
+            if self._batch:
+                self.lib.mgs_batch_close(self._batch)
+            cap = max(n, 256)
+            self._batch = ctypes.c_void_p()
+            _check(self.lib.mgs_batch_open(self._model, cap, ctypes.byref(self._batch)), "mgs_batch_open")
+            self._cap = cap
+        return self._batch
+
+    def collision_free(self, qpos, mocap_pos, mocap_quat, predicate="any"):
+        n = len(qpos)
+        out = np.zeros(n, np.uint8)
+        if n == 0:
+            return out.astype(bool)
+        pr = abi.MGS["MGS_PRED_ANY_CONTACT"] if predicate == "any" else abi.MGS["MGS_PRED_PARTITION"]
+        q = np.ascontiguousarray(qpos, np.float64)
+        mp = np.ascontiguousarray(mocap_pos, np.float64)
+        mq = np.ascontiguousarray(mocap_quat, np.float64)
+        _check(self.lib.mgs_collision_free(self.batch(n), n, ptr(q, ctypes.c_double), ptr(mp, ctypes.c_double),
+                                           ptr(mq, ctypes.c_double), pr, ptr(out, ctypes.c_uint8)),
+               "mgs_collision_free")
+        return out.astype(bool)
+
+    def rollout(self, plan):
+        n = len(plan.qpos_init)
+        sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+        label = np.zeros(n, np.uint8)
+        fail = np.zeros(n, np.int32)
+        objq = np.zeros((n, 7), np.float64)
+        stats = np.zeros((n, 4), np.int32)
+        if n == 0:
+            return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats)
+        out = abi.RolloutOut(ptr(label, ctypes.c_uint8), ptr(fail, ctypes.c_int32),
+                             ptr(objq, ctypes.c_double), ptr(stats, ctypes.c_int32))
+        q = np.ascontiguousarray(plan.qpos_init, np.float64)
+        mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
+        ps = np.ascontiguousarray(plan.phase_start, np.float64)
+        pt = np.ascontiguousarray(plan.phase_target, np.float64)
+        _check(self.lib.mgs_rollout(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
+                                    ptr(mq, ctypes.c_double), ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double),
+                                    ctypes.byref(out)), "mgs_rollout")
+        return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats,
+                    kernel_ms=self.lib.mgs_last_kernel_ms(self._batch))
+
+    def rollout_device(self, sched, n, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats, stream=None):
+        """Launch on device pointers (ints); used by bench.py with inputs in HBM."""
+        _check(self.lib.mgs_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps, d_pt,
+                                           d_label, d_fail, d_objq, d_stats, stream), "mgs_rollout_device")
+
+    def last_kernel_ms(self):
+        return self.lib.mgs_last_kernel_ms(self._batch)
+
+
+def arith_probe(x, y):
+    L = load_library()
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.zeros((len(x), 4))
+    _check(L.mgs_arith_probe(ptr(x, ctypes.c_double), ptr(y, ctypes.c_double), len(x), ptr(out, ctypes.c_double)),
+           "mgs_arith_probe")
+    return out

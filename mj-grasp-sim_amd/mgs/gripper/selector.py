@@ -1,0 +1,16 @@
+"""Gripper factory (reference: mgs/gripper/selector.py:33-66)."""
+import numpy as np
+
+from mgs.gripper.base import MjShakableOpenCloseGripper
+from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+from mgs.util.geo.transforms import SE3Pose
+
+_GRIPPERS = {"Robotiq2f85Gripper": GripperRobotiq2f85}
+
+
+def get_gripper(cfg, default_pose=None) -> MjShakableOpenCloseGripper:
+    pose = SE3Pose(np.array([0, 0, 0]), np.array([1, 0, 0, 0]), type="wxyz") if default_pose is None else default_pose
+    name = cfg["name"] if isinstance(cfg, dict) else cfg.name
+    if name not in _GRIPPERS:
+        raise ValueError(f"Unknown gripper: {name}")
+    return _GRIPPERS[name](pose)

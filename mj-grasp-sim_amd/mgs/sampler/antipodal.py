@@ -1,0 +1,136 @@
+"""Antipodal grasp candidates (reference: mgs/sampler/antipodal.py:96-298).
+
+numpy restatement of AntipodalGraspGenerator without trimesh/rtree (absent
+here): area-weighted surface sampling of 5N points, one von-Mises-Fisher ray
+direction (kappa=10) around the inward normal per point, +-ray casting against
+the object mesh (vectorised Moller-Trumbore), the reference's +-5 cm random
+fallback partner, and define_gripper_pose (x = contact1 -> contact2,
+z = x cross random, y = z cross x, centre = midpoint).  The reference's
+normalise/denormalise round trip (normalize_load + denormalize_points, :41-93)
+is kept, including its `(p - offset) * scale` formula.
+
+Unlike the reference (no seeds anywhere, :107,142,147,217), every draw comes
+from one numpy Generator so candidate sets are reproducible.
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.stats import vonmises_fisher
+
+from mgs.core.mjcf import load_mesh_bytes
+
+
+def load_obj_mesh(path):
+    v, f = load_mesh_bytes(open(path, "rb").read(), path)
+    return v, f
+
+
+def _ray_mesh(origins, dirs, tri, eps=1e-12):
+    """all hits: returns list of arrays of hit points per ray."""
+    v0, v1, v2 = tri[:, 0], tri[:, 1], tri[:, 2]
+    e1, e2 = v1 - v0, v2 - v0
+    hits = []
+    for o, d in zip(origins, dirs):
+        p = np.cross(d, e2)
+        det = np.einsum("ij,ij->i", e1, p)
+        ok = np.abs(det) > eps
+        inv = np.where(ok, 1.0 / np.where(ok, det, 1.0), 0.0)
+        tv = o - v0
+        u = np.einsum("ij,ij->i", tv, p) * inv
+        q = np.cross(tv, e1)
+        w = (q @ d) * inv
+        t = np.einsum("ij,ij->i", e2, q) * inv
+        m = ok & (u >= 0) & (w >= 0) & (u + w <= 1) & (t > 0)
+        hits.append(o + t[m, None] * d)
+    return hits
+
+
+class AntipodalGraspGenerator:
+    def __init__(self, mesh_file_path: str, rng=None):
+        self.mesh_file_path = mesh_file_path
+        self.rng = np.random.default_rng(0) if rng is None else rng
+        self.scale = 1.0
+        self.offset = np.zeros(3)
+
+    def denormalize_points(self, points):
+        return (points - self.offset) * self.scale
+
+    def normalize_load(self):
+        v, f = load_obj_mesh(self.mesh_file_path)
+        tri = v[f]
+        area = 0.5 * np.linalg.norm(np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]), axis=1)
+        centroid = (tri.mean(1) * area[:, None]).sum(0) / area.sum()
+        ext = v.max(0) - v.min(0)
+        self.scale = float(np.linalg.norm(ext))          # trimesh.Trimesh.scale
+        vn = v / self.scale
+        c_n = centroid / self.scale
+        self.offset = -c_n
+        self.verts = vn - c_n
+        self.faces = f
+
+    def generate_grasps(self, num: int, kappa: float = 10.0, eps: float = 1e-5):
+        self.normalize_load()
+        rng = self.rng
+        tri = self.verts[self.faces]
+        cr = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+        area = 0.5 * np.linalg.norm(cr, axis=1)
+        normals = cr / np.maximum(np.linalg.norm(cr, axis=1, keepdims=True), 1e-30)
+        fidx = rng.choice(len(tri), size=5 * num, p=area / area.sum())
+        r1, r2 = rng.random((2, 5 * num, 1))
+        s1 = np.sqrt(r1)
+        pts = (1 - s1) * tri[fidx, 0] + s1 * (1 - r2) * tri[fidx, 1] + s1 * r2 * tri[fidx, 2]
+        nrm = normals[fidx]
+        dirs = np.empty_like(pts)
+        for i in range(len(pts)):
+            d = vonmises_fisher.rvs(mu=-nrm[i], kappa=kappa, size=1, random_state=rng)[0]
+            dirs[i] = d / np.linalg.norm(d)
+        one, two = [], []
+        for i in range(len(pts)):
+            if len(one) >= num:
+                break
+            o = pts[i]
+            hits = _ray_mesh([o, o], [dirs[i], -dirs[i]], tri)
+            cand = [h for hh in hits for h in hh if np.linalg.norm(h - o) >= eps]
+            if cand:
+                loc = cand[rng.integers(len(cand))]
+            else:
+                loc = o + rng.uniform(-0.05, 0.05, size=3)
+            one.append(o)
+            two.append(loc)
+        while len(one) < num:
+            o = pts[rng.integers(len(pts))]
+            one.append(o)
+            two.append(o + rng.uniform(-0.05, 0.05, size=3))
+        one, two = np.array(one), np.array(two)
+        H = self.define_gripper_pose(one, two, rng)
+        H[..., :3, 3] = self.denormalize_points(H[..., :3, 3])
+        widths = np.maximum(np.linalg.norm(two - one, axis=1), 0) * self.scale
+        return H, {"width": widths}
+
+    @staticmethod
+    def define_gripper_pose(c1, c2, rng):
+        n = len(c1)
+        center = (c1 + c2) / 2.0
+        x = c2 - c1
+        nx = np.linalg.norm(x, axis=1, keepdims=True)
+        bad = np.isclose(nx, 0.0).ravel()
+        x[~bad] /= nx[~bad]
+        x[bad] = [1.0, 0.0, 0.0]
+        z = np.cross(x, rng.standard_normal((n, 3)))
+        nz = np.linalg.norm(z, axis=1, keepdims=True)
+        badz = np.isclose(nz, 0.0).ravel()
+        z[~badz] /= nz[~badz]
+        z[badz] = [0.0, 0.0, 1.0]
+        y = np.cross(z, x)
+        H = np.zeros((n, 4, 4))
+        H[:, :3, 0], H[:, :3, 1], H[:, :3, 2], H[:, :3, 3] = x, y, z, center
+        H[:, 3, 3] = 1.0
+        return H
+
+
+def robotiq_candidates(obj, num, seed=0):
+    """(pose (num,4,4) float32 contact frames, joints (num,8) zeros = open),
+    the candidates.npz layout of gen_grasp_candidates.py:79-82."""
+    gen = AntipodalGraspGenerator(obj.obj_file_path, rng=np.random.default_rng(seed))
+    H, aux = gen.generate_grasps(num)
+    return H.astype(np.float32), np.zeros((num, 8)), aux["width"]

@@ -1,0 +1,1809 @@
+/*
+ * mgs_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library.  The product path (mj-grasp-sim_amd/, libmgs_gpu.so) never
+ * links or calls it.
+ *
+ * What it restates.  The reference's hot path is
+ *   mgs/env/gravityless_object_grasping.py:90-125   grasp_collision_mask
+ *   mgs/env/gravityless_object_grasping.py:127-295  grasp_stability_evaluation_from_joints
+ *   mgs/gripper/robotiq2f85.py:240-244             close_gripper_at (ctrl 255, mj_step)
+ *   mgs/env/gravityless_object_grasping.py:306-320 check_contact / check_contact_with_object
+ * and every physics step is `mujoco.mj_step` of MuJoCo 3.2.2 (requirements.txt:1),
+ * a third-party C library that is NOT vendored in the reference and not
+ * installed here or on the GPU box.  This file restates MuJoCo's documented
+ * pipeline for the option set the reference uses (implicitfast, elliptic cones,
+ * impratio, noslip, tolerance; gravityless_object_grasping.py:36-42):
+ *   mj_kinematics -> mj_comPos -> mj_crb/LDL -> tendon/actuator/passive -> RNE
+ *   -> collision (AABB broadphase, MPR narrowphase as in libccd, multi-contact)
+ *   -> constraint assembly with solref/solimp impedance -> PGS dual solver with
+ *   elliptic cones (QCQP friction blocks) -> noslip -> implicitfast integration.
+ * PARITY vs MuJoCo IS UNPINNED (no MuJoCo anywhere, reference has no tests;
+ * SURVEY.md §8c).  The harness logic (schedule, checks, labels) is pinned by
+ * golden traces of the reference harness (tests/golden/).
+ *
+ * Numerical contract with the HIP kernel (csrc/mgs_kernels.hip): both are
+ * compiled with -ffp-contract=off and evaluate every expression in the order
+ * written here; the only cross-lane reduction the kernel uses is tree_dot()
+ * below (pairwise tree over the next power of two >= n).  sin/cos come from the
+ * polynomial o_sincos() (no libm transcendental), sqrt and division are IEEE.
+ * Under this contract the kernel's fp64 results are bit-identical.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mgs_gpu.h"
+
+#define O_MINVAL 1e-15
+#define O_MAXF 16          /* max vertices in a contact feature */
+#define O_MAXPOLY 40
+#define O_MPR_MAXIT 64
+#define O_FEAT_EPS 1e-5
+
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  const mgs_model_desc* m;
+  const int32_t* I;
+  const double* D;
+} Mdl;
+
+#define IA(md, f) ((md)->I + (md)->m->i_##f)
+#define DA(md, f) ((md)->D + (md)->m->d_##f)
+
+typedef struct {
+  int nq, nv, nb, ng, nu, ncon_max, nefc_max;
+  /* state */
+  double *qpos, *qvel, *qacc_ws, *ctrl, *mocap_pos, *mocap_quat;
+  double time;
+  /* kinematics */
+  double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis;
+  double *subtree_com, *subtree_mass, *cinert, *crb, *cdof, *cdof_dot, *cvel, *cacc, *cfrc;
+  double *geom_xpos, *geom_xmat;
+  /* dynamics */
+  double *M, *L, *Dinv, *MI, *LI, *DIinv, *qDeriv;
+  double *qfrc_bias, *qfrc_passive, *qfrc_actuator, *qfrc_smooth, *qacc_smooth;
+  double *qfrc_constraint, *qacc, *act_force, *act_moment, *act_length, *act_vel;
+  /* contacts */
+  int ncon;
+  double *con_pos, *con_frame, *con_dist;
+  int *con_pair, *con_g1, *con_g2;
+  /* constraints */
+  int nefc;
+  double *J, *K, *efc_pos, *efc_margin, *efc_vel, *efc_aref, *efc_R, *efc_A, *efc_b, *efc_f;
+  double *efc_mu, *efc_blk, *efc_floss;
+  int *efc_type, *efc_dim, *efc_con;
+  double *w;
+  int overflow;
+  int iters;
+} Dat;
+
+/* ------------------------------------------------------------------------ */
+/* math primitives (ORDER matters: left-to-right as written) */
+static void o_sincos(double x, double* s, double* c) {
+  const double inv_pio2 = 6.36619772367581382433e-01;
+  const double pio2_1 = 1.57079632673412561417e+00;
+  const double pio2_1t = 6.07710050650619224932e-11;
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  double kd = x * inv_pio2;
+  kd = (kd >= 0.0) ? floor(kd + 0.5) : -floor(0.5 - kd);
+  double r = (x - kd * pio2_1) - kd * pio2_1t;
+  double z = r * r;
+  double ps = S1 + z * (S2 + z * (S3 + z * (S4 + z * (S5 + z * S6))));
+  double sr = r + (r * z) * ps;
+  double pc = C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6))));
+  double cr = (1.0 - 0.5 * z) + (z * z) * pc;
+  long k = (long)kd;
+  int q = (int)(k & 3);
+  if (q == 0) { *s = sr; *c = cr; }
+  else if (q == 1) { *s = cr; *c = -sr; }
+  else if (q == 2) { *s = -sr; *c = -cr; }
+  else { *s = -cr; *c = sr; }
+}
+
+static inline double dot3(const double* a, const double* b) {
+  return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+}
+static inline void cross3(double* r, const double* a, const double* b) {
+  double r0 = a[1] * b[2] - a[2] * b[1];
+  double r1 = a[2] * b[0] - a[0] * b[2];
+  double r2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = r0; r[1] = r1; r[2] = r2;
+}
+static inline void sub3(double* r, const double* a, const double* b) {
+  r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2];
+}
+static inline void add3(double* r, const double* a, const double* b) {
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+}
+/* r = m*v, m row-major 3x3 */
+static inline void mulmv3(double* r, const double* m, const double* v) {
+  double r0 = (m[0] * v[0] + m[1] * v[1]) + m[2] * v[2];
+  double r1 = (m[3] * v[0] + m[4] * v[1]) + m[5] * v[2];
+  double r2 = (m[6] * v[0] + m[7] * v[1]) + m[8] * v[2];
+  r[0] = r0; r[1] = r1; r[2] = r2;
+}
+/* r = m^T*v */
+static inline void mulmtv3(double* r, const double* m, const double* v) {
+  double r0 = (m[0] * v[0] + m[3] * v[1]) + m[6] * v[2];
+  double r1 = (m[1] * v[0] + m[4] * v[1]) + m[7] * v[2];
+  double r2 = (m[2] * v[0] + m[5] * v[1]) + m[8] * v[2];
+  r[0] = r0; r[1] = r1; r[2] = r2;
+}
+static inline void quatmul(double* r, const double* a, const double* b) {
+  double r0 = ((a[0] * b[0] - a[1] * b[1]) - a[2] * b[2]) - a[3] * b[3];
+  double r1 = ((a[0] * b[1] + a[1] * b[0]) + a[2] * b[3]) - a[3] * b[2];
+  double r2 = ((a[0] * b[2] - a[1] * b[3]) + a[2] * b[0]) + a[3] * b[1];
+  double r3 = ((a[0] * b[3] + a[1] * b[2]) - a[2] * b[1]) + a[3] * b[0];
+  r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3;
+}
+static inline void quat2mat(double* m, const double* q) {
+  double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  m[0] = ((q00 + q11) - q22) - q33;
+  m[1] = 2.0 * (q12 - q03);
+  m[2] = 2.0 * (q13 + q02);
+  m[3] = 2.0 * (q12 + q03);
+  m[4] = ((q00 - q11) + q22) - q33;
+  m[5] = 2.0 * (q23 - q01);
+  m[6] = 2.0 * (q13 - q02);
+  m[7] = 2.0 * (q23 + q01);
+  m[8] = ((q00 - q11) - q22) + q33;
+}
+static inline void normalize4(double* q) {
+  double n = sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+  if (n < O_MINVAL) { q[0] = 1.0; q[1] = q[2] = q[3] = 0.0; return; }
+  double inv = 1.0 / n;
+  q[0] = q[0] * inv; q[1] = q[1] * inv; q[2] = q[2] * inv; q[3] = q[3] * inv;
+}
+static inline double normalize3(double* v) {
+  double n = sqrt(dot3(v, v));
+  if (n < O_MINVAL) { v[0] = 1.0; v[1] = v[2] = 0.0; return 0.0; }
+  double inv = 1.0 / n;
+  v[0] = v[0] * inv; v[1] = v[1] * inv; v[2] = v[2] * inv;
+  return n;
+}
+static inline void axisangle2quat(double* q, const double* axis, double angle) {
+  double s, c;
+  o_sincos(0.5 * angle, &s, &c);
+  q[0] = c; q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+/* spatial inertia (10) times motion vector (6), MuJoCo layout */
+static inline void mul_inert_vec(double* r, const double* i, const double* v) {
+  double r0 = ((i[0] * v[0] + i[3] * v[1]) + i[4] * v[2]) - i[8] * v[4] + i[7] * v[5];
+  double r1 = ((i[3] * v[0] + i[1] * v[1]) + i[5] * v[2]) + i[8] * v[3] - i[6] * v[5];
+  double r2 = ((i[4] * v[0] + i[5] * v[1]) + i[2] * v[2]) - i[7] * v[3] + i[6] * v[4];
+  double r3 = (i[8] * v[1] - i[7] * v[2]) + i[9] * v[3];
+  double r4 = (i[6] * v[2] - i[8] * v[0]) + i[9] * v[4];
+  double r5 = (i[7] * v[0] - i[6] * v[1]) + i[9] * v[5];
+  r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3; r[4] = r4; r[5] = r5;
+}
+static inline double dot6(const double* a, const double* b) {
+  return ((((a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]) + a[3] * b[3]) + a[4] * b[4]) + a[5] * b[5];
+}
+/* motion cross product v x u (spatial) */
+static inline void cross_motion(double* r, const double* v, const double* u) {
+  double r0 = v[1] * u[2] - v[2] * u[1];
+  double r1 = v[2] * u[0] - v[0] * u[2];
+  double r2 = v[0] * u[1] - v[1] * u[0];
+  double r3 = (v[1] * u[5] - v[2] * u[4]) + (v[4] * u[2] - v[5] * u[1]);
+  double r4 = (v[2] * u[3] - v[0] * u[5]) + (v[5] * u[0] - v[3] * u[2]);
+  double r5 = (v[0] * u[4] - v[1] * u[3]) + (v[3] * u[1] - v[4] * u[0]);
+  r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3; r[4] = r4; r[5] = r5;
+}
+/* force cross product v x* f (spatial) */
+static inline void cross_force(double* r, const double* v, const double* f) {
+  double r0 = (v[1] * f[2] - v[2] * f[1]) + (v[4] * f[5] - v[5] * f[4]);
+  double r1 = (v[2] * f[0] - v[0] * f[2]) + (v[5] * f[3] - v[3] * f[5]);
+  double r2 = (v[0] * f[1] - v[1] * f[0]) + (v[3] * f[4] - v[4] * f[3]);
+  double r3 = v[1] * f[5] - v[2] * f[4];
+  double r4 = v[2] * f[3] - v[0] * f[5];
+  double r5 = v[0] * f[4] - v[1] * f[3];
+  r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3; r[4] = r4; r[5] = r5;
+}
+
+/* Pairwise tree sum of a[k]*b[k], k < n, over P leaves (P = next pow2 >= n,
+ * zero leaves beyond n): level s = 1,2,4,...: leaf[k] = leaf[k] + leaf[k^s].
+ * This is the kernel's wave reduction over lanes (DPP butterfly). */
+static double tree_dot(const double* a, const double* b, int n) {
+  double leaf[128];
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int k = 0; k < P; k++) leaf[k] = (k < n) ? a[k] * b[k] : 0.0;
+  for (int s = 1; s < P; s <<= 1) {
+    double nxt[128];
+    for (int k = 0; k < P; k++) nxt[k] = leaf[k] + leaf[k ^ s];
+    memcpy(leaf, nxt, sizeof(double) * P);
+  }
+  return leaf[0];
+}
+
+/* ------------------------------------------------------------------------ */
+/* allocation */
+static Dat* dat_alloc(const Mdl* md) {
+  const mgs_model_desc* m = md->m;
+  Dat* d = (Dat*)calloc(1, sizeof(Dat));
+  d->nq = m->nq; d->nv = m->nv; d->nb = m->nbody; d->ng = m->ngeom; d->nu = m->nu;
+  d->ncon_max = m->ncon_max; d->nefc_max = m->nefc_max;
+  int nq = m->nq, nv = m->nv, nb = m->nbody, ng = m->ngeom, nu = m->nu > 0 ? m->nu : 1;
+  int nc = m->ncon_max, ne = m->nefc_max, nj = m->njnt > 0 ? m->njnt : 1;
+  size_t tot = 0;
+#define SZ(n) tot += (size_t)(n)
+  SZ(nq); SZ(nv); SZ(nv); SZ(nu); SZ(3 * m->nmocap + 3); SZ(4 * m->nmocap + 4);
+  SZ(3 * nb); SZ(4 * nb); SZ(9 * nb); SZ(3 * nb); SZ(9 * nb); SZ(3 * nj); SZ(3 * nj);
+  SZ(3 * nb); SZ(nb); SZ(10 * nb); SZ(10 * nb); SZ(6 * nv); SZ(6 * nv); SZ(6 * nb); SZ(6 * nb); SZ(6 * nb);
+  SZ(3 * ng); SZ(9 * ng);
+  SZ(nv * nv); SZ(nv * nv); SZ(nv); SZ(nv * nv); SZ(nv * nv); SZ(nv); SZ(nv * nv);
+  SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nu); SZ(nu * nv); SZ(nu); SZ(nu);
+  SZ(3 * nc); SZ(9 * nc); SZ(nc);
+  SZ(ne * nv); SZ(ne * nv); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne);
+  SZ(5 * ne); SZ(36 * ne); SZ(ne); SZ(nv);
+#undef SZ
+  double* p = (double*)calloc(tot, sizeof(double));
+#define TAKE(ptr, n) do { d->ptr = p; p += (n); } while (0)
+  TAKE(qpos, nq); TAKE(qvel, nv); TAKE(qacc_ws, nv); TAKE(ctrl, nu);
+  TAKE(mocap_pos, 3 * m->nmocap + 3); TAKE(mocap_quat, 4 * m->nmocap + 4);
+  TAKE(xpos, 3 * nb); TAKE(xquat, 4 * nb); TAKE(xmat, 9 * nb); TAKE(xipos, 3 * nb); TAKE(ximat, 9 * nb);
+  TAKE(xanchor, 3 * nj); TAKE(xaxis, 3 * nj);
+  TAKE(subtree_com, 3 * nb); TAKE(subtree_mass, nb); TAKE(cinert, 10 * nb); TAKE(crb, 10 * nb);
+  TAKE(cdof, 6 * nv); TAKE(cdof_dot, 6 * nv); TAKE(cvel, 6 * nb); TAKE(cacc, 6 * nb); TAKE(cfrc, 6 * nb);
+  TAKE(geom_xpos, 3 * ng); TAKE(geom_xmat, 9 * ng);
+  TAKE(M, nv * nv); TAKE(L, nv * nv); TAKE(Dinv, nv); TAKE(MI, nv * nv); TAKE(LI, nv * nv);
+  TAKE(DIinv, nv); TAKE(qDeriv, nv * nv);
+  TAKE(qfrc_bias, nv); TAKE(qfrc_passive, nv); TAKE(qfrc_actuator, nv); TAKE(qfrc_smooth, nv);
+  TAKE(qacc_smooth, nv); TAKE(qfrc_constraint, nv); TAKE(qacc, nv);
+  TAKE(act_force, nu); TAKE(act_moment, nu * nv); TAKE(act_length, nu); TAKE(act_vel, nu);
+  TAKE(con_pos, 3 * nc); TAKE(con_frame, 9 * nc); TAKE(con_dist, nc);
+  TAKE(J, ne * nv); TAKE(K, ne * nv); TAKE(efc_pos, ne); TAKE(efc_margin, ne); TAKE(efc_vel, ne);
+  TAKE(efc_aref, ne); TAKE(efc_R, ne); TAKE(efc_A, ne); TAKE(efc_b, ne); TAKE(efc_f, ne);
+  TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_floss, ne); TAKE(w, nv);
+#undef TAKE
+  d->con_pair = (int*)calloc((size_t)nc, sizeof(int));
+  d->con_g1 = (int*)calloc((size_t)nc, sizeof(int));
+  d->con_g2 = (int*)calloc((size_t)nc, sizeof(int));
+  d->efc_type = (int*)calloc((size_t)ne, sizeof(int));
+  d->efc_dim = (int*)calloc((size_t)ne, sizeof(int));
+  d->efc_con = (int*)calloc((size_t)ne, sizeof(int));
+  return d;
+}
+
+static void dat_free(Dat* d) {
+  if (!d) return;
+  free(d->qpos);
+  free(d->con_pair); free(d->con_g1); free(d->con_g2);
+  free(d->efc_type); free(d->efc_dim); free(d->efc_con);
+  free(d);
+}
+
+/* ------------------------------------------------------------------------ */
+/* mj_kinematics */
+static void kinematics(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  const int32_t *parent = IA(md, body_parentid), *mocapid = IA(md, body_mocapid);
+  const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
+  const int32_t *jtype = IA(md, jnt_type), *qadr = IA(md, jnt_qposadr);
+  const double *bpos = DA(md, body_pos), *bquat = DA(md, body_quat);
+  const double *ipos = DA(md, body_ipos), *iquat = DA(md, body_iquat);
+  const double *jpos = DA(md, jnt_pos), *jaxis = DA(md, jnt_axis), *qpos0 = DA(md, qpos0);
+  d->xpos[0] = d->xpos[1] = d->xpos[2] = 0.0;
+  d->xquat[0] = 1.0; d->xquat[1] = d->xquat[2] = d->xquat[3] = 0.0;
+  quat2mat(d->xmat, d->xquat);
+  for (int b = 1; b < m->nbody; b++) {
+    double pos[3], quat[4], mat[9];
+    if (mocapid[b] >= 0) {
+      const double* mp = d->mocap_pos + 3 * mocapid[b];
+      const double* mq = d->mocap_quat + 4 * mocapid[b];
+      pos[0] = mp[0]; pos[1] = mp[1]; pos[2] = mp[2];
+      quat[0] = mq[0]; quat[1] = mq[1]; quat[2] = mq[2]; quat[3] = mq[3];
+      normalize4(quat);
+    } else {
+      int p = parent[b];
+      double t[3];
+      mulmv3(t, d->xmat + 9 * p, bpos + 3 * b);
+      add3(pos, d->xpos + 3 * p, t);
+      quatmul(quat, d->xquat + 4 * p, bquat + 4 * b);
+      for (int k = 0; k < jntnum[b]; k++) {
+        int j = jntadr[b] + k;
+        int a = qadr[j];
+        if (jtype[j] == MGS_JNT_FREE) {
+          pos[0] = d->qpos[a]; pos[1] = d->qpos[a + 1]; pos[2] = d->qpos[a + 2];
+          quat[0] = d->qpos[a + 3]; quat[1] = d->qpos[a + 4]; quat[2] = d->qpos[a + 5]; quat[3] = d->qpos[a + 6];
+          normalize4(quat);
+          d->xanchor[3 * j] = pos[0]; d->xanchor[3 * j + 1] = pos[1]; d->xanchor[3 * j + 2] = pos[2];
+          d->xaxis[3 * j] = 0.0; d->xaxis[3 * j + 1] = 0.0; d->xaxis[3 * j + 2] = 1.0;
+        } else {
+          quat2mat(mat, quat);
+          mulmv3(d->xaxis + 3 * j, mat, jaxis + 3 * j);
+          mulmv3(t, mat, jpos + 3 * j);
+          add3(d->xanchor + 3 * j, t, pos);
+          if (jtype[j] == MGS_JNT_HINGE) {
+            double ql[4], qn[4];
+            axisangle2quat(ql, jaxis + 3 * j, d->qpos[a] - qpos0[a]);
+            quatmul(qn, quat, ql);
+            quat[0] = qn[0]; quat[1] = qn[1]; quat[2] = qn[2]; quat[3] = qn[3];
+            quat2mat(mat, quat);
+            mulmv3(t, mat, jpos + 3 * j);
+            sub3(pos, d->xanchor + 3 * j, t);
+          } else { /* slide */
+            double dq = d->qpos[a] - qpos0[a];
+            pos[0] = pos[0] + d->xaxis[3 * j] * dq;
+            pos[1] = pos[1] + d->xaxis[3 * j + 1] * dq;
+            pos[2] = pos[2] + d->xaxis[3 * j + 2] * dq;
+          }
+        }
+      }
+      normalize4(quat);
+    }
+    d->xpos[3 * b] = pos[0]; d->xpos[3 * b + 1] = pos[1]; d->xpos[3 * b + 2] = pos[2];
+    d->xquat[4 * b] = quat[0]; d->xquat[4 * b + 1] = quat[1]; d->xquat[4 * b + 2] = quat[2]; d->xquat[4 * b + 3] = quat[3];
+    quat2mat(d->xmat + 9 * b, quat);
+    double t[3], qi[4];
+    mulmv3(t, d->xmat + 9 * b, ipos + 3 * b);
+    add3(d->xipos + 3 * b, d->xpos + 3 * b, t);
+    quatmul(qi, quat, iquat + 4 * b);
+    quat2mat(d->ximat + 9 * b, qi);
+  }
+  /* geoms */
+  const int32_t* gbody = IA(md, geom_bodyid);
+  const double *gpos = DA(md, geom_pos), *gquat = DA(md, geom_quat);
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = gbody[g];
+    double t[3], q[4];
+    mulmv3(t, d->xmat + 9 * b, gpos + 3 * g);
+    add3(d->geom_xpos + 3 * g, d->xpos + 3 * b, t);
+    quatmul(q, d->xquat + 4 * b, gquat + 4 * g);
+    quat2mat(d->geom_xmat + 9 * g, q);
+  }
+}
+
+/* mj_comPos: subtree com, cinert, cdof */
+static void com_pos(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  const int32_t *parent = IA(md, body_parentid), *rootid = IA(md, body_rootid);
+  const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
+  const int32_t *jtype = IA(md, jnt_type), *dadr = IA(md, jnt_dofadr);
+  const double *mass = DA(md, body_mass), *inertia = DA(md, body_inertia);
+  int nb = m->nbody;
+  for (int b = 0; b < nb; b++) {
+    d->subtree_mass[b] = mass[b];
+    d->subtree_com[3 * b] = mass[b] * d->xipos[3 * b];
+    d->subtree_com[3 * b + 1] = mass[b] * d->xipos[3 * b + 1];
+    d->subtree_com[3 * b + 2] = mass[b] * d->xipos[3 * b + 2];
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = parent[b];
+    d->subtree_mass[p] = d->subtree_mass[p] + d->subtree_mass[b];
+    d->subtree_com[3 * p] = d->subtree_com[3 * p] + d->subtree_com[3 * b];
+    d->subtree_com[3 * p + 1] = d->subtree_com[3 * p + 1] + d->subtree_com[3 * b + 1];
+    d->subtree_com[3 * p + 2] = d->subtree_com[3 * p + 2] + d->subtree_com[3 * b + 2];
+  }
+  for (int b = 0; b < nb; b++) {
+    if (d->subtree_mass[b] < O_MINVAL) {
+      d->subtree_com[3 * b] = d->xipos[3 * b];
+      d->subtree_com[3 * b + 1] = d->xipos[3 * b + 1];
+      d->subtree_com[3 * b + 2] = d->xipos[3 * b + 2];
+    } else {
+      double inv = 1.0 / d->subtree_mass[b];
+      d->subtree_com[3 * b] = d->subtree_com[3 * b] * inv;
+      d->subtree_com[3 * b + 1] = d->subtree_com[3 * b + 1] * inv;
+      d->subtree_com[3 * b + 2] = d->subtree_com[3 * b + 2] * inv;
+    }
+  }
+  for (int b = 0; b < nb; b++) {
+    double* ci = d->cinert + 10 * b;
+    const double* R = d->ximat + 9 * b;
+    const double* in = inertia + 3 * b;
+    double mm = mass[b];
+    double off[3];
+    sub3(off, d->xipos + 3 * b, d->subtree_com + 3 * rootid[b]);
+    /* tmp = R diag(in) R^T */
+    double t[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        t[3 * i + j] = ((R[3 * i] * in[0]) * R[3 * j] + (R[3 * i + 1] * in[1]) * R[3 * j + 1]) +
+                       (R[3 * i + 2] * in[2]) * R[3 * j + 2];
+    ci[0] = t[0] + mm * (off[1] * off[1] + off[2] * off[2]);
+    ci[1] = t[4] + mm * (off[0] * off[0] + off[2] * off[2]);
+    ci[2] = t[8] + mm * (off[0] * off[0] + off[1] * off[1]);
+    ci[3] = t[1] - mm * (off[0] * off[1]);
+    ci[4] = t[2] - mm * (off[0] * off[2]);
+    ci[5] = t[5] - mm * (off[1] * off[2]);
+    ci[6] = mm * off[0];
+    ci[7] = mm * off[1];
+    ci[8] = mm * off[2];
+    ci[9] = mm;
+  }
+  for (int b = 1; b < nb; b++) {
+    const double* c = d->subtree_com + 3 * rootid[b];
+    for (int k = 0; k < jntnum[b]; k++) {
+      int j = jntadr[b] + k;
+      int da = dadr[j];
+      double off[3];
+      sub3(off, c, d->xanchor + 3 * j);
+      if (jtype[j] == MGS_JNT_FREE) {
+        for (int i = 0; i < 3; i++) {
+          double* cd = d->cdof + 6 * (da + i);
+          cd[0] = cd[1] = cd[2] = 0.0;
+          cd[3] = (i == 0) ? 1.0 : 0.0; cd[4] = (i == 1) ? 1.0 : 0.0; cd[5] = (i == 2) ? 1.0 : 0.0;
+        }
+        const double* R = d->xmat + 9 * b;
+        for (int i = 0; i < 3; i++) {
+          double* cd = d->cdof + 6 * (da + 3 + i);
+          double ax[3] = {R[i], R[3 + i], R[6 + i]};
+          cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+          cross3(cd + 3, ax, off);
+        }
+      } else if (jtype[j] == MGS_JNT_HINGE) {
+        double* cd = d->cdof + 6 * da;
+        const double* ax = d->xaxis + 3 * j;
+        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+        cross3(cd + 3, ax, off);
+      } else { /* slide */
+        double* cd = d->cdof + 6 * da;
+        const double* ax = d->xaxis + 3 * j;
+        cd[0] = cd[1] = cd[2] = 0.0;
+        cd[3] = ax[0]; cd[4] = ax[1]; cd[5] = ax[2];
+      }
+    }
+  }
+}
+
+/* mj_crb + armature -> M (dense) */
+static void crb(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nb = m->nbody, nv = m->nv;
+  const int32_t *parent = IA(md, body_parentid), *dbody = IA(md, dof_bodyid), *dpar = IA(md, dof_parentid);
+  const double* arm = DA(md, dof_armature);
+  memcpy(d->crb, d->cinert, sizeof(double) * 10 * nb);
+  for (int b = nb - 1; b > 0; b--) {
+    int p = parent[b];
+    if (p > 0)
+      for (int k = 0; k < 10; k++) d->crb[10 * p + k] = d->crb[10 * p + k] + d->crb[10 * b + k];
+  }
+  memset(d->M, 0, sizeof(double) * nv * nv);
+  for (int i = 0; i < nv; i++) {
+    double buf[6];
+    mul_inert_vec(buf, d->crb + 10 * dbody[i], d->cdof + 6 * i);
+    d->M[i * nv + i] = dot6(d->cdof + 6 * i, buf) + arm[i];
+    int j = dpar[i];
+    while (j >= 0) {
+      double v = dot6(d->cdof + 6 * j, buf);
+      d->M[i * nv + j] = v;
+      d->M[j * nv + i] = v;
+      j = dpar[j];
+    }
+  }
+}
+
+/* dense LDL^T: A = L D L^T, L unit lower (stored strictly lower), Dinv = 1/D */
+static void ldl_factor(int n, const double* A, double* L, double* Dinv) {
+  double W[128], Dv[128];
+  for (int j = 0; j < n; j++) {
+    for (int k = 0; k < j; k++) W[k] = L[j * n + k] * Dv[k];
+    double dj = A[j * n + j];
+    for (int k = 0; k < j; k++) dj = dj - W[k] * L[j * n + k];
+    Dv[j] = dj;
+    Dinv[j] = 1.0 / dj;
+    for (int i = j + 1; i < n; i++) {
+      double s = A[i * n + j];
+      for (int k = 0; k < j; k++) s = s - L[i * n + k] * W[k];
+      L[i * n + j] = s * Dinv[j];
+    }
+  }
+}
+static void ldl_solve(int n, const double* L, const double* Dinv, const double* b, double* x) {
+  double y[128];
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s = s - L[i * n + k] * y[k];
+    y[i] = s;
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = y[i] * Dinv[i];
+    for (int k = i + 1; k < n; k++) s = s - L[k * n + i] * x[k];
+    x[i] = s;
+  }
+}
+
+/* tendon length/moment, actuator length/moment/velocity/force, qfrc_actuator */
+static void actuation(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nv = m->nv;
+  const int32_t *trntype = IA(md, actuator_trntype), *trnid = IA(md, actuator_trnid);
+  const int32_t *gtype = IA(md, actuator_gaintype), *btype = IA(md, actuator_biastype);
+  const int32_t *clim = IA(md, actuator_ctrllimited), *flim = IA(md, actuator_forcelimited);
+  const double *gain = DA(md, actuator_gainprm), *bias = DA(md, actuator_biasprm);
+  const double *crange = DA(md, actuator_ctrlrange), *frange = DA(md, actuator_forcerange);
+  const double* gear = DA(md, actuator_gear);
+  const int32_t *tadr = IA(md, tendon_adr), *tnum = IA(md, tendon_num);
+  const int32_t *wdof = IA(md, wrap_dofid), *wq = IA(md, wrap_qposadr);
+  const double* wcoef = DA(md, wrap_coef);
+  const int32_t *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
+  for (int k = 0; k < nv; k++) d->qfrc_actuator[k] = 0.0;
+  for (int u = 0; u < m->nu; u++) {
+    double* mom = d->act_moment + u * nv;
+    for (int k = 0; k < nv; k++) mom[k] = 0.0;
+    double len;
+    if (trntype[u] == MGS_TRN_JOINT) {
+      int j = trnid[u];
+      len = d->qpos[jq[j]] * gear[u];
+      mom[jd[j]] = gear[u];
+    } else {
+      int t = trnid[u];
+      double tl = 0.0;
+      for (int w = tadr[t]; w < tadr[t] + tnum[t]; w++) {
+        tl = tl + wcoef[w] * d->qpos[wq[w]];
+        mom[wdof[w]] = mom[wdof[w]] + wcoef[w] * gear[u];
+      }
+      len = tl * gear[u];
+    }
+    double vel = 0.0;
+    for (int k = 0; k < nv; k++) vel = vel + mom[k] * d->qvel[k];
+    d->act_length[u] = len;
+    d->act_vel[u] = vel;
+    double c = d->ctrl[u];
+    if (clim[u]) {
+      if (c < crange[2 * u]) c = crange[2 * u];
+      if (c > crange[2 * u + 1]) c = crange[2 * u + 1];
+    }
+    double g = gain[3 * u];
+    if (gtype[u] == MGS_GAIN_AFFINE) g = (gain[3 * u] + gain[3 * u + 1] * len) + gain[3 * u + 2] * vel;
+    double f = g * c;
+    if (btype[u] == MGS_BIAS_AFFINE) f = f + ((bias[3 * u] + bias[3 * u + 1] * len) + bias[3 * u + 2] * vel);
+    if (flim[u]) {
+      if (f < frange[2 * u]) f = frange[2 * u];
+      if (f > frange[2 * u + 1]) f = frange[2 * u + 1];
+    }
+    d->act_force[u] = f;
+    for (int k = 0; k < nv; k++) d->qfrc_actuator[k] = d->qfrc_actuator[k] + mom[k] * f;
+  }
+}
+
+/* joint springs and dof damping */
+static void passive(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
+  const double *stiff = DA(md, jnt_stiffness), *qspring = DA(md, qpos_spring), *damp = DA(md, dof_damping);
+  for (int k = 0; k < m->nv; k++) d->qfrc_passive[k] = 0.0;
+  for (int j = 0; j < m->njnt; j++) {
+    if (stiff[j] == 0.0) continue;
+    if (jtype[j] == MGS_JNT_HINGE || jtype[j] == MGS_JNT_SLIDE)
+      d->qfrc_passive[jd[j]] = -stiff[j] * (d->qpos[jq[j]] - qspring[jq[j]]);
+  }
+  for (int k = 0; k < m->nv; k++) d->qfrc_passive[k] = d->qfrc_passive[k] - damp[k] * d->qvel[k];
+}
+
+/* mj_comVel + mj_rne (no acceleration term) -> qfrc_bias */
+static void rne(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nb = m->nbody;
+  const int32_t *parent = IA(md, body_parentid), *dnum = IA(md, body_dofnum), *dadr = IA(md, body_dofadr);
+  const int32_t* dbody = IA(md, dof_bodyid);
+  for (int k = 0; k < 6; k++) { d->cvel[k] = 0.0; d->cacc[k] = 0.0; }
+  d->cacc[3] = -m->gravity[0]; d->cacc[4] = -m->gravity[1]; d->cacc[5] = -m->gravity[2];
+  for (int b = 1; b < nb; b++) {
+    int p = parent[b];
+    double* cv = d->cvel + 6 * b;
+    double* ca = d->cacc + 6 * b;
+    for (int k = 0; k < 6; k++) { cv[k] = d->cvel[6 * p + k]; ca[k] = d->cacc[6 * p + k]; }
+    for (int i = 0; i < dnum[b]; i++) {
+      int dd = dadr[b] + i;
+      cross_motion(d->cdof_dot + 6 * dd, cv, d->cdof + 6 * dd);
+      for (int k = 0; k < 6; k++) cv[k] = cv[k] + d->cdof[6 * dd + k] * d->qvel[dd];
+    }
+    for (int i = 0; i < dnum[b]; i++) {
+      int dd = dadr[b] + i;
+      for (int k = 0; k < 6; k++) ca[k] = ca[k] + d->cdof_dot[6 * dd + k] * d->qvel[dd];
+    }
+    double f1[6], f2[6], f3[6];
+    mul_inert_vec(f1, d->cinert + 10 * b, ca);
+    mul_inert_vec(f2, d->cinert + 10 * b, cv);
+    cross_force(f3, cv, f2);
+    for (int k = 0; k < 6; k++) d->cfrc[6 * b + k] = f1[k] + f3[k];
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = parent[b];
+    if (p > 0)
+      for (int k = 0; k < 6; k++) d->cfrc[6 * p + k] = d->cfrc[6 * p + k] + d->cfrc[6 * b + k];
+  }
+  for (int i = 0; i < m->nv; i++) d->qfrc_bias[i] = dot6(d->cdof + 6 * i, d->cfrc + 6 * dbody[i]);
+}
+
+/* ------------------------------------------------------------------------ */
+/* collision */
+typedef struct { double v[3], a[3], b[3]; } SupPt;
+
+/* support point of geom g along world direction dir; returns vertex index */
+static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, double* out) {
+  int h = IA(md, geom_hullid)[g];
+  int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
+  const double* V = DA(md, hull_vert) + 3 * adr;
+  const double* R = d->geom_xmat + 9 * g;
+  double dl[3];
+  mulmtv3(dl, R, dir);
+  double best = -INFINITY;
+  int bi = 0;
+  for (int i = 0; i < num; i++) {
+    double s = (V[3 * i] * dl[0] + V[3 * i + 1] * dl[1]) + V[3 * i + 2] * dl[2];
+    if (s > best) { best = s; bi = i; }
+  }
+  double t[3];
+  mulmv3(t, R, V + 3 * bi);
+  add3(out, d->geom_xpos + 3 * g, t);
+  return bi;
+}
+
+static void mink_support(const Mdl* md, const Dat* d, int g1, int g2, const double* dir, SupPt* p) {
+  double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  support_geom(md, d, g1, dir, p->a);
+  support_geom(md, d, g2, nd, p->b);
+  sub3(p->v, p->a, p->b);
+}
+
+static void portal_normal(double* n, const SupPt* p1, const SupPt* p2, const SupPt* p3) {
+  double e1[3], e2[3];
+  sub3(e1, p2->v, p1->v);
+  sub3(e2, p3->v, p1->v);
+  cross3(n, e1, e2);
+  normalize3(n);
+}
+
+static int portal_reach_tol(const SupPt* p1, const SupPt* p2, const SupPt* p3, const SupPt* p4,
+                            const double* n, double tol) {
+  double dv4 = dot3(p4->v, n);
+  double t1 = dv4 - dot3(p1->v, n);
+  double t2 = dv4 - dot3(p2->v, n);
+  double t3 = dv4 - dot3(p3->v, n);
+  double mn = t1 < t2 ? t1 : t2;
+  mn = mn < t3 ? mn : t3;
+  return mn <= tol;
+}
+
+static void portal_expand(SupPt* p0, SupPt* p1, SupPt* p2, SupPt* p3, const SupPt* p4) {
+  double c[3];
+  cross3(c, p4->v, p0->v);
+  if (dot3(p1->v, c) > 0.0) {
+    if (dot3(p2->v, c) > 0.0) *p1 = *p4; else *p3 = *p4;
+  } else {
+    if (dot3(p3->v, c) > 0.0) *p2 = *p4; else *p1 = *p4;
+  }
+}
+
+/* Minkowski Portal Refinement (penetration variant, as in libccd, which
+ * MuJoCo 3.2.x uses for convex mesh collisions).  Returns 1 on penetration
+ * with unit normal n (from geom g1 towards g2), depth > 0 and point pos. */
+static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* n, double* depth,
+                           double* pos) {
+  const double tol = md->m->mpr_tolerance;
+  const int32_t* ghull = IA(md, geom_hullid);
+  const double* HC = DA(md, hull_center);
+  SupPt p0, p1, p2, p3, p4;
+  double t[3], dir[3];
+  mulmv3(t, d->geom_xmat + 9 * g1, HC + 3 * ghull[g1]);
+  add3(p0.a, d->geom_xpos + 3 * g1, t);
+  mulmv3(t, d->geom_xmat + 9 * g2, HC + 3 * ghull[g2]);
+  add3(p0.b, d->geom_xpos + 3 * g2, t);
+  sub3(p0.v, p0.a, p0.b);
+  if (p0.v[0] == 0.0 && p0.v[1] == 0.0 && p0.v[2] == 0.0) p0.v[0] = 1e-9;
+  dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
+  normalize3(dir);
+  mink_support(md, d, g1, g2, dir, &p1);
+  if (dot3(p1.v, dir) <= 0.0) return 0;
+  cross3(dir, p0.v, p1.v);
+  if (dot3(dir, dir) < 1e-30) {
+    /* origin on segment v0-v1 */
+    double nn = sqrt(dot3(p1.v, p1.v));
+    if (nn < O_MINVAL) return 0;
+    n[0] = p1.v[0] / nn; n[1] = p1.v[1] / nn; n[2] = p1.v[2] / nn;
+    *depth = nn;
+    pos[0] = 0.5 * (p1.a[0] + p1.b[0]); pos[1] = 0.5 * (p1.a[1] + p1.b[1]); pos[2] = 0.5 * (p1.a[2] + p1.b[2]);
+    return 1;
+  }
+  normalize3(dir);
+  mink_support(md, d, g1, g2, dir, &p2);
+  if (dot3(p2.v, dir) <= 0.0) return 0;
+  {
+    double e1[3], e2[3];
+    sub3(e1, p1.v, p0.v);
+    sub3(e2, p2.v, p0.v);
+    cross3(dir, e1, e2);
+    normalize3(dir);
+  }
+  if (dot3(dir, p0.v) > 0.0) {
+    SupPt tmp = p1; p1 = p2; p2 = tmp;
+    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+  }
+  int it;
+  for (it = 0; it < O_MPR_MAXIT; it++) {
+    mink_support(md, d, g1, g2, dir, &p3);
+    if (dot3(p3.v, dir) <= 0.0) return 0;
+    double c[3];
+    int cont = 0;
+    cross3(c, p1.v, p3.v);
+    if (dot3(c, p0.v) < 0.0) { p2 = p3; cont = 1; }
+    else {
+      cross3(c, p3.v, p2.v);
+      if (dot3(c, p0.v) < 0.0) { p1 = p3; cont = 1; }
+    }
+    if (!cont) break;
+    double e1[3], e2[3];
+    sub3(e1, p1.v, p0.v);
+    sub3(e2, p2.v, p0.v);
+    cross3(dir, e1, e2);
+    normalize3(dir);
+  }
+  if (it == O_MPR_MAXIT) return 0;
+  /* refine until the portal encloses the origin */
+  for (it = 0; it < O_MPR_MAXIT; it++) {
+    portal_normal(dir, &p1, &p2, &p3);
+    if (dot3(dir, p1.v) >= 0.0) break;
+    mink_support(md, d, g1, g2, dir, &p4);
+    if (dot3(p4.v, dir) < 0.0) return 0;
+    if (portal_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) return 0;
+    portal_expand(&p0, &p1, &p2, &p3, &p4);
+  }
+  if (it == O_MPR_MAXIT) return 0;
+  /* penetration */
+  for (it = 0;; it++) {
+    portal_normal(dir, &p1, &p2, &p3);
+    mink_support(md, d, g1, g2, dir, &p4);
+    if (it >= O_MPR_MAXIT || portal_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) {
+      double dep = dot3(dir, p1.v);
+      if (!(dep > 0.0)) return 0;
+      n[0] = dir[0]; n[1] = dir[1]; n[2] = dir[2];
+      *depth = dep;
+      double q[3] = {dir[0] * dep, dir[1] * dep, dir[2] * dep};
+      double a1[3], a2[3], a3[3], c[3];
+      sub3(a1, p1.v, q); sub3(a2, p2.v, q); sub3(a3, p3.v, q);
+      cross3(c, a2, a3); double u1 = dot3(c, dir);
+      cross3(c, a3, a1); double u2 = dot3(c, dir);
+      cross3(c, a1, a2); double u3 = dot3(c, dir);
+      double su = (u1 + u2) + u3;
+      if (fabs(su) < 1e-30) { u1 = u2 = u3 = 1.0 / 3.0; }
+      else { double inv = 1.0 / su; u1 = u1 * inv; u2 = u2 * inv; u3 = u3 * inv; }
+      for (int k = 0; k < 3; k++) {
+        double pa = (u1 * p1.a[k] + u2 * p2.a[k]) + u3 * p3.a[k];
+        double pb = (u1 * p1.b[k] + u2 * p2.b[k]) + u3 * p3.b[k];
+        pos[k] = 0.5 * (pa + pb);
+      }
+      return 1;
+    }
+    portal_expand(&p0, &p1, &p2, &p3, &p4);
+  }
+}
+
+static void make_frame(const double* n, double* t1, double* t2) {
+  double a[3];
+  if (fabs(n[0]) < 0.6) { a[0] = 1.0; a[1] = 0.0; a[2] = 0.0; }
+  else { a[0] = 0.0; a[1] = 1.0; a[2] = 0.0; }
+  double an = dot3(a, n);
+  t1[0] = a[0] - n[0] * an; t1[1] = a[1] - n[1] * an; t1[2] = a[2] - n[2] * an;
+  normalize3(t1);
+  cross3(t2, n, t1);
+}
+
+typedef struct { double x, y, h; } P2;
+
+/* collect the vertices of geom g whose height along n is within tol of the
+ * extreme (sign=+1: max, sign=-1: min); returns count (<= O_MAXF) and extreme */
+static int feature(const Mdl* md, const Dat* d, int g, const double* n, const double* t1, const double* t2,
+                   int sign, double tol, P2* out, double* ext) {
+  int h = IA(md, geom_hullid)[g];
+  int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
+  const double* V = DA(md, hull_vert) + 3 * adr;
+  const double* R = d->geom_xmat + 9 * g;
+  const double* x = d->geom_xpos + 3 * g;
+  double nl[3];
+  mulmtv3(nl, R, n);
+  double base = dot3(x, n);
+  double best = (sign > 0) ? -INFINITY : INFINITY;
+  for (int i = 0; i < num; i++) {
+    double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
+    if (sign > 0 ? (s > best) : (s < best)) best = s;
+  }
+  *ext = best;
+  int cnt = 0;
+  double lim = (sign > 0) ? best - tol : best + tol;
+  for (int i = 0; i < num && cnt < O_MAXF; i++) {
+    double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
+    if (sign > 0 ? (s >= lim) : (s <= lim)) {
+      double t[3], P[3];
+      mulmv3(t, R, V + 3 * i);
+      add3(P, x, t);
+      out[cnt].x = dot3(P, t1);
+      out[cnt].y = dot3(P, t2);
+      out[cnt].h = s;
+      cnt++;
+    }
+  }
+  return cnt;
+}
+
+static inline double cross2(const P2* o, const P2* a, const P2* b) {
+  return (a->x - o->x) * (b->y - o->y) - (a->y - o->y) * (b->x - o->x);
+}
+
+/* 2D convex hull (Andrew monotone chain), CCW, collinear points removed */
+static int hull2d(P2* pts, int n, P2* out) {
+  /* insertion sort by (x, y) */
+  for (int i = 1; i < n; i++) {
+    P2 key = pts[i];
+    int j = i - 1;
+    while (j >= 0 && (pts[j].x > key.x || (pts[j].x == key.x && pts[j].y > key.y))) {
+      pts[j + 1] = pts[j];
+      j--;
+    }
+    pts[j + 1] = key;
+  }
+  /* drop exact duplicates */
+  int m = 0;
+  for (int i = 0; i < n; i++)
+    if (m == 0 || pts[i].x != pts[m - 1].x || pts[i].y != pts[m - 1].y) pts[m++] = pts[i];
+  n = m;
+  if (n <= 2) {
+    for (int i = 0; i < n; i++) out[i] = pts[i];
+    return n;
+  }
+  int k = 0;
+  for (int i = 0; i < n; i++) {
+    while (k >= 2 && cross2(&out[k - 2], &out[k - 1], &pts[i]) <= 0.0) k--;
+    out[k++] = pts[i];
+  }
+  int lo = k + 1;
+  for (int i = n - 2; i >= 0; i--) {
+    while (k >= lo && cross2(&out[k - 2], &out[k - 1], &pts[i]) <= 0.0) k--;
+    out[k++] = pts[i];
+  }
+  return k - 1;
+}
+
+static inline P2 lerp2(const P2* a, const P2* b, double t) {
+  P2 r;
+  r.x = a->x + t * (b->x - a->x);
+  r.y = a->y + t * (b->y - a->y);
+  r.h = a->h + t * (b->h - a->h);
+  return r;
+}
+
+/* clip polygon/segment/point Q (nq) against CCW convex polygon P (np >= 3) */
+static int clip_poly(const P2* P, int np, P2* Q, int nq) {
+  P2 buf[O_MAXPOLY];
+  if (nq == 1) {
+    for (int e = 0; e < np; e++) {
+      const P2* a = &P[e];
+      const P2* b = &P[(e + 1) % np];
+      if (cross2(a, b, &Q[0]) < 0.0) return 0;
+    }
+    return 1;
+  }
+  if (nq == 2) {
+    double t0 = 0.0, t1 = 1.0;
+    for (int e = 0; e < np; e++) {
+      const P2* a = &P[e];
+      const P2* b = &P[(e + 1) % np];
+      double d0 = cross2(a, b, &Q[0]);
+      double d1 = cross2(a, b, &Q[1]);
+      if (d0 < 0.0 && d1 < 0.0) return 0;
+      if (d0 < 0.0) { double t = d0 / (d0 - d1); if (t > t0) t0 = t; }
+      else if (d1 < 0.0) { double t = d0 / (d0 - d1); if (t < t1) t1 = t; }
+    }
+    if (t0 > t1) return 0;
+    P2 a = lerp2(&Q[0], &Q[1], t0);
+    P2 b = lerp2(&Q[0], &Q[1], t1);
+    Q[0] = a; Q[1] = b;
+    return 2;
+  }
+  for (int e = 0; e < np && nq > 0; e++) {
+    const P2* a = &P[e];
+    const P2* b = &P[(e + 1) % np];
+    int no = 0;
+    for (int i = 0; i < nq; i++) {
+      const P2* cur = &Q[i];
+      const P2* prv = &Q[(i + nq - 1) % nq];
+      double dc = cross2(a, b, cur);
+      double dp = cross2(a, b, prv);
+      if (dc >= 0.0) {
+        if (dp < 0.0 && no < O_MAXPOLY) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+        if (no < O_MAXPOLY) buf[no++] = *cur;
+      } else if (dp >= 0.0) {
+        if (no < O_MAXPOLY) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+      }
+    }
+    for (int i = 0; i < no; i++) Q[i] = buf[i];
+    nq = no;
+  }
+  return nq;
+}
+
+static inline double dist2d(const P2* a, const P2* b) {
+  double dx = a->x - b->x, dy = a->y - b->y;
+  return dx * dx + dy * dy;
+}
+
+static void add_contact(const Mdl* md, Dat* d, int pair, int g1, int g2, const double* pos,
+                        const double* n, const double* t1, const double* t2, double dist) {
+  if (d->ncon >= d->ncon_max) { d->overflow |= 1; return; }
+  int c = d->ncon++;
+  (void)md;
+  d->con_pos[3 * c] = pos[0]; d->con_pos[3 * c + 1] = pos[1]; d->con_pos[3 * c + 2] = pos[2];
+  double* f = d->con_frame + 9 * c;
+  f[0] = n[0]; f[1] = n[1]; f[2] = n[2];
+  f[3] = t1[0]; f[4] = t1[1]; f[5] = t1[2];
+  f[6] = t2[0]; f[7] = t2[1]; f[8] = t2[2];
+  d->con_dist[c] = dist;
+  d->con_pair[c] = pair;
+  d->con_g1[c] = g1;
+  d->con_g2[c] = g2;
+}
+
+/* convex-convex narrowphase with multi-contact manifold (<= 4 points) */
+static void collide_pair(const Mdl* md, Dat* d, int pair) {
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  double n[3], depth, mpos[3];
+  if (!mpr_penetration(md, d, g1, g2, n, &depth, mpos)) return;
+  double t1[3], t2[3];
+  make_frame(n, t1, t2);
+  P2 fa[O_MAXF], fb[O_MAXF];
+  double s1, s2;
+  /* extremes first (tolerance uses the support depth along n) */
+  int na = feature(md, d, g1, n, t1, t2, +1, 0.0, fa, &s1);
+  int nb = feature(md, d, g2, n, t1, t2, -1, 0.0, fb, &s2);
+  double dn = s1 - s2;
+  if (!(dn > 0.0)) return;
+  double tol = dn + O_FEAT_EPS;
+  na = feature(md, d, g1, n, t1, t2, +1, tol, fa, &s1);
+  nb = feature(md, d, g2, n, t1, t2, -1, tol, fb, &s2);
+  int refB = (nb >= na);
+  P2 refpoly[O_MAXPOLY], inc[O_MAXPOLY];
+  int nr = refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly);
+  int ni = refB ? hull2d(fa, na, inc) : hull2d(fb, nb, inc);
+  P2 pts[O_MAXPOLY];
+  double dep[O_MAXPOLY];
+  int np = 0;
+  if (nr >= 3) {
+    int nc = clip_poly(refpoly, nr, inc, ni);
+    for (int i = 0; i < nc; i++) {
+      double dd = refB ? (inc[i].h - s2) : (s1 - inc[i].h);
+      if (dd > 0.0) { pts[np] = inc[i]; dep[np] = dd; np++; }
+    }
+  }
+  if (np == 0) {
+    double dist = -dn;
+    add_contact(md, d, pair, g1, g2, mpos, n, t1, t2, dist);
+    return;
+  }
+  int sel[4];
+  int ns;
+  if (np <= 4) {
+    for (int i = 0; i < np; i++) sel[i] = i;
+    ns = np;
+  } else {
+    int i0 = 0;
+    for (int i = 1; i < np; i++) if (dep[i] > dep[i0]) i0 = i;
+    int i1 = -1; double bd = -1.0;
+    for (int i = 0; i < np; i++) { if (i == i0) continue; double v = dist2d(&pts[i], &pts[i0]); if (v > bd) { bd = v; i1 = i; } }
+    int i2 = -1; bd = -1.0;
+    for (int i = 0; i < np; i++) {
+      if (i == i0 || i == i1) continue;
+      double v = fabs(cross2(&pts[i0], &pts[i1], &pts[i]));
+      if (v > bd) { bd = v; i2 = i; }
+    }
+    int i3 = -1; bd = -1.0;
+    for (int i = 0; i < np; i++) {
+      if (i == i0 || i == i1 || i == i2) continue;
+      double v0 = dist2d(&pts[i], &pts[i0]), v1 = dist2d(&pts[i], &pts[i1]), v2 = dist2d(&pts[i], &pts[i2]);
+      double v = v0 < v1 ? v0 : v1;
+      v = v < v2 ? v : v2;
+      if (v > bd) { bd = v; i3 = i; }
+    }
+    sel[0] = i0; sel[1] = i1; sel[2] = i2; sel[3] = i3;
+    ns = 4;
+  }
+  double sref = refB ? s2 : s1;
+  for (int k = 0; k < ns; k++) {
+    const P2* p = &pts[sel[k]];
+    double hm = 0.5 * (p->h + sref);
+    double pos[3];
+    for (int c = 0; c < 3; c++) pos[c] = (p->x * t1[c] + p->y * t2[c]) + hm * n[c];
+    add_contact(md, d, pair, g1, g2, pos, n, t1, t2, -dep[sel[k]]);
+  }
+}
+
+static void collision(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
+  const double *aabb = DA(md, geom_aabb), *pm = DA(md, pair_margin);
+  d->ncon = 0;
+  for (int p = 0; p < m->npair; p++) {
+    int g[2] = {p1[p], p2[p]};
+    double c[2][3], hw[2][3];
+    for (int s = 0; s < 2; s++) {
+      const double* R = d->geom_xmat + 9 * g[s];
+      const double* lc = aabb + 6 * g[s];
+      const double* lh = lc + 3;
+      double t[3];
+      mulmv3(t, R, lc);
+      add3(c[s], d->geom_xpos + 3 * g[s], t);
+      for (int k = 0; k < 3; k++)
+        hw[s][k] = (fabs(R[3 * k]) * lh[0] + fabs(R[3 * k + 1]) * lh[1]) + fabs(R[3 * k + 2]) * lh[2];
+    }
+    int ov = 1;
+    for (int k = 0; k < 3; k++)
+      if (fabs(c[0][k] - c[1][k]) > (hw[0][k] + hw[1][k]) + pm[p]) ov = 0;
+    if (ov) collide_pair(md, d, p);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Jacobians of a point on body b: jacp, jacr (3 x nv, row-major) */
+static void jac_point(const Mdl* md, const Dat* d, int b, const double* pt, double* jacp, double* jacr) {
+  int nv = md->m->nv;
+  memset(jacp, 0, sizeof(double) * 3 * nv);
+  memset(jacr, 0, sizeof(double) * 3 * nv);
+  int dof = IA(md, body_lastdof)[b];
+  const int32_t* dpar = IA(md, dof_parentid);
+  const double* c = d->subtree_com + 3 * IA(md, body_rootid)[b];
+  double off[3];
+  sub3(off, pt, c);
+  while (dof >= 0) {
+    const double* cd = d->cdof + 6 * dof;
+    double cr[3];
+    cross3(cr, cd, off);
+    for (int k = 0; k < 3; k++) {
+      jacr[k * nv + dof] = cd[k];
+      jacp[k * nv + dof] = cd[3 + k] + cr[k];
+    }
+    dof = dpar[dof];
+  }
+}
+
+/* impedance from solimp at violation x (MuJoCo getimpedance, integer power) */
+static double impedance(const double* si, double pos, double margin) {
+  if (si[0] == si[1] || si[2] <= O_MINVAL) return 0.5 * (si[0] + si[1]);
+  double x = (pos - margin) / si[2];
+  if (x < 0.0) x = -x;
+  if (x >= 1.0) return si[1];
+  if (x <= 0.0) return si[0];
+  int pw = (int)si[4];
+  double mid = si[3], y;
+  if (pw <= 1) y = x;
+  else if (x <= mid) {
+    double a = 1.0, xp = 1.0;
+    for (int k = 0; k < pw - 1; k++) a = a * mid;
+    a = 1.0 / a;
+    for (int k = 0; k < pw; k++) xp = xp * x;
+    y = a * xp;
+  } else {
+    double b = 1.0, xp = 1.0;
+    for (int k = 0; k < pw - 1; k++) b = b * (1.0 - mid);
+    b = 1.0 / b;
+    for (int k = 0; k < pw; k++) xp = xp * (1.0 - x);
+    y = 1.0 - b * xp;
+  }
+  return si[0] + y * (si[1] - si[0]);
+}
+
+static int add_row(Dat* d, int type, double pos, double margin, int dim, int con) {
+  if (d->nefc >= d->nefc_max) { d->overflow |= 2; return -1; }
+  int r = d->nefc++;
+  d->efc_type[r] = type; d->efc_pos[r] = pos; d->efc_margin[r] = margin;
+  d->efc_dim[r] = dim; d->efc_con[r] = con;
+  memset(d->J + (size_t)r * d->nv, 0, sizeof(double) * d->nv);
+  return r;
+}
+
+/* reference acceleration and regularizer for rows r..r+dim-1 sharing solref/solimp */
+static void row_params(const Mdl* md, Dat* d, int r, int dim, const double* sr, const double* si,
+                       const double* mu, int elliptic_contact) {
+  const double dt = md->m->timestep;
+  double tc = sr[0], dr = sr[1];
+  double imp = impedance(si, d->efc_pos[r], d->efc_margin[r]);
+  double dmax = si[1];
+  double B, Kc;
+  if (tc > 0.0) {
+    if (tc < 2.0 * dt) tc = 2.0 * dt;
+    B = 2.0 / (dmax * tc);
+    Kc = 1.0 / (((dmax * dmax) * (tc * tc)) * (dr * dr));
+  } else {
+    B = -dr / dmax;
+    Kc = -tc / (dmax * dmax);
+  }
+  for (int j = 0; j < dim; j++) {
+    int q = r + j;
+    double p = (j == 0) ? (d->efc_pos[q] - d->efc_margin[q]) : 0.0;
+    d->efc_aref[q] = -B * d->efc_vel[q] - (Kc * imp) * p;
+  }
+  double Rn = ((1.0 - imp) / imp) * d->efc_A[r];
+  if (Rn < O_MINVAL) Rn = O_MINVAL;
+  d->efc_R[r] = Rn;
+  if (elliptic_contact && dim > 1) {
+    double R1 = Rn / md->m->impratio;
+    d->efc_R[r + 1] = R1;
+    for (int j = 1; j < dim - 1; j++)
+      d->efc_R[r + j + 1] = (R1 * (mu[0] * mu[0])) / (mu[j] * mu[j]);
+  } else {
+    for (int j = 1; j < dim; j++) {
+      double Rj = ((1.0 - imp) / imp) * d->efc_A[r + j];
+      d->efc_R[r + j] = Rj < O_MINVAL ? O_MINVAL : Rj;
+    }
+  }
+}
+
+static void make_constraints(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nv = m->nv;
+  d->nefc = 0;
+  double jp1[3 * 128], jr1[3 * 128], jp2[3 * 128], jr2[3 * 128];
+  /* --- equality */
+  const int32_t *et = IA(md, eq_type), *eo1 = IA(md, eq_obj1id), *eo2 = IA(md, eq_obj2id);
+  const double* ed = DA(md, eq_data);
+  for (int e = 0; e < m->neq; e++) {
+    const double* data = ed + 11 * e;
+    if (et[e] == MGS_EQ_CONNECT || et[e] == MGS_EQ_WELD) {
+      int b1 = eo1[e], b2 = eo2[e];
+      double p1[3], p2[3], t[3];
+      if (et[e] == MGS_EQ_CONNECT) {
+        mulmv3(t, d->xmat + 9 * b1, data);
+        add3(p1, d->xpos + 3 * b1, t);
+        mulmv3(t, d->xmat + 9 * b2, data + 3);
+        add3(p2, d->xpos + 3 * b2, t);
+      } else {
+        mulmv3(t, d->xmat + 9 * b1, data);
+        add3(p1, d->xpos + 3 * b1, t);
+        p2[0] = d->xpos[3 * b2]; p2[1] = d->xpos[3 * b2 + 1]; p2[2] = d->xpos[3 * b2 + 2];
+      }
+      jac_point(md, d, b1, p1, jp1, jr1);
+      jac_point(md, d, b2, p2, jp2, jr2);
+      if (d->nefc + (et[e] == MGS_EQ_WELD ? 6 : 3) > d->nefc_max) { d->overflow |= 2; break; }
+      for (int k = 0; k < 3; k++) {
+        int r = add_row(d, MGS_EFC_EQUALITY, p1[k] - p2[k], 0.0, 1, e);
+        for (int c = 0; c < nv; c++) d->J[r * nv + c] = jp1[k * nv + c] - jp2[k * nv + c];
+      }
+      if (et[e] == MGS_EQ_WELD) {
+        double q1r[4], q2c[4], qe[4];
+        quatmul(q1r, d->xquat + 4 * b1, data + 3);
+        q2c[0] = d->xquat[4 * b2]; q2c[1] = -d->xquat[4 * b2 + 1];
+        q2c[2] = -d->xquat[4 * b2 + 2]; q2c[3] = -d->xquat[4 * b2 + 3];
+        quatmul(qe, q2c, q1r);
+        double ts = data[7];
+        int rr[3];
+        for (int k = 0; k < 3; k++) rr[k] = add_row(d, MGS_EFC_EQUALITY, qe[1 + k] * ts, 0.0, 1, e);
+        for (int c = 0; c < nv; c++) {
+          double ax[4] = {0.0, jr1[c] - jr2[c], jr1[nv + c] - jr2[nv + c], jr1[2 * nv + c] - jr2[2 * nv + c]};
+          double t1q[4], t2q[4];
+          quatmul(t1q, q2c, ax);
+          quatmul(t2q, t1q, q1r);
+          for (int k = 0; k < 3; k++) d->J[rr[k] * nv + c] = (0.5 * t2q[1 + k]) * ts;
+        }
+      }
+    } else if (et[e] == MGS_EQ_JOINT) {
+      int j1 = eo1[e], j2 = eo2[e];
+      const int32_t *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
+      double q1 = d->qpos[jq[j1]] - data[5];
+      double pos, deriv = 0.0;
+      if (j2 >= 0) {
+        double x = d->qpos[jq[j2]] - data[6];
+        double poly = data[0] + x * (data[1] + x * (data[2] + x * (data[3] + x * data[4])));
+        deriv = data[1] + x * (2.0 * data[2] + x * (3.0 * data[3] + x * (4.0 * data[4])));
+        pos = q1 - poly;
+      } else {
+        pos = q1 - data[0];
+      }
+      if (d->nefc + 1 > d->nefc_max) { d->overflow |= 2; break; }
+      int r = add_row(d, MGS_EFC_EQUALITY, pos, 0.0, 1, e);
+      d->J[r * nv + jd[j1]] = 1.0;
+      if (j2 >= 0) d->J[r * nv + jd[j2]] = d->J[r * nv + jd[j2]] - deriv;
+    }
+  }
+  int neqrows = d->nefc;
+  /* --- dof friction loss */
+  const double* floss = DA(md, dof_frictionloss);
+  int fr0 = d->nefc;
+  for (int k = 0; k < nv; k++) {
+    if (floss[k] > 0.0) {
+      int r = add_row(d, MGS_EFC_FRICTION, 0.0, 0.0, 1, k);
+      if (r < 0) break;
+      d->J[r * nv + k] = 1.0;
+      d->efc_floss[r] = floss[k];
+    }
+  }
+  int fr1 = d->nefc;
+  /* --- joint limits */
+  const int32_t *lim = IA(md, jnt_limited), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
+  const double *range = DA(md, jnt_range), *jmargin = DA(md, jnt_margin);
+  int lr0 = d->nefc;
+  for (int j = 0; j < m->njnt; j++) {
+    if (!lim[j]) continue;
+    double q = d->qpos[jq[j]];
+    double dlo = q - range[2 * j], dhi = range[2 * j + 1] - q;
+    if (dlo < jmargin[j]) {
+      int r = add_row(d, MGS_EFC_LIMIT, dlo, jmargin[j], 1, j);
+      if (r >= 0) d->J[r * nv + jd[j]] = 1.0;
+    }
+    if (dhi < jmargin[j]) {
+      int r = add_row(d, MGS_EFC_LIMIT, dhi, jmargin[j], 1, j);
+      if (r >= 0) d->J[r * nv + jd[j]] = -1.0;
+    }
+  }
+  int lr1 = d->nefc;
+  /* --- contacts */
+  const int32_t *gbody = IA(md, geom_bodyid), *pcd = IA(md, pair_condim);
+  const double *pfr = DA(md, pair_friction), *pmar = DA(md, pair_margin);
+  int cr0 = d->nefc;
+  for (int c = 0; c < d->ncon; c++) {
+    int p = d->con_pair[c];
+    int dim = pcd[p];
+    if (d->nefc + dim > d->nefc_max) { d->overflow |= 2; break; }
+    int b1 = gbody[d->con_g1[c]], b2 = gbody[d->con_g2[c]];
+    const double* pt = d->con_pos + 3 * c;
+    const double* fr = d->con_frame + 9 * c;
+    jac_point(md, d, b1, pt, jp1, jr1);
+    jac_point(md, d, b2, pt, jp2, jr2);
+    int r = d->nefc;
+    for (int j = 0; j < dim; j++) add_row(d, MGS_EFC_CONTACT, j == 0 ? d->con_dist[c] : 0.0, pmar[p], dim, c);
+    for (int col = 0; col < nv; col++) {
+      double dp[3] = {jp2[col] - jp1[col], jp2[nv + col] - jp1[nv + col], jp2[2 * nv + col] - jp1[2 * nv + col]};
+      for (int j = 0; j < dim && j < 3; j++) d->J[(r + j) * nv + col] = dot3(fr + 3 * j, dp);
+      if (dim >= 4) {
+        double dr[3] = {jr2[col] - jr1[col], jr2[nv + col] - jr1[nv + col], jr2[2 * nv + col] - jr1[2 * nv + col]};
+        d->J[(r + 3) * nv + col] = dot3(fr, dr);
+        if (dim == 6) {
+          d->J[(r + 4) * nv + col] = dot3(fr + 3, dr);
+          d->J[(r + 5) * nv + col] = dot3(fr + 6, dr);
+        }
+      }
+    }
+    for (int j = 0; j < dim; j++) d->efc_mu[5 * r + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
+  }
+  int cr1 = d->nefc;
+  /* --- velocities, K = M^-1 J^T, diag A, impedance, aref, R */
+  int ne = d->nefc;
+  for (int r = 0; r < ne; r++) {
+    const double* Jr = d->J + (size_t)r * nv;
+    double v = 0.0;
+    for (int k = 0; k < nv; k++) v = v + Jr[k] * d->qvel[k];
+    d->efc_vel[r] = v;
+    ldl_solve(nv, d->L, d->Dinv, Jr, d->K + (size_t)r * nv);
+    double a = 0.0;
+    for (int k = 0; k < nv; k++) a = a + Jr[k] * d->K[(size_t)r * nv + k];
+    d->efc_A[r] = a;
+  }
+  const double *eqsr = DA(md, eq_solref), *eqsi = DA(md, eq_solimp);
+  for (int r = 0; r < neqrows; r++) {
+    int e = d->efc_con[r];
+    row_params(md, d, r, 1, eqsr + 2 * e, eqsi + 5 * e, NULL, 0);
+  }
+  const double *dsr = DA(md, dof_solref), *dsi = DA(md, dof_solimp);
+  for (int r = fr0; r < fr1; r++) {
+    int k = d->efc_con[r];
+    row_params(md, d, r, 1, dsr + 2 * k, dsi + 5 * k, NULL, 0);
+  }
+  const double *jsr = DA(md, jnt_solref), *jsi = DA(md, jnt_solimp);
+  for (int r = lr0; r < lr1; r++) {
+    int j = d->efc_con[r];
+    row_params(md, d, r, 1, jsr + 2 * j, jsi + 5 * j, NULL, 0);
+  }
+  const double *psr = DA(md, pair_solref), *psi = DA(md, pair_solimp);
+  for (int r = cr0; r < cr1;) {
+    int c = d->efc_con[r];
+    int p = d->con_pair[c];
+    int dim = d->efc_dim[r];
+    row_params(md, d, r, dim, psr + 2 * p, psi + 5 * p, d->efc_mu + 5 * r, 1);
+    r += dim;
+  }
+  /* b = J qacc_smooth - aref; contact blocks of A (+R on the diagonal) */
+  for (int r = 0; r < ne; r++) {
+    const double* Jr = d->J + (size_t)r * nv;
+    double v = 0.0;
+    for (int k = 0; k < nv; k++) v = v + Jr[k] * d->qacc_smooth[k];
+    d->efc_b[r] = v - d->efc_aref[r];
+  }
+  for (int r = cr0; r < cr1;) {
+    int dim = d->efc_dim[r];
+    double* blk = d->efc_blk + 36 * r;
+    for (int i = 0; i < dim; i++)
+      for (int j = 0; j < dim; j++) {
+        const double* Ji = d->J + (size_t)(r + i) * nv;
+        const double* Kj = d->K + (size_t)(r + j) * nv;
+        double a = 0.0;
+        for (int k = 0; k < nv; k++) a = a + Ji[k] * Kj[k];
+        blk[i * dim + j] = a;
+      }
+    r += dim;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* QCQP: minimize 0.5 x'Ax + x'b  s.t.  sum (x_j/mu_j)^2 <= r^2, n in {1,2,3,5} */
+static void qcqp(int n, const double* A, const double* b, const double* mu, double r, double* x) {
+  double As[25], bs[5], y[5], P[25];
+  for (int i = 0; i < n; i++) {
+    bs[i] = b[i] * mu[i];
+    for (int j = 0; j < n; j++) As[i * n + j] = (A[i * n + j] * mu[i]) * mu[j];
+  }
+  double la = 0.0;
+  double rr = r * r;
+  for (int it = 0; it < 20; it++) {
+    /* P = inverse(As + la I) via Gauss-Jordan without pivoting (SPD) */
+    double T[25];
+    for (int i = 0; i < n * n; i++) T[i] = As[i];
+    for (int i = 0; i < n; i++) T[i * n + i] = T[i * n + i] + la;
+    for (int i = 0; i < n * n; i++) P[i] = 0.0;
+    for (int i = 0; i < n; i++) P[i * n + i] = 1.0;
+    int bad = 0;
+    for (int c = 0; c < n; c++) {
+      double piv = T[c * n + c];
+      if (piv < 1e-15) { bad = 1; break; }
+      double ip = 1.0 / piv;
+      for (int j = 0; j < n; j++) { T[c * n + j] = T[c * n + j] * ip; P[c * n + j] = P[c * n + j] * ip; }
+      for (int i = 0; i < n; i++) {
+        if (i == c) continue;
+        double f = T[i * n + c];
+        if (f == 0.0) continue;
+        for (int j = 0; j < n; j++) {
+          T[i * n + j] = T[i * n + j] - f * T[c * n + j];
+          P[i * n + j] = P[i * n + j] - f * P[c * n + j];
+        }
+      }
+    }
+    if (bad) { for (int i = 0; i < n; i++) y[i] = 0.0; break; }
+    for (int i = 0; i < n; i++) {
+      double s = 0.0;
+      for (int j = 0; j < n; j++) s = s - P[i * n + j] * bs[j];
+      y[i] = s;
+    }
+    double val = 0.0;
+    for (int i = 0; i < n; i++) val = val + y[i] * y[i];
+    val = val - rr;
+    if (val < 1e-10) break;
+    double pv[5];
+    for (int i = 0; i < n; i++) {
+      double s = 0.0;
+      for (int j = 0; j < n; j++) s = s + P[i * n + j] * y[j];
+      pv[i] = s;
+    }
+    double deriv = 0.0;
+    for (int i = 0; i < n; i++) deriv = deriv + y[i] * pv[i];
+    deriv = -2.0 * deriv;
+    double delta = -val / deriv;
+    if (delta < 1e-10) break;
+    la = la + delta;
+  }
+  for (int i = 0; i < n; i++) x[i] = y[i] * mu[i];
+}
+
+/* dual cost of f: 0.5 f'(A+R)f + f'b computed from w = M^-1 J^T f */
+static double dual_cost(const Dat* d) {
+  int nv = d->nv;
+  double c = 0.0;
+  for (int r = 0; r < d->nefc; r++) {
+    const double* Jr = d->J + (size_t)r * nv;
+    double jw = 0.0;
+    for (int k = 0; k < nv; k++) jw = jw + Jr[k] * d->w[k];
+    c = c + d->efc_f[r] * ((0.5 * (jw + d->efc_R[r] * d->efc_f[r])) + d->efc_b[r]);
+  }
+  return c;
+}
+
+static void w_from_f(Dat* d) {
+  int nv = d->nv;
+  for (int k = 0; k < nv; k++) {
+    double s = 0.0;
+    for (int r = 0; r < d->nefc; r++) s = s + d->K[(size_t)r * nv + k] * d->efc_f[r];
+    d->w[k] = s;
+  }
+}
+
+static void project_block(const Dat* d, int r, double* f) {
+  int t = d->efc_type[r];
+  if (t == MGS_EFC_FRICTION) {
+    double fl = d->efc_floss[r];
+    if (f[0] < -fl) f[0] = -fl;
+    if (f[0] > fl) f[0] = fl;
+  } else if (t == MGS_EFC_LIMIT) {
+    if (f[0] < 0.0) f[0] = 0.0;
+  } else if (t == MGS_EFC_CONTACT) {
+    int dim = d->efc_dim[r];
+    if (f[0] < 0.0) { for (int j = 0; j < dim; j++) f[j] = 0.0; return; }
+    if (dim == 1) return;
+    const double* mu = d->efc_mu + 5 * r;
+    double s = 0.0;
+    for (int j = 1; j < dim; j++) { double q = f[j] / mu[j - 1]; s = s + q * q; }
+    double nt = sqrt(s);
+    if (nt > f[0]) {
+      double sc = f[0] / nt;
+      for (int j = 1; j < dim; j++) f[j] = f[j] * sc;
+    }
+  }
+}
+
+/* PGS on the dual with elliptic cones (MuJoCo mj_solPGS restated) + noslip */
+static void solve_pgs(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nv = m->nv, ne = d->nefc;
+  double meaninertia = 0.0;
+  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d->M[k * nv + k];
+  meaninertia = meaninertia / (double)nv;
+  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
+  /* warmstart: f from qacc_warmstart through the primal map, projected */
+  for (int r = 0; r < ne; r++) {
+    const double* Jr = d->J + (size_t)r * nv;
+    double jar = 0.0;
+    for (int k = 0; k < nv; k++) jar = jar + Jr[k] * d->qacc_ws[k];
+    jar = jar - d->efc_aref[r];
+    d->efc_f[r] = -jar / d->efc_R[r];
+  }
+  for (int r = 0; r < ne;) {
+    int dim = d->efc_type[r] == MGS_EFC_CONTACT ? d->efc_dim[r] : 1;
+    if (d->efc_type[r] != MGS_EFC_EQUALITY) project_block(d, r, d->efc_f + r);
+    r += dim;
+  }
+  w_from_f(d);
+  double cw = dual_cost(d);
+  if (!(cw < 0.0)) {
+    for (int r = 0; r < ne; r++) d->efc_f[r] = 0.0;
+    for (int k = 0; k < nv; k++) d->w[k] = 0.0;
+  }
+  int it;
+  for (it = 0; it < m->iterations && ne > 0; it++) {
+    double improvement = 0.0;
+    for (int r = 0; r < ne;) {
+      int t = d->efc_type[r];
+      if (t != MGS_EFC_CONTACT || d->efc_dim[r] == 1) {
+        const double* Jr = d->J + (size_t)r * nv;
+        double res = (tree_dot(Jr, d->w, nv) + d->efc_R[r] * d->efc_f[r]) + d->efc_b[r];
+        double AR = d->efc_A[r] + d->efc_R[r];
+        double fo = d->efc_f[r];
+        double fnew[1] = {fo - res / AR};
+        if (t != MGS_EFC_EQUALITY) project_block(d, r, fnew);
+        double delta = fnew[0] - fo;
+        improvement = improvement - delta * (0.5 * AR * delta + res);
+        if (delta != 0.0) {
+          d->efc_f[r] = fnew[0];
+          const double* Kr = d->K + (size_t)r * nv;
+          for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Kr[k] * delta;
+        }
+        r += 1;
+      } else {
+        int dim = d->efc_dim[r];
+        double res[6], old[6], nw[6], Ab[36];
+        const double* blk = d->efc_blk + 36 * r;
+        for (int i = 0; i < dim; i++) {
+          res[i] = (tree_dot(d->J + (size_t)(r + i) * nv, d->w, nv) + d->efc_R[r + i] * d->efc_f[r + i]) +
+                   d->efc_b[r + i];
+          old[i] = d->efc_f[r + i];
+          for (int j = 0; j < dim; j++) Ab[i * dim + j] = blk[i * dim + j];
+          Ab[i * dim + i] = Ab[i * dim + i] + d->efc_R[r + i];
+        }
+        double fn = old[0] - res[0] / Ab[0];
+        if (fn < 0.0) fn = 0.0;
+        double dn = fn - old[0];
+        nw[0] = fn;
+        if (fn == 0.0) {
+          for (int j = 1; j < dim; j++) nw[j] = 0.0;
+        } else {
+          int nf = dim - 1;
+          double Ac[25], bq[5];
+          for (int i = 0; i < nf; i++) {
+            double v = res[1 + i] + Ab[(1 + i) * dim] * dn;
+            double s = v;
+            for (int j = 0; j < nf; j++) {
+              Ac[i * nf + j] = Ab[(1 + i) * dim + 1 + j];
+              s = s - Ac[i * nf + j] * old[1 + j];
+            }
+            bq[i] = s;
+          }
+          qcqp(nf, Ac, bq, d->efc_mu + 5 * r, fn, nw + 1);
+        }
+        double del[6];
+        for (int i = 0; i < dim; i++) del[i] = nw[i] - old[i];
+        double dc = 0.0;
+        for (int i = 0; i < dim; i++) {
+          double ad = 0.0;
+          for (int j = 0; j < dim; j++) ad = ad + Ab[i * dim + j] * del[j];
+          dc = dc + del[i] * (0.5 * ad + res[i]);
+        }
+        improvement = improvement - dc;
+        for (int i = 0; i < dim; i++) d->efc_f[r + i] = nw[i];
+        for (int k = 0; k < nv; k++) {
+          double s = d->w[k];
+          for (int i = 0; i < dim; i++) s = s + d->K[(size_t)(r + i) * nv + k] * del[i];
+          d->w[k] = s;
+        }
+        r += dim;
+      }
+    }
+    if (improvement * scale < m->tolerance) { it++; break; }
+  }
+  d->iters += it;
+  /* noslip: friction dims only, unregularized, normal forces fixed */
+  for (int ns = 0; ns < m->noslip_iterations && ne > 0; ns++) {
+    double improvement = 0.0;
+    for (int r = 0; r < ne;) {
+      int t = d->efc_type[r];
+      if (t == MGS_EFC_FRICTION) {
+        const double* Jr = d->J + (size_t)r * nv;
+        double res = tree_dot(Jr, d->w, nv) + d->efc_b[r];
+        double fo = d->efc_f[r];
+        double fnew[1] = {fo - res / d->efc_A[r]};
+        project_block(d, r, fnew);
+        double delta = fnew[0] - fo;
+        improvement = improvement - delta * (0.5 * d->efc_A[r] * delta + res);
+        if (delta != 0.0) {
+          d->efc_f[r] = fnew[0];
+          const double* Kr = d->K + (size_t)r * nv;
+          for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Kr[k] * delta;
+        }
+        r += 1;
+      } else if (t == MGS_EFC_CONTACT && d->efc_dim[r] > 1) {
+        int dim = d->efc_dim[r];
+        int nf = dim - 1;
+        const double* blk = d->efc_blk + 36 * r;
+        double res[5], old[5], Ac[25], bq[5], nw[5], del[5];
+        for (int i = 0; i < nf; i++) {
+          res[i] = tree_dot(d->J + (size_t)(r + 1 + i) * nv, d->w, nv) + d->efc_b[r + 1 + i];
+          old[i] = d->efc_f[r + 1 + i];
+        }
+        for (int i = 0; i < nf; i++) {
+          double s = res[i];
+          for (int j = 0; j < nf; j++) {
+            Ac[i * nf + j] = blk[(1 + i) * dim + 1 + j];
+            s = s - Ac[i * nf + j] * old[j];
+          }
+          bq[i] = s;
+        }
+        if (d->efc_f[r] > 0.0) qcqp(nf, Ac, bq, d->efc_mu + 5 * r, d->efc_f[r], nw);
+        else for (int i = 0; i < nf; i++) nw[i] = 0.0;
+        for (int i = 0; i < nf; i++) del[i] = nw[i] - old[i];
+        double dc = 0.0;
+        for (int i = 0; i < nf; i++) {
+          double ad = 0.0;
+          for (int j = 0; j < nf; j++) ad = ad + Ac[i * nf + j] * del[j];
+          dc = dc + del[i] * (0.5 * ad + res[i]);
+        }
+        improvement = improvement - dc;
+        for (int i = 0; i < nf; i++) d->efc_f[r + 1 + i] = nw[i];
+        for (int k = 0; k < nv; k++) {
+          double s = d->w[k];
+          for (int i = 0; i < nf; i++) s = s + d->K[(size_t)(r + 1 + i) * nv + k] * del[i];
+          d->w[k] = s;
+        }
+        r += dim;
+      } else {
+        r += (t == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
+      }
+    }
+    if (improvement * scale < m->noslip_tolerance) break;
+  }
+  /* constraint force and acceleration */
+  for (int k = 0; k < nv; k++) {
+    double s = 0.0;
+    for (int r = 0; r < ne; r++) s = s + d->J[(size_t)r * nv + k] * d->efc_f[r];
+    d->qfrc_constraint[k] = s;
+    d->qacc[k] = d->qacc_smooth[k] + d->w[k];
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* forward: kinematics + collision (+ dynamics and solver when full != 0) */
+static void forward(const Mdl* md, Dat* d, int full) {
+  const mgs_model_desc* m = md->m;
+  int nv = m->nv;
+  kinematics(md, d);
+  com_pos(md, d);
+  collision(md, d);
+  if (!full) return;
+  crb(md, d);
+  ldl_factor(nv, d->M, d->L, d->Dinv);
+  actuation(md, d);
+  passive(md, d);
+  rne(md, d);
+  for (int k = 0; k < nv; k++)
+    d->qfrc_smooth[k] = (d->qfrc_passive[k] - d->qfrc_bias[k]) + d->qfrc_actuator[k];
+  ldl_solve(nv, d->L, d->Dinv, d->qfrc_smooth, d->qacc_smooth);
+  make_constraints(md, d);
+  solve_pgs(md, d);
+}
+
+/* implicitfast velocity update + position integration */
+static void integrate(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nv = m->nv;
+  double dt = m->timestep;
+  /* qDeriv: dof damping + actuator velocity gains (skipped when force clamped) */
+  for (int i = 0; i < nv * nv; i++) d->qDeriv[i] = 0.0;
+  const double* damp = DA(md, dof_damping);
+  for (int k = 0; k < nv; k++) d->qDeriv[k * nv + k] = -damp[k];
+  const int32_t *gtype = IA(md, actuator_gaintype), *btype = IA(md, actuator_biastype);
+  const int32_t* flim = IA(md, actuator_forcelimited);
+  const double *gain = DA(md, actuator_gainprm), *bias = DA(md, actuator_biasprm);
+  const double* frange = DA(md, actuator_forcerange);
+  for (int u = 0; u < m->nu; u++) {
+    double f = d->act_force[u];
+    if (flim[u] && (f <= frange[2 * u] || f >= frange[2 * u + 1])) continue;
+    double dv = 0.0;
+    if (btype[u] == MGS_BIAS_AFFINE) dv = dv + bias[3 * u + 2];
+    if (gtype[u] == MGS_GAIN_AFFINE) dv = dv + gain[3 * u + 2] * d->ctrl[u];
+    if (dv == 0.0) continue;
+    const double* mom = d->act_moment + u * nv;
+    for (int i = 0; i < nv; i++) {
+      if (mom[i] == 0.0) continue;
+      for (int j = 0; j < nv; j++)
+        d->qDeriv[i * nv + j] = d->qDeriv[i * nv + j] + mom[i] * (mom[j] * dv);
+    }
+  }
+  for (int i = 0; i < nv * nv; i++) d->MI[i] = d->M[i] - dt * d->qDeriv[i];
+  ldl_factor(nv, d->MI, d->LI, d->DIinv);
+  double rhs[128], qa[128];
+  for (int k = 0; k < nv; k++) rhs[k] = d->qfrc_smooth[k] + d->qfrc_constraint[k];
+  ldl_solve(nv, d->LI, d->DIinv, rhs, qa);
+  for (int k = 0; k < nv; k++) d->qvel[k] = d->qvel[k] + dt * qa[k];
+  const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
+  for (int j = 0; j < m->njnt; j++) {
+    int a = jq[j], v = jd[j];
+    if (jtype[j] == MGS_JNT_FREE) {
+      d->qpos[a] = d->qpos[a] + dt * d->qvel[v];
+      d->qpos[a + 1] = d->qpos[a + 1] + dt * d->qvel[v + 1];
+      d->qpos[a + 2] = d->qpos[a + 2] + dt * d->qvel[v + 2];
+      double ax[3] = {d->qvel[v + 3], d->qvel[v + 4], d->qvel[v + 5]};
+      double nrm = normalize3(ax);
+      double qr[4], qn[4];
+      axisangle2quat(qr, ax, dt * nrm);
+      quatmul(qn, d->qpos + a + 3, qr);
+      normalize4(qn);
+      d->qpos[a + 3] = qn[0]; d->qpos[a + 4] = qn[1]; d->qpos[a + 5] = qn[2]; d->qpos[a + 6] = qn[3];
+    } else {
+      d->qpos[a] = d->qpos[a] + dt * d->qvel[v];
+    }
+  }
+  for (int k = 0; k < nv; k++) d->qacc_ws[k] = d->qacc[k];
+  d->time = d->time + dt;
+}
+
+static void step(const Mdl* md, Dat* d) {
+  forward(md, d, 1);
+  integrate(md, d);
+}
+
+static int obj_contact(const Mdl* md, const Dat* d) {
+  const int32_t* side = IA(md, geom_side);
+  for (int c = 0; c < d->ncon; c++) {
+    int s1 = side[d->con_g1[c]], s2 = side[d->con_g2[c]];
+    if ((s1 < 0 && s2 > 0) || (s1 > 0 && s2 < 0)) return 1;
+  }
+  return 0;
+}
+
+static void reset(const Mdl* md, Dat* d, const double* qpos_init, const double* mpos, const double* mquat) {
+  const mgs_model_desc* m = md->m;
+  memcpy(d->qpos, qpos_init, sizeof(double) * m->nq);
+  memset(d->qvel, 0, sizeof(double) * m->nv);
+  memset(d->qacc_ws, 0, sizeof(double) * m->nv);
+  memset(d->ctrl, 0, sizeof(double) * (m->nu > 0 ? m->nu : 1));
+  for (int k = 0; k < 3; k++) d->mocap_pos[k] = mpos ? mpos[k] : 0.0;
+  for (int k = 0; k < 4; k++) d->mocap_quat[k] = mquat[k];
+  d->time = 0.0;
+  d->overflow = 0;
+  d->iters = 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* exported API (ctypes) */
+int oracle_abi_version(void) { return MGS_ABI_VERSION; }
+
+int oracle_collision_free(const mgs_model_desc* desc, const int32_t* I, const double* D, int n,
+                          const double* qpos_init, const double* mocap_pos, const double* mocap_quat,
+                          int predicate, uint8_t* out, int nthreads) {
+  Mdl md = {desc, I, D};
+  (void)nthreads;
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+  {
+    Dat* d = dat_alloc(&md);
+#pragma omp for schedule(dynamic, 4)
+    for (int i = 0; i < n; i++) {
+      reset(&md, d, qpos_init + (size_t)i * desc->nq, mocap_pos + 3 * i, mocap_quat + 4 * i);
+      forward(&md, d, 0);
+      int hit = (predicate == MGS_PRED_ANY_CONTACT) ? (d->ncon != 0) : obj_contact(&md, d);
+      out[i] = (uint8_t)(hit ? 0 : 1);
+    }
+    dat_free(d);
+  }
+  return 0;
+}
+
+int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D,
+                   const mgs_schedule* sc, int n, const double* qpos_init,
+                   const double* mocap_quat, const double* phase_start, const double* phase_target,
+                   uint8_t* label, int32_t* fail_step, double* obj_qpos, int32_t* stats, int nthreads) {
+  Mdl md = {desc, I, D};
+  int np = sc->nphase;
+  int obj_qposadr = sc->obj_qposadr;
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+  {
+    Dat* d = dat_alloc(&md);
+#pragma omp for schedule(dynamic, 1)
+    for (int i = 0; i < n; i++) {
+      const double* ps = phase_start + (size_t)i * np * 3;
+      const double* pt = phase_target + (size_t)i * np * 3;
+      reset(&md, d, qpos_init + (size_t)i * desc->nq, ps, mocap_quat + 4 * i);
+      int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0;
+      for (int p = 0; p < np && ok; p++) {
+        for (int u = 0; u < desc->nu; u++) d->ctrl[u] = sc->ctrl[p * 32 + u];
+        int ns = sc->nsteps[p];
+        for (int t = 0; t < ns && ok; t++) {
+          double frac = (double)t / (double)ns;
+          for (int k = 0; k < 3; k++) d->mocap_pos[k] = ps[3 * p + k] + (pt[3 * p + k] - ps[3 * p + k]) * frac;
+          step(&md, d);
+          if (d->ncon > maxcon) maxcon = d->ncon;
+          if (d->nefc > maxefc) maxefc = d->nefc;
+          int ce = sc->check_every[p];
+          if (ce > 0 && t > 0 && (t % ce) == 0 && !obj_contact(&md, d)) { ok = 0; fstep = gstep; }
+          gstep++;
+        }
+        if (ok && sc->check_at_end[p] && !obj_contact(&md, d)) { ok = 0; fstep = gstep - 1; }
+      }
+      label[i] = (uint8_t)ok;
+      if (fail_step) fail_step[i] = fstep;
+      if (obj_qpos && obj_qposadr >= 0)
+        for (int k = 0; k < 7; k++) obj_qpos[7 * i + k] = d->qpos[obj_qposadr + k];
+      if (stats) {
+        stats[4 * i] = maxcon; stats[4 * i + 1] = maxefc; stats[4 * i + 2] = d->overflow; stats[4 * i + 3] = d->iters;
+      }
+    }
+    dat_free(d);
+  }
+  return 0;
+}
+
+/* Debug/KAT helper: run nsteps with a fixed mocap and ctrl from an initial
+ * state, recording qpos after every step (nsteps * nq) and ncon per step. */
+int oracle_trace(const mgs_model_desc* desc, const int32_t* I, const double* D, const double* qpos_init,
+                 const double* mocap_pos, const double* mocap_quat, const double* ctrl, int nsteps,
+                 double* qpos_trace, int32_t* ncon_trace, double* qvel_out) {
+  Mdl md = {desc, I, D};
+  Dat* d = dat_alloc(&md);
+  reset(&md, d, qpos_init, mocap_pos, mocap_quat);
+  for (int u = 0; u < desc->nu; u++) d->ctrl[u] = ctrl[u];
+  for (int s = 0; s < nsteps; s++) {
+    step(&md, d);
+    if (qpos_trace) memcpy(qpos_trace + (size_t)s * desc->nq, d->qpos, sizeof(double) * desc->nq);
+    if (ncon_trace) ncon_trace[s] = d->ncon;
+  }
+  if (qvel_out) memcpy(qvel_out, d->qvel, sizeof(double) * desc->nv);
+  dat_free(d);
+  return 0;
+}
+
+/* Debug helper: contacts of one configuration (after kinematics+collision). */
+int oracle_contacts(const mgs_model_desc* desc, const int32_t* I, const double* D, const double* qpos,
+                    const double* mocap_pos, const double* mocap_quat, int maxc, double* pos, double* frame,
+                    double* dist, int32_t* geoms) {
+  Mdl md = {desc, I, D};
+  Dat* d = dat_alloc(&md);
+  reset(&md, d, qpos, mocap_pos, mocap_quat);
+  forward(&md, d, 0);
+  int nc = d->ncon < maxc ? d->ncon : maxc;
+  for (int c = 0; c < nc; c++) {
+    memcpy(pos + 3 * c, d->con_pos + 3 * c, 3 * sizeof(double));
+    memcpy(frame + 9 * c, d->con_frame + 9 * c, 9 * sizeof(double));
+    dist[c] = d->con_dist[c];
+    geoms[2 * c] = d->con_g1[c];
+    geoms[2 * c + 1] = d->con_g2[c];
+  }
+  int r = d->ncon;
+  dat_free(d);
+  return r;
+}
+
+/* unit test hook for the shared numeric primitives */
+void oracle_sincos(const double* x, int n, double* s, double* c) {
+  for (int i = 0; i < n; i++) o_sincos(x[i], s + i, c + i);
+}

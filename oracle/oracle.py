@@ -1,0 +1,111 @@
+"""ctypes wrapper of oracle/libmgs_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg (see mgs_oracle.c's header for what the oracle restates and its parity
+status).  The product (mj-grasp-sim_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from mgs.core import abi
+from mgs.core.abi import ptr
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "libmgs_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(_HERE, "mgs_oracle.c")
+        if not os.path.isfile(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+            build()
+        L = ctypes.CDLL(_LIB)
+        c_i, c_d, c_u8 = ctypes.c_int32, ctypes.c_double, ctypes.c_uint8
+        P = ctypes.POINTER
+        L.oracle_collision_free.argtypes = [P(abi.ModelDesc), P(c_i), P(c_d), ctypes.c_int, P(c_d), P(c_d),
+                                            P(c_d), ctypes.c_int, P(c_u8), ctypes.c_int]
+        L.oracle_rollout.argtypes = [P(abi.ModelDesc), P(c_i), P(c_d), P(abi.Schedule), ctypes.c_int, P(c_d),
+                                     P(c_d), P(c_d), P(c_d), P(c_u8), P(c_i), P(c_d), P(c_i), ctypes.c_int]
+        L.oracle_trace.argtypes = [P(abi.ModelDesc), P(c_i), P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
+                                   ctypes.c_int, P(c_d), P(c_i), P(c_d)]
+        L.oracle_contacts.argtypes = [P(abi.ModelDesc), P(c_i), P(c_d), P(c_d), P(c_d), P(c_d), ctypes.c_int,
+                                      P(c_d), P(c_d), P(c_d), P(c_i)]
+        L.oracle_sincos.argtypes = [P(c_d), ctypes.c_int, P(c_d), P(c_d)]
+        _lib = L
+    return _lib
+
+
+class OracleModel:
+    def __init__(self, cm, ncon_max=16, nefc_max=None):
+        fields, self.ib, self.db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
+        self.desc = abi.make_desc(fields)
+        self.cm = cm
+
+    def _args(self):
+        return (ctypes.byref(self.desc), ptr(self.ib, ctypes.c_int32), ptr(self.db, ctypes.c_double))
+
+    def collision_free(self, qpos, mocap_pos, mocap_quat, predicate="any", nthreads=1):
+        n = len(qpos)
+        out = np.zeros(n, np.uint8)
+        pr = abi.MGS["MGS_PRED_ANY_CONTACT"] if predicate == "any" else abi.MGS["MGS_PRED_PARTITION"]
+        q = np.ascontiguousarray(qpos, np.float64)
+        mp = np.ascontiguousarray(mocap_pos, np.float64)
+        mq = np.ascontiguousarray(mocap_quat, np.float64)
+        lib().oracle_collision_free(*self._args(), n, ptr(q, ctypes.c_double), ptr(mp, ctypes.c_double),
+                                    ptr(mq, ctypes.c_double), pr, ptr(out, ctypes.c_uint8), nthreads)
+        return out.astype(bool)
+
+    def rollout(self, plan, nthreads=1):
+        n = len(plan.qpos_init)
+        sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+        label = np.zeros(n, np.uint8)
+        fail = np.zeros(n, np.int32)
+        objq = np.zeros((n, 7), np.float64)
+        stats = np.zeros((n, 4), np.int32)
+        q = np.ascontiguousarray(plan.qpos_init, np.float64)
+        mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
+        ps = np.ascontiguousarray(plan.phase_start, np.float64)
+        pt = np.ascontiguousarray(plan.phase_target, np.float64)
+        lib().oracle_rollout(*self._args(), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
+                             ptr(mq, ctypes.c_double), ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double),
+                             ptr(label, ctypes.c_uint8), ptr(fail, ctypes.c_int32), ptr(objq, ctypes.c_double),
+                             ptr(stats, ctypes.c_int32), nthreads)
+        return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats)
+
+    def trace(self, qpos, mocap_pos, mocap_quat, ctrl, nsteps):
+        nq = self.cm.nq
+        tr = np.zeros((nsteps, nq))
+        nc = np.zeros(nsteps, np.int32)
+        qv = np.zeros(self.cm.nv)
+        args = [np.ascontiguousarray(a, np.float64) for a in (qpos, mocap_pos, mocap_quat, ctrl)]
+        lib().oracle_trace(*self._args(), *[ptr(a, ctypes.c_double) for a in args], nsteps,
+                           ptr(tr, ctypes.c_double), ptr(nc, ctypes.c_int32), ptr(qv, ctypes.c_double))
+        return tr, nc, qv
+
+    def contacts(self, qpos, mocap_pos, mocap_quat, maxc=64):
+        pos = np.zeros((maxc, 3)); fr = np.zeros((maxc, 9)); dist = np.zeros(maxc); g = np.zeros((maxc, 2), np.int32)
+        args = [np.ascontiguousarray(a, np.float64) for a in (qpos, mocap_pos, mocap_quat)]
+        n = lib().oracle_contacts(*self._args(), *[ptr(a, ctypes.c_double) for a in args], maxc,
+                                  ptr(pos, ctypes.c_double), ptr(fr, ctypes.c_double), ptr(dist, ctypes.c_double),
+                                  ptr(g, ctypes.c_int32))
+        k = min(n, maxc)
+        return n, pos[:k], fr[:k], dist[:k], g[:k]
+
+
+def sincos(x):
+    x = np.ascontiguousarray(x, np.float64)
+    s = np.zeros_like(x)
+    c = np.zeros_like(x)
+    lib().oracle_sincos(ptr(x, ctypes.c_double), len(x), ptr(s, ctypes.c_double), ptr(c, ctypes.c_double))
+    return s, c
