@@ -103,6 +103,9 @@ typedef struct mgs_model_desc {
   int32_t noslip_iterations;
   int32_t cone;       /* 1 = elliptic (the only cone supported) */
   int32_t integrator; /* 2 = implicitfast (the only integrator supported) */
+  int32_t solver;     /* MuJoCo mjtSolver numbering: 0 = PGS, 2 = Newton (MuJoCo's default) */
+  int32_t ls_iterations;
+  double ls_tolerance;
   double timestep;
   double impratio;
   double tolerance;

@@ -25,7 +25,10 @@ int fail(int code, const char* fmt, const char* what = "") {
     if (_e != hipSuccess) return fail(MGS_EHIP, "HIP error: %s", hipGetErrorString(_e)); \
   } while (0)
 
-// LDS carve-up of one candidate's working set (doubles, then int counters/arrays)
+// LDS carve-up of one candidate's working set (doubles, then int counters and
+// index arrays).  U is time-multiplexed: collision scratch, then composite
+// inertias / RNE temporaries, then constraint rows (G) + solver scratch, then
+// the integrator's derivative matrix.
 Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   Lay l;
   memset(&l, 0, sizeof(l));
@@ -35,21 +38,37 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   sizes[L_qpos] = nq; sizes[L_qvel] = nv; sizes[L_qacc_ws] = nv; sizes[L_ctrl] = nu;
   sizes[L_mocap_pos] = 3 * m.nmocap + 3; sizes[L_mocap_quat] = 4 * m.nmocap + 4; sizes[L_time] = 1;
   sizes[L_xpos] = 3 * nb; sizes[L_xquat] = 4 * nb; sizes[L_xmat] = 9 * nb; sizes[L_xipos] = 3 * nb;
-  sizes[L_ximat] = 9 * nb; sizes[L_xanchor] = 3 * nj; sizes[L_xaxis] = 3 * nj;
-  sizes[L_subtree_com] = 3 * nb; sizes[L_subtree_mass] = nb; sizes[L_cinert] = 10 * nb; sizes[L_crb] = 10 * nb;
-  sizes[L_cdof] = 6 * nv; sizes[L_cdof_dot] = 6 * nv; sizes[L_cvel] = 6 * nb; sizes[L_cacc] = 6 * nb;
-  sizes[L_cfrc] = 6 * nb; sizes[L_geom_xpos] = 3 * ng; sizes[L_geom_xmat] = 9 * ng;
-  sizes[L_M] = nv * nv; sizes[L_L] = nv * nv; sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_qDeriv] = nv * nv;
+  sizes[L_xanchor] = 3 * nj; sizes[L_xaxis] = 3 * nj; sizes[L_subtree_com] = 3 * nb; sizes[L_subtree_mass] = nb;
+  sizes[L_cinert] = 10 * nb; sizes[L_cdof] = 6 * nv; sizes[L_geom_xpos] = 3 * ng; sizes[L_geom_xmat] = 9 * ng;
+  sizes[L_M] = nv * nv; sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_sD] = nv; sizes[L_isD] = nv;
+  sizes[L_tmp] = nv; sizes[L_tmp2] = nv;
   sizes[L_qfrc_bias] = nv; sizes[L_qfrc_passive] = nv; sizes[L_qfrc_actuator] = nv; sizes[L_qfrc_smooth] = nv;
   sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv; sizes[L_qacc] = nv;
   sizes[L_act_force] = nu; sizes[L_act_moment] = nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
   sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc;
-  sizes[L_J] = ne * nv; sizes[L_K] = ne * nv; sizes[L_efc_pos] = ne; sizes[L_efc_margin] = ne;
-  sizes[L_efc_vel] = ne; sizes[L_efc_aref] = ne; sizes[L_efc_R] = ne; sizes[L_efc_A] = ne; sizes[L_efc_b] = ne;
-  sizes[L_efc_f] = ne; sizes[L_efc_mu] = 5 * ne; sizes[L_efc_blk] = 36 * ne; sizes[L_efc_floss] = ne;
-  sizes[L_w] = nv; sizes[L_jac] = 12 * nv; sizes[L_scratch] = ne > 64 ? ne : 64;
-  sizes[L_poly] = 3 * 3 * K_MAXPOLY;
-  sizes[L_ints] = (16 + 3 * nc + 3 * ne + 1) / 2;
+  sizes[L_efc_R] = ne; sizes[L_efc_b] = ne; sizes[L_efc_AR] = ne; sizes[L_efc_ARinv] = ne; sizes[L_efc_A] = ne;
+  sizes[L_efc_Ainv] = ne; sizes[L_efc_floss] = ne; sizes[L_con_mu] = 5 * nc; sizes[L_con_blk] = BLKSTRIDE * nc;
+  // U sub-layout
+  int u_coll = 6 * K_MAXPOLY * 3 + K_MAXPOLY;                 // poly buffers + depths
+  int u_dyn = 10 * nb;                                        // crb
+  int u_rne = 18 * nb + 6 * nv;                               // cvel, cacc, cfrc, cdof_dot
+  int u_scr = (2 * ne > nv ? 2 * ne : nv);
+  int u_newton = 7 * ne + nv * nv + 4 * nv + 16 * nc;         // Newton solver workspace
+  int u_con = ne * nv + 12 * nv + 4 * ne + u_scr + u_newton;
+  int u_int = nv * nv;
+  int U = u_coll;
+  if (u_dyn > U) U = u_dyn;
+  if (u_rne > U) U = u_rne;
+  if (u_con > U) U = u_con;
+  if (u_int > U) U = u_int;
+  l.u_poly = 0; l.u_pdep = 6 * K_MAXPOLY * 3;
+  l.u_crb = 0;
+  l.u_cvel = 0; l.u_cacc = 6 * nb; l.u_cfrc = 12 * nb; l.u_cdof_dot = 18 * nb;
+  l.u_G = 0; l.u_jac = ne * nv; l.u_aref = l.u_jac + 12 * nv; l.u_vel = l.u_aref + ne; l.u_pos = l.u_vel + ne;
+  l.u_margin = l.u_pos + ne; l.u_scratch = l.u_margin + ne; l.u_newton = l.u_scratch + u_scr;
+  l.u_qDeriv = 0;
+  sizes[L_U] = U;
+  sizes[L_ints] = (16 + 3 * nc + 5 * ne + 1) / 2;
   int off = 0;
   for (int k = 0; k < L_COUNT; k++) {
     l.o[k] = off;
@@ -57,6 +76,7 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   }
   l.ncon_max = nc;
   l.nefc_max = ne;
+  l.nv = nv;
   l.total_doubles = off;
   *bytes = (size_t)off * sizeof(double);
   return l;
@@ -95,6 +115,11 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
     return fail(MGS_EINVAL, "only elliptic cones and implicitfast are supported%s");
   if (desc->nu > 32) return fail(MGS_EINVAL, "at most 32 actuators%s");
   if (desc->nmocap > 1) return fail(MGS_EINVAL, "at most one mocap body%s");
+  if (desc->nefc_max > 128) return fail(MGS_EINVAL, "nefc_max must be <= 128%s");
+  for (int p = 0; p < desc->npair; p++) {
+    int cd = ibuf[desc->i_pair_condim + p];
+    if (cd != 1 && cd != 3 && cd != 4) return fail(MGS_EINVAL, "condim must be 1, 3 or 4%s");
+  }
   HIPCHK(hipSetDevice(device));
   mgs_model* m = new mgs_model();
   m->desc = *desc;
@@ -259,6 +284,36 @@ int mgs_arith_probe(const double* x, const double* y, int n, double* out) {
   hipFree(dx); hipFree(dy); hipFree(dout);
   return MGS_OK;
 }
+
+// test hook: pairwise-tree wave reduction, nb blocks of 64 lanes
+int mgs_tree_probe(const double* a, const double* c, int n, int nb, double* out) {
+  double *da, *dc, *dout;
+  HIPCHK(hipMalloc(&da, sizeof(double) * nb * 64));
+  HIPCHK(hipMalloc(&dc, sizeof(double) * nb * 64));
+  HIPCHK(hipMalloc(&dout, sizeof(double) * nb));
+  HIPCHK(hipMemcpy(da, a, sizeof(double) * nb * 64, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dc, c, sizeof(double) * nb * 64, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(mgs_tree_probe_kernel, dim3(nb), dim3(64), 0, 0, da, dc, n, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, sizeof(double) * nb, hipMemcpyDeviceToHost));
+  hipFree(da); hipFree(dc); hipFree(dout);
+  return MGS_OK;
+}
+
+// diagnostic build only: read and clear the stage timers (s_memtime ticks)
+int mgs_prof_read(unsigned long long* out) {
+#ifdef MGS_PROFILE
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 32));
+  unsigned long long z[32] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+  return MGS_OK;
+#else
+  (void)out;
+  return MGS_EINVAL;
+#endif
+}
+
+int mgs_lds_bytes(mgs_model* m) { return m ? (int)m->lds_bytes : -1; }
 
 int mgs_device_count(void) {
   int n = 0;

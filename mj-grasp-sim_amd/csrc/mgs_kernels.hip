@@ -31,6 +31,7 @@
 #define K_MPR_MAXIT 64
 #define K_FEAT_EPS 1e-5
 #define WAVE 64
+#define DEVI __device__ __attribute__((always_inline)) inline
 
 struct P2 { double x, y, h; };
 
@@ -44,35 +45,56 @@ struct Mdl {
 #define IA(md, f) ((md).I + (md).m.i_##f)
 #define DA(md, f) ((md).D + (md).m.d_##f)
 
-// per-candidate working set in LDS
+// per-candidate working set in LDS (see make_layout in mgs_capi.hip for the
+// carve-up; the U region is time-multiplexed between pipeline stages)
 struct Dat {
   double *qpos, *qvel, *qacc_ws, *ctrl, *mocap_pos, *mocap_quat, *time;
-  double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis;
-  double *subtree_com, *subtree_mass, *cinert, *crb, *cdof, *cdof_dot, *cvel, *cacc, *cfrc;
+  double *xpos, *xquat, *xmat, *xipos, *xanchor, *xaxis;
+  double *subtree_com, *subtree_mass, *cinert, *cdof;
   double *geom_xpos, *geom_xmat;
-  double *M, *L, *Dv, *Dinv, *qDeriv;
+  double *M, *Dv, *Dinv, *sD, *isD, *tmp, *tmp2;
   double *qfrc_bias, *qfrc_passive, *qfrc_actuator, *qfrc_smooth, *qacc_smooth, *qfrc_constraint, *qacc;
   double *act_force, *act_moment, *act_length, *act_vel;
   double *con_pos, *con_frame, *con_dist;
-  double *J, *K, *efc_pos, *efc_margin, *efc_vel, *efc_aref, *efc_R, *efc_A, *efc_b, *efc_f, *efc_mu, *efc_blk,
-      *efc_floss;
-  double *w, *jac, *scratch;
-  int *con_pair, *con_g1, *con_g2, *efc_type, *efc_dim, *efc_con, *ints;
-  P2* poly;   // 3 * K_MAXPOLY
+  double *efc_R, *efc_b, *efc_AR, *efc_ARinv, *efc_A, *efc_Ainv, *efc_floss, *con_mu, *con_blk;
+  // U region views
+  double *crb, *cvel, *cacc, *cfrc, *cdof_dot;          // dynamics stage
+  P2* poly;                                           // collision stage
+  double* pdep;                                       // collision stage
+  double *G, *jac, *efc_aref, *efc_vel, *efc_pos, *efc_margin, *scratch;  // constraint + solver stage
+  double* qDeriv;                                     // integration stage
+  // Newton solver workspace (U region, after the constraint stage views)
+  double *efc_jar, *efc_jv, *efc_f, *efc_Dr, *efc_isR, *efc_sqR, *efc_mup, *nH, *nw, *nw0, *ng, *ndir, *con_hb;
+  int *con_pair, *con_g1, *con_g2, *efc_type, *efc_dim, *efc_con, *efc_lead, *efc_state, *ints;
 };
-// ints[]: 0 ncon, 1 nefc, 2 overflow, 3 iters, 4 maxcon, 5 maxefc, 6 cr0, 7 cr1, 8 neq rows, 9 fr0, 10 fr1,
-//         11 lr0, 12 lr1
+// ints[]: 0 ncon, 1 nefc, 2 overflow, 3 iters, 6 cr0, 7 cr1, 8 neq rows, 9 fr0, 10 fr1, 11 lr0, 12 lr1
 #define NCON ints[0]
 #define NEFC ints[1]
 #define OVERFLOW ints[2]
 #define ITERS ints[3]
+#define BLKSTRIDE 16
 
-__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+DEVI int lane_id() { return (int)__lane_id(); }
+// values that are uniform across the wave but come from LDS: move to SGPRs so
+// control flow on them is scalar
+DEVI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Diagnostic stage timers (built only with -DMGS_PROFILE; never in the product build)
+#ifdef MGS_PROFILE
+__device__ unsigned long long g_prof[32];
+#define PROF_DECL unsigned long long _pt = __builtin_amdgcn_s_memtime(), _pacc[12] = {0,0,0,0,0,0,0,0,0,0,0,0};
+#define PROF(k) do { unsigned long long _n = __builtin_amdgcn_s_memtime(); _pacc[k] += _n - _pt; _pt = _n; } while (0)
+#define PROF_FLUSH if (lane_id() == 0) for (int _k = 0; _k < 12; _k++) atomicAdd(&g_prof[_k], _pacc[_k]);
+#else
+#define PROF_DECL
+#define PROF(k)
+#define PROF_FLUSH
+#endif
+DEVI void wsync() { __syncthreads(); }
 
 // ---------------------------------------------------------------------------
 // math primitives: identical expressions to the oracle
-__device__ void k_sincos(double x, double* s, double* c) {
+DEVI void k_sincos(double x, double* s, double* c) {
   const double inv_pio2 = 6.36619772367581382433e-01;
   const double pio2_1 = 1.57079632673412561417e+00;
   const double pio2_1t = 6.07710050650619224932e-11;
@@ -98,41 +120,41 @@ __device__ void k_sincos(double x, double* s, double* c) {
   else { *s = -cr; *c = sr; }
 }
 
-__device__ __forceinline__ double dot3(const double* a, const double* b) {
+DEVI double dot3(const double* a, const double* b) {
   return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
 }
-__device__ __forceinline__ void cross3(double* r, const double* a, const double* b) {
+DEVI void cross3(double* r, const double* a, const double* b) {
   double r0 = a[1] * b[2] - a[2] * b[1];
   double r1 = a[2] * b[0] - a[0] * b[2];
   double r2 = a[0] * b[1] - a[1] * b[0];
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
-__device__ __forceinline__ void sub3(double* r, const double* a, const double* b) {
+DEVI void sub3(double* r, const double* a, const double* b) {
   r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2];
 }
-__device__ __forceinline__ void add3(double* r, const double* a, const double* b) {
+DEVI void add3(double* r, const double* a, const double* b) {
   r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
 }
-__device__ __forceinline__ void mulmv3(double* r, const double* m, const double* v) {
+DEVI void mulmv3(double* r, const double* m, const double* v) {
   double r0 = (m[0] * v[0] + m[1] * v[1]) + m[2] * v[2];
   double r1 = (m[3] * v[0] + m[4] * v[1]) + m[5] * v[2];
   double r2 = (m[6] * v[0] + m[7] * v[1]) + m[8] * v[2];
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
-__device__ __forceinline__ void mulmtv3(double* r, const double* m, const double* v) {
+DEVI void mulmtv3(double* r, const double* m, const double* v) {
   double r0 = (m[0] * v[0] + m[3] * v[1]) + m[6] * v[2];
   double r1 = (m[1] * v[0] + m[4] * v[1]) + m[7] * v[2];
   double r2 = (m[2] * v[0] + m[5] * v[1]) + m[8] * v[2];
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
-__device__ __forceinline__ void quatmul(double* r, const double* a, const double* b) {
+DEVI void quatmul(double* r, const double* a, const double* b) {
   double r0 = ((a[0] * b[0] - a[1] * b[1]) - a[2] * b[2]) - a[3] * b[3];
   double r1 = ((a[0] * b[1] + a[1] * b[0]) + a[2] * b[3]) - a[3] * b[2];
   double r2 = ((a[0] * b[2] - a[1] * b[3]) + a[2] * b[0]) + a[3] * b[1];
   double r3 = ((a[0] * b[3] + a[1] * b[2]) - a[2] * b[1]) + a[3] * b[0];
   r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3;
 }
-__device__ __forceinline__ void quat2mat(double* m, const double* q) {
+DEVI void quat2mat(double* m, const double* q) {
   double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
   double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
   double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
@@ -146,25 +168,25 @@ __device__ __forceinline__ void quat2mat(double* m, const double* q) {
   m[7] = 2.0 * (q23 + q01);
   m[8] = ((q00 - q11) - q22) + q33;
 }
-__device__ __forceinline__ void normalize4(double* q) {
+DEVI void normalize4(double* q) {
   double n = sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
   if (n < K_MINVAL) { q[0] = 1.0; q[1] = q[2] = q[3] = 0.0; return; }
   double inv = 1.0 / n;
   q[0] = q[0] * inv; q[1] = q[1] * inv; q[2] = q[2] * inv; q[3] = q[3] * inv;
 }
-__device__ __forceinline__ double normalize3(double* v) {
+DEVI double normalize3(double* v) {
   double n = sqrt(dot3(v, v));
   if (n < K_MINVAL) { v[0] = 1.0; v[1] = v[2] = 0.0; return 0.0; }
   double inv = 1.0 / n;
   v[0] = v[0] * inv; v[1] = v[1] * inv; v[2] = v[2] * inv;
   return n;
 }
-__device__ __forceinline__ void axisangle2quat(double* q, const double* axis, double angle) {
+DEVI void axisangle2quat(double* q, const double* axis, double angle) {
   double s, c;
   k_sincos(0.5 * angle, &s, &c);
   q[0] = c; q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
 }
-__device__ __forceinline__ void mul_inert_vec(double* r, const double* i, const double* v) {
+DEVI void mul_inert_vec(double* r, const double* i, const double* v) {
   double r0 = ((i[0] * v[0] + i[3] * v[1]) + i[4] * v[2]) - i[8] * v[4] + i[7] * v[5];
   double r1 = ((i[3] * v[0] + i[1] * v[1]) + i[5] * v[2]) + i[8] * v[3] - i[6] * v[5];
   double r2 = ((i[4] * v[0] + i[5] * v[1]) + i[2] * v[2]) - i[7] * v[3] + i[6] * v[4];
@@ -173,10 +195,10 @@ __device__ __forceinline__ void mul_inert_vec(double* r, const double* i, const 
   double r5 = (i[7] * v[0] - i[6] * v[1]) + i[9] * v[5];
   r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3; r[4] = r4; r[5] = r5;
 }
-__device__ __forceinline__ double dot6(const double* a, const double* b) {
+DEVI double dot6(const double* a, const double* b) {
   return ((((a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]) + a[3] * b[3]) + a[4] * b[4]) + a[5] * b[5];
 }
-__device__ __forceinline__ void cross_motion(double* r, const double* v, const double* u) {
+DEVI void cross_motion(double* r, const double* v, const double* u) {
   double r0 = v[1] * u[2] - v[2] * u[1];
   double r1 = v[2] * u[0] - v[0] * u[2];
   double r2 = v[0] * u[1] - v[1] * u[0];
@@ -185,7 +207,7 @@ __device__ __forceinline__ void cross_motion(double* r, const double* v, const d
   double r5 = (v[0] * u[4] - v[1] * u[3]) + (v[3] * u[1] - v[4] * u[0]);
   r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3; r[4] = r4; r[5] = r5;
 }
-__device__ __forceinline__ void cross_force(double* r, const double* v, const double* f) {
+DEVI void cross_force(double* r, const double* v, const double* f) {
   double r0 = (v[1] * f[2] - v[2] * f[1]) + (v[4] * f[5] - v[5] * f[4]);
   double r1 = (v[2] * f[0] - v[0] * f[2]) + (v[5] * f[3] - v[3] * f[5]);
   double r2 = (v[0] * f[1] - v[1] * f[0]) + (v[3] * f[4] - v[4] * f[3]);
@@ -195,75 +217,51 @@ __device__ __forceinline__ void cross_force(double* r, const double* v, const do
   r[0] = r0; r[1] = r1; r[2] = r2; r[3] = r3; r[4] = r4; r[5] = r5;
 }
 
-// pairwise tree reduction of lane products: leaf[k] = a[k]*b[k] (k < n),
-// level s: leaf[k] = leaf[k] + leaf[k^s] for s < P = nextpow2(n).
-__device__ __forceinline__ double tree_sum(double leaf, int P) {
-  for (int s = 1; s < P; s <<= 1) leaf = leaf + __shfl_xor(leaf, s);
-  return leaf;
+// Pairwise tree reduction over lanes, identical to the oracle's tree_dot():
+// level s (s = 1, 2, 4, ... < P) adds lane k^s to lane k.  Within a 16-lane row
+// the levels are DPP moves (xor 1 and xor 2 by quad permutes; xor 4 and xor 8 by
+// the half-row / row mirrors, which equal xor on values already uniform over
+// the lower levels); the last two levels combine the four row sums read with
+// v_readlane in the same pairing ((r0 + r1) + (r2 + r3)).  Result is uniform.
+DEVI double dpp_d(double x, int ctrl_sel) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  switch (ctrl_sel) {
+    case 0: lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false); break;
+    case 1: lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false); break;
+    case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, false); break;
+    default: lo = __builtin_amdgcn_mov_dpp(lo, 0x140, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x140, 0xF, 0xF, false); break;
+  }
+  return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ int next_pow2(int n) {
+DEVI double readlane_d(double x, int l) {
+  int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+DEVI double tree_sum(double leaf, int P) {
+  if (P > 1) leaf = leaf + dpp_d(leaf, 0);
+  if (P > 2) leaf = leaf + dpp_d(leaf, 1);
+  if (P > 4) leaf = leaf + dpp_d(leaf, 2);
+  if (P > 8) leaf = leaf + dpp_d(leaf, 3);
+  if (P > 16) {
+    double r0 = readlane_d(leaf, 0), r1 = readlane_d(leaf, 16);
+    if (P > 32) {
+      double r2 = readlane_d(leaf, 32), r3 = readlane_d(leaf, 48);
+      return (r0 + r1) + (r2 + r3);
+    }
+    return r0 + r1;
+  }
+  return readlane_d(leaf, 0);
+}
+DEVI int next_pow2(int n) {
   int P = 1;
   while (P < n) P <<= 1;
   return P;
 }
 
 // ---------------------------------------------------------------------------
-// LDS layout
-struct Lay {
-  int o[64];
-  int ncon_max;
-  int nefc_max;
-  int total_doubles;
-};
-enum {
-  L_qpos, L_qvel, L_qacc_ws, L_ctrl, L_mocap_pos, L_mocap_quat, L_time, L_xpos, L_xquat, L_xmat, L_xipos,
-  L_ximat, L_xanchor, L_xaxis, L_subtree_com, L_subtree_mass, L_cinert, L_crb, L_cdof, L_cdof_dot, L_cvel,
-  L_cacc, L_cfrc, L_geom_xpos, L_geom_xmat, L_M, L_L, L_Dv, L_Dinv, L_qDeriv, L_qfrc_bias, L_qfrc_passive,
-  L_qfrc_actuator, L_qfrc_smooth, L_qacc_smooth, L_qfrc_constraint, L_qacc, L_act_force, L_act_moment,
-  L_act_length, L_act_vel, L_con_pos, L_con_frame, L_con_dist, L_J, L_K, L_efc_pos, L_efc_margin,
-  L_efc_vel, L_efc_aref, L_efc_R, L_efc_A, L_efc_b, L_efc_f, L_efc_mu, L_efc_blk, L_efc_floss, L_w, L_jac,
-  L_scratch, L_poly, L_ints, L_COUNT
-};
-
-__device__ void bind(Dat& d, double* s, const Lay& l) {
-  d.qpos = s + l.o[L_qpos]; d.qvel = s + l.o[L_qvel]; d.qacc_ws = s + l.o[L_qacc_ws]; d.ctrl = s + l.o[L_ctrl];
-  d.mocap_pos = s + l.o[L_mocap_pos]; d.mocap_quat = s + l.o[L_mocap_quat]; d.time = s + l.o[L_time];
-  d.xpos = s + l.o[L_xpos]; d.xquat = s + l.o[L_xquat]; d.xmat = s + l.o[L_xmat]; d.xipos = s + l.o[L_xipos];
-  d.ximat = s + l.o[L_ximat]; d.xanchor = s + l.o[L_xanchor]; d.xaxis = s + l.o[L_xaxis];
-  d.subtree_com = s + l.o[L_subtree_com]; d.subtree_mass = s + l.o[L_subtree_mass];
-  d.cinert = s + l.o[L_cinert]; d.crb = s + l.o[L_crb]; d.cdof = s + l.o[L_cdof];
-  d.cdof_dot = s + l.o[L_cdof_dot]; d.cvel = s + l.o[L_cvel]; d.cacc = s + l.o[L_cacc]; d.cfrc = s + l.o[L_cfrc];
-  d.geom_xpos = s + l.o[L_geom_xpos]; d.geom_xmat = s + l.o[L_geom_xmat];
-  d.M = s + l.o[L_M]; d.L = s + l.o[L_L]; d.Dv = s + l.o[L_Dv]; d.Dinv = s + l.o[L_Dinv];
-  d.qDeriv = s + l.o[L_qDeriv];
-  d.qfrc_bias = s + l.o[L_qfrc_bias]; d.qfrc_passive = s + l.o[L_qfrc_passive];
-  d.qfrc_actuator = s + l.o[L_qfrc_actuator]; d.qfrc_smooth = s + l.o[L_qfrc_smooth];
-  d.qacc_smooth = s + l.o[L_qacc_smooth]; d.qfrc_constraint = s + l.o[L_qfrc_constraint];
-  d.qacc = s + l.o[L_qacc];
-  d.act_force = s + l.o[L_act_force]; d.act_moment = s + l.o[L_act_moment];
-  d.act_length = s + l.o[L_act_length]; d.act_vel = s + l.o[L_act_vel];
-  d.con_pos = s + l.o[L_con_pos]; d.con_frame = s + l.o[L_con_frame]; d.con_dist = s + l.o[L_con_dist];
-  d.J = s + l.o[L_J]; d.K = s + l.o[L_K]; d.efc_pos = s + l.o[L_efc_pos]; d.efc_margin = s + l.o[L_efc_margin];
-  d.efc_vel = s + l.o[L_efc_vel]; d.efc_aref = s + l.o[L_efc_aref]; d.efc_R = s + l.o[L_efc_R];
-  d.efc_A = s + l.o[L_efc_A]; d.efc_b = s + l.o[L_efc_b]; d.efc_f = s + l.o[L_efc_f];
-  d.efc_mu = s + l.o[L_efc_mu]; d.efc_blk = s + l.o[L_efc_blk]; d.efc_floss = s + l.o[L_efc_floss];
-  d.w = s + l.o[L_w]; d.jac = s + l.o[L_jac]; d.scratch = s + l.o[L_scratch];
-  d.poly = (P2*)(s + l.o[L_poly]);
-  int* ib = (int*)(s + l.o[L_ints]);
-  d.ints = ib;
-  // int arrays follow the 16 counters
-  int ncmax = l.ncon_max, nemax = l.nefc_max;
-  d.con_pair = ib + 16;
-  d.con_g1 = d.con_pair + ncmax;
-  d.con_g2 = d.con_g1 + ncmax;
-  d.efc_type = d.con_g2 + ncmax;
-  d.efc_dim = d.efc_type + nemax;
-  d.efc_con = d.efc_dim + nemax;
-}
-
-// ---------------------------------------------------------------------------
 // kinematics (lane 0)
-__device__ void kinematics(const Mdl& md, Dat& d) {
+DEVI void kinematics(const Mdl& md, Dat& d) {
   const int32_t *parent = IA(md, body_parentid), *mocapid = IA(md, body_mocapid);
   const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
   const int32_t *jtype = IA(md, jnt_type), *qadr = IA(md, jnt_qposadr);
@@ -322,11 +320,9 @@ __device__ void kinematics(const Mdl& md, Dat& d) {
     d.xpos[3 * b] = pos[0]; d.xpos[3 * b + 1] = pos[1]; d.xpos[3 * b + 2] = pos[2];
     d.xquat[4 * b] = quat[0]; d.xquat[4 * b + 1] = quat[1]; d.xquat[4 * b + 2] = quat[2]; d.xquat[4 * b + 3] = quat[3];
     quat2mat(d.xmat + 9 * b, quat);
-    double t[3], qi[4];
+    double t[3];
     mulmv3(t, d.xmat + 9 * b, ipos + 3 * b);
     add3(d.xipos + 3 * b, d.xpos + 3 * b, t);
-    quatmul(qi, quat, iquat + 4 * b);
-    quat2mat(d.ximat + 9 * b, qi);
   }
   const int32_t* gbody = IA(md, geom_bodyid);
   const double *gpos = DA(md, geom_pos), *gquat = DA(md, geom_quat);
@@ -341,7 +337,7 @@ __device__ void kinematics(const Mdl& md, Dat& d) {
 }
 
 // mj_comPos (lane 0)
-__device__ void com_pos(const Mdl& md, Dat& d) {
+DEVI void com_pos(const Mdl& md, Dat& d) {
   const int32_t *parent = IA(md, body_parentid), *rootid = IA(md, body_rootid);
   const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
   const int32_t *jtype = IA(md, jnt_type), *dadr = IA(md, jnt_dofadr);
@@ -374,7 +370,9 @@ __device__ void com_pos(const Mdl& md, Dat& d) {
   }
   for (int b = 0; b < nb; b++) {
     double* ci = d.cinert + 10 * b;
-    const double* R = d.ximat + 9 * b;
+    double qi[4], R[9];
+    quatmul(qi, d.xquat + 4 * b, DA(md, body_iquat) + 4 * b);
+    quat2mat(R, qi);
     const double* in = inertia + 3 * b;
     double mm = mass[b];
     double off[3];
@@ -431,7 +429,7 @@ __device__ void com_pos(const Mdl& md, Dat& d) {
 }
 
 // composite rigid bodies (lane 0) + mass matrix (lanes over dofs)
-__device__ void crb(const Mdl& md, Dat& d) {
+DEVI void crb(const Mdl& md, Dat& d) {
   int nb = md.m.nbody, nv = md.m.nv, lane = lane_id();
   const int32_t *parent = IA(md, body_parentid), *dbody = IA(md, dof_bodyid), *dpar = IA(md, dof_parentid);
   const double* arm = DA(md, dof_armature);
@@ -461,7 +459,8 @@ __device__ void crb(const Mdl& md, Dat& d) {
 }
 
 // dense LDL^T, columns sequential, rows across lanes (same products as oracle)
-__device__ void ldl_factor(int n, const double* A, double* L, double* Dv, double* Dinv) {
+// in place: the strict lower triangle of A is overwritten by L
+DEVI void ldl_factor(int n, double* A, double* L, double* Dv, double* Dinv) {
   int lane = lane_id();
   for (int j = 0; j < n; j++) {
     double dj = A[j * n + j];
@@ -476,9 +475,8 @@ __device__ void ldl_factor(int n, const double* A, double* L, double* Dv, double
     wsync();
   }
 }
-// single-lane solve
-__device__ void ldl_solve(int n, const double* L, const double* Dinv, const double* b, double* x) {
-  double y[64];
+// single-lane solve, y: scratch of n doubles (LDS)
+DEVI void ldl_solve(int n, const double* L, const double* Dinv, const double* b, double* x, double* y) {
   for (int i = 0; i < n; i++) {
     double s = b[i];
     for (int k = 0; k < i; k++) s = s - L[i * n + k] * y[k];
@@ -492,7 +490,7 @@ __device__ void ldl_solve(int n, const double* L, const double* Dinv, const doub
 }
 
 // actuation (lane 0)
-__device__ void actuation(const Mdl& md, Dat& d) {
+DEVI void actuation(const Mdl& md, Dat& d) {
   int nv = md.m.nv;
   const int32_t *trntype = IA(md, actuator_trntype), *trnid = IA(md, actuator_trnid);
   const int32_t *gtype = IA(md, actuator_gaintype), *btype = IA(md, actuator_biastype);
@@ -544,7 +542,7 @@ __device__ void actuation(const Mdl& md, Dat& d) {
   }
 }
 
-__device__ void passive(const Mdl& md, Dat& d) {
+DEVI void passive(const Mdl& md, Dat& d) {
   const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
   const double *stiff = DA(md, jnt_stiffness), *qspring = DA(md, qpos_spring), *damp = DA(md, dof_damping);
   for (int k = 0; k < md.m.nv; k++) d.qfrc_passive[k] = 0.0;
@@ -556,7 +554,7 @@ __device__ void passive(const Mdl& md, Dat& d) {
   for (int k = 0; k < md.m.nv; k++) d.qfrc_passive[k] = d.qfrc_passive[k] - damp[k] * d.qvel[k];
 }
 
-__device__ void rne(const Mdl& md, Dat& d) {
+DEVI void rne(const Mdl& md, Dat& d) {
   int nb = md.m.nbody;
   const int32_t *parent = IA(md, body_parentid), *dnum = IA(md, body_dofnum), *dadr = IA(md, body_dofadr);
   const int32_t* dbody = IA(md, dof_bodyid);
@@ -595,7 +593,7 @@ __device__ void rne(const Mdl& md, Dat& d) {
 struct SupPt { double v[3], a[3], b[3]; };
 
 // wave-parallel support mapping: all lanes pass the same dir, all lanes get the result
-__device__ int support_geom(const Mdl& md, const Dat& d, int g, const double* dir, double* out) {
+DEVI int support_geom(const Mdl& md, const Dat& d, int g, const double* dir, double* out) {
   int lane = lane_id();
   int h = IA(md, geom_hullid)[g];
   int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
@@ -621,21 +619,21 @@ __device__ int support_geom(const Mdl& md, const Dat& d, int g, const double* di
   return bi;
 }
 
-__device__ void mink_support(const Mdl& md, const Dat& d, int g1, int g2, const double* dir, SupPt* p) {
+DEVI void mink_support(const Mdl& md, const Dat& d, int g1, int g2, const double* dir, SupPt* p) {
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
   support_geom(md, d, g1, dir, p->a);
   support_geom(md, d, g2, nd, p->b);
   sub3(p->v, p->a, p->b);
 }
 
-__device__ void portal_normal(double* n, const SupPt* p1, const SupPt* p2, const SupPt* p3) {
+DEVI void portal_normal(double* n, const SupPt* p1, const SupPt* p2, const SupPt* p3) {
   double e1[3], e2[3];
   sub3(e1, p2->v, p1->v);
   sub3(e2, p3->v, p1->v);
   cross3(n, e1, e2);
   normalize3(n);
 }
-__device__ int portal_reach_tol(const SupPt* p1, const SupPt* p2, const SupPt* p3, const SupPt* p4,
+DEVI int portal_reach_tol(const SupPt* p1, const SupPt* p2, const SupPt* p3, const SupPt* p4,
                                 const double* n, double tol) {
   double dv4 = dot3(p4->v, n);
   double t1 = dv4 - dot3(p1->v, n);
@@ -645,7 +643,7 @@ __device__ int portal_reach_tol(const SupPt* p1, const SupPt* p2, const SupPt* p
   mn = mn < t3 ? mn : t3;
   return mn <= tol;
 }
-__device__ void portal_expand(SupPt* p0, SupPt* p1, SupPt* p2, SupPt* p3, const SupPt* p4) {
+DEVI void portal_expand(SupPt* p0, SupPt* p1, SupPt* p2, SupPt* p3, const SupPt* p4) {
   double c[3];
   cross3(c, p4->v, p0->v);
   if (dot3(p1->v, c) > 0.0) {
@@ -655,7 +653,7 @@ __device__ void portal_expand(SupPt* p0, SupPt* p1, SupPt* p2, SupPt* p3, const 
   }
 }
 
-__device__ int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n, double* depth, double* pos) {
+DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n, double* depth, double* pos) {
   const double tol = md.m.mpr_tolerance;
   const int32_t* ghull = IA(md, geom_hullid);
   const double* HC = DA(md, hull_center);
@@ -751,7 +749,7 @@ __device__ int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, doub
   }
 }
 
-__device__ void make_frame(const double* n, double* t1, double* t2) {
+DEVI void make_frame(const double* n, double* t1, double* t2) {
   double a[3];
   if (fabs(n[0]) < 0.6) { a[0] = 1.0; a[1] = 0.0; a[2] = 0.0; }
   else { a[0] = 0.0; a[1] = 1.0; a[2] = 0.0; }
@@ -763,7 +761,7 @@ __device__ void make_frame(const double* n, double* t1, double* t2) {
 
 // feature extraction: wave max over heights, then ballot compaction in vertex
 // order of the vertices within tol of the extreme; out[] written to LDS.
-__device__ int feature(const Mdl& md, const Dat& d, int g, const double* n, const double* t1, const double* t2,
+DEVI int feature(const Mdl& md, const Dat& d, int g, const double* n, const double* t1, const double* t2,
                        int sign, double tol, P2* out, double* ext) {
   int lane = lane_id();
   int h = IA(md, geom_hullid)[g];
@@ -811,11 +809,11 @@ __device__ int feature(const Mdl& md, const Dat& d, int g, const double* n, cons
   return cnt < K_MAXF ? cnt : K_MAXF;
 }
 
-__device__ __forceinline__ double cross2(const P2* o, const P2* a, const P2* b) {
+DEVI double cross2(const P2* o, const P2* a, const P2* b) {
   return (a->x - o->x) * (b->y - o->y) - (a->y - o->y) * (b->x - o->x);
 }
 
-__device__ int hull2d(P2* pts, int n, P2* out) {
+DEVI int hull2d(P2* pts, int n, P2* out) {
   for (int i = 1; i < n; i++) {
     P2 key = pts[i];
     int j = i - 1;
@@ -846,7 +844,7 @@ __device__ int hull2d(P2* pts, int n, P2* out) {
   return k - 1;
 }
 
-__device__ __forceinline__ P2 lerp2(const P2* a, const P2* b, double t) {
+DEVI P2 lerp2(const P2* a, const P2* b, double t) {
   P2 r;
   r.x = a->x + t * (b->x - a->x);
   r.y = a->y + t * (b->y - a->y);
@@ -854,7 +852,7 @@ __device__ __forceinline__ P2 lerp2(const P2* a, const P2* b, double t) {
   return r;
 }
 
-__device__ int clip_poly(const P2* P, int np, P2* Q, int nq, P2* buf) {
+DEVI int clip_poly(const P2* P, int np, P2* Q, int nq, P2* buf) {
   if (nq == 1) {
     for (int e = 0; e < np; e++) {
       const P2* a = &P[e];
@@ -902,12 +900,12 @@ __device__ int clip_poly(const P2* P, int np, P2* Q, int nq, P2* buf) {
   return nq;
 }
 
-__device__ __forceinline__ double dist2d(const P2* a, const P2* b) {
+DEVI double dist2d(const P2* a, const P2* b) {
   double dx = a->x - b->x, dy = a->y - b->y;
   return dx * dx + dy * dy;
 }
 
-__device__ void add_contact(Dat& d, int ncon_max, int pair, int g1, int g2, const double* pos, const double* n,
+DEVI void add_contact(Dat& d, int ncon_max, int pair, int g1, int g2, const double* pos, const double* n,
                             const double* t1, const double* t2, double dist) {
   if (d.NCON >= ncon_max) { d.OVERFLOW |= 1; return; }
   int c = d.NCON++;
@@ -923,7 +921,7 @@ __device__ void add_contact(Dat& d, int ncon_max, int pair, int g1, int g2, cons
 }
 
 // narrowphase of one admissible pair, all lanes participate
-__device__ void collide_pair(const Mdl& md, Dat& d, int pair) {
+DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   int lane = lane_id();
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
   double n[3], depth, mpos[3];
@@ -933,6 +931,10 @@ __device__ void collide_pair(const Mdl& md, Dat& d, int pair) {
   P2* fa = d.poly;                 // K_MAXPOLY each
   P2* fb = d.poly + K_MAXPOLY;
   P2* buf = d.poly + 2 * K_MAXPOLY;
+  P2* refpoly = d.poly + 3 * K_MAXPOLY;
+  P2* inc = d.poly + 4 * K_MAXPOLY;
+  P2* pts = d.poly + 5 * K_MAXPOLY;
+  double* dep = d.pdep;
   double s1, s2;
   int na = feature(md, d, g1, n, t1, t2, +1, 0.0, fa, &s1);
   int nb = feature(md, d, g2, n, t1, t2, -1, 0.0, fb, &s2);
@@ -943,11 +945,8 @@ __device__ void collide_pair(const Mdl& md, Dat& d, int pair) {
   nb = feature(md, d, g2, n, t1, t2, -1, tol, fb, &s2);
   if (lane == 0) {
     int refB = (nb >= na);
-    P2 refpoly[K_MAXPOLY], inc[K_MAXPOLY];
     int nr = refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly);
     int ni = refB ? hull2d(fa, na, inc) : hull2d(fb, nb, inc);
-    P2 pts[K_MAXPOLY];
-    double dep[K_MAXPOLY];
     int np = 0;
     if (nr >= 3) {
       int nc = clip_poly(refpoly, nr, inc, ni, buf);
@@ -1001,7 +1000,7 @@ __device__ void collide_pair(const Mdl& md, Dat& d, int pair) {
 }
 
 // broadphase over all admissible pairs (lanes over pairs), then narrowphase in pair order
-__device__ void collision(const Mdl& md, Dat& d) {
+DEVI void collision(const Mdl& md, Dat& d) {
   int lane = lane_id();
   const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
   const double *aabb = DA(md, geom_aabb), *pm = DA(md, pair_margin);
@@ -1038,8 +1037,70 @@ __device__ void collision(const Mdl& md, Dat& d) {
 }
 
 // ---------------------------------------------------------------------------
+// LDS layout (offsets in doubles; computed on the host by make_layout)
+enum {
+  L_qpos, L_qvel, L_qacc_ws, L_ctrl, L_mocap_pos, L_mocap_quat, L_time,
+  L_xpos, L_xquat, L_xmat, L_xipos, L_xanchor, L_xaxis, L_subtree_com, L_subtree_mass, L_cinert, L_cdof,
+  L_geom_xpos, L_geom_xmat,
+  L_M, L_Dv, L_Dinv, L_sD, L_isD, L_tmp, L_tmp2,
+  L_qfrc_bias, L_qfrc_passive, L_qfrc_actuator, L_qfrc_smooth, L_qacc_smooth, L_qfrc_constraint, L_qacc,
+  L_act_force, L_act_moment, L_act_length, L_act_vel,
+  L_con_pos, L_con_frame, L_con_dist,
+  L_efc_R, L_efc_b, L_efc_AR, L_efc_ARinv, L_efc_A, L_efc_Ainv, L_efc_floss, L_con_mu, L_con_blk,
+  L_U, L_ints, L_COUNT
+};
+struct Lay {
+  int o[L_COUNT];
+  int ncon_max, nefc_max, nv;
+  int total_doubles;
+  // U sub-offsets (relative to o[L_U])
+  int u_crb, u_cvel, u_cacc, u_cfrc, u_cdof_dot, u_poly, u_pdep, u_G, u_jac, u_aref, u_vel, u_pos, u_margin,
+      u_scratch, u_qDeriv, u_newton;
+};
+
+DEVI void bind(Dat& d, double* s, const Lay& l) {
+#define B(f) d.f = s + l.o[L_##f]
+  B(qpos); B(qvel); B(qacc_ws); B(ctrl); B(mocap_pos); B(mocap_quat); B(time);
+  B(xpos); B(xquat); B(xmat); B(xipos); B(xanchor); B(xaxis); B(subtree_com); B(subtree_mass); B(cinert); B(cdof);
+  B(geom_xpos); B(geom_xmat);
+  B(M); B(Dv); B(Dinv); B(sD); B(isD); B(tmp); B(tmp2);
+  B(qfrc_bias); B(qfrc_passive); B(qfrc_actuator); B(qfrc_smooth); B(qacc_smooth); B(qfrc_constraint); B(qacc);
+  B(act_force); B(act_moment); B(act_length); B(act_vel);
+  B(con_pos); B(con_frame); B(con_dist);
+  B(efc_R); B(efc_b); B(efc_AR); B(efc_ARinv); B(efc_A); B(efc_Ainv); B(efc_floss); B(con_mu); B(con_blk);
+#undef B
+  double* U = s + l.o[L_U];
+  d.crb = U + l.u_crb; d.cvel = U + l.u_cvel; d.cacc = U + l.u_cacc; d.cfrc = U + l.u_cfrc;
+  d.cdof_dot = U + l.u_cdof_dot;
+  d.poly = (P2*)(U + l.u_poly); d.pdep = U + l.u_pdep;
+  d.G = U + l.u_G; d.jac = U + l.u_jac; d.efc_aref = U + l.u_aref; d.efc_vel = U + l.u_vel;
+  d.efc_pos = U + l.u_pos; d.efc_margin = U + l.u_margin; d.scratch = U + l.u_scratch;
+  d.qDeriv = U + l.u_qDeriv;
+  {
+    int ne = l.nefc_max, nv = l.nv, nc = l.ncon_max;
+    double* n0 = U + l.u_newton;
+    d.efc_jar = n0; d.efc_jv = n0 + ne; d.efc_f = n0 + 2 * ne; d.efc_Dr = n0 + 3 * ne;
+    d.efc_isR = n0 + 4 * ne; d.efc_sqR = n0 + 5 * ne; d.efc_mup = n0 + 6 * ne;
+    d.nH = n0 + 7 * ne; d.nw = d.nH + nv * nv; d.nw0 = d.nw + nv; d.ng = d.nw0 + nv; d.ndir = d.ng + nv;
+    d.con_hb = d.ndir + nv;
+    (void)nc;
+  }
+  int* ib = (int*)(s + l.o[L_ints]);
+  d.ints = ib;
+  int ncmax = l.ncon_max, nemax = l.nefc_max;
+  d.con_pair = ib + 16;
+  d.con_g1 = d.con_pair + ncmax;
+  d.con_g2 = d.con_g1 + ncmax;
+  d.efc_type = d.con_g2 + ncmax;
+  d.efc_dim = d.efc_type + nemax;
+  d.efc_con = d.efc_dim + nemax;
+  d.efc_lead = d.efc_con + nemax;
+  d.efc_state = d.efc_lead + nemax;
+}
+
+// ---------------------------------------------------------------------------
 // constraints
-__device__ void jac_point(const Mdl& md, const Dat& d, int b, const double* pt, double* jacp, double* jacr) {
+DEVI void jac_point(const Mdl& md, const Dat& d, int b, const double* pt, double* jacp, double* jacr) {
   int nv = md.m.nv;
   for (int k = 0; k < 3 * nv; k++) { jacp[k] = 0.0; jacr[k] = 0.0; }
   int dof = IA(md, body_lastdof)[b];
@@ -1059,7 +1120,7 @@ __device__ void jac_point(const Mdl& md, const Dat& d, int b, const double* pt, 
   }
 }
 
-__device__ double impedance(const double* si, double pos, double margin) {
+DEVI double impedance(const double* si, double pos, double margin) {
   if (si[0] == si[1] || si[2] <= K_MINVAL) return 0.5 * (si[0] + si[1]);
   double x = (pos - margin) / si[2];
   if (x < 0.0) x = -x;
@@ -1085,15 +1146,18 @@ __device__ double impedance(const double* si, double pos, double margin) {
 }
 
 // lane 0 only
-__device__ int add_row(const Mdl& md, Dat& d, int type, double pos, double margin, int dim, int con) {
+DEVI int add_row(const Mdl& md, Dat& d, int type, double pos, double margin, int dim, int con) {
   if (d.NEFC >= md.m.nefc_max) { d.OVERFLOW |= 2; return -1; }
   int r = d.NEFC++;
   d.efc_type[r] = type; d.efc_pos[r] = pos; d.efc_margin[r] = margin;
   d.efc_dim[r] = dim; d.efc_con[r] = con;
+  d.efc_lead[r] = (type != MGS_EFC_CONTACT || r == 0 || d.efc_type[r - 1] != MGS_EFC_CONTACT ||
+                   d.efc_con[r - 1] != con) ? 1 : 0;
   return r;
 }
 
-__device__ void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, const double* si,
+// lane 0 only
+DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, const double* si,
                            const double* mu, int elliptic_contact) {
   const double dt = md.m.timestep;
   double tc = sr[0], dr = sr[1];
@@ -1128,14 +1192,16 @@ __device__ void row_params(const Mdl& md, Dat& d, int r, int dim, const double* 
   }
 }
 
-// fill J rows r..r+nr-1 from jacobian scratch according to kind (lanes over columns)
-__device__ void make_constraints(const Mdl& md, Dat& d) {
+// Build J rows (into the G slots), then per row: velocity, J.qacc_smooth,
+// whitened row G = D^-1/2 L^-1 J^T in place, A = G.G; impedance; blocks.
+DEVI void make_constraints(const Mdl& md, Dat& d) {
   int nv = md.m.nv, lane = lane_id();
   double* jp1 = d.jac;
   double* jr1 = d.jac + 3 * nv;
   double* jp2 = d.jac + 6 * nv;
   double* jr2 = d.jac + 9 * nv;
   int* ints = d.ints;
+  double* J = d.G;
   if (lane == 0) { d.NEFC = 0; }
   wsync();
   const int32_t *et = IA(md, eq_type), *eo1 = IA(md, eq_obj1id), *eo2 = IA(md, eq_obj2id);
@@ -1165,7 +1231,7 @@ __device__ void make_constraints(const Mdl& md, Dat& d) {
       if (d.OVERFLOW & 2) break;
       int r0 = d.NEFC - 3;
       for (int c = lane; c < nv; c += WAVE)
-        for (int k = 0; k < 3; k++) d.J[(r0 + k) * nv + c] = jp1[k * nv + c] - jp2[k * nv + c];
+        for (int k = 0; k < 3; k++) J[(r0 + k) * nv + c] = jp1[k * nv + c] - jp2[k * nv + c];
       if (et[e] == MGS_EQ_WELD) {
         double q1r[4], q2c[4], qe[4];
         quatmul(q1r, d.xquat + 4 * b1, data + 3);
@@ -1183,7 +1249,7 @@ __device__ void make_constraints(const Mdl& md, Dat& d) {
           double t1q[4], t2q[4];
           quatmul(t1q, q2c, ax);
           quatmul(t2q, t1q, q1r);
-          for (int k = 0; k < 3; k++) d.J[(rr + k) * nv + c] = (0.5 * t2q[1 + k]) * ts;
+          for (int k = 0; k < 3; k++) J[(rr + k) * nv + c] = (0.5 * t2q[1 + k]) * ts;
         }
       }
       wsync();
@@ -1207,31 +1273,29 @@ __device__ void make_constraints(const Mdl& md, Dat& d) {
       wsync();
       if (d.OVERFLOW & 2) break;
       int r = d.NEFC - 1;
-      for (int c = lane; c < nv; c += WAVE) d.J[r * nv + c] = 0.0;
+      for (int c = lane; c < nv; c += WAVE) J[r * nv + c] = 0.0;
       wsync();
       if (lane == 0) {
-        d.J[r * nv + jd[j1]] = 1.0;
-        if (j2 >= 0) d.J[r * nv + jd[j2]] = d.J[r * nv + jd[j2]] - deriv;
+        J[r * nv + jd[j1]] = 1.0;
+        if (j2 >= 0) J[r * nv + jd[j2]] = J[r * nv + jd[j2]] - deriv;
       }
       wsync();
     }
   }
-  if (lane == 0) ints[8] = d.NEFC;
-  // dof friction loss
-  const double* floss = DA(md, dof_frictionloss);
   if (lane == 0) {
+    ints[8] = d.NEFC;
+    const double* floss = DA(md, dof_frictionloss);
     ints[9] = d.NEFC;
     for (int k = 0; k < nv; k++) {
       if (floss[k] > 0.0) {
         int r = add_row(md, d, MGS_EFC_FRICTION, 0.0, 0.0, 1, k);
         if (r < 0) break;
-        for (int c = 0; c < nv; c++) d.J[r * nv + c] = 0.0;
-        d.J[r * nv + k] = 1.0;
+        for (int c = 0; c < nv; c++) J[r * nv + c] = 0.0;
+        J[r * nv + k] = 1.0;
         d.efc_floss[r] = floss[k];
       }
     }
     ints[10] = d.NEFC;
-    // joint limits
     const int32_t *lim = IA(md, jnt_limited), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
     const double *range = DA(md, jnt_range), *jmargin = DA(md, jnt_margin);
     ints[11] = d.NEFC;
@@ -1241,23 +1305,22 @@ __device__ void make_constraints(const Mdl& md, Dat& d) {
       double dlo = q - range[2 * j], dhi = range[2 * j + 1] - q;
       if (dlo < jmargin[j]) {
         int r = add_row(md, d, MGS_EFC_LIMIT, dlo, jmargin[j], 1, j);
-        if (r >= 0) { for (int c = 0; c < nv; c++) d.J[r * nv + c] = 0.0; d.J[r * nv + jd[j]] = 1.0; }
+        if (r >= 0) { for (int c = 0; c < nv; c++) J[r * nv + c] = 0.0; J[r * nv + jd[j]] = 1.0; }
       }
       if (dhi < jmargin[j]) {
         int r = add_row(md, d, MGS_EFC_LIMIT, dhi, jmargin[j], 1, j);
-        if (r >= 0) { for (int c = 0; c < nv; c++) d.J[r * nv + c] = 0.0; d.J[r * nv + jd[j]] = -1.0; }
+        if (r >= 0) { for (int c = 0; c < nv; c++) J[r * nv + c] = 0.0; J[r * nv + jd[j]] = -1.0; }
       }
     }
     ints[12] = d.NEFC;
     ints[6] = d.NEFC;
   }
   wsync();
-  // contacts
   const int32_t *gbody = IA(md, geom_bodyid), *pcd = IA(md, pair_condim);
   const double *pfr = DA(md, pair_friction), *pmar = DA(md, pair_margin);
-  int ncon = d.NCON;
+  int ncon = uni(d.NCON);
   for (int c = 0; c < ncon; c++) {
-    int p = d.con_pair[c];
+    int p = uni(d.con_pair[c]);
     int dim = pcd[p];
     if (d.NEFC + dim > md.m.nefc_max) {
       if (lane == 0) d.OVERFLOW |= 2;
@@ -1272,35 +1335,38 @@ __device__ void make_constraints(const Mdl& md, Dat& d) {
       jac_point(md, d, b1, pt, jp1, jr1);
       jac_point(md, d, b2, pt, jp2, jr2);
       for (int j = 0; j < dim; j++) add_row(md, d, MGS_EFC_CONTACT, j == 0 ? d.con_dist[c] : 0.0, pmar[p], dim, c);
-      for (int j = 0; j < dim; j++) d.efc_mu[5 * r + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
+      for (int j = 0; j < dim; j++) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
     }
     wsync();
     for (int col = lane; col < nv; col += WAVE) {
       double dp[3] = {jp2[col] - jp1[col], jp2[nv + col] - jp1[nv + col], jp2[2 * nv + col] - jp1[2 * nv + col]};
-      for (int j = 0; j < dim && j < 3; j++) d.J[(r + j) * nv + col] = dot3(fr + 3 * j, dp);
+      for (int j = 0; j < dim && j < 3; j++) J[(r + j) * nv + col] = dot3(fr + 3 * j, dp);
       if (dim >= 4) {
         double dr[3] = {jr2[col] - jr1[col], jr2[nv + col] - jr1[nv + col], jr2[2 * nv + col] - jr1[2 * nv + col]};
-        d.J[(r + 3) * nv + col] = dot3(fr, dr);
-        if (dim == 6) {
-          d.J[(r + 4) * nv + col] = dot3(fr + 3, dr);
-          d.J[(r + 5) * nv + col] = dot3(fr + 6, dr);
-        }
+        J[(r + 3) * nv + col] = dot3(fr, dr);
       }
     }
   }
   wsync();
   if (lane == 0) ints[7] = d.NEFC;
   wsync();
-  int ne = d.NEFC;
-  // velocities, K = M^-1 J^T, diagonal of A (lanes over rows)
+  int ne = uni(d.NEFC);
+  // per row (lanes over rows): vel, J.qacc_smooth, G in place, A
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Jr = d.J + r * nv;
-    double v = 0.0;
-    for (int k = 0; k < nv; k++) v = v + Jr[k] * d.qvel[k];
+    double* Gr = d.G + r * nv;
+    double v = 0.0, bj = 0.0;
+    for (int k = 0; k < nv; k++) v = v + Gr[k] * d.qvel[k];
+    for (int k = 0; k < nv; k++) bj = bj + Gr[k] * d.qacc_smooth[k];
     d.efc_vel[r] = v;
-    ldl_solve(nv, d.L, d.Dinv, Jr, d.K + r * nv);
+    d.efc_b[r] = bj;
+    for (int i = 0; i < nv; i++) {
+      double s = Gr[i];
+      for (int k = 0; k < i; k++) s = s - d.M[i * nv + k] * Gr[k];
+      Gr[i] = s;
+    }
+    for (int i = 0; i < nv; i++) Gr[i] = Gr[i] * d.isD[i];
     double a = 0.0;
-    for (int k = 0; k < nv; k++) a = a + Jr[k] * d.K[r * nv + k];
+    for (int k = 0; k < nv; k++) a = a + Gr[k] * Gr[k];
     d.efc_A[r] = a;
   }
   wsync();
@@ -1325,27 +1391,28 @@ __device__ void make_constraints(const Mdl& md, Dat& d) {
       int c = d.efc_con[r];
       int p = d.con_pair[c];
       int dim = d.efc_dim[r];
-      row_params(md, d, r, dim, psr + 2 * p, psi + 5 * p, d.efc_mu + 5 * r, 1);
+      row_params(md, d, r, dim, psr + 2 * p, psi + 5 * p, d.con_mu + 5 * c, 1);
       r += dim;
     }
   }
   wsync();
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Jr = d.J + r * nv;
-    double v = 0.0;
-    for (int k = 0; k < nv; k++) v = v + Jr[k] * d.qacc_smooth[k];
-    d.efc_b[r] = v - d.efc_aref[r];
+    d.efc_b[r] = d.efc_b[r] - d.efc_aref[r];
+    double ar = d.efc_A[r] + d.efc_R[r];
+    d.efc_AR[r] = ar;
+    d.efc_ARinv[r] = 1.0 / ar;
+    d.efc_Ainv[r] = 1.0 / d.efc_A[r];
   }
-  // contact blocks of A (lanes over block entries)
-  for (int r = ints[6]; r < ints[7];) {
-    int dim = d.efc_dim[r];
-    double* blk = d.efc_blk + 36 * r;
+  // contact blocks A = G G^T (lanes over block entries)
+  for (int r = uni(ints[6]); r < uni(ints[7]);) {
+    int dim = uni(d.efc_dim[r]);
+    double* blk = d.con_blk + BLKSTRIDE * uni(d.efc_con[r]);
     for (int e = lane; e < dim * dim; e += WAVE) {
       int i = e / dim, j = e % dim;
-      const double* Ji = d.J + (r + i) * nv;
-      const double* Kj = d.K + (r + j) * nv;
+      const double* Gi = d.G + (r + i) * nv;
+      const double* Gj = d.G + (r + j) * nv;
       double a = 0.0;
-      for (int k = 0; k < nv; k++) a = a + Ji[k] * Kj[k];
+      for (int k = 0; k < nv; k++) a = a + Gi[k] * Gj[k];
       blk[i * dim + j] = a;
     }
     r += dim;
@@ -1354,65 +1421,198 @@ __device__ void make_constraints(const Mdl& md, Dat& d) {
 }
 
 // ---------------------------------------------------------------------------
-// solver
-__device__ void qcqp(int n, const double* A, const double* b, const double* mu, double r, double* x) {
-  double As[25], bs[5], y[5], P[25];
-  for (int i = 0; i < n; i++) {
-    bs[i] = b[i] * mu[i];
-    for (int j = 0; j < n; j++) As[i * n + j] = (A[i * n + j] * mu[i]) * mu[j];
-  }
-  double la = 0.0;
-  double rr = r * r;
-  for (int i = 0; i < n; i++) y[i] = 0.0;
+// solver (all lanes execute the scalar logic with identical values)
+DEVI void qcqp2(double A0, double A1, double A3, double bb0, double bb1, const double* mu, double r,
+                                      double* x0, double* x1) {
+  double a11 = (A0 * mu[0]) * mu[0], a12 = (A1 * mu[0]) * mu[1], a22 = (A3 * mu[1]) * mu[1];
+  double b1 = bb0 * mu[0], b2 = bb1 * mu[1];
+  double rr = r * r, la = 0.0, v1 = 0.0, v2 = 0.0;
   for (int it = 0; it < 20; it++) {
-    double T[25];
-    for (int i = 0; i < n * n; i++) T[i] = As[i];
-    for (int i = 0; i < n; i++) T[i * n + i] = T[i * n + i] + la;
-    for (int i = 0; i < n * n; i++) P[i] = 0.0;
-    for (int i = 0; i < n; i++) P[i * n + i] = 1.0;
-    int bad = 0;
-    for (int c = 0; c < n; c++) {
-      double piv = T[c * n + c];
-      if (piv < 1e-15) { bad = 1; break; }
-      double ip = 1.0 / piv;
-      for (int j = 0; j < n; j++) { T[c * n + j] = T[c * n + j] * ip; P[c * n + j] = P[c * n + j] * ip; }
-      for (int i = 0; i < n; i++) {
-        if (i == c) continue;
-        double f = T[i * n + c];
-        if (f == 0.0) continue;
-        for (int j = 0; j < n; j++) {
-          T[i * n + j] = T[i * n + j] - f * T[c * n + j];
-          P[i * n + j] = P[i * n + j] - f * P[c * n + j];
-        }
-      }
-    }
-    if (bad) { for (int i = 0; i < n; i++) y[i] = 0.0; break; }
-    for (int i = 0; i < n; i++) {
-      double s = 0.0;
-      for (int j = 0; j < n; j++) s = s - P[i * n + j] * bs[j];
-      y[i] = s;
-    }
-    double val = 0.0;
-    for (int i = 0; i < n; i++) val = val + y[i] * y[i];
-    val = val - rr;
+    double m11 = a11 + la, m22 = a22 + la;
+    double det = m11 * m22 - a12 * a12;
+    if (det < 1e-10) { v1 = 0.0; v2 = 0.0; break; }
+    double idet = 1.0 / det;
+    double p11 = m22 * idet, p22 = m11 * idet, p12 = -a12 * idet;
+    v1 = -(p11 * b1 + p12 * b2);
+    v2 = -(p12 * b1 + p22 * b2);
+    double val = (v1 * v1 + v2 * v2) - rr;
     if (val < 1e-10) break;
-    double pv[5];
-    for (int i = 0; i < n; i++) {
-      double s = 0.0;
-      for (int j = 0; j < n; j++) s = s + P[i * n + j] * y[j];
-      pv[i] = s;
-    }
-    double deriv = 0.0;
-    for (int i = 0; i < n; i++) deriv = deriv + y[i] * pv[i];
-    deriv = -2.0 * deriv;
+    double pv1 = p11 * v1 + p12 * v2, pv2 = p12 * v1 + p22 * v2;
+    double deriv = -2.0 * (v1 * pv1 + v2 * pv2);
     double delta = -val / deriv;
     if (delta < 1e-10) break;
     la = la + delta;
   }
-  for (int i = 0; i < n; i++) x[i] = y[i] * mu[i];
+  *x0 = v1 * mu[0];
+  *x1 = v2 * mu[1];
 }
 
-__device__ void project_block(const Dat& d, int r, double* f) {
+DEVI void qcqp3(const double* A, const double* b, const double* mu, double r, double* x) {
+  double a00 = (A[0] * mu[0]) * mu[0], a01 = (A[1] * mu[0]) * mu[1], a02 = (A[2] * mu[0]) * mu[2];
+  double a11 = (A[4] * mu[1]) * mu[1], a12 = (A[5] * mu[1]) * mu[2], a22 = (A[8] * mu[2]) * mu[2];
+  double b0 = b[0] * mu[0], b1 = b[1] * mu[1], b2 = b[2] * mu[2];
+  double rr = r * r, la = 0.0, v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  for (int it = 0; it < 20; it++) {
+    double m00 = a00 + la, m11 = a11 + la, m22 = a22 + la;
+    double c00 = m11 * m22 - a12 * a12, c01 = a02 * a12 - a01 * m22, c02 = a01 * a12 - a02 * m11;
+    double c11 = m00 * m22 - a02 * a02, c12 = a01 * a02 - m00 * a12, c22 = m00 * m11 - a01 * a01;
+    double det = (m00 * c00 + a01 * c01) + a02 * c02;
+    if (det < 1e-10) { v0 = 0.0; v1 = 0.0; v2 = 0.0; break; }
+    double idet = 1.0 / det;
+    double p00 = c00 * idet, p01 = c01 * idet, p02 = c02 * idet;
+    double p11 = c11 * idet, p12 = c12 * idet, p22 = c22 * idet;
+    v0 = -((p00 * b0 + p01 * b1) + p02 * b2);
+    v1 = -((p01 * b0 + p11 * b1) + p12 * b2);
+    v2 = -((p02 * b0 + p12 * b1) + p22 * b2);
+    double val = ((v0 * v0 + v1 * v1) + v2 * v2) - rr;
+    if (val < 1e-10) break;
+    double pv0 = (p00 * v0 + p01 * v1) + p02 * v2;
+    double pv1 = (p01 * v0 + p11 * v1) + p12 * v2;
+    double pv2 = (p02 * v0 + p12 * v1) + p22 * v2;
+    double deriv = -2.0 * ((v0 * pv0 + v1 * pv1) + v2 * pv2);
+    double delta = -val / deriv;
+    if (delta < 1e-10) break;
+    la = la + delta;
+  }
+  x[0] = v0 * mu[0];
+  x[1] = v1 * mu[1];
+  x[2] = v2 * mu[2];
+}
+
+// forces live in registers: lane l holds f[l] (fr0) and f[l + 64] (fr1)
+DEVI double getf(double fr0, double fr1, int r) {
+  return r < WAVE ? readlane_d(fr0, r) : readlane_d(fr1, r - WAVE);
+}
+DEVI void setf(double& fr0, double& fr1, int r, double v, int lane) {
+  if (r < WAVE) fr0 = (lane == r) ? v : fr0;
+  else fr1 = (lane == r - WAVE) ? v : fr1;
+}
+
+// one PGS update of the contact block starting at row r with DIM rows
+template <int DIM>
+DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u, double& fr0,
+                                              double& fr1, int noslip) {
+  double g[DIM], res[DIM], old[DIM], nw[DIM];
+  const int c = uni(d.efc_con[r]);
+  const double* blk = d.con_blk + BLKSTRIDE * c;
+  const double* mu = d.con_mu + 5 * c;
+#pragma unroll
+  for (int i = 0; i < DIM; i++) {
+    g[i] = (lane < nv) ? d.G[(r + i) * nv + lane] : 0.0;
+    double jw = tree_sum(g[i] * u, P);
+    old[i] = getf(fr0, fr1, r + i);
+    res[i] = noslip ? (jw + d.efc_b[r + i]) : ((jw + d.efc_R[r + i] * old[i]) + d.efc_b[r + i]);
+  }
+  double Ab[DIM * DIM];
+#pragma unroll
+  for (int i = 0; i < DIM; i++) {
+#pragma unroll
+    for (int j = 0; j < DIM; j++) Ab[i * DIM + j] = blk[i * DIM + j];
+    if (!noslip) Ab[i * DIM + i] = Ab[i * DIM + i] + d.efc_R[r + i];
+  }
+  double dc = 0.0;
+  if (!noslip) {
+    double fn = old[0] - res[0] * d.efc_ARinv[r];
+    if (fn < 0.0) fn = 0.0;
+    double dn = fn - old[0];
+    nw[0] = fn;
+    if (fn == 0.0) {
+#pragma unroll
+      for (int j = 1; j < DIM; j++) nw[j] = 0.0;
+    } else {
+      double bq[DIM - 1];
+#pragma unroll
+      for (int i = 0; i < DIM - 1; i++) {
+        double v = res[1 + i] + Ab[(1 + i) * DIM] * dn;
+        double s = v;
+#pragma unroll
+        for (int j = 0; j < DIM - 1; j++) s = s - Ab[(1 + i) * DIM + 1 + j] * old[1 + j];
+        bq[i] = s;
+      }
+      if (DIM == 3) {
+        qcqp2(Ab[4], Ab[5], Ab[8], bq[0], bq[1], mu, fn, &nw[1], &nw[2]);
+      } else {
+        double Ac[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++) Ac[i * 3 + j] = Ab[(1 + i) * DIM + 1 + j];
+        qcqp3(Ac, bq, mu, fn, nw + 1);
+      }
+    }
+    double del[DIM];
+#pragma unroll
+    for (int i = 0; i < DIM; i++) del[i] = nw[i] - old[i];
+#pragma unroll
+    for (int i = 0; i < DIM; i++) {
+      double ad = 0.0;
+#pragma unroll
+      for (int j = 0; j < DIM; j++) ad = ad + Ab[i * DIM + j] * del[j];
+      dc = dc + del[i] * (0.5 * ad + res[i]);
+    }
+    double s = u;
+#pragma unroll
+    for (int i = 0; i < DIM; i++) s = s + g[i] * del[i];
+    if (lane < nv) u = s;
+#pragma unroll
+    for (int i = 0; i < DIM; i++) setf(fr0, fr1, r + i, nw[i], lane);
+  } else {
+    // friction dims only, normal fixed, A without R
+    const int NF = DIM - 1;
+    double bq[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+      double s = res[1 + i];
+#pragma unroll
+      for (int j = 0; j < NF; j++) s = s - Ab[(1 + i) * DIM + 1 + j] * old[1 + j];
+      bq[i] = s;
+    }
+    double fnorm = old[0];
+    if (fnorm > 0.0) {
+      if (DIM == 3) {
+        qcqp2(Ab[4], Ab[5], Ab[8], bq[0], bq[1], mu, fnorm, &nw[1], &nw[2]);
+      } else {
+        double Ac[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++) Ac[i * 3 + j] = Ab[(1 + i) * DIM + 1 + j];
+        qcqp3(Ac, bq, mu, fnorm, nw + 1);
+      }
+    } else {
+#pragma unroll
+      for (int i = 1; i < DIM; i++) nw[i] = 0.0;
+    }
+    double del[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) del[i] = nw[1 + i] - old[1 + i];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+      double ad = 0.0;
+#pragma unroll
+      for (int j = 0; j < NF; j++) ad = ad + Ab[(1 + i) * DIM + 1 + j] * del[j];
+      dc = dc + del[i] * (0.5 * ad + res[1 + i]);
+    }
+    double s = u;
+#pragma unroll
+    for (int i = 0; i < NF; i++) s = s + g[1 + i] * del[i];
+    if (lane < nv) u = s;
+#pragma unroll
+    for (int i = 0; i < NF; i++) setf(fr0, fr1, r + 1 + i, nw[1 + i], lane);
+  }
+  return dc;
+}
+
+DEVI void project_scalar(int t, double floss, double* f) {
+  if (t == MGS_EFC_FRICTION) {
+    if (f[0] < -floss) f[0] = -floss;
+    if (f[0] > floss) f[0] = floss;
+  } else if (t == MGS_EFC_LIMIT || t == MGS_EFC_CONTACT) {
+    if (f[0] < 0.0) f[0] = 0.0;
+  }
+}
+
+DEVI void project_block_lds(const Dat& d, int r, double* f) {
   int t = d.efc_type[r];
   if (t == MGS_EFC_FRICTION) {
     double fl = d.efc_floss[r];
@@ -1424,7 +1624,7 @@ __device__ void project_block(const Dat& d, int r, double* f) {
     int dim = d.efc_dim[r];
     if (f[0] < 0.0) { for (int j = 0; j < dim; j++) f[j] = 0.0; return; }
     if (dim == 1) return;
-    const double* mu = d.efc_mu + 5 * r;
+    const double* mu = d.con_mu + 5 * d.efc_con[r];
     double s = 0.0;
     for (int j = 1; j < dim; j++) { double q = f[j] / mu[j - 1]; s = s + q * q; }
     double nt = sqrt(s);
@@ -1435,211 +1635,501 @@ __device__ void project_block(const Dat& d, int r, double* f) {
   }
 }
 
-__device__ void solve_pgs(const Mdl& md, Dat& d) {
-  int nv = md.m.nv, ne = d.NEFC, lane = lane_id();
+DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
+  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
-  double meaninertia = 0.0;
-  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d.M[k * nv + k];
-  meaninertia = meaninertia / (double)nv;
-  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
-  // warmstart
+  // warmstart: hws = D^1/2 L^T qacc_ws (lane 0), f_r by lanes over rows, block projection
+  if (lane == 0) {
+    for (int i = 0; i < nv; i++) {
+      double s = d.qacc_ws[i];
+      for (int k = i + 1; k < nv; k++) s = s + d.M[k * nv + i] * d.qacc_ws[k];
+      d.tmp[i] = s * d.sD[i];
+    }
+  }
+  wsync();
+  double* fl = d.scratch;                 // f staging (ne)
+  double* terms = d.scratch + md.m.nefc_max;
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Jr = d.J + r * nv;
+    const double* Gr = d.G + r * nv;
     double jar = 0.0;
-    for (int k = 0; k < nv; k++) jar = jar + Jr[k] * d.qacc_ws[k];
+    for (int k = 0; k < nv; k++) jar = jar + Gr[k] * d.tmp[k];
     jar = jar - d.efc_aref[r];
-    d.efc_f[r] = -jar / d.efc_R[r];
+    fl[r] = -jar / d.efc_R[r];
   }
   wsync();
   if (lane == 0) {
     for (int r = 0; r < ne;) {
       int dim = d.efc_type[r] == MGS_EFC_CONTACT ? d.efc_dim[r] : 1;
-      if (d.efc_type[r] != MGS_EFC_EQUALITY) project_block(d, r, d.efc_f + r);
+      if (d.efc_type[r] != MGS_EFC_EQUALITY) project_block_lds(d, r, fl + r);
       r += dim;
     }
   }
   wsync();
-  for (int k = lane; k < nv; k += WAVE) {
+  // u = G^T f (lane k), then dual cost terms (lanes over rows), summed in row order
+  u = 0.0;
+  if (lane < nv) {
     double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d.K[r * nv + k] * d.efc_f[r];
-    d.w[k] = s;
+    for (int r = 0; r < ne; r++) s = s + d.G[r * nv + lane] * fl[r];
+    u = s;
+    d.tmp2[lane] = s;
   }
   wsync();
-  // dual cost: per-row terms by lanes, summed in row order by lane 0
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Jr = d.J + r * nv;
+    const double* Gr = d.G + r * nv;
     double jw = 0.0;
-    for (int k = 0; k < nv; k++) jw = jw + Jr[k] * d.w[k];
-    d.scratch[r] = d.efc_f[r] * ((0.5 * (jw + d.efc_R[r] * d.efc_f[r])) + d.efc_b[r]);
+    for (int k = 0; k < nv; k++) jw = jw + Gr[k] * d.tmp2[k];
+    terms[r] = fl[r] * ((0.5 * (jw + d.efc_R[r] * fl[r])) + d.efc_b[r]);
   }
   wsync();
   double cw = 0.0;
-  for (int r = 0; r < ne; r++) cw = cw + d.scratch[r];
+  for (int r = 0; r < ne; r++) cw = cw + terms[r];
+  fr0 = (lane < ne) ? fl[lane] : 0.0;
+  fr1 = (lane + WAVE < ne) ? fl[lane + WAVE] : 0.0;
   if (!(cw < 0.0)) {
-    for (int r = lane; r < ne; r += WAVE) d.efc_f[r] = 0.0;
-    for (int k = lane; k < nv; k += WAVE) d.w[k] = 0.0;
+    fr0 = 0.0; fr1 = 0.0; u = 0.0;
   }
-  wsync();
   int it;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
     double improvement = 0.0;
     for (int r = 0; r < ne;) {
-      int t = d.efc_type[r];
-      if (t != MGS_EFC_CONTACT || d.efc_dim[r] == 1) {
-        const double* Jr = d.J + r * nv;
-        double leaf = (lane < nv) ? Jr[lane] * d.w[lane] : 0.0;
-        double jw = tree_sum(leaf, P);
-        double res = (jw + d.efc_R[r] * d.efc_f[r]) + d.efc_b[r];
-        double AR = d.efc_A[r] + d.efc_R[r];
-        double fo = d.efc_f[r];
-        double fnew[1] = {fo - res / AR};
-        if (t != MGS_EFC_EQUALITY) project_block(d, r, fnew);
+      int t = uni(d.efc_type[r]);
+      int dim = uni(d.efc_dim[r]);
+      if (t != MGS_EFC_CONTACT || dim == 1) {
+        double g = (lane < nv) ? d.G[r * nv + lane] : 0.0;
+        double jw = tree_sum(g * u, P);
+        double fo = getf(fr0, fr1, r);
+        double res = (jw + d.efc_R[r] * fo) + d.efc_b[r];
+        double AR = d.efc_AR[r];
+        double fnew[1] = {fo - res * d.efc_ARinv[r]};
+        if (t != MGS_EFC_EQUALITY) project_scalar(t, d.efc_floss[r], fnew);
         double delta = fnew[0] - fo;
         improvement = improvement - delta * (0.5 * AR * delta + res);
         if (delta != 0.0) {
-          const double* Kr = d.K + r * nv;
-          if (lane < nv) d.w[lane] = d.w[lane] + Kr[lane] * delta;
-          wsync();
-          if (lane == 0) d.efc_f[r] = fnew[0];
-          wsync();
+          double s = u + g * delta;
+          if (lane < nv) u = s;
+          setf(fr0, fr1, r, fnew[0], lane);
         }
         r += 1;
+      } else if (dim == 3) {
+        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, fr0, fr1, 0);
+        r += 3;
       } else {
-        int dim = d.efc_dim[r];
-        double res[6], old[6], nw[6], Ab[36];
-        const double* blk = d.efc_blk + 36 * r;
-        for (int i = 0; i < dim; i++) {
-          const double* Ji = d.J + (r + i) * nv;
-          double leaf = (lane < nv) ? Ji[lane] * d.w[lane] : 0.0;
-          double jw = tree_sum(leaf, P);
-          res[i] = (jw + d.efc_R[r + i] * d.efc_f[r + i]) + d.efc_b[r + i];
-          old[i] = d.efc_f[r + i];
-          for (int j = 0; j < dim; j++) Ab[i * dim + j] = blk[i * dim + j];
-          Ab[i * dim + i] = Ab[i * dim + i] + d.efc_R[r + i];
-        }
-        double fn = old[0] - res[0] / Ab[0];
-        if (fn < 0.0) fn = 0.0;
-        double dn = fn - old[0];
-        nw[0] = fn;
-        if (fn == 0.0) {
-          for (int j = 1; j < dim; j++) nw[j] = 0.0;
-        } else {
-          int nf = dim - 1;
-          double Ac[25], bq[5];
-          for (int i = 0; i < nf; i++) {
-            double v = res[1 + i] + Ab[(1 + i) * dim] * dn;
-            double s = v;
-            for (int j = 0; j < nf; j++) {
-              Ac[i * nf + j] = Ab[(1 + i) * dim + 1 + j];
-              s = s - Ac[i * nf + j] * old[1 + j];
-            }
-            bq[i] = s;
-          }
-          qcqp(nf, Ac, bq, d.efc_mu + 5 * r, fn, nw + 1);
-        }
-        double del[6];
-        for (int i = 0; i < dim; i++) del[i] = nw[i] - old[i];
-        double dc = 0.0;
-        for (int i = 0; i < dim; i++) {
-          double ad = 0.0;
-          for (int j = 0; j < dim; j++) ad = ad + Ab[i * dim + j] * del[j];
-          dc = dc + del[i] * (0.5 * ad + res[i]);
-        }
-        improvement = improvement - dc;
-        if (lane < nv) {
-          double s = d.w[lane];
-          for (int i = 0; i < dim; i++) s = s + d.K[(r + i) * nv + lane] * del[i];
-          d.w[lane] = s;
-        }
-        wsync();
-        if (lane == 0)
-          for (int i = 0; i < dim; i++) d.efc_f[r + i] = nw[i];
-        wsync();
-        r += dim;
+        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, fr0, fr1, 0);
+        r += 4;
       }
     }
     if (improvement * scale < md.m.tolerance) { it++; break; }
   }
   if (lane == 0) d.ITERS += it;
-  // noslip
+}
+
+// noslip post-pass (both solvers): friction dims only, unregularised, normals fixed
+DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
+  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
+  int P = next_pow2(nv);
   for (int ns = 0; ns < md.m.noslip_iterations && ne > 0; ns++) {
     double improvement = 0.0;
     for (int r = 0; r < ne;) {
-      int t = d.efc_type[r];
+      int t = uni(d.efc_type[r]);
+      int dim = uni(d.efc_dim[r]);
       if (t == MGS_EFC_FRICTION) {
-        const double* Jr = d.J + r * nv;
-        double leaf = (lane < nv) ? Jr[lane] * d.w[lane] : 0.0;
-        double res = tree_sum(leaf, P) + d.efc_b[r];
-        double fo = d.efc_f[r];
-        double fnew[1] = {fo - res / d.efc_A[r]};
-        project_block(d, r, fnew);
+        double g = (lane < nv) ? d.G[r * nv + lane] : 0.0;
+        double res = tree_sum(g * u, P) + d.efc_b[r];
+        double fo = getf(fr0, fr1, r);
+        double fnew[1] = {fo - res * d.efc_Ainv[r]};
+        project_scalar(t, d.efc_floss[r], fnew);
         double delta = fnew[0] - fo;
         improvement = improvement - delta * (0.5 * d.efc_A[r] * delta + res);
         if (delta != 0.0) {
-          const double* Kr = d.K + r * nv;
-          if (lane < nv) d.w[lane] = d.w[lane] + Kr[lane] * delta;
-          wsync();
-          if (lane == 0) d.efc_f[r] = fnew[0];
-          wsync();
+          double s = u + g * delta;
+          if (lane < nv) u = s;
+          setf(fr0, fr1, r, fnew[0], lane);
         }
         r += 1;
-      } else if (t == MGS_EFC_CONTACT && d.efc_dim[r] > 1) {
-        int dim = d.efc_dim[r];
-        int nf = dim - 1;
-        const double* blk = d.efc_blk + 36 * r;
-        double res[5], old[5], Ac[25], bq[5], nw[5], del[5];
-        for (int i = 0; i < nf; i++) {
-          const double* Ji = d.J + (r + 1 + i) * nv;
-          double leaf = (lane < nv) ? Ji[lane] * d.w[lane] : 0.0;
-          res[i] = tree_sum(leaf, P) + d.efc_b[r + 1 + i];
-          old[i] = d.efc_f[r + 1 + i];
-        }
-        for (int i = 0; i < nf; i++) {
-          double s = res[i];
-          for (int j = 0; j < nf; j++) {
-            Ac[i * nf + j] = blk[(1 + i) * dim + 1 + j];
-            s = s - Ac[i * nf + j] * old[j];
-          }
-          bq[i] = s;
-        }
-        if (d.efc_f[r] > 0.0) qcqp(nf, Ac, bq, d.efc_mu + 5 * r, d.efc_f[r], nw);
-        else for (int i = 0; i < nf; i++) nw[i] = 0.0;
-        for (int i = 0; i < nf; i++) del[i] = nw[i] - old[i];
-        double dc = 0.0;
-        for (int i = 0; i < nf; i++) {
-          double ad = 0.0;
-          for (int j = 0; j < nf; j++) ad = ad + Ac[i * nf + j] * del[j];
-          dc = dc + del[i] * (0.5 * ad + res[i]);
-        }
-        improvement = improvement - dc;
-        if (lane < nv) {
-          double s = d.w[lane];
-          for (int i = 0; i < nf; i++) s = s + d.K[(r + 1 + i) * nv + lane] * del[i];
-          d.w[lane] = s;
-        }
-        wsync();
-        if (lane == 0)
-          for (int i = 0; i < nf; i++) d.efc_f[r + 1 + i] = nw[i];
-        wsync();
-        r += dim;
+      } else if (t == MGS_EFC_CONTACT && dim == 3) {
+        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, fr0, fr1, 1);
+        r += 3;
+      } else if (t == MGS_EFC_CONTACT && dim == 4) {
+        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, fr0, fr1, 1);
+        r += 4;
       } else {
-        r += (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
+        r += (t == MGS_EFC_CONTACT) ? dim : 1;
       }
     }
     if (improvement * scale < md.m.noslip_tolerance) break;
   }
+}
+
+DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
+  int nv = md.m.nv, lane = lane_id();
+  // qacc = qacc_smooth + L^-T D^-1/2 u ; qfrc_constraint = L D^1/2 u   (lane 0)
+  if (lane < nv) d.tmp2[lane] = u;
   wsync();
-  for (int k = lane; k < nv; k += WAVE) {
-    double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d.J[r * nv + k] * d.efc_f[r];
-    d.qfrc_constraint[k] = s;
-    d.qacc[k] = d.qacc_smooth[k] + d.w[k];
+  if (lane == 0) {
+    double* z = d.tmp;
+    for (int i = nv - 1; i >= 0; i--) {
+      double s = d.tmp2[i] * d.isD[i];
+      for (int k = i + 1; k < nv; k++) s = s - d.M[k * nv + i] * z[k];
+      z[i] = s;
+    }
+    double* t = d.scratch;
+    for (int i = 0; i < nv; i++) t[i] = d.tmp2[i] * d.sD[i];
+    for (int i = 0; i < nv; i++) {
+      double s = t[i];
+      for (int k = 0; k < i; k++) s = s + d.M[i * nv + k] * t[k];
+      d.qfrc_constraint[i] = s;
+      d.qacc[i] = d.qacc_smooth[i] + z[i];
+    }
   }
   wsync();
 }
 
+
 // ---------------------------------------------------------------------------
-__device__ void forward(const Mdl& md, Dat& d, int full) {
+// Newton solver on the primal (MuJoCo mj_solNewton restated; oracle
+// solve_newton() is the arithmetic contract).  Whitened coordinates
+// w = D^1/2 L^T qacc; Gauss cost 1/2|w - w0|^2; row violations jar = G w - aref.
+// Lanes over rows for violations / row costs (block leaders evaluate a whole
+// contact block), lanes over dofs for gradients, lanes over (i, j) for the
+// Hessian, columns of the LDL in parallel; scalar line search replicated.
+#define ST_OFF 0
+#define ST_QUAD 1
+#define ST_CONE 2
+#define ST_SAT 3
+
+// evaluate the block led by row r at violations jr[] (registers, dim <= 4):
+// forces f[], zone, cone Hessian hb[a*4+b] (if want_hb); returns cost
+DEVI double row_eval(const Dat& d, int r, int t, int dim, const double* jr, double* f, int& st, double* hb,
+                     bool want_hb) {
+  if (t == MGS_EFC_EQUALITY) {
+    double Dr = d.efc_Dr[r];
+    f[0] = -jr[0] * Dr;
+    st = ST_QUAD;
+    return ((0.5 * Dr) * jr[0]) * jr[0];
+  }
+  if (t == MGS_EFC_LIMIT || (t == MGS_EFC_CONTACT && dim == 1)) {
+    double Dr = d.efc_Dr[r];
+    if (jr[0] < 0.0) {
+      f[0] = -jr[0] * Dr;
+      st = ST_QUAD;
+      return ((0.5 * Dr) * jr[0]) * jr[0];
+    }
+    f[0] = 0.0;
+    st = ST_OFF;
+    return 0.0;
+  }
+  if (t == MGS_EFC_FRICTION) {
+    double isr = d.efc_isR[r];
+    double z = -jr[0] * isr;
+    double lim = d.efc_floss[r] * d.efc_sqR[r];
+    double y = z;
+    st = ST_QUAD;
+    if (z > lim) { y = lim; st = ST_SAT; }
+    else if (z < -lim) { y = -lim; st = ST_SAT; }
+    f[0] = y * isr;
+    return y * z - 0.5 * (y * y);
+  }
+  double mup = d.efc_mup[r];
+  double z[4], y[4], isr[4];
+#pragma unroll
+  for (int a = 0; a < 4; a++) {
+    isr[a] = (a < dim) ? d.efc_isR[r + a] : 0.0;
+    z[a] = (a < dim) ? -jr[a] * isr[a] : 0.0;
+  }
+  double t2 = 0.0;
+#pragma unroll
+  for (int a = 1; a < 4; a++)
+    if (a < dim) t2 = t2 + z[a] * z[a];
+  double tn = sqrt(t2);
+  double yn = 0.0;
+  if (tn <= mup * z[0]) {
+    st = ST_QUAD;
+#pragma unroll
+    for (int a = 0; a < 4; a++) y[a] = z[a];
+  } else if (mup * tn <= -z[0]) {
+    st = ST_OFF;
+#pragma unroll
+    for (int a = 0; a < 4; a++) y[a] = 0.0;
+  } else {
+    st = ST_CONE;
+    yn = (z[0] + mup * tn) / (1.0 + mup * mup);
+    y[0] = yn;
+    double sc = (mup * yn) / tn;
+#pragma unroll
+    for (int a = 1; a < 4; a++) y[a] = sc * z[a];
+  }
+  double c = 0.0;
+#pragma unroll
+  for (int a = 0; a < 4; a++) {
+    if (a < dim) {
+      f[a] = y[a] * isr[a];
+      c = c + y[a] * y[a];
+    }
+  }
+  if (want_hb && st == ST_CONE) {
+    double k1 = 1.0 / (1.0 + mup * mup);
+    double k2 = (mup * yn) / tn;
+    double v[4], e[4];
+    v[0] = 1.0;
+    e[0] = 0.0;
+#pragma unroll
+    for (int a = 1; a < 4; a++) { e[a] = z[a] / tn; v[a] = mup * e[a]; }
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        double Pm = (k1 * v[a]) * v[b];
+        if (a >= 1 && b >= 1) Pm = Pm + k2 * ((a == b ? 1.0 : 0.0) - e[a] * e[b]);
+        hb[a * 4 + b] = (isr[a] * isr[b]) * Pm;
+      }
+  }
+  return 0.5 * c;
+}
+
+// sum over rows in the oracle's tree_rows order: leaf l = v[l] + v[l + 64]
+DEVI double tree_rows(double v0, double v1, int ne) {
+  int n = ne < WAVE ? ne : WAVE;
+  if (n <= 0) return 0.0;
+  int lane = lane_id();
+  double leaf = (lane + WAVE < ne) ? v0 + v1 : v0;
+  if (lane >= n) leaf = 0.0;
+  return tree_sum(leaf, next_pow2(n));
+}
+
+// jar = G w - aref; forces, zones, cone Hessians into LDS; returns total cost
+DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P) {
+  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
+  double q = (lane < nv) ? w[lane] - d.nw0[lane] : 0.0;
+  double gauss = 0.5 * tree_sum(q * q, P);
+  for (int r = lane; r < ne; r += WAVE) {
+    const double* Gr = d.G + r * nv;
+    double s = 0.0;
+    for (int k = 0; k < nv; k++) s = s + Gr[k] * w[k];
+    d.efc_jar[r] = s - d.efc_aref[r];
+  }
+  wsync();
+  double cr[2] = {0.0, 0.0};
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    int r = lane + h * WAVE;
+    if (r < ne && d.efc_lead[r]) {
+      int t = d.efc_type[r];
+      int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
+      double jr[4], f[4], hb[16];
+      int st = ST_OFF;
+#pragma unroll
+      for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
+      cr[h] = row_eval(d, r, t, dim, jr, f, st, hb, true);
+#pragma unroll
+      for (int a = 0; a < 4; a++)
+        if (a < dim) { d.efc_f[r + a] = f[a]; d.efc_state[r + a] = st; }
+      if (st == ST_CONE) {
+        double* o = d.con_hb + 16 * d.efc_con[r];
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (a < dim && b < dim) o[a * dim + b] = hb[a * 4 + b];
+      }
+    }
+  }
+  double tot = gauss + tree_rows(cr[0], cr[1], ne);
+  wsync();
+  return tot;
+}
+
+// g = (w - w0) - G^T f   (lanes over dofs, rows summed in order)
+DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
+  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
+  if (lane < nv) {
+    double s = 0.0;
+    for (int r = 0; r < ne; r++) s = s + d.G[r * nv + lane] * d.efc_f[r];
+    d.ng[lane] = (w[lane] - d.nw0[lane]) - s;
+  }
+  wsync();
+}
+
+// cost derivatives along the search direction at step alpha
+DEVI void ls_eval(const Dat& d, int ne, double alpha, double A1, double A2, double* d1, double* d2) {
+  int lane = lane_id();
+  double c1[2] = {0.0, 0.0}, c2[2] = {0.0, 0.0};
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    int r = lane + h * WAVE;
+    if (r < ne && d.efc_lead[r]) {
+      int t = d.efc_type[r];
+      int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
+      double jr[4], jv[4], f[4], hb[16];
+      int st = ST_OFF;
+#pragma unroll
+      for (int a = 0; a < 4; a++) {
+        jv[a] = (a < dim) ? d.efc_jv[r + a] : 0.0;
+        jr[a] = (a < dim) ? d.efc_jar[r + a] + alpha * jv[a] : 0.0;
+      }
+      row_eval(d, r, t, dim, jr, f, st, hb, true);
+      double s1 = 0.0, s2 = 0.0;
+      if (dim == 1) {
+        s1 = -f[0] * jv[0];
+        if (st == ST_QUAD) s2 = (jv[0] * d.efc_Dr[r]) * jv[0];
+      } else {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+          if (a < dim) s1 = s1 - f[a] * jv[a];
+        if (st == ST_QUAD) {
+#pragma unroll
+          for (int a = 0; a < 4; a++)
+            if (a < dim) s2 = s2 + (jv[a] * d.efc_Dr[r + a]) * jv[a];
+        } else if (st == ST_CONE) {
+#pragma unroll
+          for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+              if (a < dim && b < dim) s2 = s2 + (jv[a] * hb[a * 4 + b]) * jv[b];
+        }
+      }
+      c1[h] = s1;
+      c2[h] = s2;
+    }
+  }
+  *d1 = (A1 + alpha * A2) + tree_rows(c1[0], c1[1], ne);
+  *d2 = A2 + tree_rows(c2[0], c2[1], ne);
+}
+
+DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
+  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
+  int P = next_pow2(nv);
+  for (int r = lane; r < ne; r += WAVE) {
+    double sq = sqrt(d.efc_R[r]);
+    d.efc_sqR[r] = sq;
+    d.efc_isR[r] = 1.0 / sq;
+    d.efc_Dr[r] = 1.0 / d.efc_R[r];
+    if (d.efc_type[r] == MGS_EFC_CONTACT && d.efc_lead[r] && d.efc_dim[r] > 1)
+      d.efc_mup[r] = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
+  }
+  // w0 = W(qacc_smooth), w = W(qacc_ws)   (lane i: s_i = a_i + sum_{k>i} L_ki a_k)
+  if (lane < nv) {
+    double s = d.qacc_smooth[lane], s2 = d.qacc_ws[lane];
+    for (int k = lane + 1; k < nv; k++) s = s + d.M[k * nv + lane] * d.qacc_smooth[k];
+    for (int k = lane + 1; k < nv; k++) s2 = s2 + d.M[k * nv + lane] * d.qacc_ws[k];
+    d.nw0[lane] = s * d.sD[lane];
+    d.nw[lane] = s2 * d.sD[lane];
+  }
+  wsync();
+  double C = 0.0;
+  if (ne > 0) {
+    double cws = newton_eval(md, d, d.nw, P);
+    double c0 = newton_eval(md, d, d.nw0, P);
+    if (cws < c0) {
+      C = newton_eval(md, d, d.nw, P);
+    } else {
+      if (lane < nv) d.nw[lane] = d.nw0[lane];
+      C = c0;
+      wsync();
+    }
+  } else {
+    if (lane < nv) d.nw[lane] = d.nw0[lane];
+    wsync();
+  }
+  newton_grad(md, d, d.nw);
+  int npair = (nv * (nv + 1)) / 2;
+  int it;
+  for (it = 0; it < md.m.iterations && ne > 0; it++) {
+    // Hessian I + G' h G: lanes over lower-triangle entries, blocks in row order
+    for (int e = lane; e < npair; e += WAVE) {
+      int i = 0, j = e;
+      while (j > i) { j -= i + 1; i++; }
+      double s = 0.0;
+      for (int r = 0; r < ne;) {
+        int t = uni(d.efc_type[r]);
+        int dim = (t == MGS_EFC_CONTACT) ? uni(d.efc_dim[r]) : 1;
+        int st = uni(d.efc_state[r]);
+        if (dim > 1 && st == ST_CONE) {
+          const double* hb = d.con_hb + 16 * uni(d.efc_con[r]);
+          for (int a = 0; a < dim; a++)
+            for (int b = 0; b < dim; b++)
+              s = s + (d.G[(r + a) * nv + i] * hb[a * dim + b]) * d.G[(r + b) * nv + j];
+        } else if (st == ST_QUAD) {
+          for (int a = 0; a < dim; a++)
+            s = s + (d.G[(r + a) * nv + i] * d.efc_Dr[r + a]) * d.G[(r + a) * nv + j];
+        }
+        r += dim;
+      }
+      double hv = (i == j ? 1.0 : 0.0) + s;
+      d.nH[i * nv + j] = hv;
+      d.nH[j * nv + i] = hv;
+    }
+    wsync();
+    ldl_factor(nv, d.nH, d.nH, d.tmp, d.tmp2);
+    if (lane == 0) ldl_solve(nv, d.nH, d.tmp2, d.ng, d.ndir, d.scratch);
+    wsync();
+    if (lane < nv) d.ndir[lane] = -d.ndir[lane];
+    wsync();
+    for (int r = lane; r < ne; r += WAVE) {
+      const double* Gr = d.G + r * nv;
+      double s = 0.0;
+      for (int k = 0; k < nv; k++) s = s + Gr[k] * d.ndir[k];
+      d.efc_jv[r] = s;
+    }
+    wsync();
+    double dl = (lane < nv) ? d.ndir[lane] : 0.0;
+    double q = (lane < nv) ? d.nw[lane] - d.nw0[lane] : 0.0;
+    double A1 = tree_sum(q * dl, P);
+    double A2 = tree_sum(dl * dl, P);
+    double p0, q0, alpha = 0.0;
+    ls_eval(d, ne, 0.0, A1, A2, &p0, &q0);
+    if (p0 < 0.0) {
+      double lo = 0.0, hi = 0.0;
+      int hi_ok = 0;
+      alpha = -p0 / q0;
+      for (int ls = 0; ls < md.m.ls_iterations; ls++) {
+        double pp, qq;
+        ls_eval(d, ne, alpha, A1, A2, &pp, &qq);
+        if (fabs(pp) < md.m.ls_tolerance * (-p0)) break;
+        if (pp < 0.0) lo = alpha;
+        else { hi = alpha; hi_ok = 1; }
+        double an = alpha - pp / qq;
+        if (!(an > lo) || (hi_ok && !(an < hi))) an = hi_ok ? 0.5 * (lo + hi) : 2.0 * alpha;
+        alpha = an;
+      }
+    }
+    if (!(alpha > 0.0)) { it++; break; }
+    if (lane < nv) d.nw[lane] = d.nw[lane] + alpha * dl;
+    wsync();
+    double Cn = newton_eval(md, d, d.nw, P);
+    newton_grad(md, d, d.nw);
+    double improvement = scale * (C - Cn);
+    C = Cn;
+    double gl = (lane < nv) ? d.ng[lane] : 0.0;
+    double gn = scale * sqrt(tree_sum(gl * gl, P));
+    if (improvement < md.m.tolerance || gn < md.m.tolerance) { it++; break; }
+  }
+  if (lane == 0) d.ITERS += it;
+  // forces to registers, u = G^T f
+  fr0 = (lane < ne) ? d.efc_f[lane] : 0.0;
+  fr1 = (lane + WAVE < ne) ? d.efc_f[lane + WAVE] : 0.0;
+  u = 0.0;
+  if (lane < nv) {
+    double s = 0.0;
+    for (int r = 0; r < ne; r++) s = s + d.G[r * nv + lane] * d.efc_f[r];
+    u = s;
+  }
+}
+
+DEVI void solve(const Mdl& md, Dat& d) {
+  int nv = md.m.nv;
+  double meaninertia = 0.0;
+  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d.M[k * nv + k];
+  meaninertia = meaninertia / (double)nv;
+  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
+  double fr0, fr1, u;
+  if (md.m.solver == 0) solve_pgs(md, d, scale, fr0, fr1, u);
+  else solve_newton(md, d, scale, fr0, fr1, u);
+  noslip(md, d, scale, fr0, fr1, u);
+  finalize_solution(md, d, u);
+}
+
+// ---------------------------------------------------------------------------
+DEVI void forward(const Mdl& md, Dat& d, int full) {
   int nv = md.m.nv, lane = lane_id();
   if (lane == 0) {
     kinematics(md, d);
@@ -1649,22 +2139,29 @@ __device__ void forward(const Mdl& md, Dat& d, int full) {
   collision(md, d);
   if (!full) return;
   crb(md, d);
-  ldl_factor(nv, d.M, d.L, d.Dv, d.Dinv);
+  ldl_factor(nv, d.M, d.M, d.Dv, d.Dinv);
+  for (int k = lane; k < nv; k += WAVE) {
+    double sd = sqrt(d.Dv[k]);
+    d.sD[k] = sd;
+    d.isD[k] = 1.0 / sd;
+  }
   if (lane == 0) {
     actuation(md, d);
     passive(md, d);
     rne(md, d);
     for (int k = 0; k < nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
-    ldl_solve(nv, d.L, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
+    ldl_solve(nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth, d.tmp);
   }
   wsync();
   make_constraints(md, d);
-  solve_pgs(md, d);
+  solve(md, d);
 }
 
-__device__ void integrate(const Mdl& md, Dat& d) {
+DEVI void integrate(const Mdl& md, Dat& d) {
   int nv = md.m.nv, lane = lane_id();
   double dt = md.m.timestep;
+  // recompute M (it was factored in place), then MI = M - dt*qDeriv
+  crb(md, d);
   if (lane == 0) {
     for (int i = 0; i < nv * nv; i++) d.qDeriv[i] = 0.0;
     const double* damp = DA(md, dof_damping);
@@ -1688,14 +2185,14 @@ __device__ void integrate(const Mdl& md, Dat& d) {
     }
   }
   wsync();
-  // MI = M - dt*qDeriv (in place into M; M no longer needed this step)
   for (int i = lane; i < nv * nv; i += WAVE) d.M[i] = d.M[i] - dt * d.qDeriv[i];
   wsync();
-  ldl_factor(nv, d.M, d.L, d.Dv, d.Dinv);
+  ldl_factor(nv, d.M, d.M, d.Dv, d.Dinv);
   if (lane == 0) {
-    double rhs[64], qa[64];
+    double* rhs = d.tmp2;
+    double* qa = d.scratch;
     for (int k = 0; k < nv; k++) rhs[k] = d.qfrc_smooth[k] + d.qfrc_constraint[k];
-    ldl_solve(nv, d.L, d.Dinv, rhs, qa);
+    ldl_solve(nv, d.M, d.Dinv, rhs, qa, d.tmp);
     for (int k = 0; k < nv; k++) d.qvel[k] = d.qvel[k] + dt * qa[k];
     const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
     for (int j = 0; j < md.m.njnt; j++) {
@@ -1721,9 +2218,9 @@ __device__ void integrate(const Mdl& md, Dat& d) {
   wsync();
 }
 
-__device__ int obj_contact(const Mdl& md, const Dat& d) {
+DEVI int obj_contact(const Mdl& md, const Dat& d) {
   const int32_t* side = IA(md, geom_side);
-  int ncon = d.NCON;
+  int ncon = uni(d.NCON);
   for (int c = 0; c < ncon; c++) {
     int s1 = side[d.con_g1[c]], s2 = side[d.con_g2[c]];
     if ((s1 < 0 && s2 > 0) || (s1 > 0 && s2 < 0)) return 1;
@@ -1731,7 +2228,7 @@ __device__ int obj_contact(const Mdl& md, const Dat& d) {
   return 0;
 }
 
-__device__ void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mpos, const double* mquat) {
+DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mpos, const double* mquat) {
   int lane = lane_id();
   for (int k = lane; k < md.m.nq; k += WAVE) d.qpos[k] = qpos_init[k];
   for (int k = lane; k < md.m.nv; k += WAVE) { d.qvel[k] = 0.0; d.qacc_ws[k] = 0.0; }
@@ -1746,7 +2243,7 @@ __device__ void reset(const Mdl& md, Dat& d, const double* qpos_init, const doub
 }
 
 // ---------------------------------------------------------------------------
-// kernels
+// kernels: one 64-lane workgroup per candidate
 extern "C" __global__ void __launch_bounds__(64)
 mgs_collision_kernel(Mdl md, Lay lay, int n, const double* __restrict__ qpos_init,
                      const double* __restrict__ mocap_pos, const double* __restrict__ mocap_quat, int predicate,
@@ -1780,6 +2277,7 @@ mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __rest
   const double* pt = phase_target + (size_t)i * np * 3;
   reset(md, d, qpos_init + (size_t)i * md.m.nq, ps, mocap_quat + 4 * i);
   int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0;
+  PROF_DECL
   for (int p = 0; p < np && ok; p++) {
     if (lane == 0)
       for (int u = 0; u < md.m.nu; u++) d.ctrl[u] = sc.ctrl[p * 32 + u];
@@ -1789,10 +2287,30 @@ mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __rest
       if (lane == 0)
         for (int k = 0; k < 3; k++) d.mocap_pos[k] = ps[3 * p + k] + (pt[3 * p + k] - ps[3 * p + k]) * frac;
       wsync();
+#ifdef MGS_PROFILE
+      PROF(0);
+      if (lane == 0) { kinematics(md, d); com_pos(md, d); }
+      wsync(); PROF(1);
+      collision(md, d); PROF(2);
+      crb(md, d);
+      ldl_factor(md.m.nv, d.M, d.M, d.Dv, d.Dinv);
+      for (int k = lane; k < md.m.nv; k += WAVE) { double sd = sqrt(d.Dv[k]); d.sD[k] = sd; d.isD[k] = 1.0 / sd; }
+      PROF(3);
+      if (lane == 0) {
+        actuation(md, d); passive(md, d); rne(md, d);
+        for (int k = 0; k < md.m.nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
+        ldl_solve(md.m.nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth, d.tmp);
+      }
+      wsync(); PROF(4);
+      make_constraints(md, d); PROF(5);
+      solve(md, d); PROF(6);
+      integrate(md, d); PROF(7);
+#else
       forward(md, d, 1);
       integrate(md, d);
-      if (d.NCON > maxcon) maxcon = d.NCON;
-      if (d.NEFC > maxefc) maxefc = d.NEFC;
+#endif
+      if (uni(d.NCON) > maxcon) maxcon = uni(d.NCON);
+      if (uni(d.NEFC) > maxefc) maxefc = uni(d.NEFC);
       int ce = sc.check_every[p];
       if (ce > 0 && t > 0 && (t % ce) == 0 && !obj_contact(md, d)) { ok = 0; fstep = gstep; }
       gstep++;
@@ -1807,6 +2325,7 @@ mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __rest
     }
   }
   if (obj_qpos && sc.obj_qposadr >= 0 && lane < 7) obj_qpos[7 * i + lane] = d.qpos[sc.obj_qposadr + lane];
+  PROF_FLUSH
 }
 
 // device-side arithmetic probe (tests): sqrt, division, sincos against the oracle
@@ -1819,4 +2338,14 @@ extern "C" __global__ void mgs_arith_probe_kernel(const double* x, const double*
   out[4 * i + 1] = x[i] / y[i];
   out[4 * i + 2] = s;
   out[4 * i + 3] = c;
+}
+
+// tree-reduction probe (tests): out[b] = tree_sum over lanes of a[b*64+l]*c[b*64+l] with P = nextpow2(n)
+extern "C" __global__ void __launch_bounds__(64) mgs_tree_probe_kernel(const double* a, const double* c, int n,
+                                                                         double* out) {
+  int l = lane_id();
+  int b = blockIdx.x;
+  double leaf = (l < n) ? a[b * 64 + l] * c[b * 64 + l] : 0.0;
+  double s = tree_sum(leaf, next_pow2(n));
+  if (l == 0) out[b] = s;
 }

@@ -44,6 +44,8 @@ def load_library():
     L.mgs_last_kernel_ms.argtypes = [vp]
     L.mgs_last_kernel_ms.restype = ctypes.c_double
     L.mgs_arith_probe.argtypes = [P(c_d), P(c_d), ctypes.c_int, P(c_d)]
+    L.mgs_tree_probe.argtypes = [P(c_d), P(c_d), ctypes.c_int, ctypes.c_int, P(c_d)]
+    L.mgs_lds_bytes.argtypes = [vp]
     L.mgs_device_count.restype = ctypes.c_int
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
         raise EngineError("libmgs_gpu.so ABI version mismatch with include/mgs_gpu.h")
@@ -139,8 +141,22 @@ class Engine:
         _check(self.lib.mgs_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps, d_pt,
                                            d_label, d_fail, d_objq, d_stats, stream), "mgs_rollout_device")
 
+    def lds_bytes(self):
+        return self.lib.mgs_lds_bytes(self._model)
+
     def last_kernel_ms(self):
         return self.lib.mgs_last_kernel_ms(self._batch)
+
+
+def tree_probe(a, c, n):
+    """Device pairwise-tree reduction of a*c over the first n of 64 lanes, per row."""
+    L = load_library()
+    a = np.ascontiguousarray(a, np.float64).reshape(-1, 64)
+    c = np.ascontiguousarray(c, np.float64).reshape(-1, 64)
+    out = np.zeros(len(a))
+    _check(L.mgs_tree_probe(ptr(a, ctypes.c_double), ptr(c, ctypes.c_double), n, len(a), ptr(out, ctypes.c_double)),
+           "mgs_tree_probe")
+    return out
 
 
 def arith_probe(x, y):

@@ -220,7 +220,8 @@ class Compiler:
         self.assets = dict(assets or {})
         self.options = dict(timestep=0.002, impratio=1.0, tolerance=1e-8, iterations=100,
                             noslip_iterations=0, noslip_tolerance=1e-6, gravity=np.array([0, 0, -9.81]),
-                            cone="pyramidal", integrator="Euler", mpr_tolerance=1e-6)
+                            cone="pyramidal", integrator="Euler", mpr_tolerance=1e-6, solver="Newton",
+                            ls_iterations=50, ls_tolerance=0.01)
         self.compiler = dict(angle="degree", meshdir="", autolimits=True, discardvisual=False)
         self.defaults: Dict[str, dict] = {"main": {"parent": None}}
         self.meshes: Dict[str, dict] = {}
@@ -304,9 +305,9 @@ class Compiler:
     def _parse_option(self, el):
         o = self.options
         for k, v in el.attrib.items():
-            if k in ("timestep", "impratio", "tolerance", "noslip_tolerance", "mpr_tolerance"):
+            if k in ("timestep", "impratio", "tolerance", "noslip_tolerance", "mpr_tolerance", "ls_tolerance"):
                 o[k] = float(v)
-            elif k in ("iterations", "noslip_iterations"):
+            elif k in ("iterations", "noslip_iterations", "ls_iterations"):
                 o[k] = int(v)
             elif k == "gravity":
                 o[k] = _f(v, 3)
@@ -1004,7 +1005,9 @@ class CompiledModel:
             ncon_max=ncon_max, nefc_max=nefc_max,
             maxhullvert=int(self.hull_vertnum.max()) if len(self.hull_vertnum) else 0,
             iterations=int(o["iterations"]), noslip_iterations=int(o["noslip_iterations"]),
-            cone=1, integrator=2, timestep=float(o["timestep"]), impratio=float(o["impratio"]),
+            cone=1, integrator=2, solver={"PGS": 0, "CG": 2, "Newton": 2}[o.get("solver", "Newton")],
+            ls_iterations=int(o.get("ls_iterations", 50)), ls_tolerance=float(o.get("ls_tolerance", 0.01)),
+            timestep=float(o["timestep"]), impratio=float(o["impratio"]),
             tolerance=float(o["tolerance"]), noslip_tolerance=float(o["noslip_tolerance"]),
             mpr_tolerance=float(o.get("mpr_tolerance", 1e-6)),
             gravity=[float(x) for x in o["gravity"]], isize=len(ib), dsize=len(db))

@@ -73,7 +73,10 @@ typedef struct {
   /* constraints */
   int nefc;
   double *J, *K, *efc_pos, *efc_margin, *efc_vel, *efc_aref, *efc_R, *efc_A, *efc_b, *efc_f;
-  double *efc_mu, *efc_blk, *efc_floss;
+  double *efc_mu, *efc_blk, *efc_hb, *efc_floss, *efc_AR, *efc_ARinv, *efc_Ainv;
+  double *efc_Dr, *efc_sqR, *efc_isR, *efc_mup, *efc_jar, *efc_jv;
+  int* efc_state;
+  double *Dv, *sD, *isD;
   int *efc_type, *efc_dim, *efc_con;
   double *w;
   int overflow;
@@ -235,20 +238,12 @@ static Dat* dat_alloc(const Mdl* md) {
   d->ncon_max = m->ncon_max; d->nefc_max = m->nefc_max;
   int nq = m->nq, nv = m->nv, nb = m->nbody, ng = m->ngeom, nu = m->nu > 0 ? m->nu : 1;
   int nc = m->ncon_max, ne = m->nefc_max, nj = m->njnt > 0 ? m->njnt : 1;
+  /* pass 0 counts, pass 1 assigns: one list of fields, no separate size table */
+  double* base = NULL;
+  for (int pass = 0; pass < 2; pass++) {
+  double* p = base;
   size_t tot = 0;
-#define SZ(n) tot += (size_t)(n)
-  SZ(nq); SZ(nv); SZ(nv); SZ(nu); SZ(3 * m->nmocap + 3); SZ(4 * m->nmocap + 4);
-  SZ(3 * nb); SZ(4 * nb); SZ(9 * nb); SZ(3 * nb); SZ(9 * nb); SZ(3 * nj); SZ(3 * nj);
-  SZ(3 * nb); SZ(nb); SZ(10 * nb); SZ(10 * nb); SZ(6 * nv); SZ(6 * nv); SZ(6 * nb); SZ(6 * nb); SZ(6 * nb);
-  SZ(3 * ng); SZ(9 * ng);
-  SZ(nv * nv); SZ(nv * nv); SZ(nv); SZ(nv * nv); SZ(nv * nv); SZ(nv); SZ(nv * nv);
-  SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nv); SZ(nu); SZ(nu * nv); SZ(nu); SZ(nu);
-  SZ(3 * nc); SZ(9 * nc); SZ(nc);
-  SZ(ne * nv); SZ(ne * nv); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne); SZ(ne);
-  SZ(5 * ne); SZ(36 * ne); SZ(ne); SZ(nv);
-#undef SZ
-  double* p = (double*)calloc(tot, sizeof(double));
-#define TAKE(ptr, n) do { d->ptr = p; p += (n); } while (0)
+#define TAKE(ptr, n) do { d->ptr = p; if (p) p += (n); tot += (size_t)(n); } while (0)
   TAKE(qpos, nq); TAKE(qvel, nv); TAKE(qacc_ws, nv); TAKE(ctrl, nu);
   TAKE(mocap_pos, 3 * m->nmocap + 3); TAKE(mocap_quat, 4 * m->nmocap + 4);
   TAKE(xpos, 3 * nb); TAKE(xquat, 4 * nb); TAKE(xmat, 9 * nb); TAKE(xipos, 3 * nb); TAKE(ximat, 9 * nb);
@@ -264,14 +259,19 @@ static Dat* dat_alloc(const Mdl* md) {
   TAKE(con_pos, 3 * nc); TAKE(con_frame, 9 * nc); TAKE(con_dist, nc);
   TAKE(J, ne * nv); TAKE(K, ne * nv); TAKE(efc_pos, ne); TAKE(efc_margin, ne); TAKE(efc_vel, ne);
   TAKE(efc_aref, ne); TAKE(efc_R, ne); TAKE(efc_A, ne); TAKE(efc_b, ne); TAKE(efc_f, ne);
-  TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_floss, ne); TAKE(w, nv);
+  TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_hb, 36 * ne); TAKE(efc_floss, ne); TAKE(w, nv);
+  TAKE(efc_AR, ne); TAKE(efc_ARinv, ne); TAKE(efc_Ainv, ne); TAKE(Dv, nv); TAKE(sD, nv); TAKE(isD, nv);
+  TAKE(efc_Dr, ne); TAKE(efc_sqR, ne); TAKE(efc_isR, ne); TAKE(efc_mup, ne); TAKE(efc_jar, ne); TAKE(efc_jv, ne);
 #undef TAKE
+  if (pass == 0) base = (double*)calloc(tot, sizeof(double));
+  }
   d->con_pair = (int*)calloc((size_t)nc, sizeof(int));
   d->con_g1 = (int*)calloc((size_t)nc, sizeof(int));
   d->con_g2 = (int*)calloc((size_t)nc, sizeof(int));
   d->efc_type = (int*)calloc((size_t)ne, sizeof(int));
   d->efc_dim = (int*)calloc((size_t)ne, sizeof(int));
   d->efc_con = (int*)calloc((size_t)ne, sizeof(int));
+  d->efc_state = (int*)calloc((size_t)ne, sizeof(int));
   return d;
 }
 
@@ -279,7 +279,7 @@ static void dat_free(Dat* d) {
   if (!d) return;
   free(d->qpos);
   free(d->con_pair); free(d->con_g1); free(d->con_g2);
-  free(d->efc_type); free(d->efc_dim); free(d->efc_con);
+  free(d->efc_type); free(d->efc_dim); free(d->efc_con); free(d->efc_state);
   free(d);
 }
 
@@ -484,8 +484,8 @@ static void crb(const Mdl* md, Dat* d) {
 }
 
 /* dense LDL^T: A = L D L^T, L unit lower (stored strictly lower), Dinv = 1/D */
-static void ldl_factor(int n, const double* A, double* L, double* Dinv) {
-  double W[128], Dv[128];
+static void ldl_factor(int n, const double* A, double* L, double* Dinv, double* Dv) {
+  double W[128];
   for (int j = 0; j < n; j++) {
     for (int k = 0; k < j; k++) W[k] = L[j * n + k] * Dv[k];
     double dj = A[j * n + j];
@@ -1264,16 +1264,25 @@ static void make_constraints(const Mdl* md, Dat* d) {
     for (int j = 0; j < dim; j++) d->efc_mu[5 * r + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
   }
   int cr1 = d->nefc;
-  /* --- velocities, K = M^-1 J^T, diag A, impedance, aref, R */
+  /* --- per row: velocity, J.qacc_smooth, whitened row G = D^-1/2 L^-1 J^T
+   * (stored in K), diagonal A = G.G */
   int ne = d->nefc;
   for (int r = 0; r < ne; r++) {
     const double* Jr = d->J + (size_t)r * nv;
-    double v = 0.0;
+    double* Gr = d->K + (size_t)r * nv;
+    double v = 0.0, bj = 0.0;
     for (int k = 0; k < nv; k++) v = v + Jr[k] * d->qvel[k];
+    for (int k = 0; k < nv; k++) bj = bj + Jr[k] * d->qacc_smooth[k];
     d->efc_vel[r] = v;
-    ldl_solve(nv, d->L, d->Dinv, Jr, d->K + (size_t)r * nv);
+    d->efc_b[r] = bj;
+    for (int i = 0; i < nv; i++) {
+      double s = Jr[i];
+      for (int k = 0; k < i; k++) s = s - d->L[i * nv + k] * Gr[k];
+      Gr[i] = s;
+    }
+    for (int i = 0; i < nv; i++) Gr[i] = Gr[i] * d->isD[i];
     double a = 0.0;
-    for (int k = 0; k < nv; k++) a = a + Jr[k] * d->K[(size_t)r * nv + k];
+    for (int k = 0; k < nv; k++) a = a + Gr[k] * Gr[k];
     d->efc_A[r] = a;
   }
   const double *eqsr = DA(md, eq_solref), *eqsi = DA(md, eq_solimp);
@@ -1299,22 +1308,23 @@ static void make_constraints(const Mdl* md, Dat* d) {
     row_params(md, d, r, dim, psr + 2 * p, psi + 5 * p, d->efc_mu + 5 * r, 1);
     r += dim;
   }
-  /* b = J qacc_smooth - aref; contact blocks of A (+R on the diagonal) */
   for (int r = 0; r < ne; r++) {
-    const double* Jr = d->J + (size_t)r * nv;
-    double v = 0.0;
-    for (int k = 0; k < nv; k++) v = v + Jr[k] * d->qacc_smooth[k];
-    d->efc_b[r] = v - d->efc_aref[r];
+    d->efc_b[r] = d->efc_b[r] - d->efc_aref[r];
+    double ar = d->efc_A[r] + d->efc_R[r];
+    d->efc_AR[r] = ar;
+    d->efc_ARinv[r] = 1.0 / ar;
+    d->efc_Ainv[r] = 1.0 / d->efc_A[r];
   }
+  /* contact blocks of A = G G^T */
   for (int r = cr0; r < cr1;) {
     int dim = d->efc_dim[r];
     double* blk = d->efc_blk + 36 * r;
     for (int i = 0; i < dim; i++)
       for (int j = 0; j < dim; j++) {
-        const double* Ji = d->J + (size_t)(r + i) * nv;
-        const double* Kj = d->K + (size_t)(r + j) * nv;
+        const double* Gi = d->K + (size_t)(r + i) * nv;
+        const double* Gj = d->K + (size_t)(r + j) * nv;
         double a = 0.0;
-        for (int k = 0; k < nv; k++) a = a + Ji[k] * Kj[k];
+        for (int k = 0; k < nv; k++) a = a + Gi[k] * Gj[k];
         blk[i * dim + j] = a;
       }
     r += dim;
@@ -1322,84 +1332,68 @@ static void make_constraints(const Mdl* md, Dat* d) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* QCQP: minimize 0.5 x'Ax + x'b  s.t.  sum (x_j/mu_j)^2 <= r^2, n in {1,2,3,5} */
-static void qcqp(int n, const double* A, const double* b, const double* mu, double r, double* x) {
-  double As[25], bs[5], y[5], P[25];
-  for (int i = 0; i < n; i++) {
-    bs[i] = b[i] * mu[i];
-    for (int j = 0; j < n; j++) As[i * n + j] = (A[i * n + j] * mu[i]) * mu[j];
-  }
-  double la = 0.0;
-  double rr = r * r;
+/* QCQP: minimize 0.5 x'Ax + x'b  s.t.  sum (x_j/mu_j)^2 <= r^2 (n = 2, 3),
+ * Newton on the Lagrange multiplier with closed-form inverses (cf. MuJoCo's
+ * mju_QCQP2 / mju_QCQP3). */
+static void qcqp2(const double* A, const double* b, const double* mu, double r, double* x) {
+  double a11 = (A[0] * mu[0]) * mu[0], a12 = (A[1] * mu[0]) * mu[1], a22 = (A[3] * mu[1]) * mu[1];
+  double b1 = b[0] * mu[0], b2 = b[1] * mu[1];
+  double rr = r * r, la = 0.0, v1 = 0.0, v2 = 0.0;
   for (int it = 0; it < 20; it++) {
-    /* P = inverse(As + la I) via Gauss-Jordan without pivoting (SPD) */
-    double T[25];
-    for (int i = 0; i < n * n; i++) T[i] = As[i];
-    for (int i = 0; i < n; i++) T[i * n + i] = T[i * n + i] + la;
-    for (int i = 0; i < n * n; i++) P[i] = 0.0;
-    for (int i = 0; i < n; i++) P[i * n + i] = 1.0;
-    int bad = 0;
-    for (int c = 0; c < n; c++) {
-      double piv = T[c * n + c];
-      if (piv < 1e-15) { bad = 1; break; }
-      double ip = 1.0 / piv;
-      for (int j = 0; j < n; j++) { T[c * n + j] = T[c * n + j] * ip; P[c * n + j] = P[c * n + j] * ip; }
-      for (int i = 0; i < n; i++) {
-        if (i == c) continue;
-        double f = T[i * n + c];
-        if (f == 0.0) continue;
-        for (int j = 0; j < n; j++) {
-          T[i * n + j] = T[i * n + j] - f * T[c * n + j];
-          P[i * n + j] = P[i * n + j] - f * P[c * n + j];
-        }
-      }
-    }
-    if (bad) { for (int i = 0; i < n; i++) y[i] = 0.0; break; }
-    for (int i = 0; i < n; i++) {
-      double s = 0.0;
-      for (int j = 0; j < n; j++) s = s - P[i * n + j] * bs[j];
-      y[i] = s;
-    }
-    double val = 0.0;
-    for (int i = 0; i < n; i++) val = val + y[i] * y[i];
-    val = val - rr;
+    double m11 = a11 + la, m22 = a22 + la;
+    double det = m11 * m22 - a12 * a12;
+    if (det < 1e-10) { v1 = 0.0; v2 = 0.0; break; }
+    double idet = 1.0 / det;
+    double p11 = m22 * idet, p22 = m11 * idet, p12 = -a12 * idet;
+    v1 = -(p11 * b1 + p12 * b2);
+    v2 = -(p12 * b1 + p22 * b2);
+    double val = (v1 * v1 + v2 * v2) - rr;
     if (val < 1e-10) break;
-    double pv[5];
-    for (int i = 0; i < n; i++) {
-      double s = 0.0;
-      for (int j = 0; j < n; j++) s = s + P[i * n + j] * y[j];
-      pv[i] = s;
-    }
-    double deriv = 0.0;
-    for (int i = 0; i < n; i++) deriv = deriv + y[i] * pv[i];
-    deriv = -2.0 * deriv;
+    double pv1 = p11 * v1 + p12 * v2, pv2 = p12 * v1 + p22 * v2;
+    double deriv = -2.0 * (v1 * pv1 + v2 * pv2);
     double delta = -val / deriv;
     if (delta < 1e-10) break;
     la = la + delta;
   }
-  for (int i = 0; i < n; i++) x[i] = y[i] * mu[i];
+  x[0] = v1 * mu[0];
+  x[1] = v2 * mu[1];
 }
 
-/* dual cost of f: 0.5 f'(A+R)f + f'b computed from w = M^-1 J^T f */
-static double dual_cost(const Dat* d) {
-  int nv = d->nv;
-  double c = 0.0;
-  for (int r = 0; r < d->nefc; r++) {
-    const double* Jr = d->J + (size_t)r * nv;
-    double jw = 0.0;
-    for (int k = 0; k < nv; k++) jw = jw + Jr[k] * d->w[k];
-    c = c + d->efc_f[r] * ((0.5 * (jw + d->efc_R[r] * d->efc_f[r])) + d->efc_b[r]);
+static void qcqp3(const double* A, const double* b, const double* mu, double r, double* x) {
+  double a00 = (A[0] * mu[0]) * mu[0], a01 = (A[1] * mu[0]) * mu[1], a02 = (A[2] * mu[0]) * mu[2];
+  double a11 = (A[4] * mu[1]) * mu[1], a12 = (A[5] * mu[1]) * mu[2], a22 = (A[8] * mu[2]) * mu[2];
+  double b0 = b[0] * mu[0], b1 = b[1] * mu[1], b2 = b[2] * mu[2];
+  double rr = r * r, la = 0.0, v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  for (int it = 0; it < 20; it++) {
+    double m00 = a00 + la, m11 = a11 + la, m22 = a22 + la;
+    double c00 = m11 * m22 - a12 * a12, c01 = a02 * a12 - a01 * m22, c02 = a01 * a12 - a02 * m11;
+    double c11 = m00 * m22 - a02 * a02, c12 = a01 * a02 - m00 * a12, c22 = m00 * m11 - a01 * a01;
+    double det = (m00 * c00 + a01 * c01) + a02 * c02;
+    if (det < 1e-10) { v0 = 0.0; v1 = 0.0; v2 = 0.0; break; }
+    double idet = 1.0 / det;
+    double p00 = c00 * idet, p01 = c01 * idet, p02 = c02 * idet;
+    double p11 = c11 * idet, p12 = c12 * idet, p22 = c22 * idet;
+    v0 = -((p00 * b0 + p01 * b1) + p02 * b2);
+    v1 = -((p01 * b0 + p11 * b1) + p12 * b2);
+    v2 = -((p02 * b0 + p12 * b1) + p22 * b2);
+    double val = ((v0 * v0 + v1 * v1) + v2 * v2) - rr;
+    if (val < 1e-10) break;
+    double pv0 = (p00 * v0 + p01 * v1) + p02 * v2;
+    double pv1 = (p01 * v0 + p11 * v1) + p12 * v2;
+    double pv2 = (p02 * v0 + p12 * v1) + p22 * v2;
+    double deriv = -2.0 * ((v0 * pv0 + v1 * pv1) + v2 * pv2);
+    double delta = -val / deriv;
+    if (delta < 1e-10) break;
+    la = la + delta;
   }
-  return c;
+  x[0] = v0 * mu[0];
+  x[1] = v1 * mu[1];
+  x[2] = v2 * mu[2];
 }
 
-static void w_from_f(Dat* d) {
-  int nv = d->nv;
-  for (int k = 0; k < nv; k++) {
-    double s = 0.0;
-    for (int r = 0; r < d->nefc; r++) s = s + d->K[(size_t)r * nv + k] * d->efc_f[r];
-    d->w[k] = s;
-  }
+static void qcqp(int n, const double* A, const double* b, const double* mu, double r, double* x) {
+  if (n == 2) qcqp2(A, b, mu, r, x);
+  else qcqp3(A, b, mu, r, x);
 }
 
 static void project_block(const Dat* d, int r, double* f) {
@@ -1425,19 +1419,27 @@ static void project_block(const Dat* d, int r, double* f) {
   }
 }
 
-/* PGS on the dual with elliptic cones (MuJoCo mj_solPGS restated) + noslip */
-static void solve_pgs(const Mdl* md, Dat* d) {
+/* PGS on the dual with elliptic cones (MuJoCo mj_solPGS restated) in the
+ * whitened form A = G G^T, u = G^T f, followed by noslip. */
+static void solve_pgs_main(const Mdl* md, Dat* d) {
   const mgs_model_desc* m = md->m;
   int nv = m->nv, ne = d->nefc;
   double meaninertia = 0.0;
   for (int k = 0; k < nv; k++) meaninertia = meaninertia + d->M[k * nv + k];
   meaninertia = meaninertia / (double)nv;
   double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
-  /* warmstart: f from qacc_warmstart through the primal map, projected */
+  /* warmstart: f from qacc_warmstart through the primal map, projected;
+   * J_r . qacc_ws = G_r . (D^1/2 L^T qacc_ws) */
+  double hws[128];
+  for (int i = 0; i < nv; i++) {
+    double s = d->qacc_ws[i];
+    for (int k = i + 1; k < nv; k++) s = s + d->L[k * nv + i] * d->qacc_ws[k];
+    hws[i] = s * d->sD[i];
+  }
   for (int r = 0; r < ne; r++) {
-    const double* Jr = d->J + (size_t)r * nv;
+    const double* Gr = d->K + (size_t)r * nv;
     double jar = 0.0;
-    for (int k = 0; k < nv; k++) jar = jar + Jr[k] * d->qacc_ws[k];
+    for (int k = 0; k < nv; k++) jar = jar + Gr[k] * hws[k];
     jar = jar - d->efc_aref[r];
     d->efc_f[r] = -jar / d->efc_R[r];
   }
@@ -1446,8 +1448,18 @@ static void solve_pgs(const Mdl* md, Dat* d) {
     if (d->efc_type[r] != MGS_EFC_EQUALITY) project_block(d, r, d->efc_f + r);
     r += dim;
   }
-  w_from_f(d);
-  double cw = dual_cost(d);
+  for (int k = 0; k < nv; k++) {
+    double s = 0.0;
+    for (int r = 0; r < ne; r++) s = s + d->K[(size_t)r * nv + k] * d->efc_f[r];
+    d->w[k] = s;
+  }
+  double cw = 0.0;
+  for (int r = 0; r < ne; r++) {
+    const double* Gr = d->K + (size_t)r * nv;
+    double jw = 0.0;
+    for (int k = 0; k < nv; k++) jw = jw + Gr[k] * d->w[k];
+    cw = cw + d->efc_f[r] * ((0.5 * (jw + d->efc_R[r] * d->efc_f[r])) + d->efc_b[r]);
+  }
   if (!(cw < 0.0)) {
     for (int r = 0; r < ne; r++) d->efc_f[r] = 0.0;
     for (int k = 0; k < nv; k++) d->w[k] = 0.0;
@@ -1458,18 +1470,17 @@ static void solve_pgs(const Mdl* md, Dat* d) {
     for (int r = 0; r < ne;) {
       int t = d->efc_type[r];
       if (t != MGS_EFC_CONTACT || d->efc_dim[r] == 1) {
-        const double* Jr = d->J + (size_t)r * nv;
-        double res = (tree_dot(Jr, d->w, nv) + d->efc_R[r] * d->efc_f[r]) + d->efc_b[r];
-        double AR = d->efc_A[r] + d->efc_R[r];
+        const double* Gr = d->K + (size_t)r * nv;
+        double res = (tree_dot(Gr, d->w, nv) + d->efc_R[r] * d->efc_f[r]) + d->efc_b[r];
+        double AR = d->efc_AR[r];
         double fo = d->efc_f[r];
-        double fnew[1] = {fo - res / AR};
+        double fnew[1] = {fo - res * d->efc_ARinv[r]};
         if (t != MGS_EFC_EQUALITY) project_block(d, r, fnew);
         double delta = fnew[0] - fo;
         improvement = improvement - delta * (0.5 * AR * delta + res);
         if (delta != 0.0) {
           d->efc_f[r] = fnew[0];
-          const double* Kr = d->K + (size_t)r * nv;
-          for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Kr[k] * delta;
+          for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Gr[k] * delta;
         }
         r += 1;
       } else {
@@ -1477,13 +1488,13 @@ static void solve_pgs(const Mdl* md, Dat* d) {
         double res[6], old[6], nw[6], Ab[36];
         const double* blk = d->efc_blk + 36 * r;
         for (int i = 0; i < dim; i++) {
-          res[i] = (tree_dot(d->J + (size_t)(r + i) * nv, d->w, nv) + d->efc_R[r + i] * d->efc_f[r + i]) +
+          res[i] = (tree_dot(d->K + (size_t)(r + i) * nv, d->w, nv) + d->efc_R[r + i] * d->efc_f[r + i]) +
                    d->efc_b[r + i];
           old[i] = d->efc_f[r + i];
           for (int j = 0; j < dim; j++) Ab[i * dim + j] = blk[i * dim + j];
           Ab[i * dim + i] = Ab[i * dim + i] + d->efc_R[r + i];
         }
-        double fn = old[0] - res[0] / Ab[0];
+        double fn = old[0] - res[0] * d->efc_ARinv[r];
         if (fn < 0.0) fn = 0.0;
         double dn = fn - old[0];
         nw[0] = fn;
@@ -1524,23 +1535,33 @@ static void solve_pgs(const Mdl* md, Dat* d) {
     if (improvement * scale < m->tolerance) { it++; break; }
   }
   d->iters += it;
+}
+
+/* noslip (MuJoCo mj_solNoSlip restated): PGS over friction dims only,
+ * unregularized, normal forces fixed; u = G^T f must be current. */
+static void noslip(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nv = m->nv, ne = d->nefc;
+  double meaninertia = 0.0;
+  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d->M[k * nv + k];
+  meaninertia = meaninertia / (double)nv;
+  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
   /* noslip: friction dims only, unregularized, normal forces fixed */
   for (int ns = 0; ns < m->noslip_iterations && ne > 0; ns++) {
     double improvement = 0.0;
     for (int r = 0; r < ne;) {
       int t = d->efc_type[r];
       if (t == MGS_EFC_FRICTION) {
-        const double* Jr = d->J + (size_t)r * nv;
-        double res = tree_dot(Jr, d->w, nv) + d->efc_b[r];
+        const double* Gr = d->K + (size_t)r * nv;
+        double res = tree_dot(Gr, d->w, nv) + d->efc_b[r];
         double fo = d->efc_f[r];
-        double fnew[1] = {fo - res / d->efc_A[r]};
+        double fnew[1] = {fo - res * d->efc_Ainv[r]};
         project_block(d, r, fnew);
         double delta = fnew[0] - fo;
         improvement = improvement - delta * (0.5 * d->efc_A[r] * delta + res);
         if (delta != 0.0) {
           d->efc_f[r] = fnew[0];
-          const double* Kr = d->K + (size_t)r * nv;
-          for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Kr[k] * delta;
+          for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Gr[k] * delta;
         }
         r += 1;
       } else if (t == MGS_EFC_CONTACT && d->efc_dim[r] > 1) {
@@ -1549,7 +1570,7 @@ static void solve_pgs(const Mdl* md, Dat* d) {
         const double* blk = d->efc_blk + 36 * r;
         double res[5], old[5], Ac[25], bq[5], nw[5], del[5];
         for (int i = 0; i < nf; i++) {
-          res[i] = tree_dot(d->J + (size_t)(r + 1 + i) * nv, d->w, nv) + d->efc_b[r + 1 + i];
+          res[i] = tree_dot(d->K + (size_t)(r + 1 + i) * nv, d->w, nv) + d->efc_b[r + 1 + i];
           old[i] = d->efc_f[r + 1 + i];
         }
         for (int i = 0; i < nf; i++) {
@@ -1583,13 +1604,306 @@ static void solve_pgs(const Mdl* md, Dat* d) {
     }
     if (improvement * scale < m->noslip_tolerance) break;
   }
-  /* constraint force and acceleration */
+}
+
+/* qacc = qacc_smooth + L^-T D^-1/2 u ;  qfrc_constraint = L D^1/2 u */
+static void finalize_solution(const Mdl* md, Dat* d) {
+  int nv = md->m->nv;
+  double z[128];
+  for (int i = nv - 1; i >= 0; i--) {
+    double s = d->w[i] * d->isD[i];
+    for (int k = i + 1; k < nv; k++) s = s - d->L[k * nv + i] * z[k];
+    z[i] = s;
+  }
+  double t[128];
+  for (int i = 0; i < nv; i++) t[i] = d->w[i] * d->sD[i];
+  for (int i = 0; i < nv; i++) {
+    double s = t[i];
+    for (int k = 0; k < i; k++) s = s + d->L[i * nv + k] * t[k];
+    d->qfrc_constraint[i] = s;
+    d->qacc[i] = d->qacc_smooth[i] + z[i];
+  }
+}
+
+/* ---------------------------------------------------------------------- */
+/* Newton solver on the primal (MuJoCo mj_solNewton restated), in whitened
+ * coordinates w = D^1/2 L^T qacc, where the Gauss cost is 1/2||w - w0||^2 and
+ * every constraint row is jar = G_r.w - aref.  The soft-constraint cost of a
+ * row block is the convex conjugate of the dual (PGS) problem:
+ *   s(jar) = max_{f in K} (-f.jar - 1/2 f'Rf),   z = -R^-1/2 jar,  y = Proj_{R^1/2 K}(z),
+ *   f = R^-1/2 y,  s = y.z - 1/2|y|^2  (= 1/2|y|^2 for cones),
+ * which for elliptic contacts with R_t = R_n mu0^2/(impratio mu_j^2) is the
+ * isotropic second-order cone |y_t| <= mu' y_n, mu' = mu0/sqrt(impratio)
+ * (MuJoCo's "mu = friction[0]/sqrt(impratio)").  Reductions over dofs use
+ * tree_dot (lanes over dofs), reductions over rows use tree_rows (lanes over
+ * rows, rows >= 64 pre-added to row - 64). */
+static double tree_rows(const double* v, int ne) {
+  double leaf[64], one[64];
+  int n = ne < 64 ? ne : 64;
+  if (n <= 0) return 0.0;
+  for (int k = 0; k < n; k++) { leaf[k] = (k + 64 < ne) ? v[k] + v[k + 64] : v[k]; one[k] = 1.0; }
+  /* tree_dot multiplies by 1.0: exact */
+  return tree_dot(leaf, one, n);
+}
+
+#define ST_OFF 0
+#define ST_QUAD 1
+#define ST_CONE 2
+#define ST_SAT 3
+
+/* evaluate row r (or the block starting at r) at violations jr[];
+ * writes forces f[], returns cost; state per row; hb = Hessian block (dim x dim) for cones */
+static double row_eval(const Dat* d, int r, const double* jr, double* f, int* st, double* hb) {
+  int t = d->efc_type[r];
+  if (t == MGS_EFC_EQUALITY) {
+    double Dr = d->efc_Dr[r];
+    f[0] = -jr[0] * Dr;
+    st[0] = ST_QUAD;
+    return ((0.5 * Dr) * jr[0]) * jr[0];
+  }
+  if (t == MGS_EFC_LIMIT || (t == MGS_EFC_CONTACT && d->efc_dim[r] == 1)) {
+    double Dr = d->efc_Dr[r];
+    if (jr[0] < 0.0) {
+      f[0] = -jr[0] * Dr;
+      st[0] = ST_QUAD;
+      return ((0.5 * Dr) * jr[0]) * jr[0];
+    }
+    f[0] = 0.0;
+    st[0] = ST_OFF;
+    return 0.0;
+  }
+  if (t == MGS_EFC_FRICTION) {
+    double z = -jr[0] * d->efc_isR[r];
+    double lim = d->efc_floss[r] * d->efc_sqR[r];
+    double y = z;
+    st[0] = ST_QUAD;
+    if (z > lim) { y = lim; st[0] = ST_SAT; }
+    else if (z < -lim) { y = -lim; st[0] = ST_SAT; }
+    f[0] = y * d->efc_isR[r];
+    return y * z - 0.5 * (y * y);
+  }
+  /* elliptic contact block */
+  int dim = d->efc_dim[r];
+  double mup = d->efc_mup[r];
+  double z[6], y[6];
+  for (int a = 0; a < dim; a++) z[a] = -jr[a] * d->efc_isR[r + a];
+  double t2 = 0.0;
+  for (int a = 1; a < dim; a++) t2 = t2 + z[a] * z[a];
+  double tn = sqrt(t2);
+  int zone;
+  double yn = 0.0;
+  if (tn <= mup * z[0]) {
+    zone = ST_QUAD;
+    for (int a = 0; a < dim; a++) y[a] = z[a];
+  } else if (mup * tn <= -z[0]) {
+    zone = ST_OFF;
+    for (int a = 0; a < dim; a++) y[a] = 0.0;
+  } else {
+    zone = ST_CONE;
+    yn = (z[0] + mup * tn) / (1.0 + mup * mup);
+    y[0] = yn;
+    double s = (mup * yn) / tn;
+    for (int a = 1; a < dim; a++) y[a] = s * z[a];
+  }
+  double c = 0.0;
+  for (int a = 0; a < dim; a++) {
+    f[a] = y[a] * d->efc_isR[r + a];
+    st[a] = zone;
+    c = c + y[a] * y[a];
+  }
+  if (hb && zone == ST_CONE) {
+    double k1 = 1.0 / (1.0 + mup * mup);
+    double k2 = (mup * yn) / tn;
+    double v[6], e[6];
+    v[0] = 1.0;
+    e[0] = 0.0;
+    for (int a = 1; a < dim; a++) { e[a] = z[a] / tn; v[a] = mup * e[a]; }
+    for (int a = 0; a < dim; a++)
+      for (int b = 0; b < dim; b++) {
+        double P = (k1 * v[a]) * v[b];
+        if (a >= 1 && b >= 1) P = P + k2 * ((a == b ? 1.0 : 0.0) - e[a] * e[b]);
+        hb[a * dim + b] = (d->efc_isR[r + a] * d->efc_isR[r + b]) * P;
+      }
+  }
+  return 0.5 * c;
+}
+
+/* jar = G w - aref ; forces, states, cone Hessian blocks ; returns total cost */
+static double newton_eval(const Mdl* md, Dat* d, const double* w, const double* w0) {
+  int nv = md->m->nv, ne = d->nefc;
+  double q[128], cr[256];
+  for (int k = 0; k < nv; k++) q[k] = w[k] - w0[k];
+  double gauss = 0.5 * tree_dot(q, q, nv);
+  for (int r = 0; r < ne; r++) {
+    const double* Gr = d->K + (size_t)r * nv;
+    double s = 0.0;
+    for (int k = 0; k < nv; k++) s = s + Gr[k] * w[k];
+    d->efc_jar[r] = s - d->efc_aref[r];
+  }
+  for (int r = 0; r < ne;) {
+    int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
+    cr[r] = row_eval(d, r, d->efc_jar + r, d->efc_f + r, d->efc_state + r, d->efc_hb + 36 * r);
+    for (int a = 1; a < dim; a++) cr[r + a] = 0.0;
+    r += dim;
+  }
+  return gauss + tree_rows(cr, ne);
+}
+
+static void newton_grad(const Dat* d, int nv, const double* w, const double* w0, double* g) {
   for (int k = 0; k < nv; k++) {
     double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d->J[(size_t)r * nv + k] * d->efc_f[r];
-    d->qfrc_constraint[k] = s;
-    d->qacc[k] = d->qacc_smooth[k] + d->w[k];
+    for (int r = 0; r < d->nefc; r++) s = s + d->K[(size_t)r * nv + k] * d->efc_f[r];
+    g[k] = (w[k] - w0[k]) - s;
   }
+}
+
+/* line-search derivatives at step alpha along direction with jv = G dir */
+static void ls_eval(const Dat* d, double alpha, double A1, double A2, double* d1, double* d2) {
+  int ne = d->nefc;
+  double c1[256], c2[256];
+  for (int r = 0; r < ne;) {
+    int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
+    double jr[6], f[6], hb[36];
+    int st[6];
+    for (int a = 0; a < dim; a++) jr[a] = d->efc_jar[r + a] + alpha * d->efc_jv[r + a];
+    row_eval(d, r, jr, f, st, hb);
+    double s1 = 0.0, s2 = 0.0;
+    if (dim == 1) {
+      s1 = -f[0] * d->efc_jv[r];
+      if (st[0] == ST_QUAD) s2 = (d->efc_jv[r] * d->efc_Dr[r]) * d->efc_jv[r];
+    } else {
+      for (int a = 0; a < dim; a++) s1 = s1 - f[a] * d->efc_jv[r + a];
+      if (st[0] == ST_QUAD) {
+        for (int a = 0; a < dim; a++) s2 = s2 + (d->efc_jv[r + a] * d->efc_Dr[r + a]) * d->efc_jv[r + a];
+      } else if (st[0] == ST_CONE) {
+        for (int a = 0; a < dim; a++)
+          for (int b = 0; b < dim; b++) s2 = s2 + (d->efc_jv[r + a] * hb[a * dim + b]) * d->efc_jv[r + b];
+      }
+    }
+    c1[r] = s1;
+    c2[r] = s2;
+    for (int a = 1; a < dim; a++) { c1[r + a] = 0.0; c2[r + a] = 0.0; }
+    r += dim;
+  }
+  *d1 = (A1 + alpha * A2) + tree_rows(c1, ne);
+  *d2 = A2 + tree_rows(c2, ne);
+}
+
+static void solve_newton(const Mdl* md, Dat* d) {
+  const mgs_model_desc* m = md->m;
+  int nv = m->nv, ne = d->nefc;
+  double meaninertia = 0.0;
+  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d->M[k * nv + k];
+  meaninertia = meaninertia / (double)nv;
+  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
+  /* per-row constants */
+  for (int r = 0; r < ne; r++) {
+    double sq = sqrt(d->efc_R[r]);
+    d->efc_sqR[r] = sq;
+    d->efc_isR[r] = 1.0 / sq;
+    d->efc_Dr[r] = 1.0 / d->efc_R[r];
+  }
+  for (int r = 0; r < ne;) {
+    int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
+    if (dim > 1) d->efc_mup[r] = d->efc_mu[5 * r] / sqrt(m->impratio);
+    r += dim;
+  }
+  /* whitened smooth and warmstart accelerations: W(a)_i = sD_i (a_i + sum_{k>i} L_ki a_k) */
+  double w0[64], w[64], g[64], dir[64], H[64 * 64], HL[64 * 64], HDinv[64], HDv[64];
+  for (int i = 0; i < nv; i++) {
+    double s = d->qacc_smooth[i], s2 = d->qacc_ws[i];
+    for (int k = i + 1; k < nv; k++) s = s + d->L[k * nv + i] * d->qacc_smooth[k];
+    for (int k = i + 1; k < nv; k++) s2 = s2 + d->L[k * nv + i] * d->qacc_ws[k];
+    w0[i] = s * d->sD[i];
+    w[i] = s2 * d->sD[i];
+  }
+  double C = 0.0;
+  if (ne > 0) {
+    double cws = newton_eval(md, d, w, w0);
+    double c0 = newton_eval(md, d, w0, w0);
+    if (cws < c0) C = newton_eval(md, d, w, w0);
+    else { for (int k = 0; k < nv; k++) w[k] = w0[k]; C = c0; }
+  } else {
+    for (int k = 0; k < nv; k++) w[k] = w0[k];
+  }
+  newton_grad(d, nv, w, w0, g);
+  int it = 0;
+  for (it = 0; it < m->iterations && ne > 0; it++) {
+    /* Hessian I + G' h G (lower triangle then mirrored), blocks in row order */
+    for (int i = 0; i < nv; i++)
+      for (int j = 0; j <= i; j++) {
+        double s = 0.0;
+        for (int r = 0; r < ne;) {
+          int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
+          int st = d->efc_state[r];
+          if (dim > 1 && st == ST_CONE) {
+            const double* hb = d->efc_hb + 36 * r;
+            for (int a = 0; a < dim; a++)
+              for (int b = 0; b < dim; b++)
+                s = s + (d->K[(size_t)(r + a) * nv + i] * hb[a * dim + b]) * d->K[(size_t)(r + b) * nv + j];
+          } else if (st == ST_QUAD) {
+            for (int a = 0; a < dim; a++)
+              s = s + (d->K[(size_t)(r + a) * nv + i] * d->efc_Dr[r + a]) * d->K[(size_t)(r + a) * nv + j];
+          }
+          r += dim;
+        }
+        H[i * nv + j] = (i == j ? 1.0 : 0.0) + s;
+        H[j * nv + i] = H[i * nv + j];
+      }
+    ldl_factor(nv, H, HL, HDinv, HDv);
+    ldl_solve(nv, HL, HDinv, g, dir);
+    for (int k = 0; k < nv; k++) dir[k] = -dir[k];
+    for (int r = 0; r < ne; r++) {
+      const double* Gr = d->K + (size_t)r * nv;
+      double s = 0.0;
+      for (int k = 0; k < nv; k++) s = s + Gr[k] * dir[k];
+      d->efc_jv[r] = s;
+    }
+    double q[64];
+    for (int k = 0; k < nv; k++) q[k] = w[k] - w0[k];
+    double A1 = tree_dot(q, dir, nv);
+    double A2 = tree_dot(dir, dir, nv);
+    /* exact line search: 1-D Newton with bracketing on the cost derivative */
+    double p0, q0, alpha = 0.0;
+    ls_eval(d, 0.0, A1, A2, &p0, &q0);
+    if (p0 < 0.0) {
+      double lo = 0.0, hi = 0.0;
+      int hi_ok = 0;
+      alpha = -p0 / q0;
+      for (int ls = 0; ls < m->ls_iterations; ls++) {
+        double p, qq;
+        ls_eval(d, alpha, A1, A2, &p, &qq);
+        if (fabs(p) < m->ls_tolerance * (-p0)) break;
+        if (p < 0.0) lo = alpha;
+        else { hi = alpha; hi_ok = 1; }
+        double an = alpha - p / qq;
+        if (!(an > lo) || (hi_ok && !(an < hi))) an = hi_ok ? 0.5 * (lo + hi) : 2.0 * alpha;
+        alpha = an;
+      }
+    }
+    if (!(alpha > 0.0)) { it++; break; }
+    for (int k = 0; k < nv; k++) w[k] = w[k] + alpha * dir[k];
+    double Cn = newton_eval(md, d, w, w0);
+    newton_grad(d, nv, w, w0, g);
+    double improvement = scale * (C - Cn);
+    C = Cn;
+    double gn = scale * sqrt(tree_dot(g, g, nv));
+    if (improvement < m->tolerance || gn < m->tolerance) { it++; break; }
+  }
+  d->iters += it;
+  /* u = G^T f */
+  for (int k = 0; k < nv; k++) {
+    double s = 0.0;
+    for (int r = 0; r < ne; r++) s = s + d->K[(size_t)r * nv + k] * d->efc_f[r];
+    d->w[k] = s;
+  }
+}
+
+static void solve(const Mdl* md, Dat* d) {
+  if (md->m->solver == 0) solve_pgs_main(md, d);
+  else solve_newton(md, d);
+  noslip(md, d);
+  finalize_solution(md, d);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1602,7 +1916,11 @@ static void forward(const Mdl* md, Dat* d, int full) {
   collision(md, d);
   if (!full) return;
   crb(md, d);
-  ldl_factor(nv, d->M, d->L, d->Dinv);
+  ldl_factor(nv, d->M, d->L, d->Dinv, d->Dv);
+  for (int k = 0; k < nv; k++) {
+    d->sD[k] = sqrt(d->Dv[k]);
+    d->isD[k] = 1.0 / d->sD[k];
+  }
   actuation(md, d);
   passive(md, d);
   rne(md, d);
@@ -1610,7 +1928,7 @@ static void forward(const Mdl* md, Dat* d, int full) {
     d->qfrc_smooth[k] = (d->qfrc_passive[k] - d->qfrc_bias[k]) + d->qfrc_actuator[k];
   ldl_solve(nv, d->L, d->Dinv, d->qfrc_smooth, d->qacc_smooth);
   make_constraints(md, d);
-  solve_pgs(md, d);
+  solve(md, d);
 }
 
 /* implicitfast velocity update + position integration */
@@ -1641,7 +1959,7 @@ static void integrate(const Mdl* md, Dat* d) {
     }
   }
   for (int i = 0; i < nv * nv; i++) d->MI[i] = d->M[i] - dt * d->qDeriv[i];
-  ldl_factor(nv, d->MI, d->LI, d->DIinv);
+  ldl_factor(nv, d->MI, d->LI, d->DIinv, d->Dv);
   double rhs[128], qa[128];
   for (int k = 0; k < nv; k++) rhs[k] = d->qfrc_smooth[k] + d->qfrc_constraint[k];
   ldl_solve(nv, d->LI, d->DIinv, rhs, qa);
@@ -1806,4 +2124,35 @@ int oracle_contacts(const mgs_model_desc* desc, const int32_t* I, const double* 
 /* unit test hook for the shared numeric primitives */
 void oracle_sincos(const double* x, int n, double* s, double* c) {
   for (int i = 0; i < n; i++) o_sincos(x[i], s + i, c + i);
+}
+
+/* unit test hook for the canonical lane reduction */
+double oracle_tree_dot(const double* a, const double* b, int n) { return tree_dot(a, b, n); }
+
+/* Debug hook: one forward() at a given state with a given solver; returns
+ * nefc and copies efc_f (nefc), qacc (nv), types/dims and the Newton/PGS
+ * iteration count. */
+int oracle_forward_debug(const mgs_model_desc* desc, const int32_t* I, const double* D, const double* qpos,
+                         const double* qvel, const double* qacc_ws, const double* mocap_pos,
+                         const double* mocap_quat, const double* ctrl, int solver, double* f_out, double* qacc_out,
+                         int32_t* type_out, int32_t* iters_out, double* G_out, double* aref_out, double* R_out) {
+  mgs_model_desc m2 = *desc;
+  m2.solver = solver;
+  Mdl md = {&m2, I, D};
+  Dat* d = dat_alloc(&md);
+  reset(&md, d, qpos, mocap_pos, mocap_quat);
+  memcpy(d->qvel, qvel, sizeof(double) * desc->nv);
+  memcpy(d->qacc_ws, qacc_ws, sizeof(double) * desc->nv);
+  for (int u = 0; u < desc->nu; u++) d->ctrl[u] = ctrl[u];
+  forward(&md, d, 1);
+  int ne = d->nefc;
+  memcpy(f_out, d->efc_f, sizeof(double) * ne);
+  memcpy(qacc_out, d->qacc, sizeof(double) * desc->nv);
+  for (int r = 0; r < ne; r++) type_out[r] = d->efc_type[r] * 16 + d->efc_dim[r];
+  if (G_out) memcpy(G_out, d->K, sizeof(double) * ne * desc->nv);
+  if (aref_out) memcpy(aref_out, d->efc_aref, sizeof(double) * ne);
+  if (R_out) { memcpy(R_out, d->efc_R, sizeof(double) * ne); memcpy(R_out + ne, d->efc_b, sizeof(double) * ne); }
+  *iters_out = d->iters;
+  dat_free(d);
+  return ne;
 }

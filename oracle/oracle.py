@@ -42,6 +42,8 @@ def lib():
         L.oracle_contacts.argtypes = [P(abi.ModelDesc), P(c_i), P(c_d), P(c_d), P(c_d), P(c_d), ctypes.c_int,
                                       P(c_d), P(c_d), P(c_d), P(c_i)]
         L.oracle_sincos.argtypes = [P(c_d), ctypes.c_int, P(c_d), P(c_d)]
+        L.oracle_tree_dot.argtypes = [P(c_d), P(c_d), ctypes.c_int]
+        L.oracle_tree_dot.restype = c_d
         _lib = L
     return _lib
 
@@ -109,3 +111,9 @@ def sincos(x):
     c = np.zeros_like(x)
     lib().oracle_sincos(ptr(x, ctypes.c_double), len(x), ptr(s, ctypes.c_double), ptr(c, ctypes.c_double))
     return s, c
+
+
+def tree_dot(a, b, n):
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    return lib().oracle_tree_dot(ptr(a, ctypes.c_double), ptr(b, ctypes.c_double), n)

@@ -1,0 +1,38 @@
+"""Diagnostic: per-stage s_memtime breakdown of the rollout kernel (MGS_PROFILE build)."""
+import sys, os, ctypes
+import numpy as np
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'mj-grasp-sim_amd'))
+import mgs.core.engine as E
+E.LIB_PATH = E.LIB_PATH.replace('libmgs_gpu.so', 'libmgs_gpu_prof.so')
+from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+from mgs.obj.selector import get_object
+from mgs.util.geo.transforms import SE3Pose
+from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, HORIZONS
+from mgs.sampler.antipodal import robotiq_candidates
+grip = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1, 0, 0, 0]), 'wxyz'))
+obj = get_object('003_cracker_box')
+env = GravitylessObjectGrasping(grip, obj)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+H, J, W = robotiq_candidates(obj, 4 * N, seed=2)
+poses = SE3Pose.from_mat(H)
+q, mp, mq, _ = env.initial_state(poses, J)
+free = env.engine.collision_free(q, mp, mq)
+idx = np.nonzero(free)[0][:N]
+h = HORIZONS['h200']
+plan = env.rollout_plan(poses[idx], J[idx], nstep_lift=h['nstep_lift'], shake_steps=h['shake_steps'],
+                        close_steps=h['close_steps'], lift_check_every=h['lift_check_every'])
+L = E.load_library()
+L.mgs_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+buf = (ctypes.c_ulonglong * 32)()
+L.mgs_prof_read(buf)
+r = env.engine.rollout(plan)
+L.mgs_prof_read(buf)
+v = np.array(buf[:8], dtype=np.float64)
+names = ['loop/ctrl', 'kin+com', 'collision', 'crb+ldl', 'smooth(act,pas,rne,solve)', 'make_constraints', 'pgs+noslip', 'integrate']
+tot = v.sum()
+print('N=%d collision-free candidates, kernel %.1f ms, labels %d, mean iters/step %.1f, overflow %d' % (
+    len(idx), r['kernel_ms'], r['label'].sum(), r['stats'][:, 3].sum() / max(1, r['stats'][:, 3].size) / 200, (r['stats'][:, 2] != 0).sum()))
+for n_, x in zip(names, v):
+    print('%-28s %6.1f%%  %.3g ticks' % (n_, 100 * x / tot, x))
+steps = len(idx) * 200
+print('ticks per candidate-step: %.0f' % (tot / steps))
