@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 1
+#define MGS_ABI_VERSION 2
 
 /* error codes */
 #define MGS_OK 0
@@ -128,6 +128,8 @@ typedef struct mgs_model_desc {
   int32_t d_body_iquat;     /* 4 */
   int32_t d_body_mass;      /* 1 */
   int32_t d_body_inertia;   /* 3 */
+  int32_t d_body_invweight0; /* 2: translational, rotational (MuJoCo mj_setConst) */
+  int32_t d_dof_invweight0;  /* nv (indexed by dof) */
   /* joints */
   int32_t i_jnt_type;
   int32_t i_jnt_qposadr;

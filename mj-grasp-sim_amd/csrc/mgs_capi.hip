@@ -47,7 +47,7 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   sizes[L_act_force] = nu; sizes[L_act_moment] = nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
   sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc;
   sizes[L_efc_R] = ne; sizes[L_efc_b] = ne; sizes[L_efc_AR] = ne; sizes[L_efc_ARinv] = ne; sizes[L_efc_A] = ne;
-  sizes[L_efc_Ainv] = ne; sizes[L_efc_floss] = ne; sizes[L_con_mu] = 5 * nc; sizes[L_con_blk] = BLKSTRIDE * nc;
+  sizes[L_efc_Ainv] = ne; sizes[L_efc_floss] = ne; sizes[L_efc_dA] = ne; sizes[L_con_mu] = 5 * nc; sizes[L_con_blk] = BLKSTRIDE * nc;
   // U sub-layout
   int u_coll = 6 * K_MAXPOLY * 3 + K_MAXPOLY;                 // poly buffers + depths
   int u_dyn = 10 * nb;                                        // crb

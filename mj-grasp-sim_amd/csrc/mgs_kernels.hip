@@ -56,7 +56,7 @@ struct Dat {
   double *qfrc_bias, *qfrc_passive, *qfrc_actuator, *qfrc_smooth, *qacc_smooth, *qfrc_constraint, *qacc;
   double *act_force, *act_moment, *act_length, *act_vel;
   double *con_pos, *con_frame, *con_dist;
-  double *efc_R, *efc_b, *efc_AR, *efc_ARinv, *efc_A, *efc_Ainv, *efc_floss, *con_mu, *con_blk;
+  double *efc_R, *efc_b, *efc_AR, *efc_ARinv, *efc_A, *efc_Ainv, *efc_floss, *efc_dA, *con_mu, *con_blk;
   // U region views
   double *crb, *cvel, *cacc, *cfrc, *cdof_dot;          // dynamics stage
   P2* poly;                                           // collision stage
@@ -751,8 +751,9 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
 
 DEVI void make_frame(const double* n, double* t1, double* t2) {
   double a[3];
-  if (fabs(n[0]) < 0.6) { a[0] = 1.0; a[1] = 0.0; a[2] = 0.0; }
-  else { a[0] = 0.0; a[1] = 1.0; a[2] = 0.0; }
+  /* mju_makeFrame: tangent seed (0,1,0) unless |n_y| >= 0.5, then (0,0,1) */
+  if (n[1] < 0.5 && n[1] > -0.5) { a[0] = 0.0; a[1] = 1.0; a[2] = 0.0; }
+  else { a[0] = 0.0; a[1] = 0.0; a[2] = 1.0; }
   double an = dot3(a, n);
   t1[0] = a[0] - n[0] * an; t1[1] = a[1] - n[1] * an; t1[2] = a[2] - n[2] * an;
   normalize3(t1);
@@ -1046,7 +1047,7 @@ enum {
   L_qfrc_bias, L_qfrc_passive, L_qfrc_actuator, L_qfrc_smooth, L_qacc_smooth, L_qfrc_constraint, L_qacc,
   L_act_force, L_act_moment, L_act_length, L_act_vel,
   L_con_pos, L_con_frame, L_con_dist,
-  L_efc_R, L_efc_b, L_efc_AR, L_efc_ARinv, L_efc_A, L_efc_Ainv, L_efc_floss, L_con_mu, L_con_blk,
+  L_efc_R, L_efc_b, L_efc_AR, L_efc_ARinv, L_efc_A, L_efc_Ainv, L_efc_floss, L_efc_dA, L_con_mu, L_con_blk,
   L_U, L_ints, L_COUNT
 };
 struct Lay {
@@ -1067,7 +1068,7 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   B(qfrc_bias); B(qfrc_passive); B(qfrc_actuator); B(qfrc_smooth); B(qacc_smooth); B(qfrc_constraint); B(qacc);
   B(act_force); B(act_moment); B(act_length); B(act_vel);
   B(con_pos); B(con_frame); B(con_dist);
-  B(efc_R); B(efc_b); B(efc_AR); B(efc_ARinv); B(efc_A); B(efc_Ainv); B(efc_floss); B(con_mu); B(con_blk);
+  B(efc_R); B(efc_b); B(efc_AR); B(efc_ARinv); B(efc_A); B(efc_Ainv); B(efc_floss); B(efc_dA); B(con_mu); B(con_blk);
 #undef B
   double* U = s + l.o[L_U];
   d.crb = U + l.u_crb; d.cvel = U + l.u_cvel; d.cacc = U + l.u_cacc; d.cfrc = U + l.u_cfrc;
@@ -1177,7 +1178,7 @@ DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, co
     double p = (j == 0) ? (d.efc_pos[q] - d.efc_margin[q]) : 0.0;
     d.efc_aref[q] = -B * d.efc_vel[q] - (Kc * imp) * p;
   }
-  double Rn = ((1.0 - imp) / imp) * d.efc_A[r];
+  double Rn = ((1.0 - imp) / imp) * d.efc_dA[r];
   if (Rn < K_MINVAL) Rn = K_MINVAL;
   d.efc_R[r] = Rn;
   if (elliptic_contact && dim > 1) {
@@ -1186,9 +1187,39 @@ DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, co
     for (int j = 1; j < dim - 1; j++) d.efc_R[r + j + 1] = (R1 * (mu[0] * mu[0])) / (mu[j] * mu[j]);
   } else {
     for (int j = 1; j < dim; j++) {
-      double Rj = ((1.0 - imp) / imp) * d.efc_A[r + j];
+      double Rj = ((1.0 - imp) / imp) * d.efc_dA[r + j];
       d.efc_R[r + j] = Rj < K_MINVAL ? K_MINVAL : Rj;
     }
+  }
+}
+
+// MuJoCo mj_diagApprox from the qpos0 inverse weights (oracle diag_approx()); lane 0
+DEVI void diag_approx(const Mdl& md, Dat& d, int ne) {
+  const double *biw = DA(md, body_invweight0), *diw = DA(md, dof_invweight0);
+  const int32_t *et = IA(md, eq_type), *eo1 = IA(md, eq_obj1id), *eo2 = IA(md, eq_obj2id);
+  const int32_t *jd = IA(md, jnt_dofadr), *gbody = IA(md, geom_bodyid);
+  int start = 0;
+  for (int r = 0; r < ne; r++) {
+    int t = d.efc_type[r], id = d.efc_con[r];
+    if (r == 0 || d.efc_type[r - 1] != t || d.efc_con[r - 1] != id) start = r;
+    int k = r - start;
+    double v = 0.0;
+    if (t == MGS_EFC_EQUALITY) {
+      if (et[id] == MGS_EQ_CONNECT) v = biw[2 * eo1[id]] + biw[2 * eo2[id]];
+      else if (et[id] == MGS_EQ_WELD) v = biw[2 * eo1[id] + (k > 2)] + biw[2 * eo2[id] + (k > 2)];
+      else {
+        v = diw[jd[eo1[id]]];
+        if (eo2[id] >= 0) v = v + diw[jd[eo2[id]]];
+      }
+    } else if (t == MGS_EFC_FRICTION) {
+      v = diw[id];
+    } else if (t == MGS_EFC_LIMIT) {
+      v = diw[jd[id]];
+    } else {
+      int b1 = gbody[d.con_g1[id]], b2 = gbody[d.con_g2[id]];
+      v = (k < 3) ? biw[2 * b1] + biw[2 * b2] : biw[2 * b1 + 1] + biw[2 * b2 + 1];
+    }
+    d.efc_dA[r] = v;
   }
 }
 
@@ -1371,6 +1402,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   }
   wsync();
   if (lane == 0) {
+    diag_approx(md, d, ne);
     const double *eqsr = DA(md, eq_solref), *eqsi = DA(md, eq_solimp);
     for (int r = 0; r < ints[8]; r++) {
       int e = d.efc_con[r];
@@ -1427,10 +1459,11 @@ DEVI void qcqp2(double A0, double A1, double A3, double bb0, double bb1, const d
   double a11 = (A0 * mu[0]) * mu[0], a12 = (A1 * mu[0]) * mu[1], a22 = (A3 * mu[1]) * mu[1];
   double b1 = bb0 * mu[0], b2 = bb1 * mu[1];
   double rr = r * r, la = 0.0, v1 = 0.0, v2 = 0.0;
+  int sing = 0;
   for (int it = 0; it < 20; it++) {
     double m11 = a11 + la, m22 = a22 + la;
     double det = m11 * m22 - a12 * a12;
-    if (det < 1e-10) { v1 = 0.0; v2 = 0.0; break; }
+    if (det < 1e-10) { v1 = 0.0; v2 = 0.0; sing = 1; break; }
     double idet = 1.0 / det;
     double p11 = m22 * idet, p22 = m11 * idet, p12 = -a12 * idet;
     v1 = -(p11 * b1 + p12 * b2);
@@ -1443,8 +1476,16 @@ DEVI void qcqp2(double A0, double A1, double A3, double bb0, double bb1, const d
     if (delta < 1e-10) break;
     la = la + delta;
   }
-  *x0 = v1 * mu[0];
-  *x1 = v2 * mu[1];
+  double o0 = v1 * mu[0], o1 = v2 * mu[1];
+  // active constraint: put the result on the ellipsoid (MuJoCo PGS / noslip)
+  if (!sing && la != 0.0) {
+    double s = (o0 * o0) / (mu[0] * mu[0]) + (o1 * o1) / (mu[1] * mu[1]);
+    s = sqrt((r * r) / (s > K_MINVAL ? s : K_MINVAL));
+    o0 = o0 * s;
+    o1 = o1 * s;
+  }
+  *x0 = o0;
+  *x1 = o1;
 }
 
 DEVI void qcqp3(const double* A, const double* b, const double* mu, double r, double* x) {
@@ -1452,12 +1493,13 @@ DEVI void qcqp3(const double* A, const double* b, const double* mu, double r, do
   double a11 = (A[4] * mu[1]) * mu[1], a12 = (A[5] * mu[1]) * mu[2], a22 = (A[8] * mu[2]) * mu[2];
   double b0 = b[0] * mu[0], b1 = b[1] * mu[1], b2 = b[2] * mu[2];
   double rr = r * r, la = 0.0, v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  int sing = 0;
   for (int it = 0; it < 20; it++) {
     double m00 = a00 + la, m11 = a11 + la, m22 = a22 + la;
     double c00 = m11 * m22 - a12 * a12, c01 = a02 * a12 - a01 * m22, c02 = a01 * a12 - a02 * m11;
     double c11 = m00 * m22 - a02 * a02, c12 = a01 * a02 - m00 * a12, c22 = m00 * m11 - a01 * a01;
     double det = (m00 * c00 + a01 * c01) + a02 * c02;
-    if (det < 1e-10) { v0 = 0.0; v1 = 0.0; v2 = 0.0; break; }
+    if (det < 1e-10) { v0 = 0.0; v1 = 0.0; v2 = 0.0; sing = 1; break; }
     double idet = 1.0 / det;
     double p00 = c00 * idet, p01 = c01 * idet, p02 = c02 * idet;
     double p11 = c11 * idet, p12 = c12 * idet, p22 = c22 * idet;
@@ -1477,6 +1519,13 @@ DEVI void qcqp3(const double* A, const double* b, const double* mu, double r, do
   x[0] = v0 * mu[0];
   x[1] = v1 * mu[1];
   x[2] = v2 * mu[2];
+  if (!sing && la != 0.0) {
+    double s = ((x[0] * x[0]) / (mu[0] * mu[0]) + (x[1] * x[1]) / (mu[1] * mu[1])) + (x[2] * x[2]) / (mu[2] * mu[2]);
+    s = sqrt((r * r) / (s > K_MINVAL ? s : K_MINVAL));
+    x[0] = x[0] * s;
+    x[1] = x[1] * s;
+    x[2] = x[2] * s;
+  }
 }
 
 // forces live in registers: lane l holds f[l] (fr0) and f[l + 64] (fr1)
@@ -1729,6 +1778,12 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
   int P = next_pow2(nv);
   for (int ns = 0; ns < md.m.noslip_iterations && ne > 0; ns++) {
     double improvement = 0.0;
+    // the noslip cost drops the regulariser: count its removal at iteration 0
+    if (ns == 0)
+      for (int r = 0; r < ne; r++) {
+        double f = getf(fr0, fr1, r);
+        improvement = improvement + ((0.5 * f) * f) * d.efc_R[r];
+      }
     for (int r = 0; r < ne;) {
       int t = uni(d.efc_type[r]);
       int dim = uni(d.efc_dim[r]);

@@ -907,7 +907,82 @@ class Compiler:
         cm.actuator_gear = np.array([a["gear"] for a in acts], np.float64)
         cm.body_xpos0 = xpos
         cm.body_xquat0 = xquat
+        cm.body_invweight0, cm.dof_invweight0 = _invweight0(cm)
         return cm
+
+
+def _invweight0(cm):
+    """MuJoCo's mj_setConst inverse weights at qpos0 (engine_setconst.c):
+
+      body_invweight0[b] = (mean diag of Jt M^-1 Jt', mean diag of Jr M^-1 Jr')
+                           with J the body-COM Jacobian (0 for world-welded bodies),
+      dof_invweight0[d]  = diag(M^-1) (free joints: mean over the 3 translational
+                           and over the 3 rotational dofs).
+
+    They define efc_diagApprox, from which the constraint regulariser R is built
+    (R = (1 - imp) / imp * diagApprox; engine_core_constraint.c mj_diagApprox /
+    mj_makeImpedance).  Joint values at qpos0 are the reference configuration,
+    so body frames are the compiled body_xpos0 / body_xquat0."""
+    nb, nv = cm.nbody, cm.nv
+    xpos, xquat = cm.body_xpos0, cm.body_xquat0
+    xmat = np.array([quat2mat(q) for q in xquat])
+    xipos = np.array([xpos[b] + xmat[b] @ cm.body_ipos[b] for b in range(nb)])
+    ximat = np.array([xmat[b] @ quat2mat(cm.body_iquat[b]) for b in range(nb)])
+    # world-frame dof axes (angular part) and anchors
+    dof_w = np.zeros((nv, 3))      # angular direction (0 for translations)
+    dof_v = np.zeros((nv, 3))      # translational direction (slide / free xyz)
+    dof_anchor = np.zeros((nv, 3))
+    for j in range(len(cm.jnt_type)):
+        b, da, t = cm.jnt_bodyid[j], cm.jnt_dofadr[j], cm.jnt_type[j]
+        anchor = xpos[b] + xmat[b] @ cm.jnt_pos[j]
+        axis = xmat[b] @ cm.jnt_axis[j]
+        if t == 0:
+            for k in range(3):
+                dof_v[da + k, k] = 1.0
+                dof_w[da + 3 + k] = xmat[b][:, k]
+                dof_anchor[da + 3 + k] = anchor
+        elif t == 1:
+            for k in range(3):
+                dof_w[da + k] = xmat[b][:, k]
+                dof_anchor[da + k] = anchor
+        elif t == 2:
+            dof_v[da] = axis
+        else:
+            dof_w[da] = axis
+            dof_anchor[da] = anchor
+    # body COM Jacobians (dofs on the path to the root)
+    def jac(b):
+        Jt, Jr = np.zeros((3, nv)), np.zeros((3, nv))
+        d = cm.body_lastdof[b]
+        while d >= 0:
+            Jr[:, d] = dof_w[d]
+            Jt[:, d] = dof_v[d] + np.cross(dof_w[d], xipos[b] - dof_anchor[d])
+            d = cm.dof_parentid[d]
+        return Jt, Jr
+    M = np.diag(np.asarray(cm.dof_armature, np.float64)).copy() if nv else np.zeros((0, 0))
+    Js = [None] * nb
+    for b in range(1, nb):
+        Jt, Jr = jac(b)
+        Js[b] = (Jt, Jr)
+        I = ximat[b] @ np.diag(cm.body_inertia[b]) @ ximat[b].T
+        M += cm.body_mass[b] * Jt.T @ Jt + Jr.T @ I @ Jr
+    Minv = np.linalg.inv(M) if nv else M
+    biw = np.zeros((nb, 2))
+    for b in range(1, nb):
+        if cm.body_weldid[b] == 0 or cm.body_lastdof[b] < 0:
+            continue
+        Jt, Jr = Js[b]
+        biw[b, 0] = max(_MINVAL, np.trace(Jt @ Minv @ Jt.T) / 3.0)
+        biw[b, 1] = max(_MINVAL, np.trace(Jr @ Minv @ Jr.T) / 3.0)
+    diw = np.diag(Minv).copy() if nv else np.zeros(0)
+    for j in range(len(cm.jnt_type)):
+        da, t = cm.jnt_dofadr[j], cm.jnt_type[j]
+        if t == 0:
+            diw[da:da + 3] = diw[da:da + 3].mean()
+            diw[da + 3:da + 6] = diw[da + 3:da + 6].mean()
+        elif t == 1:
+            diw[da:da + 3] = diw[da:da + 3].mean()
+    return biw, diw
 
 
 class CompiledModel:
@@ -951,7 +1026,8 @@ class CompiledModel:
         for n in ["body_parentid", "body_rootid", "body_mocapid", "body_jntnum", "body_jntadr",
                   "body_dofnum", "body_dofadr", "body_lastdof"]:
             put_i(n, getattr(self, n))
-        for n in ["body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia"]:
+        for n in ["body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia",
+                  "body_invweight0", "dof_invweight0"]:
             put_d(n, getattr(self, n))
         for n in ["jnt_type", "jnt_qposadr", "jnt_dofadr", "jnt_bodyid", "jnt_limited"]:
             put_i(n, getattr(self, n))

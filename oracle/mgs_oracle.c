@@ -73,7 +73,7 @@ typedef struct {
   /* constraints */
   int nefc;
   double *J, *K, *efc_pos, *efc_margin, *efc_vel, *efc_aref, *efc_R, *efc_A, *efc_b, *efc_f;
-  double *efc_mu, *efc_blk, *efc_hb, *efc_floss, *efc_AR, *efc_ARinv, *efc_Ainv;
+  double *efc_mu, *efc_blk, *efc_hb, *efc_dA, *efc_floss, *efc_AR, *efc_ARinv, *efc_Ainv;
   double *efc_Dr, *efc_sqR, *efc_isR, *efc_mup, *efc_jar, *efc_jv;
   int* efc_state;
   double *Dv, *sD, *isD;
@@ -259,7 +259,7 @@ static Dat* dat_alloc(const Mdl* md) {
   TAKE(con_pos, 3 * nc); TAKE(con_frame, 9 * nc); TAKE(con_dist, nc);
   TAKE(J, ne * nv); TAKE(K, ne * nv); TAKE(efc_pos, ne); TAKE(efc_margin, ne); TAKE(efc_vel, ne);
   TAKE(efc_aref, ne); TAKE(efc_R, ne); TAKE(efc_A, ne); TAKE(efc_b, ne); TAKE(efc_f, ne);
-  TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_hb, 36 * ne); TAKE(efc_floss, ne); TAKE(w, nv);
+  TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_hb, 36 * ne); TAKE(efc_dA, ne); TAKE(efc_floss, ne); TAKE(w, nv);
   TAKE(efc_AR, ne); TAKE(efc_ARinv, ne); TAKE(efc_Ainv, ne); TAKE(Dv, nv); TAKE(sD, nv); TAKE(isD, nv);
   TAKE(efc_Dr, ne); TAKE(efc_sqR, ne); TAKE(efc_isR, ne); TAKE(efc_mup, ne); TAKE(efc_jar, ne); TAKE(efc_jv, ne);
 #undef TAKE
@@ -782,8 +782,9 @@ static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* 
 
 static void make_frame(const double* n, double* t1, double* t2) {
   double a[3];
-  if (fabs(n[0]) < 0.6) { a[0] = 1.0; a[1] = 0.0; a[2] = 0.0; }
-  else { a[0] = 0.0; a[1] = 1.0; a[2] = 0.0; }
+  /* mju_makeFrame: tangent seed (0,1,0) unless |n_y| >= 0.5, then (0,0,1) */
+  if (n[1] < 0.5 && n[1] > -0.5) { a[0] = 0.0; a[1] = 1.0; a[2] = 0.0; }
+  else { a[0] = 0.0; a[1] = 0.0; a[2] = 1.0; }
   double an = dot3(a, n);
   t1[0] = a[0] - n[0] * an; t1[1] = a[1] - n[1] * an; t1[2] = a[2] - n[2] * an;
   normalize3(t1);
@@ -1121,7 +1122,7 @@ static void row_params(const Mdl* md, Dat* d, int r, int dim, const double* sr, 
     double p = (j == 0) ? (d->efc_pos[q] - d->efc_margin[q]) : 0.0;
     d->efc_aref[q] = -B * d->efc_vel[q] - (Kc * imp) * p;
   }
-  double Rn = ((1.0 - imp) / imp) * d->efc_A[r];
+  double Rn = ((1.0 - imp) / imp) * d->efc_dA[r];
   if (Rn < O_MINVAL) Rn = O_MINVAL;
   d->efc_R[r] = Rn;
   if (elliptic_contact && dim > 1) {
@@ -1131,9 +1132,44 @@ static void row_params(const Mdl* md, Dat* d, int r, int dim, const double* sr, 
       d->efc_R[r + j + 1] = (R1 * (mu[0] * mu[0])) / (mu[j] * mu[j]);
   } else {
     for (int j = 1; j < dim; j++) {
-      double Rj = ((1.0 - imp) / imp) * d->efc_A[r + j];
+      double Rj = ((1.0 - imp) / imp) * d->efc_dA[r + j];
       d->efc_R[r + j] = Rj < O_MINVAL ? O_MINVAL : Rj;
     }
+  }
+}
+
+/* MuJoCo mj_diagApprox (engine_core_constraint.c): the approximate diagonal of
+ * A used for R, from the qpos0 inverse weights (body_invweight0: translation,
+ * rotation; dof_invweight0).  Connect rows: translation of both bodies; weld
+ * rows 0-2 translation, 3-5 rotation; joint equality: dof weights of both
+ * joints; dof friction / joint limits: the dof weight; contacts: translation of
+ * both geom bodies for the normal and tangent rows, rotation beyond row 2. */
+static void diag_approx(const Mdl* md, Dat* d) {
+  const double *biw = DA(md, body_invweight0), *diw = DA(md, dof_invweight0);
+  const int32_t *et = IA(md, eq_type), *eo1 = IA(md, eq_obj1id), *eo2 = IA(md, eq_obj2id);
+  const int32_t *jd = IA(md, jnt_dofadr), *gbody = IA(md, geom_bodyid);
+  int start = 0;
+  for (int r = 0; r < d->nefc; r++) {
+    int t = d->efc_type[r], id = d->efc_con[r];
+    if (r == 0 || d->efc_type[r - 1] != t || d->efc_con[r - 1] != id) start = r;
+    int k = r - start;
+    double v = 0.0;
+    if (t == MGS_EFC_EQUALITY) {
+      if (et[id] == MGS_EQ_CONNECT) v = biw[2 * eo1[id]] + biw[2 * eo2[id]];
+      else if (et[id] == MGS_EQ_WELD) v = biw[2 * eo1[id] + (k > 2)] + biw[2 * eo2[id] + (k > 2)];
+      else {
+        v = diw[jd[eo1[id]]];
+        if (eo2[id] >= 0) v = v + diw[jd[eo2[id]]];
+      }
+    } else if (t == MGS_EFC_FRICTION) {
+      v = diw[id];
+    } else if (t == MGS_EFC_LIMIT) {
+      v = diw[jd[id]];
+    } else {
+      int b1 = gbody[d->con_g1[id]], b2 = gbody[d->con_g2[id]];
+      v = (k < 3) ? biw[2 * b1] + biw[2 * b2] : biw[2 * b1 + 1] + biw[2 * b2 + 1];
+    }
+    d->efc_dA[r] = v;
   }
 }
 
@@ -1285,6 +1321,7 @@ static void make_constraints(const Mdl* md, Dat* d) {
     for (int k = 0; k < nv; k++) a = a + Gr[k] * Gr[k];
     d->efc_A[r] = a;
   }
+  diag_approx(md, d);
   const double *eqsr = DA(md, eq_solref), *eqsi = DA(md, eq_solimp);
   for (int r = 0; r < neqrows; r++) {
     int e = d->efc_con[r];
@@ -1339,10 +1376,11 @@ static void qcqp2(const double* A, const double* b, const double* mu, double r, 
   double a11 = (A[0] * mu[0]) * mu[0], a12 = (A[1] * mu[0]) * mu[1], a22 = (A[3] * mu[1]) * mu[1];
   double b1 = b[0] * mu[0], b2 = b[1] * mu[1];
   double rr = r * r, la = 0.0, v1 = 0.0, v2 = 0.0;
+  int sing = 0;
   for (int it = 0; it < 20; it++) {
     double m11 = a11 + la, m22 = a22 + la;
     double det = m11 * m22 - a12 * a12;
-    if (det < 1e-10) { v1 = 0.0; v2 = 0.0; break; }
+    if (det < 1e-10) { v1 = 0.0; v2 = 0.0; sing = 1; break; }
     double idet = 1.0 / det;
     double p11 = m22 * idet, p22 = m11 * idet, p12 = -a12 * idet;
     v1 = -(p11 * b1 + p12 * b2);
@@ -1357,6 +1395,13 @@ static void qcqp2(const double* A, const double* b, const double* mu, double r, 
   }
   x[0] = v1 * mu[0];
   x[1] = v2 * mu[1];
+  /* active constraint: put the result on the ellipsoid (MuJoCo PGS / noslip) */
+  if (!sing && la != 0.0) {
+    double s = (x[0] * x[0]) / (mu[0] * mu[0]) + (x[1] * x[1]) / (mu[1] * mu[1]);
+    s = sqrt((r * r) / (s > O_MINVAL ? s : O_MINVAL));
+    x[0] = x[0] * s;
+    x[1] = x[1] * s;
+  }
 }
 
 static void qcqp3(const double* A, const double* b, const double* mu, double r, double* x) {
@@ -1364,12 +1409,13 @@ static void qcqp3(const double* A, const double* b, const double* mu, double r, 
   double a11 = (A[4] * mu[1]) * mu[1], a12 = (A[5] * mu[1]) * mu[2], a22 = (A[8] * mu[2]) * mu[2];
   double b0 = b[0] * mu[0], b1 = b[1] * mu[1], b2 = b[2] * mu[2];
   double rr = r * r, la = 0.0, v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  int sing = 0;
   for (int it = 0; it < 20; it++) {
     double m00 = a00 + la, m11 = a11 + la, m22 = a22 + la;
     double c00 = m11 * m22 - a12 * a12, c01 = a02 * a12 - a01 * m22, c02 = a01 * a12 - a02 * m11;
     double c11 = m00 * m22 - a02 * a02, c12 = a01 * a02 - m00 * a12, c22 = m00 * m11 - a01 * a01;
     double det = (m00 * c00 + a01 * c01) + a02 * c02;
-    if (det < 1e-10) { v0 = 0.0; v1 = 0.0; v2 = 0.0; break; }
+    if (det < 1e-10) { v0 = 0.0; v1 = 0.0; v2 = 0.0; sing = 1; break; }
     double idet = 1.0 / det;
     double p00 = c00 * idet, p01 = c01 * idet, p02 = c02 * idet;
     double p11 = c11 * idet, p12 = c12 * idet, p22 = c22 * idet;
@@ -1389,6 +1435,13 @@ static void qcqp3(const double* A, const double* b, const double* mu, double r, 
   x[0] = v0 * mu[0];
   x[1] = v1 * mu[1];
   x[2] = v2 * mu[2];
+  if (!sing && la != 0.0) {
+    double s = ((x[0] * x[0]) / (mu[0] * mu[0]) + (x[1] * x[1]) / (mu[1] * mu[1])) + (x[2] * x[2]) / (mu[2] * mu[2]);
+    s = sqrt((r * r) / (s > O_MINVAL ? s : O_MINVAL));
+    x[0] = x[0] * s;
+    x[1] = x[1] * s;
+    x[2] = x[2] * s;
+  }
 }
 
 static void qcqp(int n, const double* A, const double* b, const double* mu, double r, double* x) {
@@ -1549,6 +1602,9 @@ static void noslip(const Mdl* md, Dat* d) {
   /* noslip: friction dims only, unregularized, normal forces fixed */
   for (int ns = 0; ns < m->noslip_iterations && ne > 0; ns++) {
     double improvement = 0.0;
+    /* the noslip cost drops the regulariser: count its removal at iteration 0 */
+    if (ns == 0)
+      for (int r = 0; r < ne; r++) improvement = improvement + ((0.5 * d->efc_f[r]) * d->efc_f[r]) * d->efc_R[r];
     for (int r = 0; r < ne;) {
       int t = d->efc_type[r];
       if (t == MGS_EFC_FRICTION) {
