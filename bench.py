@@ -1,0 +1,240 @@
+"""Headline benchmark: grasp candidates evaluated / s at a 200-step horizon,
+Robotiq 2F-85 x YCB 003_cracker_box (BASELINE.json configs[1]: 8192 candidates
+x 200 steps per MI355X).
+
+One step = the reference's filter_to_stable pipeline (mgs/cli/filter_to_stable.py:
+39-50) over one batch: collision mask of every candidate, then the close ->
+lift -> shake rollout of the collision-free ones (h200 horizon).  Inputs are
+host-prepared once (float32 SE3 processing, mocap schedule), uploaded, and
+resident in HBM when the timed region starts; both kernels run back-to-back on
+one stream with no host round trip (the rollout reads the mask on the device).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--candidates 8192]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Multi-GPU: weak scaling, one process per GPU, each rank evaluates its own
+8192-candidate block (seed = rank); no data-path collective -- only the
+timing barrier and the max-over-ranks reduction.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mj-grasp-sim_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(cm, steps, sum_ncon, sum_nefc, w=8):
+    """SURVEY.md §8(d) B_cs summed over the executed candidate-steps of a launch:
+    every per-candidate SoA array read once and written once per step (fp64)."""
+    ngeom = len(cm.geom_bodyid)
+    per_step = (2 * (cm.nq + 2 * cm.nv + cm.nu + 7 * cm.nmocap + 1) + 2 * 7 * cm.nbody
+                + 2 * 12 * ngeom + 2 * cm.nv * cm.nv)
+    return w * (per_step * steps + 2 * 18 * sum_ncon + 2 * (cm.nv + 6) * sum_nefc)
+
+
+def executed_steps(labels, fail_step, active, horizon):
+    """candidate-steps actually simulated (early exits stop a rollout)."""
+    s = np.where(labels, horizon, fail_step + 1)
+    return int(np.sum(np.where(active, s, 0)))
+
+
+def load_traffic(launch_steps):
+    """HBM bytes per rollout launch from the committed PMC pass (profiles/), scaled
+    to this launch's candidate-steps; None if no PMC summary is present."""
+    p = os.path.join(ROOT, "profiles", "pmc_rollout.json")
+    if not os.path.isfile(p):
+        return None
+    with open(p) as f:
+        j = json.load(f)
+    per_cs = j.get("hbm_bytes_per_candidate_step")
+    return None if per_cs is None else float(per_cs) * launch_steps
+
+
+def cpu_baseline(env, poses, joints, h, budget_s, threads):
+    """The oracle (C restatement, OpenMP over candidates) on the host cores, on a
+    bounded leading sample of the same candidate block; returns a dict."""
+    from oracle import oracle as O
+    om = O.OracleModel(env.model)
+    q, mp, mq, _ = env.initial_state(poses, joints)
+    # pilot on 256 candidates to size the sample to the time budget
+    n_pilot = min(256, len(poses))
+    t0 = time.perf_counter()
+    free = om.collision_free(q[:n_pilot], mp[:n_pilot], mq[:n_pilot], nthreads=threads)
+    idx = np.nonzero(free)[0]
+    if len(idx):
+        plan = env.rollout_plan(poses[idx], joints[idx], nstep_lift=h["nstep_lift"], shake_steps=h["shake_steps"],
+                                close_steps=h["close_steps"], lift_check_every=h["lift_check_every"])
+        om.rollout(plan, nthreads=threads)
+    dt_pilot = max(time.perf_counter() - t0, 1e-6)
+    n = int(min(len(poses), max(n_pilot, n_pilot * budget_s / dt_pilot)))
+    t0 = time.perf_counter()
+    free = om.collision_free(q[:n], mp[:n], mq[:n], nthreads=threads)
+    idx = np.nonzero(free)[0]
+    labels = np.zeros(n, bool)
+    if len(idx):
+        plan = env.rollout_plan(poses[idx], joints[idx], nstep_lift=h["nstep_lift"], shake_steps=h["shake_steps"],
+                                close_steps=h["close_steps"], lift_check_every=h["lift_check_every"])
+        labels[idx] = om.rollout(plan, nthreads=threads)["label"]
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, n=n, seconds=dt, free=free, labels=labels)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--candidates", type=int, default=8192)
+    ap.add_argument("--horizon", default="h200")
+    ap.add_argument("--solver", default=None, help="override the model's solver (Newton | PGS)")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from mgs.core import abi
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, HORIZONS
+    from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+    from mgs.obj.selector import get_object
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+
+    grip = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz"))
+    obj = get_object("003_cracker_box")
+    env = GravitylessObjectGrasping(grip, obj, device=local)
+    if args.solver:
+        env.model.options["solver"] = args.solver
+    h = HORIZONS[args.horizon]
+    N = args.candidates
+    H, J, _ = robotiq_candidates(obj, N, seed=rank)
+    poses = SE3Pose.from_mat(H)
+    qpos, mpos, mquat, _ = env.initial_state(poses, J)
+    plan = env.rollout_plan(poses, J, nstep_lift=h["nstep_lift"], shake_steps=h["shake_steps"],
+                            close_steps=h["close_steps"], lift_check_every=h["lift_check_every"])
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+    horizon = plan.horizon
+    eng = env.engine
+    dev = torch.device("cuda", local)
+    f64 = dict(dtype=torch.float64, device=dev)
+    d_q = torch.as_tensor(qpos, **f64).contiguous()
+    d_mp = torch.as_tensor(mpos, **f64).contiguous()
+    d_mq = torch.as_tensor(mquat, **f64).contiguous()
+    d_ps = torch.as_tensor(plan.phase_start, **f64).contiguous()
+    d_pt = torch.as_tensor(plan.phase_target, **f64).contiguous()
+    d_free = torch.zeros(N, dtype=torch.uint8, device=dev)
+    d_label = torch.zeros(N, dtype=torch.uint8, device=dev)
+    d_fail = torch.zeros(N, dtype=torch.int32, device=dev)
+    d_objq = torch.zeros((N, 7), **f64)
+    d_stats = torch.zeros((N, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        eng.collision_free_device(N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(), d_free.data_ptr(),
+                                  predicate="any", stream=sp)
+        eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
+                           d_label.data_ptr(), d_fail.data_ptr(), d_objq.data_ptr(), d_stats.data_ptr(),
+                           d_active=d_free.data_ptr(), stream=sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    roll_ms, coll_ms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        # per-launch kernel durations (HIP events recorded on this stream by the library)
+        roll_ms.append(eng.last_kernel_ms())
+        coll_ms.append(eng.last_collision_ms())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+
+    free = d_free.cpu().numpy().astype(bool)
+    labels = d_label.cpu().numpy().astype(bool)
+    fail = d_fail.cpu().numpy()
+    stats = d_stats.cpu().numpy()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    steps_exec = executed_steps(labels, fail, free, horizon)
+    alg = algorithmic_bytes(env.model, steps_exec, int(stats[:, 4].sum()), int(stats[:, 5].sum()))
+    roll_avg = float(np.mean(roll_ms))
+    achieved = alg / (roll_avg * 1e-3) / 1e9
+    traffic = load_traffic(steps_exec)
+    out = {
+        "metric": "grasp candidates evaluated/sec at 200-step horizon, Robotiq2F85xYCB",
+        "value": N * world * args.steps / dt,
+        "unit": "candidates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded antipodal candidates on a 003_cracker_box stand-in; rank r uses seed r)",
+        "config": {"workload": f"Robotiq2F85 x YCB 003_cracker_box, {N} candidates/GPU, collision mask + "
+                               f"{args.horizon} close-lift-shake rollout ({horizon} steps, dt 1 ms)",
+                   "candidates_per_gpu": N, "horizon_steps": horizon, "solver": env.model.options.get("solver"),
+                   "parallelism": f"batch split x{world}"},
+        "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
+                   "rollout_kernel_ms": roll_avg, "collision_kernel_ms": float(np.mean(coll_ms)),
+                   "executed_candidate_steps": steps_exec,
+                   "mean_ncon": float(stats[:, 4].sum() / max(1, steps_exec)),
+                   "mean_nefc": float(stats[:, 5].sum() / max(1, steps_exec)),
+                   "solver_iters_per_step": float(stats[:, 3].sum() / max(1, steps_exec)),
+                   "overflow_candidates": int((stats[:, 2] != 0).sum())},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic,
+                     "kernel": "mgs_rollout_kernel",
+                     "algorithmic_bytes_per_launch": alg},
+        "cpu_baseline": None,
+    }
+    if world == 1 and args.cpu_budget > 0:
+        cb = cpu_baseline(env, poses, J, h, args.cpu_budget, args.cpu_threads)
+        n = cb["n"]
+        agree = bool(np.array_equal(cb["free"], free[:n]) and np.array_equal(cb["labels"], labels[:n]))
+        out["cpu_baseline"] = {"value": cb["value"], "unit": "candidates/s", "cores": args.cpu_threads,
+                               "kind": "port",
+                               "sample": f"first {n} of the {N} candidates (mask + h200 rollouts of the "
+                                         f"collision-free ones), oracle/ C restatement, OpenMP "
+                                         f"{args.cpu_threads} threads, {cb['seconds']:.1f} s",
+                               "labels_identical_to_gpu": agree}
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -43,6 +43,7 @@ extern "C" {
 #endif
 
 #define MGS_ABI_VERSION 2
+#define MGS_NSTATS 6
 
 /* error codes */
 #define MGS_OK 0
@@ -227,7 +228,8 @@ typedef struct mgs_rollout_out {
   uint8_t* label;          /* n: 1 = every check passed */
   int32_t* fail_step;      /* n: global step index of the failed check, -1 if none */
   double* obj_qpos;        /* n * 7: object free-joint qpos when the candidate stopped (may be NULL) */
-  int32_t* stats;          /* n * 4: max ncon, max nefc, overflow flags, total solver iterations (may be NULL) */
+  int32_t* stats;          /* n * MGS_NSTATS: max ncon, max nefc, overflow flags, total solver
+                              iterations, sum of ncon and sum of nefc over executed steps (may be NULL) */
 } mgs_rollout_out;
 
 typedef struct mgs_model mgs_model;
@@ -252,6 +254,12 @@ int mgs_collision_free(mgs_batch* batch, int n, const double* qpos_init,
                        const double* mocap_pos, const double* mocap_quat,
                        int predicate, uint8_t* out_free);
 
+/* Same on device-resident inputs (HBM), asynchronous on `stream` (a
+ * hipStream_t, NULL = default stream); d_out_free: n bytes on the device. */
+int mgs_collision_free_device(mgs_batch* batch, int n, const double* d_qpos_init,
+                              const double* d_mocap_pos, const double* d_mocap_quat,
+                              int predicate, uint8_t* d_out_free, void* stream);
+
 /* Close -> lift -> shake rollout.  phase_start / phase_target: n * nphase * 3
  * mocap endpoints per candidate and phase. */
 int mgs_rollout(mgs_batch* batch, const mgs_schedule* sched, int n,
@@ -261,16 +269,22 @@ int mgs_rollout(mgs_batch* batch, const mgs_schedule* sched, int n,
 
 /* Same as mgs_rollout but with inputs already resident on the device (device
  * pointers, same layouts); outputs stay on the device.  Used to time the
- * kernel with inputs in HBM.  stream may be NULL (default stream). */
+ * kernel with inputs in HBM.  stream may be NULL (default stream).
+ * d_active (n bytes, may be NULL = all): candidates with d_active[i] == 0 are
+ * not simulated (the collision-mask rejects of filter_to_stable.py:39-44):
+ * label 0, fail_step -2, obj_qpos = the initial object pose, stats 0. */
 int mgs_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n,
                        const double* d_qpos_init, const double* d_mocap_quat,
                        const double* d_phase_start, const double* d_phase_target,
-                       uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
-                       int32_t* d_stats, void* stream);
+                       const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step,
+                       double* d_obj_qpos, int32_t* d_stats, void* stream);
 
-/* Average duration (ms) of the last timed rollout kernel launch, measured
- * with HIP events on the launch stream. */
+/* Duration (ms) of the last rollout kernel launch, measured with HIP events
+ * on the launch stream (waits for it). */
 double mgs_last_kernel_ms(mgs_batch* batch);
+
+/* Same for the last collision-mask kernel launch. */
+double mgs_last_collision_ms(mgs_batch* batch);
 
 #ifdef __cplusplus
 }

@@ -98,7 +98,7 @@ struct mgs_batch {
   double *d_qpos, *d_mpos, *d_mquat, *d_ps, *d_pt, *d_objq;
   uint8_t *d_label, *d_free;
   int32_t *d_fail, *d_stats;
-  hipEvent_t e0, e1;
+  hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
 
@@ -172,13 +172,15 @@ int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out) {
             hipMalloc(&b->d_objq, sizeof(double) * n * 7) == hipSuccess &&
             hipMalloc(&b->d_label, n) == hipSuccess && hipMalloc(&b->d_free, n) == hipSuccess &&
             hipMalloc(&b->d_fail, sizeof(int32_t) * n) == hipSuccess &&
-            hipMalloc(&b->d_stats, sizeof(int32_t) * n * 4) == hipSuccess;
+            hipMalloc(&b->d_stats, sizeof(int32_t) * n * MGS_NSTATS) == hipSuccess;
   if (!ok) {
     mgs_batch_close(b);
     return fail(MGS_ENOMEM, "device allocation failed%s");
   }
   HIPCHK(hipEventCreate(&b->e0));
   HIPCHK(hipEventCreate(&b->e1));
+  HIPCHK(hipEventCreate(&b->e2));
+  HIPCHK(hipEventCreate(&b->e3));
   *out = b;
   return MGS_OK;
 }
@@ -189,6 +191,8 @@ void mgs_batch_close(mgs_batch* b) {
   hipFree(b->d_objq); hipFree(b->d_label); hipFree(b->d_free); hipFree(b->d_fail); hipFree(b->d_stats);
   if (b->e0) hipEventDestroy(b->e0);
   if (b->e1) hipEventDestroy(b->e1);
+  if (b->e2) hipEventDestroy(b->e2);
+  if (b->e3) hipEventDestroy(b->e3);
   delete b;
 }
 
@@ -198,6 +202,24 @@ static Mdl device_model(const mgs_model* m) {
   md.I = m->dI;
   md.D = m->dD;
   return md;
+}
+
+int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, const double* d_mocap_pos,
+                              const double* d_mocap_quat, int predicate, uint8_t* d_out_free, void* stream) {
+  if (!b || n < 0) return fail(MGS_EINVAL, "mgs_collision_free_device: bad argument%s");
+  if (n == 0) return MGS_OK;
+  if (!d_qpos_init || !d_mocap_pos || !d_mocap_quat || !d_out_free) return fail(MGS_EINVAL, "null argument%s");
+  if (predicate != MGS_PRED_ANY_CONTACT && predicate != MGS_PRED_PARTITION)
+    return fail(MGS_EINVAL, "unknown contact predicate%s");
+  HIPCHK(hipSetDevice(b->m->device));
+  hipStream_t st = (hipStream_t)stream;
+  Mdl md = device_model(b->m);
+  HIPCHK(hipEventRecord(b->e2, st));
+  hipLaunchKernelGGL(mgs_collision_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, b->m->lay, n, d_qpos_init,
+                     d_mocap_pos, d_mocap_quat, predicate, d_out_free);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(b->e3, st));
+  return MGS_OK;
 }
 
 int mgs_collision_free(mgs_batch* b, int n, const double* qpos_init, const double* mocap_pos,
@@ -210,18 +232,16 @@ int mgs_collision_free(mgs_batch* b, int n, const double* qpos_init, const doubl
   HIPCHK(hipMemcpy(b->d_qpos, qpos_init, sizeof(double) * n * d.nq, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_mpos, mocap_pos, sizeof(double) * n * 3, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_mquat, mocap_quat, sizeof(double) * n * 4, hipMemcpyHostToDevice));
-  Mdl md = device_model(b->m);
-  hipLaunchKernelGGL(mgs_collision_kernel, dim3(n), dim3(64), b->m->lds_bytes, 0, md, b->m->lay, n, b->d_qpos,
-                     b->d_mpos, b->d_mquat, predicate, b->d_free);
-  HIPCHK(hipGetLastError());
+  int rc = mgs_collision_free_device(b, n, b->d_qpos, b->d_mpos, b->d_mquat, predicate, b->d_free, nullptr);
+  if (rc) return rc;
   HIPCHK(hipMemcpy(out_free, b->d_free, n, hipMemcpyDeviceToHost));
   return MGS_OK;
 }
 
 int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
                        const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
-                       uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats,
-                       void* stream) {
+                       const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
+                       int32_t* d_stats, void* stream) {
   if (!b || !sched || n < 0) return fail(MGS_EINVAL, "mgs_rollout_device: bad argument%s");
   if (sched->nphase < 1 || sched->nphase > MGS_MAX_PHASES) return fail(MGS_EINVAL, "bad phase count%s");
   if (n == 0) return MGS_OK;
@@ -230,11 +250,19 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
   Mdl md = device_model(b->m);
   HIPCHK(hipEventRecord(b->e0, st));
   hipLaunchKernelGGL(mgs_rollout_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, b->m->lay, *sched, n,
-                     d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_label, d_fail_step, d_obj_qpos,
-                     d_stats);
+                     d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, d_fail_step,
+                     d_obj_qpos, d_stats);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->e1, st));
   return MGS_OK;
+}
+
+double mgs_last_collision_ms(mgs_batch* b) {
+  if (!b) return -1.0;
+  float ms = 0.f;
+  if (hipEventSynchronize(b->e3) != hipSuccess) return -1.0;
+  if (hipEventElapsedTime(&ms, b->e2, b->e3) != hipSuccess) return -1.0;
+  return ms;
 }
 
 double mgs_last_kernel_ms(mgs_batch* b) {
@@ -260,13 +288,13 @@ int mgs_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* qp
   HIPCHK(hipMemcpy(b->d_mquat, mocap_quat, sizeof(double) * n * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_ps, phase_start, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_pt, phase_target, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
-  int rc = mgs_rollout_device(b, sched, n, b->d_qpos, b->d_mquat, b->d_ps, b->d_pt, b->d_label, b->d_fail,
-                              b->d_objq, b->d_stats, nullptr);
+  int rc = mgs_rollout_device(b, sched, n, b->d_qpos, b->d_mquat, b->d_ps, b->d_pt, nullptr, b->d_label,
+                              b->d_fail, b->d_objq, b->d_stats, nullptr);
   if (rc) return rc;
   HIPCHK(hipMemcpy(out->label, b->d_label, n, hipMemcpyDeviceToHost));
   if (out->fail_step) HIPCHK(hipMemcpy(out->fail_step, b->d_fail, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   if (out->obj_qpos) HIPCHK(hipMemcpy(out->obj_qpos, b->d_objq, sizeof(double) * n * 7, hipMemcpyDeviceToHost));
-  if (out->stats) HIPCHK(hipMemcpy(out->stats, b->d_stats, sizeof(int32_t) * n * 4, hipMemcpyDeviceToHost));
+  if (out->stats) HIPCHK(hipMemcpy(out->stats, b->d_stats, sizeof(int32_t) * n * MGS_NSTATS, hipMemcpyDeviceToHost));
   return MGS_OK;
 }
 

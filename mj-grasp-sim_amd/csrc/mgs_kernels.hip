@@ -2319,19 +2319,32 @@ mgs_collision_kernel(Mdl md, Lay lay, int n, const double* __restrict__ qpos_ini
 extern "C" __global__ void __launch_bounds__(64)
 mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __restrict__ qpos_init,
                    const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
-                   const double* __restrict__ phase_target, uint8_t* __restrict__ label,
-                   int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats) {
+                   const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
+                   uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
+                   int32_t* __restrict__ stats) {
   extern __shared__ double smem[];
   int i = blockIdx.x;
   if (i >= n) return;
   int lane = lane_id();
+  if (active && !active[i]) {
+    // collision-mask reject: not simulated (filter_to_stable.py:39-44)
+    if (lane == 0) {
+      label[i] = 0;
+      if (fail_step) fail_step[i] = -2;
+      if (stats)
+        for (int k = 0; k < MGS_NSTATS; k++) stats[MGS_NSTATS * i + k] = 0;
+    }
+    if (obj_qpos && sc.obj_qposadr >= 0 && lane < 7)
+      obj_qpos[7 * i + lane] = qpos_init[(size_t)i * md.m.nq + sc.obj_qposadr + lane];
+    return;
+  }
   Dat d;
   bind(d, smem, lay);
   int np = sc.nphase;
   const double* ps = phase_start + (size_t)i * np * 3;
   const double* pt = phase_target + (size_t)i * np * 3;
   reset(md, d, qpos_init + (size_t)i * md.m.nq, ps, mocap_quat + 4 * i);
-  int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0;
+  int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
   PROF_DECL
   for (int p = 0; p < np && ok; p++) {
     if (lane == 0)
@@ -2366,6 +2379,8 @@ mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __rest
 #endif
       if (uni(d.NCON) > maxcon) maxcon = uni(d.NCON);
       if (uni(d.NEFC) > maxefc) maxefc = uni(d.NEFC);
+      sumcon += uni(d.NCON);
+      sumefc += uni(d.NEFC);
       int ce = sc.check_every[p];
       if (ce > 0 && t > 0 && (t % ce) == 0 && !obj_contact(md, d)) { ok = 0; fstep = gstep; }
       gstep++;
@@ -2376,7 +2391,8 @@ mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __rest
     label[i] = (uint8_t)ok;
     if (fail_step) fail_step[i] = fstep;
     if (stats) {
-      stats[4 * i] = maxcon; stats[4 * i + 1] = maxefc; stats[4 * i + 2] = d.OVERFLOW; stats[4 * i + 3] = d.ITERS;
+      int32_t* st = stats + MGS_NSTATS * i;
+      st[0] = maxcon; st[1] = maxefc; st[2] = d.OVERFLOW; st[3] = d.ITERS; st[4] = sumcon; st[5] = sumefc;
     }
   }
   if (obj_qpos && sc.obj_qposadr >= 0 && lane < 7) obj_qpos[7 * i + lane] = d.qpos[sc.obj_qposadr + lane];

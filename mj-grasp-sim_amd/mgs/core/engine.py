@@ -38,11 +38,14 @@ def load_library():
     L.mgs_batch_open.argtypes = [vp, ctypes.c_int, P(vp)]
     L.mgs_batch_close.argtypes = [vp]
     L.mgs_collision_free.argtypes = [vp, ctypes.c_int, P(c_d), P(c_d), P(c_d), ctypes.c_int, P(c_u8)]
+    L.mgs_collision_free_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, vp]
     L.mgs_rollout.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d),
                               P(abi.RolloutOut)]
-    L.mgs_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mgs_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mgs_last_kernel_ms.argtypes = [vp]
     L.mgs_last_kernel_ms.restype = ctypes.c_double
+    L.mgs_last_collision_ms.argtypes = [vp]
+    L.mgs_last_collision_ms.restype = ctypes.c_double
     L.mgs_arith_probe.argtypes = [P(c_d), P(c_d), ctypes.c_int, P(c_d)]
     L.mgs_tree_probe.argtypes = [P(c_d), P(c_d), ctypes.c_int, ctypes.c_int, P(c_d)]
     L.mgs_lds_bytes.argtypes = [vp]
@@ -121,7 +124,7 @@ class Engine:
         label = np.zeros(n, np.uint8)
         fail = np.zeros(n, np.int32)
         objq = np.zeros((n, 7), np.float64)
-        stats = np.zeros((n, 4), np.int32)
+        stats = np.zeros((n, abi.MGS["MGS_NSTATS"]), np.int32)
         if n == 0:
             return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats)
         out = abi.RolloutOut(ptr(label, ctypes.c_uint8), ptr(fail, ctypes.c_int32),
@@ -136,10 +139,22 @@ class Engine:
         return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats,
                     kernel_ms=self.lib.mgs_last_kernel_ms(self._batch))
 
-    def rollout_device(self, sched, n, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats, stream=None):
-        """Launch on device pointers (ints); used by bench.py with inputs in HBM."""
+    def collision_free_device(self, n, d_qpos, d_mpos, d_mquat, d_out, predicate="any", stream=None):
+        """Asynchronous launch on device pointers (ints) with inputs resident in HBM."""
+        pr = abi.MGS["MGS_PRED_ANY_CONTACT"] if predicate == "any" else abi.MGS["MGS_PRED_PARTITION"]
+        _check(self.lib.mgs_collision_free_device(self.batch(1), n, d_qpos, d_mpos, d_mquat, pr, d_out, stream),
+               "mgs_collision_free_device")
+
+    def rollout_device(self, sched, n, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats,
+                       d_active=None, stream=None):
+        """Asynchronous launch on device pointers (ints) with inputs resident in HBM;
+        d_active (optional) masks out collision-mask rejects."""
         _check(self.lib.mgs_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps, d_pt,
-                                           d_label, d_fail, d_objq, d_stats, stream), "mgs_rollout_device")
+                                           d_active, d_label, d_fail, d_objq, d_stats, stream),
+               "mgs_rollout_device")
+
+    def last_collision_ms(self):
+        return self.lib.mgs_last_collision_ms(self._batch)
 
     def lds_bytes(self):
         return self.lib.mgs_lds_bytes(self._model)

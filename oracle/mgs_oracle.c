@@ -2108,7 +2108,7 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
       const double* ps = phase_start + (size_t)i * np * 3;
       const double* pt = phase_target + (size_t)i * np * 3;
       reset(&md, d, qpos_init + (size_t)i * desc->nq, ps, mocap_quat + 4 * i);
-      int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0;
+      int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
       for (int p = 0; p < np && ok; p++) {
         for (int u = 0; u < desc->nu; u++) d->ctrl[u] = sc->ctrl[p * 32 + u];
         int ns = sc->nsteps[p];
@@ -2118,6 +2118,8 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
           step(&md, d);
           if (d->ncon > maxcon) maxcon = d->ncon;
           if (d->nefc > maxefc) maxefc = d->nefc;
+          sumcon += d->ncon;
+          sumefc += d->nefc;
           int ce = sc->check_every[p];
           if (ce > 0 && t > 0 && (t % ce) == 0 && !obj_contact(&md, d)) { ok = 0; fstep = gstep; }
           gstep++;
@@ -2129,7 +2131,8 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
       if (obj_qpos && obj_qposadr >= 0)
         for (int k = 0; k < 7; k++) obj_qpos[7 * i + k] = d->qpos[obj_qposadr + k];
       if (stats) {
-        stats[4 * i] = maxcon; stats[4 * i + 1] = maxefc; stats[4 * i + 2] = d->overflow; stats[4 * i + 3] = d->iters;
+        int32_t* st = stats + MGS_NSTATS * i;
+        st[0] = maxcon; st[1] = maxefc; st[2] = d->overflow; st[3] = d->iters; st[4] = sumcon; st[5] = sumefc;
       }
     }
     dat_free(d);

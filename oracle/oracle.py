@@ -74,7 +74,7 @@ class OracleModel:
         label = np.zeros(n, np.uint8)
         fail = np.zeros(n, np.int32)
         objq = np.zeros((n, 7), np.float64)
-        stats = np.zeros((n, 4), np.int32)
+        stats = np.zeros((n, abi.MGS["MGS_NSTATS"]), np.int32)
         q = np.ascontiguousarray(plan.qpos_init, np.float64)
         mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
         ps = np.ascontiguousarray(plan.phase_start, np.float64)

@@ -1,7 +1,10 @@
 #!/bin/bash
-# Build libmgs_gpu.so (product) and the diagnostic stage-timer variant.
+# Build libmgs_gpu.so (product), the CPU oracle, and optionally the
+# diagnostic stage-timer variant (libmgs_gpu_prof.so): `tools/build_gpu.sh prof`.
 set -e
-cd "$(dirname "$0")/../mj-grasp-sim_amd"
-FLAGS="--offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 -Wno-unused-value -Wno-unused-result"
-hipcc $FLAGS csrc/mgs_capi.hip -o mgs/_lib/libmgs_gpu.so
-if [ "$1" == "prof" ]; then hipcc $FLAGS -DMGS_PROFILE csrc/mgs_capi.hip -o mgs/_lib/libmgs_gpu_prof.so; fi
+cd "$(dirname "$0")/.."
+if [ "$1" == "prof" ]; then
+  python -c "import __graft_entry__ as g; g.build(profile_variant=True)"
+else
+  python -c "import __graft_entry__ as g; g.build()"
+fi
