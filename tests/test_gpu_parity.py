@@ -1,0 +1,199 @@
+"""HIP engine vs the oracle, through the C-ABI (libmgs_gpu.so), on an MI355X.
+
+Bar: bit-exact.  The kernels and the oracle follow one arithmetic contract
+(-ffp-contract=off, identical operation order, pairwise tree reductions that
+mirror the wave's DPP tree, IEEE sqrt/div, polynomial sincos), so labels,
+fail steps, final object poses and solver statistics must be identical, not
+merely close.  At the full 8192-candidate size the checks are size-independent
+properties (permutation invariance, run-to-run determinism, sub-batch
+consistency) tied back to the oracle on a slice."""
+import copy
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(env):
+    return env.engine
+
+
+def _variant(env, **opts):
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    e2 = copy.copy(env)
+    e2.model = copy.copy(env.model)
+    e2.model.options = dict(env.model.options, **opts)
+    e2._engine = None
+    e2._sim = type(env._sim)(e2)
+    return e2
+
+
+def _assert_same(rg, ro, what=""):
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(rg[k], ro[k]), f"{what}: {k} differs"
+
+
+def test_arith_probe_exact():
+    from mgs.core import engine as E
+    from oracle import oracle as O
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.uniform(-20, 20, 20000), rng.uniform(-1e-3, 1e-3, 1000), [0.0, np.pi, -np.pi / 2]])
+    y = rng.uniform(0.1, 10, len(x))
+    g = E.arith_probe(x, y)
+    s, c = O.sincos(x)
+    assert np.array_equal(g[:, 0], np.sqrt(np.abs(x)))
+    assert np.array_equal(g[:, 1], x / y)
+    assert np.array_equal(g[:, 2], s) and np.array_equal(g[:, 3], c)
+
+
+def test_tree_probe_exact():
+    from mgs.core import engine as E
+    from oracle import oracle as O
+    rng = np.random.default_rng(2)
+    for n in [1, 2, 3, 5, 8, 9, 16, 17, 20, 31, 32, 33, 50, 64]:
+        a, c = rng.standard_normal((16, 64)), rng.standard_normal((16, 64))
+        dev = E.tree_probe(a, c, n)
+        ref = np.array([O.tree_dot(a[i], c[i], n) for i in range(16)])
+        assert np.array_equal(dev, ref), n
+
+
+@pytest.mark.parametrize("predicate", ["any", "partition"])
+def test_collision_mask_parity(env, eng, candidates, oracle_model, predicate):
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    assert np.array_equal(eng.collision_free(q, mp, mq, predicate=predicate),
+                          oracle_model.collision_free(q, mp, mq, predicate=predicate, nthreads=8))
+
+
+def test_collision_mask_api(env, candidates, oracle_model):
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    assert np.array_equal(env.grasp_collision_mask(poses, J), oracle_model.collision_free(q, mp, mq, nthreads=8))
+
+
+@pytest.mark.parametrize("solver", ["Newton", "PGS"])
+def test_rollout_parity_h200(env, candidates, solver):
+    from conftest import plan_for
+    from oracle import oracle as O
+    e2 = _variant(env, solver=solver)
+    om = O.OracleModel(e2.model)
+    poses, J = candidates
+    q, mp, mq, _ = e2.initial_state(poses, J)
+    idx = np.nonzero(om.collision_free(q, mp, mq, nthreads=8))[0]
+    plan = plan_for(e2, poses[idx], J[idx])
+    _assert_same(e2.engine.rollout(plan), om.rollout(plan, nthreads=8), solver)
+
+
+def test_rollout_parity_reference_horizon(env, eng, candidates, oracle_model):
+    """The reference's own 8000-step schedule (close 3000, lift 3000 checked
+    every 100, shake 500/500/1000) on a few candidates."""
+    from conftest import plan_for
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(oracle_model.collision_free(q, mp, mq, nthreads=8))[0][:3]
+    plan = plan_for(env, poses[idx], J[idx], horizon="ref8000")
+    _assert_same(eng.rollout(plan), oracle_model.rollout(plan, nthreads=8), "ref8000")
+
+
+def test_rollout_parity_unfiltered_with_overflow(env, candidates):
+    """Colliding candidates too (deep initial penetration, many contacts) with a
+    small contact cap: overflow handling must match as well."""
+    from conftest import plan_for
+    from mgs.core.engine import Engine
+    from oracle import oracle as O
+    poses, J = candidates
+    plan = plan_for(env, poses[:48], J[:48])
+    e = Engine(env.model, ncon_max=6)
+    om = O.OracleModel(env.model, ncon_max=6)
+    rg, ro = e.rollout(plan), om.rollout(plan, nthreads=8)
+    _assert_same(rg, ro, "ncon_max=6")
+    assert (rg["stats"][:, 2] != 0).any()
+
+
+def test_stability_api_and_enough_stable(env, candidates, oracle_model):
+    from conftest import plan_for
+    from mgs.env.gravityless_object_grasping import HORIZONS, apply_enough_stable
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(oracle_model.collision_free(q, mp, mq, nthreads=8))[0][:16]
+    h = HORIZONS["h200"]
+    lab = env.grasp_stability_evaluation_from_joints(poses[idx], J[idx], nstep_lift=h["nstep_lift"],
+                                                     shake_steps=h["shake_steps"], close_steps=h["close_steps"],
+                                                     lift_check_every=h["lift_check_every"], enough_stable=2)
+    ro = oracle_model.rollout(plan_for(env, poses[idx], J[idx]), nthreads=8)
+    assert np.array_equal(lab, apply_enough_stable(ro["label"], 2))
+
+
+def test_empty_and_single(env, eng, candidates):
+    from conftest import plan_for
+    from mgs.util.geo.transforms import SE3Pose
+    poses, J = candidates
+    empty = SE3Pose(np.zeros((0, 3), np.float32), np.zeros((0, 4), np.float32), "wxyz")
+    assert env.grasp_collision_mask(empty, np.zeros((0, 8))).shape == (0,)
+    assert env.grasp_stability_evaluation_from_joints(empty, np.zeros((0, 8))).shape == (0,)
+    r1 = eng.rollout(plan_for(env, poses[:1], J[:1]))
+    assert r1["label"].shape == (1,)
+
+
+def test_device_entry_with_active_mask(env, eng, candidates, oracle_model):
+    """mgs_collision_free_device + mgs_rollout_device(active) (the bench path)
+    equal the host entry points; masked candidates are reported unevaluated."""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    plan = plan_for(env, poses, J)
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+    n = len(q)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+    dq, dmp, dmq, dps, dpt = t(q), t(mp), t(mq), t(plan.phase_start), t(plan.phase_target)
+    free = torch.zeros(n, dtype=torch.uint8, device=dev)
+    lab = torch.zeros(n, dtype=torch.uint8, device=dev)
+    fail = torch.zeros(n, dtype=torch.int32, device=dev)
+    objq = torch.zeros((n, 7), dtype=torch.float64, device=dev)
+    st = torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
+    eng.collision_free_device(n, dq.data_ptr(), dmp.data_ptr(), dmq.data_ptr(), free.data_ptr())
+    eng.rollout_device(sched, n, dq.data_ptr(), dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(), lab.data_ptr(),
+                       fail.data_ptr(), objq.data_ptr(), st.data_ptr(), d_active=free.data_ptr())
+    torch.cuda.synchronize()
+    mask = free.cpu().numpy().astype(bool)
+    assert np.array_equal(mask, oracle_model.collision_free(q, mp, mq, nthreads=8))
+    idx = np.nonzero(mask)[0]
+    ro = oracle_model.rollout(plan_for(env, poses[idx], J[idx]), nthreads=8)
+    assert np.array_equal(lab.cpu().numpy().astype(bool)[idx], ro["label"])
+    assert np.array_equal(fail.cpu().numpy()[idx], ro["fail_step"])
+    assert np.array_equal(objq.cpu().numpy()[idx], ro["obj_qpos"])
+    rej = np.nonzero(~mask)[0]
+    assert np.all(lab.cpu().numpy()[rej] == 0) and np.all(fail.cpu().numpy()[rej] == -2)
+    assert np.array_equal(objq.cpu().numpy()[rej], q[rej][:, plan.obj_qposadr:plan.obj_qposadr + 7])
+
+
+def test_full_size_properties(env, eng, oracle_model):
+    """8192 candidates (the benchmark size): determinism, permutation
+    invariance and sub-batch consistency, tied to the oracle on a slice."""
+    from conftest import plan_for
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    H, J, _ = robotiq_candidates(env.obj, 8192, seed=5)
+    poses = SE3Pose.from_mat(H)
+    J = np.asarray(J, np.float64)
+    q, mp, mq, _ = env.initial_state(poses, J)
+    mask = eng.collision_free(q, mp, mq)
+    assert np.array_equal(mask, eng.collision_free(q, mp, mq))
+    idx = np.nonzero(mask)[0]
+    plan = plan_for(env, poses[idx], J[idx])
+    r1 = eng.rollout(plan)
+    r2 = eng.rollout(plan)
+    _assert_same(r1, r2, "rerun")
+    perm = np.random.default_rng(0).permutation(len(idx))
+    rp = eng.rollout(plan_for(env, poses[idx[perm]], J[idx[perm]]))
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(rp[k], r1[k][perm]), k
+    k = min(24, len(idx))
+    ro = oracle_model.rollout(plan_for(env, poses[idx[:k]], J[idx[:k]]), nthreads=8)
+    for key in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(r1[key][:k], ro[key]), key

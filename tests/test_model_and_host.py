@@ -1,0 +1,82 @@
+"""Model compiler (the MjModel.from_xml_string replacement) and the host-side
+mirror of the reference interface."""
+import numpy as np
+import pytest
+
+
+def test_robotiq_env_sizes(env):
+    cm = env.model
+    # Robotiq x object nq 22, nv 20, nbody 18, collision geoms 15 + K (K = 1)
+    assert (cm.nq, cm.nv, cm.nbody, cm.nmocap, cm.nu) == (22, 20, 18, 1, 1)
+    assert len(cm.geom_bodyid) == 16
+    assert sum({0: 3, 1: 6, 2: 1}[int(t)] for t in cm.eq_type) == 13      # 2 connect + weld + joint
+    assert len(cm.pair_geom1) == 95
+
+
+def test_option_merge_order(env):
+    o = env.model.options
+    # env XML then gripper <option>: impratio 3 -> 10, noslip 1 -> 2 (gravityless_object_grasping.py:36-42)
+    assert o["impratio"] == 10.0
+    assert o["noslip_iterations"] == 2
+    assert o["tolerance"] == 1e-8 and o["noslip_tolerance"] == 1e-8
+    assert o["cone"] == "elliptic" and o["integrator"] == "implicitfast"
+    assert list(o["gravity"]) == [0.0, 0.0, 0.0]
+
+
+def test_geom_partition(env):
+    cm = env.model
+    side = np.asarray(cm.geom_side)
+    names = cm.geom_names
+    assert side[names.index("geom:ground")] == 0
+    assert all(side[i] < 0 for i, n in enumerate(names) if n.startswith(("right_", "left_")))
+    assert side[-1] > 0                       # object geoms after the ground
+
+
+def test_invweights(env):
+    cm = env.model
+    biw, diw = cm.body_invweight0, cm.dof_invweight0
+    assert biw.shape == (cm.nbody, 2) and diw.shape == (cm.nv,)
+    assert np.all(biw[0] == 0)
+    mocap = list(cm.body_mocapid).index(0)
+    assert np.all(biw[mocap] == 0)            # world-welded
+    assert np.all(diw > 0)
+    obj = cm.body_names.index("003_cracker_box") if "003_cracker_box" in cm.body_names else cm.nbody - 1
+    # free body alone: translational inverse weight = 1 / mass
+    assert biw[obj, 0] == pytest.approx(1.0 / cm.body_mass[obj], rel=1e-9)
+
+
+def test_apply_enough_stable():
+    from mgs.env.gravityless_object_grasping import apply_enough_stable
+    lab = np.array([1, 0, 1, 1, 0, 1], bool)
+    assert apply_enough_stable(lab, None).tolist() == lab.tolist()
+    assert apply_enough_stable(lab, 2).tolist() == [True, False, True, False, False, False]
+    assert apply_enough_stable(lab, 0).tolist() == [False] * 6
+
+
+def test_horizons():
+    from mgs.env.gravityless_object_grasping import HORIZONS
+    h = HORIZONS["h200"]
+    assert h["close_steps"] + h["nstep_lift"] + 4 * h["shake_steps"] == 200
+    r = HORIZONS["ref8000"]
+    assert r["close_steps"] + r["nstep_lift"] + 4 * r["shake_steps"] == 8000
+
+
+def test_input_validation_mirrors_reference(env, candidates):
+    poses, J = candidates
+    with pytest.raises(ValueError, match="must match number of joint configurations"):
+        env.grasp_collision_mask(poses[:3], J[:2])
+    with pytest.raises(ValueError, match="incorrect dimension"):
+        env.grasp_collision_mask(poses[:2], J[:2, :5])
+    with pytest.raises(ValueError, match="must match number of joint configurations"):
+        env.grasp_stability_evaluation_from_joints(poses[:3], J[:2])
+
+
+def test_plan_layout(env, candidates):
+    from conftest import plan_for
+    poses, J = candidates
+    plan = plan_for(env, poses[:5], J[:5])
+    assert plan.horizon == 200
+    assert plan.qpos_init.shape == (5, env.model.nq)
+    assert plan.phase_start.shape == (5, 5, 3) and plan.phase_target.shape == (5, 5, 3)
+    # left shake restarts from the pre-right position (gravityless_object_grasping.py:264-272)
+    assert np.array_equal(plan.phase_start[:, 4], plan.phase_start[:, 3])

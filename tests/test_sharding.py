@@ -1,0 +1,90 @@
+"""Multi-process path on CPU (gloo, world size 2): the batch split + gather of
+mgs.env.sharding gives exactly the single-process result.  The per-rank
+compute here is the oracle (CPU); on GPUs each rank runs the HIP engine."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outq):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mj-grasp-sim_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, apply_enough_stable
+    from mgs.env.sharding import gather_results, shard_bounds
+    from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+    from mgs.obj.selector import get_object
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    from oracle import oracle as O
+    from conftest import plan_for
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
+                                    get_object("003_cracker_box"))
+    H, J, _ = robotiq_candidates(env.obj, 96, seed=3)
+    poses = SE3Pose.from_mat(H)
+    lo, hi = shard_bounds(len(poses), world, rank)
+    om = O.OracleModel(env.model)
+    q, mp, mq, _ = env.initial_state(poses[lo:hi], J[lo:hi])
+    mask = om.collision_free(q, mp, mq)
+    stable = np.zeros(hi - lo, bool)
+    idx = np.nonzero(mask)[0]
+    if len(idx):
+        stable[idx] = om.rollout(plan_for(env, poses[lo:hi][idx], J[lo:hi][idx]))["label"]
+    out = gather_results({"mask": mask, "stable": stable})
+    out["stable"] = apply_enough_stable(out["stable"], 3)
+    if rank == 0:
+        outq.put({k: v.tolist() for k, v in out.items()})
+    dist.destroy_process_group()
+
+
+def test_shard_bounds_cover():
+    from mgs.env.sharding import shard_bounds
+    for n in [0, 1, 7, 8192, 8193]:
+        for w in [1, 2, 3, 8]:
+            b = [shard_bounds(n, w, r) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+            assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
+
+
+def test_two_rank_gloo_equals_single_process(env):
+    import torch.multiprocessing as mp
+    from conftest import plan_for
+    from mgs.env.gravityless_object_grasping import apply_enough_stable
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    H, J, _ = robotiq_candidates(env.obj, 96, seed=3)
+    poses = SE3Pose.from_mat(H)
+    om = O.OracleModel(env.model)
+    qq, mpos, mq, _ = env.initial_state(poses, J)
+    mask = om.collision_free(qq, mpos, mq)
+    stable = np.zeros(len(poses), bool)
+    idx = np.nonzero(mask)[0]
+    stable[idx] = om.rollout(plan_for(env, poses[idx], J[idx]))["label"]
+    assert got["mask"] == mask.tolist()
+    assert got["stable"] == apply_enough_stable(stable, 3).tolist()
