@@ -14,6 +14,16 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+# torch (used here only to hold device buffers for the device-pointer entry
+# points) bundles its own HIP runtime; it must initialise before
+# libmgs_gpu.so pulls in /opt/rocm's, or torch finds no device.
+try:
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
+except Exception:  # pragma: no cover - CPU containers
+    pass
+
 
 @pytest.fixture(scope="module")
 def eng(env):
