@@ -110,7 +110,7 @@ const char* mgs_last_error(void) { return g_err.c_str(); }
 int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const double* dbuf, int device,
                      mgs_model** out) {
   if (!desc || !ibuf || !dbuf || !out) return fail(MGS_EINVAL, "mgs_model_create: null argument%s");
-  if (desc->nv > 64 || desc->nv < 1) return fail(MGS_EINVAL, "nv must be in [1, 64]%s");
+  if (desc->nv > MGS_MAXNV || desc->nv < 1) return fail(MGS_EINVAL, "nv must be in [1, MGS_MAXNV=32]%s");
   if (desc->cone != 1 || desc->integrator != 2)
     return fail(MGS_EINVAL, "only elliptic cones and implicitfast are supported%s");
   if (desc->nu > 32) return fail(MGS_EINVAL, "at most 32 actuators%s");
@@ -215,7 +215,7 @@ int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, co
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
   HIPCHK(hipEventRecord(b->e2, st));
-  hipLaunchKernelGGL(mgs_collision_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, b->m->lay, n, d_qpos_init,
+  hipLaunchKernelGGL(mgs_collision_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, md.I, md.D, b->m->lay, n, d_qpos_init,
                      d_mocap_pos, d_mocap_quat, predicate, d_out_free);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->e3, st));
@@ -249,7 +249,7 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
   HIPCHK(hipEventRecord(b->e0, st));
-  hipLaunchKernelGGL(mgs_rollout_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, b->m->lay, *sched, n,
+  hipLaunchKernelGGL(mgs_rollout_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, md.I, md.D, b->m->lay, *sched, n,
                      d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, d_fail_step,
                      d_obj_qpos, d_stats);
   HIPCHK(hipGetLastError());

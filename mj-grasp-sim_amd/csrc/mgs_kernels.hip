@@ -82,10 +82,16 @@ DEVI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 // Diagnostic stage timers (built only with -DMGS_PROFILE; never in the product build)
 #ifdef MGS_PROFILE
 __device__ unsigned long long g_prof[32];
-#define PROF_DECL unsigned long long _pt = __builtin_amdgcn_s_memtime(), _pacc[12] = {0,0,0,0,0,0,0,0,0,0,0,0};
-#define PROF(k) do { unsigned long long _n = __builtin_amdgcn_s_memtime(); _pacc[k] += _n - _pt; _pt = _n; } while (0)
-#define PROF_FLUSH if (lane_id() == 0) for (int _k = 0; _k < 12; _k++) atomicAdd(&g_prof[_k], _pacc[_k]);
+// per-workgroup accumulators in static LDS; PT(k) at wave-uniform points only
+__shared__ unsigned long long s_prof[33];
+#define PT(k) do { unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+    if (__lane_id() == 0) { s_prof[k] += _n - s_prof[32]; s_prof[32] = _n; } } while (0)
+#define PROF_DECL if (__lane_id() == 0) { for (int _k = 0; _k < 32; _k++) s_prof[_k] = 0; \
+    s_prof[32] = __builtin_amdgcn_s_memtime(); }
+#define PROF(k) PT(k)
+#define PROF_FLUSH if (lane_id() == 0) for (int _k = 0; _k < 32; _k++) atomicAdd(&g_prof[_k], s_prof[_k]);
 #else
+#define PT(k)
 #define PROF_DECL
 #define PROF(k)
 #define PROF_FLUSH
@@ -458,35 +464,67 @@ DEVI void crb(const Mdl& md, Dat& d) {
   wsync();
 }
 
-// dense LDL^T, columns sequential, rows across lanes (same products as oracle)
-// in place: the strict lower triangle of A is overwritten by L
-DEVI void ldl_factor(int n, double* A, double* L, double* Dv, double* Dinv) {
+// Dense LDL^T, register resident: lane i holds row i (MGS_MAXNV doubles);
+// column j's row L[j, 0:j] is broadcast from lane j with v_readlane, so a column
+// costs j scalar reads and 2j FMAs-worth of VALU with no LDS round trip.  The
+// per-element expressions are the oracle's ldl_factor():
+//   W_k = L_jk Dv_k,  D_j = A_jj - sum_k W_k L_jk,  L_ij = (A_ij - sum_k L_ik W_k) / D_j.
+// On exit the strict lower triangle of A (row-major in LDS) holds L, Dv/Dinv
+// the diagonal.  Requires n <= MGS_MAXNV (checked at model creation).
+#define MGS_MAXNV 32
+DEVI void ldl_factor(int n, double* A, double* Dv, double* Dinv) {
   int lane = lane_id();
-  for (int j = 0; j < n; j++) {
-    double dj = A[j * n + j];
-    for (int k = 0; k < j; k++) dj = dj - (L[j * n + k] * Dv[k]) * L[j * n + k];
-    double inv = 1.0 / dj;
-    for (int i = j + 1 + lane; i < n; i += WAVE) {
-      double s = A[i * n + j];
-      for (int k = 0; k < j; k++) s = s - L[i * n + k] * (L[j * n + k] * Dv[k]);
-      L[i * n + j] = s * inv;
+  double r[MGS_MAXNV];
+#pragma unroll
+  for (int k = 0; k < MGS_MAXNV; k++) r[k] = (lane < n && k < n) ? A[lane * n + k] : 0.0;
+#pragma unroll
+  for (int j = 0; j < MGS_MAXNV; j++) {
+    if (j < n) {
+      double dj = readlane_d(r[j], j);
+      double sj = r[j];
+#pragma unroll
+      for (int k = 0; k < j; k++) {
+        double l = readlane_d(r[k], j);
+        double w = l * Dv[k];
+        dj = dj - w * l;
+        sj = sj - r[k] * w;
+      }
+      double inv = 1.0 / dj;
+      if (lane > j) r[j] = sj * inv;
+      if (lane == 0) { Dv[j] = dj; Dinv[j] = inv; }
     }
-    if (lane == 0) { Dv[j] = dj; Dinv[j] = inv; }
-    wsync();
   }
+#pragma unroll
+  for (int k = 0; k < MGS_MAXNV; k++)
+    if (k < lane && lane < n) A[lane * n + k] = r[k];
+  wsync();
 }
-// single-lane solve, y: scratch of n doubles (LDS)
-DEVI void ldl_solve(int n, const double* L, const double* Dinv, const double* b, double* x, double* y) {
-  for (int i = 0; i < n; i++) {
-    double s = b[i];
-    for (int k = 0; k < i; k++) s = s - L[i * n + k] * y[k];
-    y[i] = s;
+
+// x = (L D L^T)^-1 b, all lanes (lane i owns x_i).  Forward substitution
+// column by column (y_k broadcast, lanes i > k subtract L_ik y_k: the oracle's
+// ascending-k order per row), then backward with k descending (oracle order).
+// b and x may alias.
+DEVI void ldl_solve(int n, const double* L, const double* Dinv, const double* b, double* x) {
+  int lane = lane_id();
+  double acc = (lane < n) ? b[lane] : 0.0;
+#pragma unroll
+  for (int k = 0; k < MGS_MAXNV; k++) {
+    if (k < n) {
+      double yk = readlane_d(acc, k);
+      if (lane > k && lane < n) acc = acc - L[lane * n + k] * yk;
+    }
   }
-  for (int i = n - 1; i >= 0; i--) {
-    double s = y[i] * Dinv[i];
-    for (int k = i + 1; k < n; k++) s = s - L[k * n + i] * x[k];
-    x[i] = s;
+  acc = (lane < n) ? acc * Dinv[lane] : 0.0;
+#pragma unroll
+  for (int k = MGS_MAXNV - 1; k >= 0; k--) {
+    if (k < n) {
+      double xk = readlane_d(acc, k);
+      if (lane < k) acc = acc - L[k * n + lane] * xk;
+    }
   }
+  wsync();
+  if (lane < n) x[lane] = acc;
+  wsync();
 }
 
 // actuation (lane 0)
@@ -592,37 +630,101 @@ DEVI void rne(const Mdl& md, Dat& d) {
 // collision
 struct SupPt { double v[3], a[3], b[3]; };
 
-// wave-parallel support mapping: all lanes pass the same dir, all lanes get the result
-DEVI int support_geom(const Mdl& md, const Dat& d, int g, const double* dir, double* out) {
+// wave-parallel support mapping (oracle support_geom()): argmax over hull
+// vertices of v.dl, ties -> smallest index.  Lanes stride the vertices and keep
+// their best vertex in registers; the (value, index) pair is reduced with DPP
+// inside each 16-lane row (max with index tie-break is order independent), the
+// four row winners are combined uniformly, and the winning vertex is read from
+// its lane (index & 63) -- no shuffle through LDS, no dependent global reload.
+struct SupAcc {
+  double best, vx, vy, vz;
+  int bi;
+};
+DEVI void sup_init(SupAcc& a) { a.best = -INFINITY; a.bi = 0x7fffffff; a.vx = a.vy = a.vz = 0.0; }
+DEVI void sup_take(SupAcc& a, double ob, int oi) {
+  if (ob > a.best || (ob == a.best && oi < a.bi)) { a.best = ob; a.bi = oi; }
+}
+DEVI void sup_dpp_level(SupAcc& a, int sel) {
+  double ob = dpp_d(a.best, sel);
+  int oi;
+  switch (sel) {
+    case 0: oi = __builtin_amdgcn_mov_dpp(a.bi, 0xB1, 0xF, 0xF, false); break;
+    case 1: oi = __builtin_amdgcn_mov_dpp(a.bi, 0x4E, 0xF, 0xF, false); break;
+    case 2: oi = __builtin_amdgcn_mov_dpp(a.bi, 0x141, 0xF, 0xF, false); break;
+    default: oi = __builtin_amdgcn_mov_dpp(a.bi, 0x140, 0xF, 0xF, false); break;
+  }
+  sup_take(a, ob, oi);
+}
+// reduce and return the winning local-frame vertex (uniform)
+DEVI void sup_finish(SupAcc& a, double* v) {
+  // lanes keep their own best vertex; the wave winner's lane holds it
+  double lb = a.best;
+  int li = a.bi;
+  sup_dpp_level(a, 0);
+  sup_dpp_level(a, 1);
+  sup_dpp_level(a, 2);
+  sup_dpp_level(a, 3);
+  double b0 = readlane_d(a.best, 0), b1 = readlane_d(a.best, 16), b2 = readlane_d(a.best, 32),
+         b3 = readlane_d(a.best, 48);
+  int i0 = __builtin_amdgcn_readlane(a.bi, 0), i1 = __builtin_amdgcn_readlane(a.bi, 16),
+      i2 = __builtin_amdgcn_readlane(a.bi, 32), i3 = __builtin_amdgcn_readlane(a.bi, 48);
+  SupAcc u;
+  u.best = b0; u.bi = i0;
+  sup_take(u, b1, i1);
+  sup_take(u, b2, i2);
+  sup_take(u, b3, i3);
+  (void)lb; (void)li;
+  int bi = (u.bi == 0x7fffffff) ? 0 : u.bi;
+  int wl = bi & (WAVE - 1);
+  v[0] = readlane_d(a.vx, wl);
+  v[1] = readlane_d(a.vy, wl);
+  v[2] = readlane_d(a.vz, wl);
+  a.bi = bi;
+}
+
+// supports of geom g1 along dir and geom g2 along -dir in one pass (two
+// independent reductions interleaved); results in world frame
+DEVI void support_pair(const Mdl& md, const Dat& d, int g1, int g2, const double* dir, double* out1,
+                       double* out2) {
   int lane = lane_id();
-  int h = IA(md, geom_hullid)[g];
-  int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
-  const double* V = DA(md, hull_vert) + 3 * adr;
-  const double* R = d.geom_xmat + 9 * g;
-  double dl[3];
-  mulmtv3(dl, R, dir);
-  double best = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int i = lane; i < num; i += WAVE) {
-    double s = (V[3 * i] * dl[0] + V[3 * i + 1] * dl[1]) + V[3 * i + 2] * dl[2];
-    if (s > best) { best = s; bi = i; }
+  const int32_t *ghull = IA(md, geom_hullid), *hadr = IA(md, hull_vertadr), *hnum = IA(md, hull_vertnum);
+  int h1 = ghull[g1], h2 = ghull[g2];
+  int n1 = hnum[h1], n2 = hnum[h2];
+  const double* V1 = DA(md, hull_vert) + 3 * hadr[h1];
+  const double* V2 = DA(md, hull_vert) + 3 * hadr[h2];
+  const double* R1 = d.geom_xmat + 9 * g1;
+  const double* R2 = d.geom_xmat + 9 * g2;
+  double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  double dl1[3], dl2[3];
+  mulmtv3(dl1, R1, dir);
+  mulmtv3(dl2, R2, nd);
+  SupAcc a1, a2;
+  sup_init(a1);
+  sup_init(a2);
+  int nmax = n1 > n2 ? n1 : n2;
+  for (int i = lane; i < nmax; i += WAVE) {
+    if (i < n1) {
+      double x = V1[3 * i], y = V1[3 * i + 1], z = V1[3 * i + 2];
+      double sc = (x * dl1[0] + y * dl1[1]) + z * dl1[2];
+      if (sc > a1.best) { a1.best = sc; a1.bi = i; a1.vx = x; a1.vy = y; a1.vz = z; }
+    }
+    if (i < n2) {
+      double x = V2[3 * i], y = V2[3 * i + 1], z = V2[3 * i + 2];
+      double sc = (x * dl2[0] + y * dl2[1]) + z * dl2[2];
+      if (sc > a2.best) { a2.best = sc; a2.bi = i; a2.vx = x; a2.vy = y; a2.vz = z; }
+    }
   }
-  for (int s = 32; s >= 1; s >>= 1) {
-    double ob = __shfl_xor(best, s);
-    int oi = __shfl_xor(bi, s);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-  }
-  if (bi == 0x7fffffff) bi = 0;
-  double t[3];
-  mulmv3(t, R, V + 3 * bi);
-  add3(out, d.geom_xpos + 3 * g, t);
-  return bi;
+  double v1[3], v2[3], t[3];
+  sup_finish(a1, v1);
+  sup_finish(a2, v2);
+  mulmv3(t, R1, v1);
+  add3(out1, d.geom_xpos + 3 * g1, t);
+  mulmv3(t, R2, v2);
+  add3(out2, d.geom_xpos + 3 * g2, t);
 }
 
 DEVI void mink_support(const Mdl& md, const Dat& d, int g1, int g2, const double* dir, SupPt* p) {
-  double nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support_geom(md, d, g1, dir, p->a);
-  support_geom(md, d, g2, nd, p->b);
+  support_pair(md, d, g1, g2, dir, p->a, p->b);
   sub3(p->v, p->a, p->b);
 }
 
@@ -778,9 +880,18 @@ DEVI int feature(const Mdl& md, const Dat& d, int g, const double* n, const doub
     double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
     if (sign > 0 ? (s > best) : (s < best)) best = s;
   }
-  for (int s = 32; s >= 1; s >>= 1) {
-    double ob = __shfl_xor(best, s);
+  // extreme over the wave: DPP inside 16-lane rows, then the four row values
+#pragma unroll
+  for (int sel = 0; sel < 4; sel++) {
+    double ob = dpp_d(best, sel);
     if (sign > 0 ? (ob > best) : (ob < best)) best = ob;
+  }
+  {
+    double r1 = readlane_d(best, 16), r2 = readlane_d(best, 32), r3 = readlane_d(best, 48);
+    best = readlane_d(best, 0);
+    if (sign > 0 ? (r1 > best) : (r1 < best)) best = r1;
+    if (sign > 0 ? (r2 > best) : (r2 < best)) best = r2;
+    if (sign > 0 ? (r3 > best) : (r3 < best)) best = r3;
   }
   *ext = best;
   double lim = (sign > 0) ? best - tol : best + tol;
@@ -926,7 +1037,9 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   int lane = lane_id();
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
   double n[3], depth, mpos[3];
-  if (!mpr_penetration(md, d, g1, g2, n, &depth, mpos)) return;
+  int hit = mpr_penetration(md, d, g1, g2, n, &depth, mpos);
+  PT(4);
+  if (!hit) return;
   double t1[3], t2[3];
   make_frame(n, t1, t2);
   P2* fa = d.poly;                 // K_MAXPOLY each
@@ -998,6 +1111,7 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
     }
   }
   wsync();
+  PT(5);
 }
 
 // broadphase over all admissible pairs (lanes over pairs), then narrowphase in pair order
@@ -1029,6 +1143,7 @@ DEVI void collision(const Mdl& md, Dat& d) {
         if (fabs(c[0][k] - c[1][k]) > (hw[0][k] + hw[1][k]) + pm[p]) ov = 0;
     }
     unsigned long long mask = __ballot(ov);
+    PT(3);
     while (mask) {
       int b = __ffsll((long long)mask) - 1;
       mask &= mask - 1ull;
@@ -1381,6 +1496,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   wsync();
   if (lane == 0) ints[7] = d.NEFC;
   wsync();
+  PT(9);
   int ne = uni(d.NEFC);
   // per row (lanes over rows): vel, J.qacc_smooth, G in place, A
   for (int r = lane; r < ne; r += WAVE) {
@@ -1401,6 +1517,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     d.efc_A[r] = a;
   }
   wsync();
+  PT(10);
   if (lane == 0) {
     diag_approx(md, d, ne);
     const double *eqsr = DA(md, eq_solref), *eqsi = DA(md, eq_solimp);
@@ -1450,6 +1567,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     r += dim;
   }
   wsync();
+  PT(11);
 }
 
 // ---------------------------------------------------------------------------
@@ -2086,6 +2204,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     wsync();
   }
   newton_grad(md, d, d.nw);
+  PT(12);
   int npair = (nv * (nv + 1)) / 2;
   int it;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
@@ -2114,9 +2233,9 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
       d.nH[j * nv + i] = hv;
     }
     wsync();
-    ldl_factor(nv, d.nH, d.nH, d.tmp, d.tmp2);
-    if (lane == 0) ldl_solve(nv, d.nH, d.tmp2, d.ng, d.ndir, d.scratch);
-    wsync();
+    PT(13);
+    ldl_factor(nv, d.nH, d.tmp, d.tmp2);
+    ldl_solve(nv, d.nH, d.tmp2, d.ng, d.ndir);
     if (lane < nv) d.ndir[lane] = -d.ndir[lane];
     wsync();
     for (int r = lane; r < ne; r += WAVE) {
@@ -2126,6 +2245,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
       d.efc_jv[r] = s;
     }
     wsync();
+    PT(14);
     double dl = (lane < nv) ? d.ndir[lane] : 0.0;
     double q = (lane < nv) ? d.nw[lane] - d.nw0[lane] : 0.0;
     double A1 = tree_sum(q * dl, P);
@@ -2147,6 +2267,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
         alpha = an;
       }
     }
+    PT(15);
     if (!(alpha > 0.0)) { it++; break; }
     if (lane < nv) d.nw[lane] = d.nw[lane] + alpha * dl;
     wsync();
@@ -2156,6 +2277,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     C = Cn;
     double gl = (lane < nv) ? d.ng[lane] : 0.0;
     double gn = scale * sqrt(tree_sum(gl * gl, P));
+    PT(16);
     if (improvement < md.m.tolerance || gn < md.m.tolerance) { it++; break; }
   }
   if (lane == 0) d.ITERS += it;
@@ -2179,8 +2301,11 @@ DEVI void solve(const Mdl& md, Dat& d) {
   double fr0, fr1, u;
   if (md.m.solver == 0) solve_pgs(md, d, scale, fr0, fr1, u);
   else solve_newton(md, d, scale, fr0, fr1, u);
+  PT(16);
   noslip(md, d, scale, fr0, fr1, u);
+  PT(17);
   finalize_solution(md, d, u);
+  PT(18);
 }
 
 // ---------------------------------------------------------------------------
@@ -2194,7 +2319,7 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
   collision(md, d);
   if (!full) return;
   crb(md, d);
-  ldl_factor(nv, d.M, d.M, d.Dv, d.Dinv);
+  ldl_factor(nv, d.M, d.Dv, d.Dinv);
   for (int k = lane; k < nv; k += WAVE) {
     double sd = sqrt(d.Dv[k]);
     d.sD[k] = sd;
@@ -2205,9 +2330,9 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
     passive(md, d);
     rne(md, d);
     for (int k = 0; k < nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
-    ldl_solve(nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth, d.tmp);
   }
   wsync();
+  ldl_solve(nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
   make_constraints(md, d);
   solve(md, d);
 }
@@ -2217,6 +2342,7 @@ DEVI void integrate(const Mdl& md, Dat& d) {
   double dt = md.m.timestep;
   // recompute M (it was factored in place), then MI = M - dt*qDeriv
   crb(md, d);
+  PT(19);
   if (lane == 0) {
     for (int i = 0; i < nv * nv; i++) d.qDeriv[i] = 0.0;
     const double* damp = DA(md, dof_damping);
@@ -2242,12 +2368,13 @@ DEVI void integrate(const Mdl& md, Dat& d) {
   wsync();
   for (int i = lane; i < nv * nv; i += WAVE) d.M[i] = d.M[i] - dt * d.qDeriv[i];
   wsync();
-  ldl_factor(nv, d.M, d.M, d.Dv, d.Dinv);
+  PT(20);
+  ldl_factor(nv, d.M, d.Dv, d.Dinv);
+  double* qa = d.scratch;
+  for (int k = lane; k < nv; k += WAVE) qa[k] = d.qfrc_smooth[k] + d.qfrc_constraint[k];
+  wsync();
+  ldl_solve(nv, d.M, d.Dinv, qa, qa);
   if (lane == 0) {
-    double* rhs = d.tmp2;
-    double* qa = d.scratch;
-    for (int k = 0; k < nv; k++) rhs[k] = d.qfrc_smooth[k] + d.qfrc_constraint[k];
-    ldl_solve(nv, d.M, d.Dinv, rhs, qa, d.tmp);
     for (int k = 0; k < nv; k++) d.qvel[k] = d.qvel[k] + dt * qa[k];
     const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
     for (int j = 0; j < md.m.njnt; j++) {
@@ -2300,10 +2427,14 @@ DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mp
 // ---------------------------------------------------------------------------
 // kernels: one 64-lane workgroup per candidate
 extern "C" __global__ void __launch_bounds__(64)
-mgs_collision_kernel(Mdl md, Lay lay, int n, const double* __restrict__ qpos_init,
+mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
+                     const double* __restrict__ qpos_init,
                      const double* __restrict__ mocap_pos, const double* __restrict__ mocap_quat, int predicate,
                      uint8_t* __restrict__ out) {
   extern __shared__ double smem[];
+  Mdl md = mdarg;
+  md.I = mI;
+  md.D = mD;
   int i = blockIdx.x;
   if (i >= n) return;
   Dat d;
@@ -2317,12 +2448,16 @@ mgs_collision_kernel(Mdl md, Lay lay, int n, const double* __restrict__ qpos_ini
 }
 
 extern "C" __global__ void __launch_bounds__(64)
-mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __restrict__ qpos_init,
+mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
+                   mgs_schedule sc, int n, const double* __restrict__ qpos_init,
                    const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
                    const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
                    uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
                    int32_t* __restrict__ stats) {
   extern __shared__ double smem[];
+  Mdl md = mdarg;
+  md.I = mI;
+  md.D = mD;
   int i = blockIdx.x;
   if (i >= n) return;
   int lane = lane_id();
@@ -2356,23 +2491,26 @@ mgs_rollout_kernel(Mdl md, Lay lay, mgs_schedule sc, int n, const double* __rest
         for (int k = 0; k < 3; k++) d.mocap_pos[k] = ps[3 * p + k] + (pt[3 * p + k] - ps[3 * p + k]) * frac;
       wsync();
 #ifdef MGS_PROFILE
-      PROF(0);
-      if (lane == 0) { kinematics(md, d); com_pos(md, d); }
-      wsync(); PROF(1);
-      collision(md, d); PROF(2);
-      crb(md, d);
-      ldl_factor(md.m.nv, d.M, d.M, d.Dv, d.Dinv);
+      PT(0);
+      if (lane == 0) kinematics(md, d);
+      wsync(); PT(1);
+      if (lane == 0) com_pos(md, d);
+      wsync(); PT(2);
+      collision(md, d); PT(5);
+      crb(md, d); PT(6);
+      ldl_factor(md.m.nv, d.M, d.Dv, d.Dinv);
       for (int k = lane; k < md.m.nv; k += WAVE) { double sd = sqrt(d.Dv[k]); d.sD[k] = sd; d.isD[k] = 1.0 / sd; }
-      PROF(3);
+      wsync(); PT(7);
       if (lane == 0) {
         actuation(md, d); passive(md, d); rne(md, d);
         for (int k = 0; k < md.m.nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
-        ldl_solve(md.m.nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth, d.tmp);
       }
-      wsync(); PROF(4);
-      make_constraints(md, d); PROF(5);
-      solve(md, d); PROF(6);
-      integrate(md, d); PROF(7);
+      wsync();
+      ldl_solve(md.m.nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
+      PT(8);
+      make_constraints(md, d);
+      solve(md, d);
+      integrate(md, d); PT(21);
 #else
       forward(md, d, 1);
       integrate(md, d);

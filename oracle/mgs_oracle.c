@@ -506,9 +506,10 @@ static void ldl_solve(int n, const double* L, const double* Dinv, const double* 
     for (int k = 0; k < i; k++) s = s - L[i * n + k] * y[k];
     y[i] = s;
   }
+  /* backward substitution, k descending (the kernel's column order) */
   for (int i = n - 1; i >= 0; i--) {
     double s = y[i] * Dinv[i];
-    for (int k = i + 1; k < n; k++) s = s - L[k * n + i] * x[k];
+    for (int k = n - 1; k > i; k--) s = s - L[k * n + i] * x[k];
     x[i] = s;
   }
 }
