@@ -83,6 +83,34 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
 }
 }  // namespace
 
+// dof counts with a compiled kernel instantiation (Robotiq 2F-85 + free object = 20)
+#define MGS_NV_LIST(X) X(20)
+
+static bool nv_supported(int nv) {
+  switch (nv) {
+#define MGS_CASE(NV_) case NV_: return true;
+    MGS_NV_LIST(MGS_CASE)
+#undef MGS_CASE
+    default: return false;
+  }
+}
+
+static hipError_t set_lds_limit(int nv, int bytes) {
+  switch (nv) {
+#define MGS_CASE(NV_)                                                                                      \
+  case NV_: {                                                                                              \
+    hipError_t e = hipFuncSetAttribute((const void*)mgs_rollout_kernel<NV_>,                               \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);                 \
+    if (e != hipSuccess) return e;                                                                         \
+    return hipFuncSetAttribute((const void*)mgs_collision_kernel<NV_>,                                     \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);                         \
+  }
+    MGS_NV_LIST(MGS_CASE)
+#undef MGS_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
 struct mgs_model {
   mgs_model_desc desc;
   int device;
@@ -110,7 +138,7 @@ const char* mgs_last_error(void) { return g_err.c_str(); }
 int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const double* dbuf, int device,
                      mgs_model** out) {
   if (!desc || !ibuf || !dbuf || !out) return fail(MGS_EINVAL, "mgs_model_create: null argument%s");
-  if (desc->nv > MGS_MAXNV || desc->nv < 1) return fail(MGS_EINVAL, "nv must be in [1, MGS_MAXNV=32]%s");
+  if (!nv_supported(desc->nv)) return fail(MGS_EINVAL, "no kernel instantiated for this nv (MGS_NV_LIST)%s");
   if (desc->cone != 1 || desc->integrator != 2)
     return fail(MGS_EINVAL, "only elliptic cones and implicitfast are supported%s");
   if (desc->nu > 32) return fail(MGS_EINVAL, "at most 32 actuators%s");
@@ -140,10 +168,7 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
     snprintf(buf, sizeof(buf), "%zu", need);
     return fail(MGS_ECAPACITY, "per-candidate working set %s B exceeds 160 KiB LDS; lower ncon_max", buf);
   }
-  HIPCHK(hipFuncSetAttribute((const void*)mgs_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)m->lds_bytes));
-  HIPCHK(hipFuncSetAttribute((const void*)mgs_collision_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)m->lds_bytes));
+  HIPCHK(set_lds_limit(desc->nv, (int)m->lds_bytes));
   *out = m;
   return MGS_OK;
 }
@@ -215,8 +240,14 @@ int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, co
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
   HIPCHK(hipEventRecord(b->e2, st));
-  hipLaunchKernelGGL(mgs_collision_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, md.I, md.D, b->m->lay, n, d_qpos_init,
-                     d_mocap_pos, d_mocap_quat, predicate, d_out_free);
+#define MGS_LAUNCH_COLL(NV_) hipLaunchKernelGGL(mgs_collision_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
+      md.I, md.D, b->m->lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free)
+  switch (md.m.nv) {
+#define MGS_CASE(NV_) case NV_: MGS_LAUNCH_COLL(NV_); break;
+    MGS_NV_LIST(MGS_CASE)
+#undef MGS_CASE
+    default: return fail(MGS_EINVAL, "no kernel for this nv%s");
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->e3, st));
   return MGS_OK;
@@ -249,9 +280,15 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
   HIPCHK(hipEventRecord(b->e0, st));
-  hipLaunchKernelGGL(mgs_rollout_kernel, dim3(n), dim3(64), b->m->lds_bytes, st, md, md.I, md.D, b->m->lay, *sched, n,
-                     d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, d_fail_step,
-                     d_obj_qpos, d_stats);
+#define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
+      md.I, md.D, b->m->lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
+      d_fail_step, d_obj_qpos, d_stats)
+  switch (md.m.nv) {
+#define MGS_CASE(NV_) case NV_: MGS_LAUNCH_ROLL(NV_); break;
+    MGS_NV_LIST(MGS_CASE)
+#undef MGS_CASE
+    default: return fail(MGS_EINVAL, "no kernel for this nv%s");
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->e1, st));
   return MGS_OK;

@@ -464,66 +464,81 @@ DEVI void crb(const Mdl& md, Dat& d) {
   wsync();
 }
 
-// Dense LDL^T, register resident: lane i holds row i (MGS_MAXNV doubles);
+// Dense LDL^T, register resident: lane i holds row i (NV doubles);
 // column j's row L[j, 0:j] is broadcast from lane j with v_readlane, so a column
 // costs j scalar reads and 2j FMAs-worth of VALU with no LDS round trip.  The
 // per-element expressions are the oracle's ldl_factor():
 //   W_k = L_jk Dv_k,  D_j = A_jj - sum_k W_k L_jk,  L_ij = (A_ij - sum_k L_ik W_k) / D_j.
 // On exit the strict lower triangle of A (row-major in LDS) holds L, Dv/Dinv
-// the diagonal.  Requires n <= MGS_MAXNV (checked at model creation).
-#define MGS_MAXNV 32
-DEVI void ldl_factor(int n, double* A, double* Dv, double* Dinv) {
+// the diagonal.
+// NV: the model's dof count as a compile-time constant (kernels are
+// instantiated per supported nv, see MGS_NV_LIST in mgs_capi.hip), so the
+// register rows and their loops are fully static.
+template <int NV>
+DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
   int lane = lane_id();
-  double r[MGS_MAXNV];
 #pragma unroll
-  for (int k = 0; k < MGS_MAXNV; k++) r[k] = (lane < n && k < n) ? A[lane * n + k] : 0.0;
+  for (int j = 0; j < NV; j++) {
+    double dj = readlane_d(r[j], j);
+    double sj = r[j];
 #pragma unroll
-  for (int j = 0; j < MGS_MAXNV; j++) {
-    if (j < n) {
-      double dj = readlane_d(r[j], j);
-      double sj = r[j];
-#pragma unroll
-      for (int k = 0; k < j; k++) {
-        double l = readlane_d(r[k], j);
-        double w = l * Dv[k];
-        dj = dj - w * l;
-        sj = sj - r[k] * w;
-      }
-      double inv = 1.0 / dj;
-      if (lane > j) r[j] = sj * inv;
-      if (lane == 0) { Dv[j] = dj; Dinv[j] = inv; }
+    for (int k = 0; k < j; k++) {
+      double l = readlane_d(r[k], j);
+      double w = l * Dv[k];
+      dj = dj - w * l;
+      sj = sj - r[k] * w;
     }
+    double inv = 1.0 / dj;
+    if (lane > j) r[j] = sj * inv;
+    if (lane == 0) { Dv[j] = dj; Dinv[j] = inv; }
   }
+}
+template <int NV>
+DEVI void store_lower(double* A, const double (&r)[NV]) {
+  int lane = lane_id();
+  if (lane < NV) {
 #pragma unroll
-  for (int k = 0; k < MGS_MAXNV; k++)
-    if (k < lane && lane < n) A[lane * n + k] = r[k];
+    for (int k = 0; k < NV; k++)
+      if (k < lane) A[lane * NV + k] = r[k];
+  }
   wsync();
+}
+template <int NV>
+DEVI void ldl_factor(double* A, double* Dv, double* Dinv) {
+  int lane = lane_id();
+  int li = lane < NV ? lane : 0;
+  double r[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) r[k] = A[li * NV + k];
+  ldl_factor_regs<NV>(r, Dv, Dinv);
+  store_lower<NV>(A, r);
 }
 
 // x = (L D L^T)^-1 b, all lanes (lane i owns x_i).  Forward substitution
 // column by column (y_k broadcast, lanes i > k subtract L_ik y_k: the oracle's
 // ascending-k order per row), then backward with k descending (oracle order).
 // b and x may alias.
-DEVI void ldl_solve(int n, const double* L, const double* Dinv, const double* b, double* x) {
+template <int NV>
+DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double* x) {
   int lane = lane_id();
-  double acc = (lane < n) ? b[lane] : 0.0;
+  int li = lane < NV ? lane : 0;
+  double Lr[NV], Lc[NV];
 #pragma unroll
-  for (int k = 0; k < MGS_MAXNV; k++) {
-    if (k < n) {
-      double yk = readlane_d(acc, k);
-      if (lane > k && lane < n) acc = acc - L[lane * n + k] * yk;
-    }
+  for (int k = 0; k < NV; k++) { Lr[k] = L[li * NV + k]; Lc[k] = L[k * NV + li]; }
+  double acc = b[li];
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    double yk = readlane_d(acc, k);
+    if (lane > k) acc = acc - Lr[k] * yk;
   }
-  acc = (lane < n) ? acc * Dinv[lane] : 0.0;
+  acc = acc * Dinv[li];
 #pragma unroll
-  for (int k = MGS_MAXNV - 1; k >= 0; k--) {
-    if (k < n) {
-      double xk = readlane_d(acc, k);
-      if (lane < k) acc = acc - L[k * n + lane] * xk;
-    }
+  for (int k = NV - 1; k >= 0; k--) {
+    double xk = readlane_d(acc, k);
+    if (lane < k) acc = acc - Lc[k] * xk;
   }
   wsync();
-  if (lane < n) x[lane] = acc;
+  if (lane < NV) x[lane] = acc;
   wsync();
 }
 
@@ -1114,6 +1129,38 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   PT(5);
 }
 
+#define OBB_FN DEVI
+/* Second broadphase stage: separating-axis test between the geoms' oriented
+ * bounding boxes (their local AABBs posed in the world; 15 axes).  Each convex
+ * hull lies inside its box, so separated boxes cannot produce a contact and the
+ * narrowphase is skipped (MuJoCo would run MPR and find nothing; on the round-1
+ * benchmark this removes ~55% of narrowphase calls).  Returns 1 if separated. */
+OBB_FN int obb_separated(const double* R1, const double* x1, const double* b1, const double* R2,
+                         const double* x2, const double* b2, double margin) {
+  double c1[3], c2[3], t[3], D[3];
+  mulmv3(t, R1, b1);
+  add3(c1, x1, t);
+  mulmv3(t, R2, b2);
+  add3(c2, x2, t);
+  sub3(D, c2, c1);
+  const double *h1 = b1 + 3, *h2 = b2 + 3;
+  double A1[9], A2[9];  /* box axes as rows: A[k] = column k of R */
+  for (int k = 0; k < 3; k++)
+    for (int i = 0; i < 3; i++) { A1[3 * k + i] = R1[3 * i + k]; A2[3 * k + i] = R2[3 * i + k]; }
+  for (int q = 0; q < 15; q++) {
+    double L[3];
+    if (q < 3) { L[0] = A1[3 * q]; L[1] = A1[3 * q + 1]; L[2] = A1[3 * q + 2]; }
+    else if (q < 6) { L[0] = A2[3 * (q - 3)]; L[1] = A2[3 * (q - 3) + 1]; L[2] = A2[3 * (q - 3) + 2]; }
+    else { int a = (q - 6) / 3, b = (q - 6) % 3; cross3(L, A1 + 3 * a, A2 + 3 * b); }
+    double ll = dot3(L, L);
+    if (ll < 1e-20) continue;
+    double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));
+    double r2 = (h2[0] * fabs(dot3(A2, L)) + h2[1] * fabs(dot3(A2 + 3, L))) + h2[2] * fabs(dot3(A2 + 6, L));
+    if (fabs(dot3(D, L)) > (r1 + r2) + (margin + 1e-12) * sqrt(ll)) return 1;
+  }
+  return 0;
+}
+
 // broadphase over all admissible pairs (lanes over pairs), then narrowphase in pair order
 DEVI void collision(const Mdl& md, Dat& d) {
   int lane = lane_id();
@@ -1141,6 +1188,9 @@ DEVI void collision(const Mdl& md, Dat& d) {
       ov = 1;
       for (int k = 0; k < 3; k++)
         if (fabs(c[0][k] - c[1][k]) > (hw[0][k] + hw[1][k]) + pm[p]) ov = 0;
+      if (ov && obb_separated(d.geom_xmat + 9 * g[0], d.geom_xpos + 3 * g[0], aabb + 6 * g[0],
+                              d.geom_xmat + 9 * g[1], d.geom_xpos + 3 * g[1], aabb + 6 * g[1], pm[p]))
+        ov = 0;
     }
     unsigned long long mask = __ballot(ov);
     PT(3);
@@ -2168,6 +2218,7 @@ DEVI void ls_eval(const Dat& d, int ne, double alpha, double A1, double A2, doub
   *d2 = A2 + tree_rows(c2[0], c2[1], ne);
 }
 
+template <int NV>
 DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
@@ -2208,34 +2259,46 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   int npair = (nv * (nv + 1)) / 2;
   int it;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
-    // Hessian I + G' h G: lanes over lower-triangle entries, blocks in row order
-    for (int e = lane; e < npair; e += WAVE) {
-      int i = 0, j = e;
-      while (j > i) { j -= i + 1; i++; }
-      double s = 0.0;
+    // Hessian I + G' h G: lane i accumulates row i (j <= i) in registers over the
+    // row blocks in order (quad rows: (G_ri Dr) G_rj; cone blocks: x_b = sum_a
+    // G_{a,i} hb_ab, then x_b G_bj), then factors it in place (register LDL).
+    {
+      double hr[NV];
+#pragma unroll
+      for (int j = 0; j < NV; j++) hr[j] = 0.0;
+      int li = lane < nv ? lane : 0;
+      asm volatile("; HESS_BEGIN");
       for (int r = 0; r < ne;) {
         int t = uni(d.efc_type[r]);
         int dim = (t == MGS_EFC_CONTACT) ? uni(d.efc_dim[r]) : 1;
         int st = uni(d.efc_state[r]);
         if (dim > 1 && st == ST_CONE) {
           const double* hb = d.con_hb + 16 * uni(d.efc_con[r]);
-          for (int a = 0; a < dim; a++)
-            for (int b = 0; b < dim; b++)
-              s = s + (d.G[(r + a) * nv + i] * hb[a * dim + b]) * d.G[(r + b) * nv + j];
+          for (int b = 0; b < dim; b++) {
+            double x = 0.0;
+            for (int a = 0; a < dim; a++) x = x + d.G[(r + a) * nv + li] * hb[a * dim + b];
+            const double* Gb = d.G + (r + b) * nv;
+#pragma unroll
+            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * Gb[j];
+          }
         } else if (st == ST_QUAD) {
-          for (int a = 0; a < dim; a++)
-            s = s + (d.G[(r + a) * nv + i] * d.efc_Dr[r + a]) * d.G[(r + a) * nv + j];
+          for (int a = 0; a < dim; a++) {
+            const double* Ga = d.G + (r + a) * nv;
+            double x = Ga[li] * d.efc_Dr[r + a];
+#pragma unroll
+            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * Ga[j];
+          }
         }
         r += dim;
       }
-      double hv = (i == j ? 1.0 : 0.0) + s;
-      d.nH[i * nv + j] = hv;
-      d.nH[j * nv + i] = hv;
+      asm volatile("; HESS_END");
+#pragma unroll
+      for (int j = 0; j < NV; j++) hr[j] = (j == lane ? 1.0 : 0.0) + hr[j];
+      ldl_factor_regs<NV>(hr, d.tmp, d.tmp2);
+      store_lower<NV>(d.nH, hr);
     }
-    wsync();
     PT(13);
-    ldl_factor(nv, d.nH, d.tmp, d.tmp2);
-    ldl_solve(nv, d.nH, d.tmp2, d.ng, d.ndir);
+    ldl_solve<NV>(d.nH, d.tmp2, d.ng, d.ndir);
     if (lane < nv) d.ndir[lane] = -d.ndir[lane];
     wsync();
     for (int r = lane; r < ne; r += WAVE) {
@@ -2292,6 +2355,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   }
 }
 
+template <int NV>
 DEVI void solve(const Mdl& md, Dat& d) {
   int nv = md.m.nv;
   double meaninertia = 0.0;
@@ -2300,7 +2364,7 @@ DEVI void solve(const Mdl& md, Dat& d) {
   double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
   double fr0, fr1, u;
   if (md.m.solver == 0) solve_pgs(md, d, scale, fr0, fr1, u);
-  else solve_newton(md, d, scale, fr0, fr1, u);
+  else solve_newton<NV>(md, d, scale, fr0, fr1, u);
   PT(16);
   noslip(md, d, scale, fr0, fr1, u);
   PT(17);
@@ -2309,6 +2373,7 @@ DEVI void solve(const Mdl& md, Dat& d) {
 }
 
 // ---------------------------------------------------------------------------
+template <int NV>
 DEVI void forward(const Mdl& md, Dat& d, int full) {
   int nv = md.m.nv, lane = lane_id();
   if (lane == 0) {
@@ -2319,7 +2384,7 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
   collision(md, d);
   if (!full) return;
   crb(md, d);
-  ldl_factor(nv, d.M, d.Dv, d.Dinv);
+  ldl_factor<NV>(d.M, d.Dv, d.Dinv);
   for (int k = lane; k < nv; k += WAVE) {
     double sd = sqrt(d.Dv[k]);
     d.sD[k] = sd;
@@ -2332,11 +2397,12 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
     for (int k = 0; k < nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
   }
   wsync();
-  ldl_solve(nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
+  ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
   make_constraints(md, d);
-  solve(md, d);
+  solve<NV>(md, d);
 }
 
+template <int NV>
 DEVI void integrate(const Mdl& md, Dat& d) {
   int nv = md.m.nv, lane = lane_id();
   double dt = md.m.timestep;
@@ -2369,11 +2435,11 @@ DEVI void integrate(const Mdl& md, Dat& d) {
   for (int i = lane; i < nv * nv; i += WAVE) d.M[i] = d.M[i] - dt * d.qDeriv[i];
   wsync();
   PT(20);
-  ldl_factor(nv, d.M, d.Dv, d.Dinv);
+  ldl_factor<NV>(d.M, d.Dv, d.Dinv);
   double* qa = d.scratch;
   for (int k = lane; k < nv; k += WAVE) qa[k] = d.qfrc_smooth[k] + d.qfrc_constraint[k];
   wsync();
-  ldl_solve(nv, d.M, d.Dinv, qa, qa);
+  ldl_solve<NV>(d.M, d.Dinv, qa, qa);
   if (lane == 0) {
     for (int k = 0; k < nv; k++) d.qvel[k] = d.qvel[k] + dt * qa[k];
     const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
@@ -2426,7 +2492,8 @@ DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mp
 
 // ---------------------------------------------------------------------------
 // kernels: one 64-lane workgroup per candidate
-extern "C" __global__ void __launch_bounds__(64)
+template <int NV>
+__global__ void __launch_bounds__(64)
 mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
                      const double* __restrict__ qpos_init,
                      const double* __restrict__ mocap_pos, const double* __restrict__ mocap_quat, int predicate,
@@ -2440,14 +2507,15 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   Dat d;
   bind(d, smem, lay);
   reset(md, d, qpos_init + (size_t)i * md.m.nq, mocap_pos + 3 * i, mocap_quat + 4 * i);
-  forward(md, d, 0);
+  forward<NV>(md, d, 0);
   if (lane_id() == 0) {
     int hit = (predicate == MGS_PRED_ANY_CONTACT) ? (d.NCON != 0) : obj_contact(md, d);
     out[i] = (uint8_t)(hit ? 0 : 1);
   }
 }
 
-extern "C" __global__ void __launch_bounds__(64)
+template <int NV>
+__global__ void __launch_bounds__(64)
 mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
                    mgs_schedule sc, int n, const double* __restrict__ qpos_init,
                    const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
@@ -2498,7 +2566,7 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       wsync(); PT(2);
       collision(md, d); PT(5);
       crb(md, d); PT(6);
-      ldl_factor(md.m.nv, d.M, d.Dv, d.Dinv);
+      ldl_factor<NV>(d.M, d.Dv, d.Dinv);
       for (int k = lane; k < md.m.nv; k += WAVE) { double sd = sqrt(d.Dv[k]); d.sD[k] = sd; d.isD[k] = 1.0 / sd; }
       wsync(); PT(7);
       if (lane == 0) {
@@ -2506,14 +2574,14 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
         for (int k = 0; k < md.m.nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
       }
       wsync();
-      ldl_solve(md.m.nv, d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
+      ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
       PT(8);
       make_constraints(md, d);
-      solve(md, d);
-      integrate(md, d); PT(21);
+      solve<NV>(md, d);
+      integrate<NV>(md, d); PT(21);
 #else
-      forward(md, d, 1);
-      integrate(md, d);
+      forward<NV>(md, d, 1);
+      integrate<NV>(md, d);
 #endif
       if (uni(d.NCON) > maxcon) maxcon = uni(d.NCON);
       if (uni(d.NEFC) > maxefc) maxefc = uni(d.NEFC);

@@ -1019,6 +1019,38 @@ static void collide_pair(const Mdl* md, Dat* d, int pair) {
   }
 }
 
+#define OBB_FN static
+/* Second broadphase stage: separating-axis test between the geoms' oriented
+ * bounding boxes (their local AABBs posed in the world; 15 axes).  Each convex
+ * hull lies inside its box, so separated boxes cannot produce a contact and the
+ * narrowphase is skipped (MuJoCo would run MPR and find nothing; on the round-1
+ * benchmark this removes ~55% of narrowphase calls).  Returns 1 if separated. */
+OBB_FN int obb_separated(const double* R1, const double* x1, const double* b1, const double* R2,
+                         const double* x2, const double* b2, double margin) {
+  double c1[3], c2[3], t[3], D[3];
+  mulmv3(t, R1, b1);
+  add3(c1, x1, t);
+  mulmv3(t, R2, b2);
+  add3(c2, x2, t);
+  sub3(D, c2, c1);
+  const double *h1 = b1 + 3, *h2 = b2 + 3;
+  double A1[9], A2[9];  /* box axes as rows: A[k] = column k of R */
+  for (int k = 0; k < 3; k++)
+    for (int i = 0; i < 3; i++) { A1[3 * k + i] = R1[3 * i + k]; A2[3 * k + i] = R2[3 * i + k]; }
+  for (int q = 0; q < 15; q++) {
+    double L[3];
+    if (q < 3) { L[0] = A1[3 * q]; L[1] = A1[3 * q + 1]; L[2] = A1[3 * q + 2]; }
+    else if (q < 6) { L[0] = A2[3 * (q - 3)]; L[1] = A2[3 * (q - 3) + 1]; L[2] = A2[3 * (q - 3) + 2]; }
+    else { int a = (q - 6) / 3, b = (q - 6) % 3; cross3(L, A1 + 3 * a, A2 + 3 * b); }
+    double ll = dot3(L, L);
+    if (ll < 1e-20) continue;
+    double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));
+    double r2 = (h2[0] * fabs(dot3(A2, L)) + h2[1] * fabs(dot3(A2 + 3, L))) + h2[2] * fabs(dot3(A2 + 6, L));
+    if (fabs(dot3(D, L)) > (r1 + r2) + (margin + 1e-12) * sqrt(ll)) return 1;
+  }
+  return 0;
+}
+
 static void collision(const Mdl* md, Dat* d) {
   const mgs_model_desc* m = md->m;
   const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
@@ -1040,6 +1072,9 @@ static void collision(const Mdl* md, Dat* d) {
     int ov = 1;
     for (int k = 0; k < 3; k++)
       if (fabs(c[0][k] - c[1][k]) > (hw[0][k] + hw[1][k]) + pm[p]) ov = 0;
+    if (ov && obb_separated(d->geom_xmat + 9 * g[0], d->geom_xpos + 3 * g[0], aabb + 6 * g[0],
+                            d->geom_xmat + 9 * g[1], d->geom_xpos + 3 * g[1], aabb + 6 * g[1], pm[p]))
+      ov = 0;
     if (ov) collide_pair(md, d, p);
   }
 }
@@ -1894,10 +1929,13 @@ static void solve_newton(const Mdl* md, Dat* d) {
           int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
           int st = d->efc_state[r];
           if (dim > 1 && st == ST_CONE) {
+            /* x_b = sum_a G_{r+a,i} hb_ab, then s += x_b G_{r+b,j} (the kernel's per-lane order) */
             const double* hb = d->efc_hb + 36 * r;
-            for (int a = 0; a < dim; a++)
-              for (int b = 0; b < dim; b++)
-                s = s + (d->K[(size_t)(r + a) * nv + i] * hb[a * dim + b]) * d->K[(size_t)(r + b) * nv + j];
+            for (int b = 0; b < dim; b++) {
+              double x = 0.0;
+              for (int a = 0; a < dim; a++) x = x + d->K[(size_t)(r + a) * nv + i] * hb[a * dim + b];
+              s = s + x * d->K[(size_t)(r + b) * nv + j];
+            }
           } else if (st == ST_QUAD) {
             for (int a = 0; a < dim; a++)
               s = s + (d->K[(size_t)(r + a) * nv + i] * d->efc_Dr[r + a]) * d->K[(size_t)(r + a) * nv + j];
