@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 2
+#define MGS_ABI_VERSION 3
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -122,6 +122,7 @@ typedef struct mgs_model_desc {
   int32_t i_body_dofnum;
   int32_t i_body_dofadr;
   int32_t i_body_lastdof;   /* last dof in the body's kinematic chain, -1 if none */
+  int32_t i_body_dofmask;   /* 2: bit d set if dof d moves the body (dofs 0-31, 32-63) */
   /* body arrays: double */
   int32_t d_body_pos;       /* 3 */
   int32_t d_body_quat;      /* 4 */

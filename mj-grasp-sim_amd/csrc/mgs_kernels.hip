@@ -1286,6 +1286,26 @@ DEVI void jac_point(const Mdl& md, const Dat& d, int b, const double* pt, double
   }
 }
 
+// column `col` of the point Jacobian of body b at pt (oracle jac_point(), one
+// dof per lane): zero unless dof col moves the body (model body_dofmask).
+DEVI void jac_col(const Mdl& md, const Dat& d, int b, const double* pt, int col, double* jp, double* jr) {
+  const int32_t* mask = IA(md, body_dofmask) + 2 * b;
+  int in = (col < 32) ? ((mask[0] >> col) & 1) : ((mask[1] >> (col - 32)) & 1);
+  if (in) {
+    const double* cd = d.cdof + 6 * col;
+    const double* c = d.subtree_com + 3 * IA(md, body_rootid)[b];
+    double off[3], cr[3];
+    sub3(off, pt, c);
+    cross3(cr, cd, off);
+    for (int k = 0; k < 3; k++) {
+      jr[k] = cd[k];
+      jp[k] = cd[3 + k] + cr[k];
+    }
+  } else {
+    for (int k = 0; k < 3; k++) { jr[k] = 0.0; jp[k] = 0.0; }
+  }
+}
+
 DEVI double impedance(const double* si, double pos, double margin) {
   if (si[0] == si[1] || si[2] <= K_MINVAL) return 0.5 * (si[0] + si[1]);
   double x = (pos - margin) / si[2];
@@ -1418,16 +1438,18 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         p2[0] = d.xpos[3 * b2]; p2[1] = d.xpos[3 * b2 + 1]; p2[2] = d.xpos[3 * b2 + 2];
       }
       if (lane == 0) {
-        jac_point(md, d, b1, p1, jp1, jr1);
-        jac_point(md, d, b2, p2, jp2, jr2);
         if (d.NEFC + (et[e] == MGS_EQ_WELD ? 6 : 3) > md.m.nefc_max) d.OVERFLOW |= 2;
         else for (int k = 0; k < 3; k++) add_row(md, d, MGS_EFC_EQUALITY, p1[k] - p2[k], 0.0, 1, e);
       }
       wsync();
       if (d.OVERFLOW & 2) break;
       int r0 = d.NEFC - 3;
-      for (int c = lane; c < nv; c += WAVE)
-        for (int k = 0; k < 3; k++) J[(r0 + k) * nv + c] = jp1[k * nv + c] - jp2[k * nv + c];
+      double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
+      int col = lane < nv ? lane : 0;
+      jac_col(md, d, b1, p1, col, cjp1, cjr1);
+      jac_col(md, d, b2, p2, col, cjp2, cjr2);
+      if (lane < nv)
+        for (int k = 0; k < 3; k++) J[(r0 + k) * nv + lane] = cjp1[k] - cjp2[k];
       if (et[e] == MGS_EQ_WELD) {
         double q1r[4], q2c[4], qe[4];
         quatmul(q1r, d.xquat + 4 * b1, data + 3);
@@ -1440,12 +1462,12 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
           for (int k = 0; k < 3; k++) add_row(md, d, MGS_EFC_EQUALITY, qe[1 + k] * ts, 0.0, 1, e);
         wsync();
         int rr = d.NEFC - 3;
-        for (int c = lane; c < nv; c += WAVE) {
-          double ax[4] = {0.0, jr1[c] - jr2[c], jr1[nv + c] - jr2[nv + c], jr1[2 * nv + c] - jr2[2 * nv + c]};
+        if (lane < nv) {
+          double ax[4] = {0.0, cjr1[0] - cjr2[0], cjr1[1] - cjr2[1], cjr1[2] - cjr2[2]};
           double t1q[4], t2q[4];
           quatmul(t1q, q2c, ax);
           quatmul(t2q, t1q, q1r);
-          for (int k = 0; k < 3; k++) J[(rr + k) * nv + c] = (0.5 * t2q[1 + k]) * ts;
+          for (int k = 0; k < 3; k++) J[(rr + k) * nv + lane] = (0.5 * t2q[1 + k]) * ts;
         }
       }
       wsync();
@@ -1528,18 +1550,22 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     int r = d.NEFC;
     wsync();
     if (lane == 0) {
-      jac_point(md, d, b1, pt, jp1, jr1);
-      jac_point(md, d, b2, pt, jp2, jr2);
       for (int j = 0; j < dim; j++) add_row(md, d, MGS_EFC_CONTACT, j == 0 ? d.con_dist[c] : 0.0, pmar[p], dim, c);
       for (int j = 0; j < dim; j++) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
     }
     wsync();
-    for (int col = lane; col < nv; col += WAVE) {
-      double dp[3] = {jp2[col] - jp1[col], jp2[nv + col] - jp1[nv + col], jp2[2 * nv + col] - jp1[2 * nv + col]};
-      for (int j = 0; j < dim && j < 3; j++) J[(r + j) * nv + col] = dot3(fr + 3 * j, dp);
-      if (dim >= 4) {
-        double dr[3] = {jr2[col] - jr1[col], jr2[nv + col] - jr1[nv + col], jr2[2 * nv + col] - jr1[2 * nv + col]};
-        J[(r + 3) * nv + col] = dot3(fr, dr);
+    {
+      int col = lane < nv ? lane : 0;
+      double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
+      jac_col(md, d, b1, pt, col, cjp1, cjr1);
+      jac_col(md, d, b2, pt, col, cjp2, cjr2);
+      if (lane < nv) {
+        double dp[3] = {cjp2[0] - cjp1[0], cjp2[1] - cjp1[1], cjp2[2] - cjp1[2]};
+        for (int j = 0; j < dim && j < 3; j++) J[(r + j) * nv + col] = dot3(fr + 3 * j, dp);
+        if (dim >= 4) {
+          double dr[3] = {cjr2[0] - cjr1[0], cjr2[1] - cjr1[1], cjr2[2] - cjr1[2]};
+          J[(r + 3) * nv + col] = dot3(fr, dr);
+        }
       }
     }
   }
@@ -2267,26 +2293,44 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
 #pragma unroll
       for (int j = 0; j < NV; j++) hr[j] = 0.0;
       int li = lane < nv ? lane : 0;
-      asm volatile("; HESS_BEGIN");
+      // row metadata for all rows in registers (lane r holds row r / r + 64), read
+      // per row with v_readlane: no LDS round trip on the loop-control path
+      int meta0 = 0, meta1 = 0;
+      if (lane < ne) {
+        int t = d.efc_type[lane];
+        int dm = (t == MGS_EFC_CONTACT) ? d.efc_dim[lane] : 1;
+        meta0 = dm | (d.efc_state[lane] << 4) | (d.efc_con[lane] << 8);
+      }
+      if (lane + WAVE < ne) {
+        int rr = lane + WAVE;
+        int t = d.efc_type[rr];
+        int dm = (t == MGS_EFC_CONTACT) ? d.efc_dim[rr] : 1;
+        meta1 = dm | (d.efc_state[rr] << 4) | (d.efc_con[rr] << 8);
+      }
       for (int r = 0; r < ne;) {
-        int t = uni(d.efc_type[r]);
-        int dim = (t == MGS_EFC_CONTACT) ? uni(d.efc_dim[r]) : 1;
-        int st = uni(d.efc_state[r]);
+        int m = (r < WAVE) ? __builtin_amdgcn_readlane(meta0, r) : __builtin_amdgcn_readlane(meta1, r - WAVE);
+        int dim = m & 15, st = (m >> 4) & 15, con = m >> 8;
         if (dim > 1 && st == ST_CONE) {
-          const double* hb = d.con_hb + 16 * uni(d.efc_con[r]);
+          const double* hb = d.con_hb + 16 * con;
           for (int b = 0; b < dim; b++) {
             double x = 0.0;
             for (int a = 0; a < dim; a++) x = x + d.G[(r + a) * nv + li] * hb[a * dim + b];
             const double* Gb = d.G + (r + b) * nv;
+            double g[NV];
 #pragma unroll
-            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * Gb[j];
+            for (int j = 0; j < NV; j++) g[j] = Gb[j];
+#pragma unroll
+            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * g[j];
           }
         } else if (st == ST_QUAD) {
           for (int a = 0; a < dim; a++) {
             const double* Ga = d.G + (r + a) * nv;
+            double g[NV];
+#pragma unroll
+            for (int j = 0; j < NV; j++) g[j] = Ga[j];
             double x = Ga[li] * d.efc_Dr[r + a];
 #pragma unroll
-            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * Ga[j];
+            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * g[j];
           }
         }
         r += dim;

@@ -1001,6 +1001,16 @@ class CompiledModel:
             jid = -1
         return int(self.jnt_qposadr[jid])
 
+    def body_dofmask(self):
+        """(nbody, 2) int32 bit masks of the dofs on each body's chain to the root."""
+        m = np.zeros((self.nbody, 2), np.uint32)
+        for b in range(self.nbody):
+            d = int(self.body_lastdof[b])
+            while d >= 0:
+                m[b, d // 32] |= np.uint32(1) << np.uint32(d % 32)
+                d = int(self.dof_parentid[d])
+        return m.view(np.int32)
+
     @property
     def nu(self):
         return len(self.actuator_trntype)
@@ -1026,6 +1036,7 @@ class CompiledModel:
         for n in ["body_parentid", "body_rootid", "body_mocapid", "body_jntnum", "body_jntadr",
                   "body_dofnum", "body_dofadr", "body_lastdof"]:
             put_i(n, getattr(self, n))
+        put_i("body_dofmask", self.body_dofmask())
         for n in ["body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia",
                   "body_invweight0", "dof_invweight0"]:
             put_d(n, getattr(self, n))
