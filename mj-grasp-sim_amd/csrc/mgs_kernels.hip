@@ -266,73 +266,94 @@ DEVI int next_pow2(int n) {
 }
 
 // ---------------------------------------------------------------------------
-// kinematics (lane 0)
-DEVI void kinematics(const Mdl& md, Dat& d) {
+// Tree-level parallel forward kinematics (oracle kinematics()): lane b owns
+// body b; bodies of one tree depth are independent given their parents, so the
+// levels run in order and the bodies of a level in parallel.  Per-body
+// arithmetic is the oracle's.
+DEVI void body_kin(const Mdl& md, Dat& d, int b) {
   const int32_t *parent = IA(md, body_parentid), *mocapid = IA(md, body_mocapid);
   const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
   const int32_t *jtype = IA(md, jnt_type), *qadr = IA(md, jnt_qposadr);
   const double *bpos = DA(md, body_pos), *bquat = DA(md, body_quat);
-  const double *ipos = DA(md, body_ipos), *iquat = DA(md, body_iquat);
+  const double *ipos = DA(md, body_ipos);
   const double *jpos = DA(md, jnt_pos), *jaxis = DA(md, jnt_axis), *qpos0 = DA(md, qpos0);
-  d.xpos[0] = d.xpos[1] = d.xpos[2] = 0.0;
-  d.xquat[0] = 1.0; d.xquat[1] = d.xquat[2] = d.xquat[3] = 0.0;
-  quat2mat(d.xmat, d.xquat);
-  for (int b = 1; b < md.m.nbody; b++) {
-    double pos[3], quat[4], mat[9];
-    if (mocapid[b] >= 0) {
-      const double* mp = d.mocap_pos + 3 * mocapid[b];
-      const double* mq = d.mocap_quat + 4 * mocapid[b];
-      pos[0] = mp[0]; pos[1] = mp[1]; pos[2] = mp[2];
-      quat[0] = mq[0]; quat[1] = mq[1]; quat[2] = mq[2]; quat[3] = mq[3];
-      normalize4(quat);
-    } else {
-      int p = parent[b];
-      double t[3];
-      mulmv3(t, d.xmat + 9 * p, bpos + 3 * b);
-      add3(pos, d.xpos + 3 * p, t);
-      quatmul(quat, d.xquat + 4 * p, bquat + 4 * b);
-      for (int k = 0; k < jntnum[b]; k++) {
-        int j = jntadr[b] + k;
-        int a = qadr[j];
-        if (jtype[j] == MGS_JNT_FREE) {
-          pos[0] = d.qpos[a]; pos[1] = d.qpos[a + 1]; pos[2] = d.qpos[a + 2];
-          quat[0] = d.qpos[a + 3]; quat[1] = d.qpos[a + 4]; quat[2] = d.qpos[a + 5]; quat[3] = d.qpos[a + 6];
-          normalize4(quat);
-          d.xanchor[3 * j] = pos[0]; d.xanchor[3 * j + 1] = pos[1]; d.xanchor[3 * j + 2] = pos[2];
-          d.xaxis[3 * j] = 0.0; d.xaxis[3 * j + 1] = 0.0; d.xaxis[3 * j + 2] = 1.0;
-        } else {
+  double pos[3], quat[4], mat[9];
+  if (mocapid[b] >= 0) {
+    const double* mp = d.mocap_pos + 3 * mocapid[b];
+    const double* mq = d.mocap_quat + 4 * mocapid[b];
+    pos[0] = mp[0]; pos[1] = mp[1]; pos[2] = mp[2];
+    quat[0] = mq[0]; quat[1] = mq[1]; quat[2] = mq[2]; quat[3] = mq[3];
+    normalize4(quat);
+  } else {
+    int p = parent[b];
+    double t[3];
+    mulmv3(t, d.xmat + 9 * p, bpos + 3 * b);
+    add3(pos, d.xpos + 3 * p, t);
+    quatmul(quat, d.xquat + 4 * p, bquat + 4 * b);
+    for (int k = 0; k < jntnum[b]; k++) {
+      int j = jntadr[b] + k;
+      int a = qadr[j];
+      if (jtype[j] == MGS_JNT_FREE) {
+        pos[0] = d.qpos[a]; pos[1] = d.qpos[a + 1]; pos[2] = d.qpos[a + 2];
+        quat[0] = d.qpos[a + 3]; quat[1] = d.qpos[a + 4]; quat[2] = d.qpos[a + 5]; quat[3] = d.qpos[a + 6];
+        normalize4(quat);
+        d.xanchor[3 * j] = pos[0]; d.xanchor[3 * j + 1] = pos[1]; d.xanchor[3 * j + 2] = pos[2];
+        d.xaxis[3 * j] = 0.0; d.xaxis[3 * j + 1] = 0.0; d.xaxis[3 * j + 2] = 1.0;
+      } else {
+        double anc[3], axw[3];
+        quat2mat(mat, quat);
+        mulmv3(axw, mat, jaxis + 3 * j);
+        mulmv3(t, mat, jpos + 3 * j);
+        add3(anc, t, pos);
+        d.xaxis[3 * j] = axw[0]; d.xaxis[3 * j + 1] = axw[1]; d.xaxis[3 * j + 2] = axw[2];
+        d.xanchor[3 * j] = anc[0]; d.xanchor[3 * j + 1] = anc[1]; d.xanchor[3 * j + 2] = anc[2];
+        if (jtype[j] == MGS_JNT_HINGE) {
+          double ql[4], qn[4];
+          axisangle2quat(ql, jaxis + 3 * j, d.qpos[a] - qpos0[a]);
+          quatmul(qn, quat, ql);
+          quat[0] = qn[0]; quat[1] = qn[1]; quat[2] = qn[2]; quat[3] = qn[3];
           quat2mat(mat, quat);
-          mulmv3(d.xaxis + 3 * j, mat, jaxis + 3 * j);
           mulmv3(t, mat, jpos + 3 * j);
-          add3(d.xanchor + 3 * j, t, pos);
-          if (jtype[j] == MGS_JNT_HINGE) {
-            double ql[4], qn[4];
-            axisangle2quat(ql, jaxis + 3 * j, d.qpos[a] - qpos0[a]);
-            quatmul(qn, quat, ql);
-            quat[0] = qn[0]; quat[1] = qn[1]; quat[2] = qn[2]; quat[3] = qn[3];
-            quat2mat(mat, quat);
-            mulmv3(t, mat, jpos + 3 * j);
-            sub3(pos, d.xanchor + 3 * j, t);
-          } else {
-            double dq = d.qpos[a] - qpos0[a];
-            pos[0] = pos[0] + d.xaxis[3 * j] * dq;
-            pos[1] = pos[1] + d.xaxis[3 * j + 1] * dq;
-            pos[2] = pos[2] + d.xaxis[3 * j + 2] * dq;
-          }
+          sub3(pos, anc, t);
+        } else {
+          double dq = d.qpos[a] - qpos0[a];
+          pos[0] = pos[0] + axw[0] * dq;
+          pos[1] = pos[1] + axw[1] * dq;
+          pos[2] = pos[2] + axw[2] * dq;
         }
       }
-      normalize4(quat);
     }
-    d.xpos[3 * b] = pos[0]; d.xpos[3 * b + 1] = pos[1]; d.xpos[3 * b + 2] = pos[2];
-    d.xquat[4 * b] = quat[0]; d.xquat[4 * b + 1] = quat[1]; d.xquat[4 * b + 2] = quat[2]; d.xquat[4 * b + 3] = quat[3];
-    quat2mat(d.xmat + 9 * b, quat);
-    double t[3];
-    mulmv3(t, d.xmat + 9 * b, ipos + 3 * b);
-    add3(d.xipos + 3 * b, d.xpos + 3 * b, t);
+    normalize4(quat);
+  }
+  d.xpos[3 * b] = pos[0]; d.xpos[3 * b + 1] = pos[1]; d.xpos[3 * b + 2] = pos[2];
+  d.xquat[4 * b] = quat[0]; d.xquat[4 * b + 1] = quat[1]; d.xquat[4 * b + 2] = quat[2]; d.xquat[4 * b + 3] = quat[3];
+  quat2mat(mat, quat);
+  for (int k = 0; k < 9; k++) d.xmat[9 * b + k] = mat[k];
+  double t[3];
+  mulmv3(t, mat, ipos + 3 * b);
+  add3(d.xipos + 3 * b, pos, t);
+}
+
+DEVI int max_depth(const Mdl& md) { return IA(md, body_depth)[md.m.nbody]; }
+
+DEVI void kinematics(const Mdl& md, Dat& d) {
+  int lane = lane_id(), nb = md.m.nbody;
+  const int32_t* depth = IA(md, body_depth);
+  if (lane == 0) {
+    d.xpos[0] = d.xpos[1] = d.xpos[2] = 0.0;
+    d.xquat[0] = 1.0; d.xquat[1] = d.xquat[2] = d.xquat[3] = 0.0;
+    quat2mat(d.xmat, d.xquat);
+  }
+  wsync();
+  int maxd = max_depth(md);
+  int myd = (lane < nb) ? depth[lane] : -1;
+  for (int L = 1; L <= maxd; L++) {
+    if (myd == L) body_kin(md, d, lane);
+    wsync();
   }
   const int32_t* gbody = IA(md, geom_bodyid);
   const double *gpos = DA(md, geom_pos), *gquat = DA(md, geom_quat);
-  for (int g = 0; g < md.m.ngeom; g++) {
+  for (int g = lane; g < md.m.ngeom; g += WAVE) {
     int b = gbody[g];
     double t[3], q[4];
     mulmv3(t, d.xmat + 9 * b, gpos + 3 * g);
@@ -340,41 +361,69 @@ DEVI void kinematics(const Mdl& md, Dat& d) {
     quatmul(q, d.xquat + 4 * b, gquat + 4 * g);
     quat2mat(d.geom_xmat + 9 * g, q);
   }
+  wsync();
 }
 
-// mj_comPos (lane 0)
+// arr[p] += arr[c] over the tree from the leaves up, children of each parent in
+// decreasing body index (the oracle's `for b = nb-1..1: arr[parent] += arr[b]`
+// order per parent); W doubles per body; world included iff with_world.
+template <int W>
+DEVI void accumulate_up(const Mdl& md, double* arr, int with_world) {
+  int lane = lane_id(), nb = md.m.nbody;
+  const int32_t *depth = IA(md, body_depth), *parent = IA(md, body_parentid);
+  int maxd = max_depth(md);
+  int myd = (lane < nb) ? depth[lane] : -1;
+  for (int L = maxd; L >= 1; L--) {
+    if (myd == L - 1 && (with_world || lane > 0)) {
+      double acc[W];
+#pragma unroll
+      for (int k = 0; k < W; k++) acc[k] = arr[W * lane + k];
+      for (int c = nb - 1; c > lane; c--) {
+        if (parent[c] == lane) {
+#pragma unroll
+          for (int k = 0; k < W; k++) acc[k] = acc[k] + arr[W * c + k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; k++) arr[W * lane + k] = acc[k];
+    }
+    wsync();
+  }
+}
+
+// mj_comPos (oracle com_pos()), lanes over bodies / dofs
 DEVI void com_pos(const Mdl& md, Dat& d) {
-  const int32_t *parent = IA(md, body_parentid), *rootid = IA(md, body_rootid);
+  int lane = lane_id(), nb = md.m.nbody;
+  const int32_t *rootid = IA(md, body_rootid);
   const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
   const int32_t *jtype = IA(md, jnt_type), *dadr = IA(md, jnt_dofadr);
   const double *mass = DA(md, body_mass), *inertia = DA(md, body_inertia);
-  int nb = md.m.nbody;
-  for (int b = 0; b < nb; b++) {
-    d.subtree_mass[b] = mass[b];
-    d.subtree_com[3 * b] = mass[b] * d.xipos[3 * b];
-    d.subtree_com[3 * b + 1] = mass[b] * d.xipos[3 * b + 1];
-    d.subtree_com[3 * b + 2] = mass[b] * d.xipos[3 * b + 2];
+  // subtree mass + mass-weighted com packed as 4 doubles per body in scratch
+  double* sc = d.scratch;
+  for (int b = lane; b < nb; b += WAVE) {
+    sc[4 * b] = mass[b];
+    sc[4 * b + 1] = mass[b] * d.xipos[3 * b];
+    sc[4 * b + 2] = mass[b] * d.xipos[3 * b + 1];
+    sc[4 * b + 3] = mass[b] * d.xipos[3 * b + 2];
   }
-  for (int b = nb - 1; b > 0; b--) {
-    int p = parent[b];
-    d.subtree_mass[p] = d.subtree_mass[p] + d.subtree_mass[b];
-    d.subtree_com[3 * p] = d.subtree_com[3 * p] + d.subtree_com[3 * b];
-    d.subtree_com[3 * p + 1] = d.subtree_com[3 * p + 1] + d.subtree_com[3 * b + 1];
-    d.subtree_com[3 * p + 2] = d.subtree_com[3 * p + 2] + d.subtree_com[3 * b + 2];
-  }
-  for (int b = 0; b < nb; b++) {
-    if (d.subtree_mass[b] < K_MINVAL) {
+  wsync();
+  accumulate_up<4>(md, sc, 1);
+  for (int b = lane; b < nb; b += WAVE) {
+    double m = sc[4 * b];
+    d.subtree_mass[b] = m;
+    if (m < K_MINVAL) {
       d.subtree_com[3 * b] = d.xipos[3 * b];
       d.subtree_com[3 * b + 1] = d.xipos[3 * b + 1];
       d.subtree_com[3 * b + 2] = d.xipos[3 * b + 2];
     } else {
-      double inv = 1.0 / d.subtree_mass[b];
-      d.subtree_com[3 * b] = d.subtree_com[3 * b] * inv;
-      d.subtree_com[3 * b + 1] = d.subtree_com[3 * b + 1] * inv;
-      d.subtree_com[3 * b + 2] = d.subtree_com[3 * b + 2] * inv;
+      double inv = 1.0 / m;
+      d.subtree_com[3 * b] = sc[4 * b + 1] * inv;
+      d.subtree_com[3 * b + 1] = sc[4 * b + 2] * inv;
+      d.subtree_com[3 * b + 2] = sc[4 * b + 3] * inv;
     }
   }
-  for (int b = 0; b < nb; b++) {
+  wsync();
+  for (int b = lane; b < nb; b += WAVE) {
     double* ci = d.cinert + 10 * b;
     double qi[4], R[9];
     quatmul(qi, d.xquat + 4 * b, DA(md, body_iquat) + 4 * b);
@@ -398,32 +447,31 @@ DEVI void com_pos(const Mdl& md, Dat& d) {
     ci[7] = mm * off[1];
     ci[8] = mm * off[2];
     ci[9] = mm;
-  }
-  for (int b = 1; b < nb; b++) {
+    if (b == 0) continue;
     const double* c = d.subtree_com + 3 * rootid[b];
     for (int k = 0; k < jntnum[b]; k++) {
       int j = jntadr[b] + k;
       int da = dadr[j];
-      double off[3];
-      sub3(off, c, d.xanchor + 3 * j);
+      double off2[3];
+      sub3(off2, c, d.xanchor + 3 * j);
       if (jtype[j] == MGS_JNT_FREE) {
         for (int i = 0; i < 3; i++) {
           double* cd = d.cdof + 6 * (da + i);
           cd[0] = cd[1] = cd[2] = 0.0;
           cd[3] = (i == 0) ? 1.0 : 0.0; cd[4] = (i == 1) ? 1.0 : 0.0; cd[5] = (i == 2) ? 1.0 : 0.0;
         }
-        const double* R = d.xmat + 9 * b;
+        const double* Rb = d.xmat + 9 * b;
         for (int i = 0; i < 3; i++) {
           double* cd = d.cdof + 6 * (da + 3 + i);
-          double ax[3] = {R[i], R[3 + i], R[6 + i]};
+          double ax[3] = {Rb[i], Rb[3 + i], Rb[6 + i]};
           cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
-          cross3(cd + 3, ax, off);
+          cross3(cd + 3, ax, off2);
         }
       } else if (jtype[j] == MGS_JNT_HINGE) {
         double* cd = d.cdof + 6 * da;
         const double* ax = d.xaxis + 3 * j;
         cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
-        cross3(cd + 3, ax, off);
+        cross3(cd + 3, ax, off2);
       } else {
         double* cd = d.cdof + 6 * da;
         const double* ax = d.xaxis + 3 * j;
@@ -432,21 +480,17 @@ DEVI void com_pos(const Mdl& md, Dat& d) {
       }
     }
   }
+  wsync();
 }
 
-// composite rigid bodies (lane 0) + mass matrix (lanes over dofs)
+// composite rigid bodies + mass matrix (oracle crb()), tree-parallel
 DEVI void crb(const Mdl& md, Dat& d) {
   int nb = md.m.nbody, nv = md.m.nv, lane = lane_id();
-  const int32_t *parent = IA(md, body_parentid), *dbody = IA(md, dof_bodyid), *dpar = IA(md, dof_parentid);
+  const int32_t *dbody = IA(md, dof_bodyid), *dpar = IA(md, dof_parentid);
   const double* arm = DA(md, dof_armature);
-  if (lane == 0) {
-    for (int k = 0; k < 10 * nb; k++) d.crb[k] = d.cinert[k];
-    for (int b = nb - 1; b > 0; b--) {
-      int p = parent[b];
-      if (p > 0)
-        for (int k = 0; k < 10; k++) d.crb[10 * p + k] = d.crb[10 * p + k] + d.crb[10 * b + k];
-    }
-  }
+  for (int k = lane; k < 10 * nb; k += WAVE) d.crb[k] = d.cinert[k];
+  wsync();
+  accumulate_up<10>(md, d.crb, 0);
   for (int k = lane; k < nv * nv; k += WAVE) d.M[k] = 0.0;
   wsync();
   for (int i = lane; i < nv; i += WAVE) {
@@ -2420,11 +2464,8 @@ DEVI void solve(const Mdl& md, Dat& d) {
 template <int NV>
 DEVI void forward(const Mdl& md, Dat& d, int full) {
   int nv = md.m.nv, lane = lane_id();
-  if (lane == 0) {
-    kinematics(md, d);
-    com_pos(md, d);
-  }
-  wsync();
+  kinematics(md, d);
+  com_pos(md, d);
   collision(md, d);
   if (!full) return;
   crb(md, d);
@@ -2604,9 +2645,9 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       wsync();
 #ifdef MGS_PROFILE
       PT(0);
-      if (lane == 0) kinematics(md, d);
+      kinematics(md, d);
       wsync(); PT(1);
-      if (lane == 0) com_pos(md, d);
+      com_pos(md, d);
       wsync(); PT(2);
       collision(md, d); PT(5);
       crb(md, d); PT(6);

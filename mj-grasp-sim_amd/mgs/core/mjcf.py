@@ -1037,6 +1037,11 @@ class CompiledModel:
                   "body_dofnum", "body_dofadr", "body_lastdof"]:
             put_i(n, getattr(self, n))
         put_i("body_dofmask", self.body_dofmask())
+        depth = np.zeros(self.nbody + 1, np.int32)
+        for b in range(1, self.nbody):
+            depth[b] = depth[self.body_parentid[b]] + 1
+        depth[self.nbody] = depth[:self.nbody].max()
+        put_i("body_depth", depth)
         for n in ["body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia",
                   "body_invweight0", "dof_invweight0"]:
             put_d(n, getattr(self, n))
