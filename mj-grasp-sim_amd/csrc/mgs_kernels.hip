@@ -639,50 +639,62 @@ DEVI void actuation(const Mdl& md, Dat& d) {
   }
 }
 
+// passive forces (oracle passive()), one dof per lane
 DEVI void passive(const Mdl& md, Dat& d) {
-  const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
+  const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *djnt = IA(md, dof_jntid);
   const double *stiff = DA(md, jnt_stiffness), *qspring = DA(md, qpos_spring), *damp = DA(md, dof_damping);
-  for (int k = 0; k < md.m.nv; k++) d.qfrc_passive[k] = 0.0;
-  for (int j = 0; j < md.m.njnt; j++) {
-    if (stiff[j] == 0.0) continue;
-    if (jtype[j] == MGS_JNT_HINGE || jtype[j] == MGS_JNT_SLIDE)
-      d.qfrc_passive[jd[j]] = -stiff[j] * (d.qpos[jq[j]] - qspring[jq[j]]);
+  int lane = lane_id();
+  if (lane < md.m.nv) {
+    int j = djnt[lane];
+    double v = 0.0;
+    if (stiff[j] != 0.0 && (jtype[j] == MGS_JNT_HINGE || jtype[j] == MGS_JNT_SLIDE))
+      v = -stiff[j] * (d.qpos[jq[j]] - qspring[jq[j]]);
+    d.qfrc_passive[lane] = v - damp[lane] * d.qvel[lane];
   }
-  for (int k = 0; k < md.m.nv; k++) d.qfrc_passive[k] = d.qfrc_passive[k] - damp[k] * d.qvel[k];
+}
+
+// recursive Newton-Euler bias forces (oracle rne()): forward velocity /
+// acceleration pass by tree level (lane per body), cfrc accumulated up the tree
+// in the oracle's child order, then one dof per lane.
+DEVI void rne_body(const Mdl& md, Dat& d, int b) {
+  const int32_t *parent = IA(md, body_parentid), *dnum = IA(md, body_dofnum), *dadr = IA(md, body_dofadr);
+  int p = parent[b];
+  double cv[6], ca[6];
+  for (int k = 0; k < 6; k++) { cv[k] = d.cvel[6 * p + k]; ca[k] = d.cacc[6 * p + k]; }
+  for (int i = 0; i < dnum[b]; i++) {
+    int dd = dadr[b] + i;
+    cross_motion(d.cdof_dot + 6 * dd, cv, d.cdof + 6 * dd);
+    for (int k = 0; k < 6; k++) cv[k] = cv[k] + d.cdof[6 * dd + k] * d.qvel[dd];
+  }
+  for (int i = 0; i < dnum[b]; i++) {
+    int dd = dadr[b] + i;
+    for (int k = 0; k < 6; k++) ca[k] = ca[k] + d.cdof_dot[6 * dd + k] * d.qvel[dd];
+  }
+  for (int k = 0; k < 6; k++) { d.cvel[6 * b + k] = cv[k]; d.cacc[6 * b + k] = ca[k]; }
+  double f1[6], f2[6], f3[6];
+  mul_inert_vec(f1, d.cinert + 10 * b, ca);
+  mul_inert_vec(f2, d.cinert + 10 * b, cv);
+  cross_force(f3, cv, f2);
+  for (int k = 0; k < 6; k++) d.cfrc[6 * b + k] = f1[k] + f3[k];
 }
 
 DEVI void rne(const Mdl& md, Dat& d) {
-  int nb = md.m.nbody;
-  const int32_t *parent = IA(md, body_parentid), *dnum = IA(md, body_dofnum), *dadr = IA(md, body_dofadr);
-  const int32_t* dbody = IA(md, dof_bodyid);
-  for (int k = 0; k < 6; k++) { d.cvel[k] = 0.0; d.cacc[k] = 0.0; }
-  d.cacc[3] = -md.m.gravity[0]; d.cacc[4] = -md.m.gravity[1]; d.cacc[5] = -md.m.gravity[2];
-  for (int b = 1; b < nb; b++) {
-    int p = parent[b];
-    double* cv = d.cvel + 6 * b;
-    double* ca = d.cacc + 6 * b;
-    for (int k = 0; k < 6; k++) { cv[k] = d.cvel[6 * p + k]; ca[k] = d.cacc[6 * p + k]; }
-    for (int i = 0; i < dnum[b]; i++) {
-      int dd = dadr[b] + i;
-      cross_motion(d.cdof_dot + 6 * dd, cv, d.cdof + 6 * dd);
-      for (int k = 0; k < 6; k++) cv[k] = cv[k] + d.cdof[6 * dd + k] * d.qvel[dd];
-    }
-    for (int i = 0; i < dnum[b]; i++) {
-      int dd = dadr[b] + i;
-      for (int k = 0; k < 6; k++) ca[k] = ca[k] + d.cdof_dot[6 * dd + k] * d.qvel[dd];
-    }
-    double f1[6], f2[6], f3[6];
-    mul_inert_vec(f1, d.cinert + 10 * b, ca);
-    mul_inert_vec(f2, d.cinert + 10 * b, cv);
-    cross_force(f3, cv, f2);
-    for (int k = 0; k < 6; k++) d.cfrc[6 * b + k] = f1[k] + f3[k];
+  int lane = lane_id(), nb = md.m.nbody;
+  const int32_t *dbody = IA(md, dof_bodyid), *depth = IA(md, body_depth);
+  if (lane == 0) {
+    for (int k = 0; k < 6; k++) { d.cvel[k] = 0.0; d.cacc[k] = 0.0; }
+    d.cacc[3] = -md.m.gravity[0]; d.cacc[4] = -md.m.gravity[1]; d.cacc[5] = -md.m.gravity[2];
   }
-  for (int b = nb - 1; b > 0; b--) {
-    int p = parent[b];
-    if (p > 0)
-      for (int k = 0; k < 6; k++) d.cfrc[6 * p + k] = d.cfrc[6 * p + k] + d.cfrc[6 * b + k];
+  wsync();
+  int maxd = max_depth(md);
+  int myd = (lane < nb) ? depth[lane] : -1;
+  for (int L = 1; L <= maxd; L++) {
+    if (myd == L) rne_body(md, d, lane);
+    wsync();
   }
-  for (int i = 0; i < md.m.nv; i++) d.qfrc_bias[i] = dot6(d.cdof + 6 * i, d.cfrc + 6 * dbody[i]);
+  accumulate_up<6>(md, d.cfrc, 0);
+  if (lane < md.m.nv) d.qfrc_bias[lane] = dot6(d.cdof + 6 * lane, d.cfrc + 6 * dbody[lane]);
+  wsync();
 }
 
 // ---------------------------------------------------------------------------
@@ -2475,12 +2487,10 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
     d.sD[k] = sd;
     d.isD[k] = 1.0 / sd;
   }
-  if (lane == 0) {
-    actuation(md, d);
-    passive(md, d);
-    rne(md, d);
-    for (int k = 0; k < nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
-  }
+  if (lane == 0) actuation(md, d);
+  passive(md, d);
+  rne(md, d);
+  if (lane < nv) d.qfrc_smooth[lane] = (d.qfrc_passive[lane] - d.qfrc_bias[lane]) + d.qfrc_actuator[lane];
   wsync();
   ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
   make_constraints(md, d);
@@ -2654,10 +2664,10 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       ldl_factor<NV>(d.M, d.Dv, d.Dinv);
       for (int k = lane; k < md.m.nv; k += WAVE) { double sd = sqrt(d.Dv[k]); d.sD[k] = sd; d.isD[k] = 1.0 / sd; }
       wsync(); PT(7);
-      if (lane == 0) {
-        actuation(md, d); passive(md, d); rne(md, d);
-        for (int k = 0; k < md.m.nv; k++) d.qfrc_smooth[k] = (d.qfrc_passive[k] - d.qfrc_bias[k]) + d.qfrc_actuator[k];
-      }
+      if (lane == 0) actuation(md, d);
+      passive(md, d);
+      rne(md, d);
+      if (lane < md.m.nv) d.qfrc_smooth[lane] = (d.qfrc_passive[lane] - d.qfrc_bias[lane]) + d.qfrc_actuator[lane];
       wsync();
       ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
       PT(8);
