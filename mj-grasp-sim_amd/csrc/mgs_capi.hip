@@ -37,39 +37,55 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   int sizes[L_COUNT];
   sizes[L_qpos] = nq; sizes[L_qvel] = nv; sizes[L_qacc_ws] = nv; sizes[L_ctrl] = nu;
   sizes[L_mocap_pos] = 3 * m.nmocap + 3; sizes[L_mocap_quat] = 4 * m.nmocap + 4; sizes[L_time] = 1;
-  sizes[L_xpos] = 3 * nb; sizes[L_xquat] = 4 * nb; sizes[L_xmat] = 9 * nb; sizes[L_xipos] = 3 * nb;
-  sizes[L_xanchor] = 3 * nj; sizes[L_xaxis] = 3 * nj; sizes[L_subtree_com] = 3 * nb; sizes[L_subtree_mass] = nb;
-  sizes[L_cinert] = 10 * nb; sizes[L_cdof] = 6 * nv; sizes[L_geom_xpos] = 3 * ng; sizes[L_geom_xmat] = 9 * ng;
+  sizes[L_xpos] = 3 * nb; sizes[L_xquat] = 4 * nb; sizes[L_xmat] = 9 * nb; sizes[L_subtree_com] = 3 * nb;
+  sizes[L_cinert] = 10 * nb; sizes[L_cdof] = 6 * nv;
   sizes[L_M] = nv * nv; sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_sD] = nv; sizes[L_isD] = nv;
   sizes[L_tmp] = nv; sizes[L_tmp2] = nv;
-  sizes[L_qfrc_bias] = nv; sizes[L_qfrc_passive] = nv; sizes[L_qfrc_actuator] = nv; sizes[L_qfrc_smooth] = nv;
-  sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv; sizes[L_qacc] = nv;
+  sizes[L_qfrc_smooth] = nv; sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv;
   sizes[L_act_force] = nu; sizes[L_act_moment] = nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
-  sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc;
-  sizes[L_efc_R] = ne; sizes[L_efc_b] = ne; sizes[L_efc_AR] = ne; sizes[L_efc_ARinv] = ne; sizes[L_efc_A] = ne;
-  sizes[L_efc_Ainv] = ne; sizes[L_efc_floss] = ne; sizes[L_efc_dA] = ne; sizes[L_con_mu] = 5 * nc; sizes[L_con_blk] = BLKSTRIDE * nc;
-  // U sub-layout
-  int u_coll = 6 * K_MAXPOLY * 3 + K_MAXPOLY;                 // poly buffers + depths
-  int u_dyn = 10 * nb;                                        // crb
-  int u_rne = 18 * nb + 6 * nv;                               // cvel, cacc, cfrc, cdof_dot
-  int u_scr = (2 * ne > nv ? 2 * ne : nv);
-  int u_newton = 7 * ne + nv * nv + 4 * nv + 16 * nc;         // Newton solver workspace
-  int u_con = ne * nv + 12 * nv + 4 * ne + u_scr + u_newton;
-  int u_int = nv * nv;
-  int U = u_coll;
-  if (u_dyn > U) U = u_dyn;
-  if (u_rne > U) U = u_rne;
-  if (u_con > U) U = u_con;
-  if (u_int > U) U = u_int;
-  l.u_poly = 0; l.u_pdep = 6 * K_MAXPOLY * 3;
-  l.u_crb = 0;
-  l.u_cvel = 0; l.u_cacc = 6 * nb; l.u_cfrc = 12 * nb; l.u_cdof_dot = 18 * nb;
-  l.u_G = 0; l.u_jac = ne * nv; l.u_aref = l.u_jac + 12 * nv; l.u_vel = l.u_aref + ne; l.u_pos = l.u_vel + ne;
-  l.u_margin = l.u_pos + ne; l.u_scratch = l.u_margin + ne; l.u_newton = l.u_scratch + u_scr;
-  l.u_qDeriv = 0;
+  sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = 5 * nc;
+  sizes[L_con_blk] = BLKSTRIDE * nc;
+  sizes[L_efc_R] = ne; sizes[L_efc_b] = ne;
+  // U: per-stage sub-layouts, each packed from offset 0 (see the kernel's Lay comment)
+  int us[U_COUNT];
+  for (int k = 0; k < U_COUNT; k++) us[k] = 0;
+  us[U_poly] = 6 * K_MAXPOLY * 3; us[U_pdep] = K_MAXPOLY; us[U_geom_xpos] = 3 * ng; us[U_geom_xmat] = 9 * ng;
+  us[U_xipos] = 3 * nb; us[U_xanchor] = 3 * nj; us[U_xaxis] = 3 * nj; us[U_subtree_mass] = nb;
+  us[U_comacc] = 4 * nb;
+  us[U_cvel] = 6 * nb; us[U_cacc] = 6 * nb; us[U_cfrc] = 6 * nb; us[U_cdof_dot] = 6 * nv;
+  us[U_qfrc_bias] = nv; us[U_qfrc_passive] = nv; us[U_qfrc_actuator] = nv;
+  us[U_G] = ne * nv; us[U_aref] = ne;
+  us[U_scratch] = (2 * ne > nv ? 2 * ne : nv);
+  // {vel, pos, margin} (make_constraints) | Newton Hessian, which may run on into
+  // the scratch slot (scratch is idle while the Hessian is live)
+  int xreg = 3 * ne;
+  if (xreg + us[U_scratch] < nv * nv) xreg = nv * nv - us[U_scratch];
+  us[U_jar] = ne; us[U_jv] = ne; us[U_f] = ne; us[U_Dr] = ne; us[U_isR] = ne;
+  us[U_nw] = nv; us[U_nw0] = nv; us[U_ng] = nv; us[U_ndir] = nv;
+  int U = 0, off;
+  // kin / collision stage
+  off = 0;
+  for (int k = U_poly; k <= U_comacc; k++) { l.u[k] = off; off += us[k]; }
+  if (off > U) U = off;
+  // dynamics: crb alone, then rne arrays (crb is dead by then) + qfrc parts
+  l.u[U_crb] = 0;
+  if (10 * nb > U) U = 10 * nb;
+  off = 0;
+  for (int k = U_cvel; k <= U_qfrc_actuator; k++) { l.u[k] = off; off += us[k]; }
+  if (off > U) U = off;
+  // constraints + solver
+  off = 0;
+  l.u[U_G] = off; off += us[U_G];
+  l.u[U_aref] = off; off += us[U_aref];
+  l.u[U_vel] = off; l.u[U_pos] = off + ne; l.u[U_margin] = off + 2 * ne; l.u[U_nH] = off; off += xreg;
+  for (int k = U_scratch; k <= U_ndir; k++) { l.u[k] = off; off += us[k]; }
+  if (off > U) U = off;
+  // integration
+  l.u[U_qDeriv] = 0;
+  if (nv * nv > U) U = nv * nv;
   sizes[L_U] = U;
-  sizes[L_ints] = (16 + 3 * nc + 5 * ne + 1) / 2;
-  int off = 0;
+  sizes[L_ints] = (16 + 3 * nc + 4 * ne + 1) / 2;
+  off = 0;
   for (int k = 0; k < L_COUNT; k++) {
     l.o[k] = off;
     off += sizes[k];

@@ -53,19 +53,20 @@ struct Dat {
   double *subtree_com, *subtree_mass, *cinert, *cdof;
   double *geom_xpos, *geom_xmat;
   double *M, *Dv, *Dinv, *sD, *isD, *tmp, *tmp2;
-  double *qfrc_bias, *qfrc_passive, *qfrc_actuator, *qfrc_smooth, *qacc_smooth, *qfrc_constraint, *qacc;
+  double *qfrc_bias, *qfrc_passive, *qfrc_actuator, *qfrc_smooth, *qacc_smooth, *qfrc_constraint;
   double *act_force, *act_moment, *act_length, *act_vel;
   double *con_pos, *con_frame, *con_dist;
-  double *efc_R, *efc_b, *efc_AR, *efc_ARinv, *efc_A, *efc_Ainv, *efc_floss, *efc_dA, *con_mu, *con_blk;
+  double *efc_R, *efc_b, *con_mu, *con_blk;
   // U region views
   double *crb, *cvel, *cacc, *cfrc, *cdof_dot;          // dynamics stage
   P2* poly;                                           // collision stage
   double* pdep;                                       // collision stage
-  double *G, *jac, *efc_aref, *efc_vel, *efc_pos, *efc_margin, *scratch;  // constraint + solver stage
+  double *comacc;                                     // comPos stage
+  double *G, *efc_aref, *efc_vel, *efc_pos, *efc_margin, *scratch;  // constraint + solver stage
   double* qDeriv;                                     // integration stage
   // Newton solver workspace (U region, after the constraint stage views)
-  double *efc_jar, *efc_jv, *efc_f, *efc_Dr, *efc_isR, *efc_sqR, *efc_mup, *nH, *nw, *nw0, *ng, *ndir, *con_hb;
-  int *con_pair, *con_g1, *con_g2, *efc_type, *efc_dim, *efc_con, *efc_lead, *efc_state, *ints;
+  double *efc_jar, *efc_jv, *efc_f, *efc_Dr, *efc_isR, *nH, *nw, *nw0, *ng, *ndir, *con_hb;
+  int *con_pair, *con_g1, *con_g2, *efc_type, *efc_dim, *efc_con, *efc_state, *ints;
 };
 // ints[]: 0 ncon, 1 nefc, 2 overflow, 3 iters, 6 cr0, 7 cr1, 8 neq rows, 9 fr0, 10 fr1, 11 lr0, 12 lr1
 #define NCON ints[0]
@@ -398,8 +399,8 @@ DEVI void com_pos(const Mdl& md, Dat& d) {
   const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
   const int32_t *jtype = IA(md, jnt_type), *dadr = IA(md, jnt_dofadr);
   const double *mass = DA(md, body_mass), *inertia = DA(md, body_inertia);
-  // subtree mass + mass-weighted com packed as 4 doubles per body in scratch
-  double* sc = d.scratch;
+  // subtree mass + mass-weighted com packed as 4 doubles per body
+  double* sc = d.comacc;
   for (int b = lane; b < nb; b += WAVE) {
     sc[4 * b] = mass[b];
     sc[4 * b + 1] = mass[b] * d.xipos[3 * b];
@@ -1260,53 +1261,58 @@ DEVI void collision(const Mdl& md, Dat& d) {
 
 // ---------------------------------------------------------------------------
 // LDS layout (offsets in doubles; computed on the host by make_layout)
+// LDS carve-up (make_layout in mgs_capi.hip).  Persistent arrays live for the
+// whole step; the U region is time-multiplexed between stages:
+//   kin/collision: polygon buffers, geom poses, xipos/xanchor/xaxis, comPos sums
+//   dynamics:      crb | cvel, cacc, cfrc, cdof_dot, qfrc_bias/passive/actuator
+//   constraints:   G, aref, {vel,pos,margin | Newton Hessian}, scratch, Newton rows
+//   integration:   qDeriv
 enum {
   L_qpos, L_qvel, L_qacc_ws, L_ctrl, L_mocap_pos, L_mocap_quat, L_time,
-  L_xpos, L_xquat, L_xmat, L_xipos, L_xanchor, L_xaxis, L_subtree_com, L_subtree_mass, L_cinert, L_cdof,
-  L_geom_xpos, L_geom_xmat,
+  L_xpos, L_xquat, L_xmat, L_subtree_com, L_cinert, L_cdof,
   L_M, L_Dv, L_Dinv, L_sD, L_isD, L_tmp, L_tmp2,
-  L_qfrc_bias, L_qfrc_passive, L_qfrc_actuator, L_qfrc_smooth, L_qacc_smooth, L_qfrc_constraint, L_qacc,
+  L_qfrc_smooth, L_qacc_smooth, L_qfrc_constraint,
   L_act_force, L_act_moment, L_act_length, L_act_vel,
-  L_con_pos, L_con_frame, L_con_dist,
-  L_efc_R, L_efc_b, L_efc_AR, L_efc_ARinv, L_efc_A, L_efc_Ainv, L_efc_floss, L_efc_dA, L_con_mu, L_con_blk,
+  L_con_pos, L_con_frame, L_con_dist, L_con_mu, L_con_blk,
+  L_efc_R, L_efc_b,
   L_U, L_ints, L_COUNT
+};
+enum {
+  U_poly, U_pdep, U_geom_xpos, U_geom_xmat, U_xipos, U_xanchor, U_xaxis, U_subtree_mass, U_comacc,
+  U_crb, U_cvel, U_cacc, U_cfrc, U_cdof_dot, U_qfrc_bias, U_qfrc_passive, U_qfrc_actuator,
+  U_G, U_aref, U_vel, U_pos, U_margin, U_nH, U_scratch, U_jar, U_jv, U_f, U_Dr, U_isR, U_nw, U_nw0, U_ng,
+  U_ndir, U_qDeriv, U_COUNT
 };
 struct Lay {
   int o[L_COUNT];
+  int u[U_COUNT];   // offsets relative to o[L_U]
   int ncon_max, nefc_max, nv;
   int total_doubles;
-  // U sub-offsets (relative to o[L_U])
-  int u_crb, u_cvel, u_cacc, u_cfrc, u_cdof_dot, u_poly, u_pdep, u_G, u_jac, u_aref, u_vel, u_pos, u_margin,
-      u_scratch, u_qDeriv, u_newton;
 };
 
 DEVI void bind(Dat& d, double* s, const Lay& l) {
 #define B(f) d.f = s + l.o[L_##f]
   B(qpos); B(qvel); B(qacc_ws); B(ctrl); B(mocap_pos); B(mocap_quat); B(time);
-  B(xpos); B(xquat); B(xmat); B(xipos); B(xanchor); B(xaxis); B(subtree_com); B(subtree_mass); B(cinert); B(cdof);
-  B(geom_xpos); B(geom_xmat);
+  B(xpos); B(xquat); B(xmat); B(subtree_com); B(cinert); B(cdof);
   B(M); B(Dv); B(Dinv); B(sD); B(isD); B(tmp); B(tmp2);
-  B(qfrc_bias); B(qfrc_passive); B(qfrc_actuator); B(qfrc_smooth); B(qacc_smooth); B(qfrc_constraint); B(qacc);
+  B(qfrc_smooth); B(qacc_smooth); B(qfrc_constraint);
   B(act_force); B(act_moment); B(act_length); B(act_vel);
-  B(con_pos); B(con_frame); B(con_dist);
-  B(efc_R); B(efc_b); B(efc_AR); B(efc_ARinv); B(efc_A); B(efc_Ainv); B(efc_floss); B(efc_dA); B(con_mu); B(con_blk);
+  B(con_pos); B(con_frame); B(con_dist); B(con_mu); B(con_blk);
+  B(efc_R); B(efc_b);
 #undef B
   double* U = s + l.o[L_U];
-  d.crb = U + l.u_crb; d.cvel = U + l.u_cvel; d.cacc = U + l.u_cacc; d.cfrc = U + l.u_cfrc;
-  d.cdof_dot = U + l.u_cdof_dot;
-  d.poly = (P2*)(U + l.u_poly); d.pdep = U + l.u_pdep;
-  d.G = U + l.u_G; d.jac = U + l.u_jac; d.efc_aref = U + l.u_aref; d.efc_vel = U + l.u_vel;
-  d.efc_pos = U + l.u_pos; d.efc_margin = U + l.u_margin; d.scratch = U + l.u_scratch;
-  d.qDeriv = U + l.u_qDeriv;
-  {
-    int ne = l.nefc_max, nv = l.nv, nc = l.ncon_max;
-    double* n0 = U + l.u_newton;
-    d.efc_jar = n0; d.efc_jv = n0 + ne; d.efc_f = n0 + 2 * ne; d.efc_Dr = n0 + 3 * ne;
-    d.efc_isR = n0 + 4 * ne; d.efc_sqR = n0 + 5 * ne; d.efc_mup = n0 + 6 * ne;
-    d.nH = n0 + 7 * ne; d.nw = d.nH + nv * nv; d.nw0 = d.nw + nv; d.ng = d.nw0 + nv; d.ndir = d.ng + nv;
-    d.con_hb = d.ndir + nv;
-    (void)nc;
-  }
+#define BU(f, k) d.f = U + l.u[k]
+  d.poly = (P2*)(U + l.u[U_poly]);
+  BU(pdep, U_pdep); BU(geom_xpos, U_geom_xpos); BU(geom_xmat, U_geom_xmat); BU(xipos, U_xipos);
+  BU(xanchor, U_xanchor); BU(xaxis, U_xaxis); BU(subtree_mass, U_subtree_mass); BU(comacc, U_comacc);
+  BU(crb, U_crb); BU(cvel, U_cvel); BU(cacc, U_cacc); BU(cfrc, U_cfrc); BU(cdof_dot, U_cdof_dot);
+  BU(qfrc_bias, U_qfrc_bias); BU(qfrc_passive, U_qfrc_passive); BU(qfrc_actuator, U_qfrc_actuator);
+  BU(G, U_G); BU(efc_aref, U_aref); BU(efc_vel, U_vel); BU(efc_pos, U_pos); BU(efc_margin, U_margin);
+  BU(nH, U_nH); BU(scratch, U_scratch); BU(efc_jar, U_jar); BU(efc_jv, U_jv); BU(efc_f, U_f);
+  BU(efc_Dr, U_Dr); BU(efc_isR, U_isR); BU(nw, U_nw); BU(nw0, U_nw0); BU(ng, U_ng); BU(ndir, U_ndir);
+  BU(qDeriv, U_qDeriv);
+#undef BU
+  d.con_hb = d.con_blk;   // Newton cone Hessians reuse the contact-block slots
   int* ib = (int*)(s + l.o[L_ints]);
   d.ints = ib;
   int ncmax = l.ncon_max, nemax = l.nefc_max;
@@ -1316,8 +1322,26 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   d.efc_type = d.con_g2 + ncmax;
   d.efc_dim = d.efc_type + nemax;
   d.efc_con = d.efc_dim + nemax;
-  d.efc_lead = d.efc_con + nemax;
-  d.efc_state = d.efc_lead + nemax;
+  d.efc_state = d.efc_con + nemax;
+}
+
+// A_rr = G_r . G_r in the oracle's order (its efc_A)
+DEVI double row_sqnorm(const Dat& d, int r, int nv) {
+  const double* Gr = d.G + r * nv;
+  double a = 0.0;
+  for (int k = 0; k < nv; k++) a = a + Gr[k] * Gr[k];
+  return a;
+}
+
+// first row of its block (contacts span dim rows with one efc_con)
+DEVI int efc_lead(const Dat& d, int r) {
+  return d.efc_type[r] != MGS_EFC_CONTACT || r == 0 || d.efc_type[r - 1] != MGS_EFC_CONTACT ||
+         d.efc_con[r - 1] != d.efc_con[r];
+}
+
+// frictionloss of a FRICTION row (its efc_con is the dof), 0 otherwise
+DEVI double row_floss(const Mdl& md, const Dat& d, int r) {
+  return d.efc_type[r] == MGS_EFC_FRICTION ? DA(md, dof_frictionloss)[d.efc_con[r]] : 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1393,8 +1417,6 @@ DEVI int add_row(const Mdl& md, Dat& d, int type, double pos, double margin, int
   int r = d.NEFC++;
   d.efc_type[r] = type; d.efc_pos[r] = pos; d.efc_margin[r] = margin;
   d.efc_dim[r] = dim; d.efc_con[r] = con;
-  d.efc_lead[r] = (type != MGS_EFC_CONTACT || r == 0 || d.efc_type[r - 1] != MGS_EFC_CONTACT ||
-                   d.efc_con[r - 1] != con) ? 1 : 0;
   return r;
 }
 
@@ -1419,7 +1441,7 @@ DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, co
     double p = (j == 0) ? (d.efc_pos[q] - d.efc_margin[q]) : 0.0;
     d.efc_aref[q] = -B * d.efc_vel[q] - (Kc * imp) * p;
   }
-  double Rn = ((1.0 - imp) / imp) * d.efc_dA[r];
+  double Rn = ((1.0 - imp) / imp) * d.scratch[r];
   if (Rn < K_MINVAL) Rn = K_MINVAL;
   d.efc_R[r] = Rn;
   if (elliptic_contact && dim > 1) {
@@ -1428,7 +1450,7 @@ DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, co
     for (int j = 1; j < dim - 1; j++) d.efc_R[r + j + 1] = (R1 * (mu[0] * mu[0])) / (mu[j] * mu[j]);
   } else {
     for (int j = 1; j < dim; j++) {
-      double Rj = ((1.0 - imp) / imp) * d.efc_dA[r + j];
+      double Rj = ((1.0 - imp) / imp) * d.scratch[r + j];
       d.efc_R[r + j] = Rj < K_MINVAL ? K_MINVAL : Rj;
     }
   }
@@ -1460,7 +1482,7 @@ DEVI void diag_approx(const Mdl& md, Dat& d, int ne) {
       int b1 = gbody[d.con_g1[id]], b2 = gbody[d.con_g2[id]];
       v = (k < 3) ? biw[2 * b1] + biw[2 * b2] : biw[2 * b1 + 1] + biw[2 * b2 + 1];
     }
-    d.efc_dA[r] = v;
+    d.scratch[r] = v;   // efc_diagApprox, consumed by row_params
   }
 }
 
@@ -1468,10 +1490,6 @@ DEVI void diag_approx(const Mdl& md, Dat& d, int ne) {
 // whitened row G = D^-1/2 L^-1 J^T in place, A = G.G; impedance; blocks.
 DEVI void make_constraints(const Mdl& md, Dat& d) {
   int nv = md.m.nv, lane = lane_id();
-  double* jp1 = d.jac;
-  double* jr1 = d.jac + 3 * nv;
-  double* jp2 = d.jac + 6 * nv;
-  double* jr2 = d.jac + 9 * nv;
   int* ints = d.ints;
   double* J = d.G;
   if (lane == 0) { d.NEFC = 0; }
@@ -1566,7 +1584,6 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         if (r < 0) break;
         for (int c = 0; c < nv; c++) J[r * nv + c] = 0.0;
         J[r * nv + k] = 1.0;
-        d.efc_floss[r] = floss[k];
       }
     }
     ints[10] = d.NEFC;
@@ -1644,9 +1661,6 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       Gr[i] = s;
     }
     for (int i = 0; i < nv; i++) Gr[i] = Gr[i] * d.isD[i];
-    double a = 0.0;
-    for (int k = 0; k < nv; k++) a = a + Gr[k] * Gr[k];
-    d.efc_A[r] = a;
   }
   wsync();
   PT(10);
@@ -1677,14 +1691,16 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     }
   }
   wsync();
-  for (int r = lane; r < ne; r += WAVE) {
-    d.efc_b[r] = d.efc_b[r] - d.efc_aref[r];
-    double ar = d.efc_A[r] + d.efc_R[r];
-    d.efc_AR[r] = ar;
-    d.efc_ARinv[r] = 1.0 / ar;
-    d.efc_Ainv[r] = 1.0 / d.efc_A[r];
-  }
-  // contact blocks A = G G^T (lanes over block entries)
+  for (int r = lane; r < ne; r += WAVE) d.efc_b[r] = d.efc_b[r] - d.efc_aref[r];
+  wsync();
+  PT(11);
+}
+
+// contact blocks of A = G G^T for the (PGS / noslip) block updates, lanes over
+// block entries; they share storage with the Newton cone Hessians
+DEVI void contact_blocks(const Mdl& md, Dat& d) {
+  int nv = md.m.nv, lane = lane_id();
+  int* ints = d.ints;
   for (int r = uni(ints[6]); r < uni(ints[7]);) {
     int dim = uni(d.efc_dim[r]);
     double* blk = d.con_blk + BLKSTRIDE * uni(d.efc_con[r]);
@@ -1699,7 +1715,6 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     r += dim;
   }
   wsync();
-  PT(11);
 }
 
 // ---------------------------------------------------------------------------
@@ -1811,7 +1826,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
   }
   double dc = 0.0;
   if (!noslip) {
-    double fn = old[0] - res[0] * d.efc_ARinv[r];
+    double fn = old[0] - res[0] * (1.0 / (blk[0] + d.efc_R[r]));
     if (fn < 0.0) fn = 0.0;
     double dn = fn - old[0];
     nw[0] = fn;
@@ -1911,10 +1926,10 @@ DEVI void project_scalar(int t, double floss, double* f) {
   }
 }
 
-DEVI void project_block_lds(const Dat& d, int r, double* f) {
+DEVI void project_block_lds(const Mdl& md, const Dat& d, int r, double* f) {
   int t = d.efc_type[r];
   if (t == MGS_EFC_FRICTION) {
-    double fl = d.efc_floss[r];
+    double fl = row_floss(md, d, r);
     if (f[0] < -fl) f[0] = -fl;
     if (f[0] > fl) f[0] = fl;
   } else if (t == MGS_EFC_LIMIT) {
@@ -1959,7 +1974,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
   if (lane == 0) {
     for (int r = 0; r < ne;) {
       int dim = d.efc_type[r] == MGS_EFC_CONTACT ? d.efc_dim[r] : 1;
-      if (d.efc_type[r] != MGS_EFC_EQUALITY) project_block_lds(d, r, fl + r);
+      if (d.efc_type[r] != MGS_EFC_EQUALITY) project_block_lds(md, d, r, fl + r);
       r += dim;
     }
   }
@@ -1998,9 +2013,9 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
         double jw = tree_sum(g * u, P);
         double fo = getf(fr0, fr1, r);
         double res = (jw + d.efc_R[r] * fo) + d.efc_b[r];
-        double AR = d.efc_AR[r];
-        double fnew[1] = {fo - res * d.efc_ARinv[r]};
-        if (t != MGS_EFC_EQUALITY) project_scalar(t, d.efc_floss[r], fnew);
+        double AR = row_sqnorm(d, r, nv) + d.efc_R[r];
+        double fnew[1] = {fo - res * (1.0 / AR)};
+        if (t != MGS_EFC_EQUALITY) project_scalar(t, row_floss(md, d, r), fnew);
         double delta = fnew[0] - fo;
         improvement = improvement - delta * (0.5 * AR * delta + res);
         if (delta != 0.0) {
@@ -2041,10 +2056,11 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
         double g = (lane < nv) ? d.G[r * nv + lane] : 0.0;
         double res = tree_sum(g * u, P) + d.efc_b[r];
         double fo = getf(fr0, fr1, r);
-        double fnew[1] = {fo - res * d.efc_Ainv[r]};
-        project_scalar(t, d.efc_floss[r], fnew);
+        double Arr = row_sqnorm(d, r, nv);
+        double fnew[1] = {fo - res * (1.0 / Arr)};
+        project_scalar(t, row_floss(md, d, r), fnew);
         double delta = fnew[0] - fo;
-        improvement = improvement - delta * (0.5 * d.efc_A[r] * delta + res);
+        improvement = improvement - delta * (0.5 * Arr * delta + res);
         if (delta != 0.0) {
           double s = u + g * delta;
           if (lane < nv) u = s;
@@ -2083,7 +2099,7 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
       double s = t[i];
       for (int k = 0; k < i; k++) s = s + d.M[i * nv + k] * t[k];
       d.qfrc_constraint[i] = s;
-      d.qacc[i] = d.qacc_smooth[i] + z[i];
+      d.qacc_ws[i] = d.qacc_smooth[i] + z[i];   // qacc, kept as next step's warmstart
     }
   }
   wsync();
@@ -2104,7 +2120,8 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
 
 // evaluate the block led by row r at violations jr[] (registers, dim <= 4):
 // forces f[], zone, cone Hessian hb[a*4+b] (if want_hb); returns cost
-DEVI double row_eval(const Dat& d, int r, int t, int dim, const double* jr, double* f, int& st, double* hb,
+DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const double* jr, double* f, int& st,
+                     double* hb,
                      bool want_hb) {
   if (t == MGS_EFC_EQUALITY) {
     double Dr = d.efc_Dr[r];
@@ -2126,7 +2143,7 @@ DEVI double row_eval(const Dat& d, int r, int t, int dim, const double* jr, doub
   if (t == MGS_EFC_FRICTION) {
     double isr = d.efc_isR[r];
     double z = -jr[0] * isr;
-    double lim = d.efc_floss[r] * d.efc_sqR[r];
+    double lim = row_floss(md, d, r) * sqrt(d.efc_R[r]);
     double y = z;
     st = ST_QUAD;
     if (z > lim) { y = lim; st = ST_SAT; }
@@ -2134,7 +2151,8 @@ DEVI double row_eval(const Dat& d, int r, int t, int dim, const double* jr, doub
     f[0] = y * isr;
     return y * z - 0.5 * (y * y);
   }
-  double mup = d.efc_mup[r];
+  // mu' = mu0 / sqrt(impratio) (oracle efc_mup)
+  double mup = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
   double z[4], y[4], isr[4];
 #pragma unroll
   for (int a = 0; a < 4; a++) {
@@ -2217,14 +2235,14 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P) {
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     int r = lane + h * WAVE;
-    if (r < ne && d.efc_lead[r]) {
+    if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
       int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
       double jr[4], f[4], hb[16];
       int st = ST_OFF;
 #pragma unroll
       for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
-      cr[h] = row_eval(d, r, t, dim, jr, f, st, hb, true);
+      cr[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true);
 #pragma unroll
       for (int a = 0; a < 4; a++)
         if (a < dim) { d.efc_f[r + a] = f[a]; d.efc_state[r + a] = st; }
@@ -2255,13 +2273,13 @@ DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
 }
 
 // cost derivatives along the search direction at step alpha
-DEVI void ls_eval(const Dat& d, int ne, double alpha, double A1, double A2, double* d1, double* d2) {
+DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, double A2, double* d1, double* d2) {
   int lane = lane_id();
   double c1[2] = {0.0, 0.0}, c2[2] = {0.0, 0.0};
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     int r = lane + h * WAVE;
-    if (r < ne && d.efc_lead[r]) {
+    if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
       int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
       double jr[4], jv[4], f[4], hb[16];
@@ -2271,7 +2289,7 @@ DEVI void ls_eval(const Dat& d, int ne, double alpha, double A1, double A2, doub
         jv[a] = (a < dim) ? d.efc_jv[r + a] : 0.0;
         jr[a] = (a < dim) ? d.efc_jar[r + a] + alpha * jv[a] : 0.0;
       }
-      row_eval(d, r, t, dim, jr, f, st, hb, true);
+      row_eval(md, d, r, t, dim, jr, f, st, hb, true);
       double s1 = 0.0, s2 = 0.0;
       if (dim == 1) {
         s1 = -f[0] * jv[0];
@@ -2306,11 +2324,8 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   int P = next_pow2(nv);
   for (int r = lane; r < ne; r += WAVE) {
     double sq = sqrt(d.efc_R[r]);
-    d.efc_sqR[r] = sq;
     d.efc_isR[r] = 1.0 / sq;
     d.efc_Dr[r] = 1.0 / d.efc_R[r];
-    if (d.efc_type[r] == MGS_EFC_CONTACT && d.efc_lead[r] && d.efc_dim[r] > 1)
-      d.efc_mup[r] = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
   }
   // w0 = W(qacc_smooth), w = W(qacc_ws)   (lane i: s_i = a_i + sum_{k>i} L_ki a_k)
   if (lane < nv) {
@@ -2414,14 +2429,14 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     double A1 = tree_sum(q * dl, P);
     double A2 = tree_sum(dl * dl, P);
     double p0, q0, alpha = 0.0;
-    ls_eval(d, ne, 0.0, A1, A2, &p0, &q0);
+    ls_eval(md, d, ne, 0.0, A1, A2, &p0, &q0);
     if (p0 < 0.0) {
       double lo = 0.0, hi = 0.0;
       int hi_ok = 0;
       alpha = -p0 / q0;
       for (int ls = 0; ls < md.m.ls_iterations; ls++) {
         double pp, qq;
-        ls_eval(d, ne, alpha, A1, A2, &pp, &qq);
+        ls_eval(md, d, ne, alpha, A1, A2, &pp, &qq);
         if (fabs(pp) < md.m.ls_tolerance * (-p0)) break;
         if (pp < 0.0) lo = alpha;
         else { hi = alpha; hi_ok = 1; }
@@ -2463,8 +2478,13 @@ DEVI void solve(const Mdl& md, Dat& d) {
   meaninertia = meaninertia / (double)nv;
   double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
   double fr0, fr1, u;
-  if (md.m.solver == 0) solve_pgs(md, d, scale, fr0, fr1, u);
-  else solve_newton<NV>(md, d, scale, fr0, fr1, u);
+  if (md.m.solver == 0) {
+    contact_blocks(md, d);
+    solve_pgs(md, d, scale, fr0, fr1, u);
+  } else {
+    solve_newton<NV>(md, d, scale, fr0, fr1, u);
+    if (md.m.noslip_iterations > 0) contact_blocks(md, d);   // overwrites the cone Hessians
+  }
   PT(16);
   noslip(md, d, scale, fr0, fr1, u);
   PT(17);
@@ -2555,7 +2575,6 @@ DEVI void integrate(const Mdl& md, Dat& d) {
         d.qpos[a] = d.qpos[a] + dt * d.qvel[v];
       }
     }
-    for (int k = 0; k < nv; k++) d.qacc_ws[k] = d.qacc[k];
     d.time[0] = d.time[0] + dt;
   }
   wsync();
