@@ -796,8 +796,10 @@ DEVI void support_pair(const Mdl& md, const Dat& d, int g1, int g2, const double
 }
 
 DEVI void mink_support(const Mdl& md, const Dat& d, int g1, int g2, const double* dir, SupPt* p) {
+  PT(4);
   support_pair(md, d, g1, g2, dir, p->a, p->b);
   sub3(p->v, p->a, p->b);
+  PT(22);
 }
 
 DEVI void portal_normal(double* n, const SupPt* p1, const SupPt* p2, const SupPt* p3) {
@@ -817,15 +819,21 @@ DEVI int portal_reach_tol(const SupPt* p1, const SupPt* p2, const SupPt* p3, con
   mn = mn < t3 ? mn : t3;
   return mn <= tol;
 }
-DEVI void portal_expand(SupPt* p0, SupPt* p1, SupPt* p2, SupPt* p3, const SupPt* p4) {
+// which portal vertex p4 replaces (1, 2 or 3); value semantics keep the
+// support points in registers (pointer-selected stores spilled them to scratch)
+DEVI int portal_choose(const SupPt& p0, const SupPt& p1, const SupPt& p2, const SupPt& p3, const SupPt& p4) {
   double c[3];
-  cross3(c, p4->v, p0->v);
-  if (dot3(p1->v, c) > 0.0) {
-    if (dot3(p2->v, c) > 0.0) *p1 = *p4; else *p3 = *p4;
-  } else {
-    if (dot3(p3->v, c) > 0.0) *p2 = *p4; else *p1 = *p4;
-  }
+  cross3(c, p4.v, p0.v);
+  if (dot3(p1.v, c) > 0.0) return (dot3(p2.v, c) > 0.0) ? 1 : 3;
+  return (dot3(p3.v, c) > 0.0) ? 2 : 1;
 }
+#define PORTAL_EXPAND(p0, p1, p2, p3, p4)             \
+  do {                                                \
+    int _k = portal_choose(p0, p1, p2, p3, p4);       \
+    if (_k == 1) p1 = p4;                             \
+    else if (_k == 2) p2 = p4;                        \
+    else p3 = p4;                                     \
+  } while (0)
 
 DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n, double* depth, double* pos) {
   const double tol = md.m.mpr_tolerance;
@@ -892,7 +900,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
     mink_support(md, d, g1, g2, dir, &p4);
     if (dot3(p4.v, dir) < 0.0) return 0;
     if (portal_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) return 0;
-    portal_expand(&p0, &p1, &p2, &p3, &p4);
+    PORTAL_EXPAND(p0, p1, p2, p3, p4);
   }
   if (it == K_MPR_MAXIT) return 0;
   for (it = 0;; it++) {
@@ -919,7 +927,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
       }
       return 1;
     }
-    portal_expand(&p0, &p1, &p2, &p3, &p4);
+    PORTAL_EXPAND(p0, p1, p2, p3, p4);
   }
 }
 
@@ -1457,33 +1465,31 @@ DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, co
 }
 
 // MuJoCo mj_diagApprox from the qpos0 inverse weights (oracle diag_approx()); lane 0
-DEVI void diag_approx(const Mdl& md, Dat& d, int ne) {
+DEVI void diag_approx_row(const Mdl& md, Dat& d, int r) {
   const double *biw = DA(md, body_invweight0), *diw = DA(md, dof_invweight0);
   const int32_t *et = IA(md, eq_type), *eo1 = IA(md, eq_obj1id), *eo2 = IA(md, eq_obj2id);
   const int32_t *jd = IA(md, jnt_dofadr), *gbody = IA(md, geom_bodyid);
-  int start = 0;
-  for (int r = 0; r < ne; r++) {
-    int t = d.efc_type[r], id = d.efc_con[r];
-    if (r == 0 || d.efc_type[r - 1] != t || d.efc_con[r - 1] != id) start = r;
-    int k = r - start;
-    double v = 0.0;
-    if (t == MGS_EFC_EQUALITY) {
-      if (et[id] == MGS_EQ_CONNECT) v = biw[2 * eo1[id]] + biw[2 * eo2[id]];
-      else if (et[id] == MGS_EQ_WELD) v = biw[2 * eo1[id] + (k > 2)] + biw[2 * eo2[id] + (k > 2)];
-      else {
-        v = diw[jd[eo1[id]]];
-        if (eo2[id] >= 0) v = v + diw[jd[eo2[id]]];
-      }
-    } else if (t == MGS_EFC_FRICTION) {
-      v = diw[id];
-    } else if (t == MGS_EFC_LIMIT) {
-      v = diw[jd[id]];
-    } else {
-      int b1 = gbody[d.con_g1[id]], b2 = gbody[d.con_g2[id]];
-      v = (k < 3) ? biw[2 * b1] + biw[2 * b2] : biw[2 * b1 + 1] + biw[2 * b2 + 1];
+  int t = d.efc_type[r], id = d.efc_con[r];
+  int start = r;
+  while (start > 0 && d.efc_type[start - 1] == t && d.efc_con[start - 1] == id) start--;
+  int k = r - start;
+  double v = 0.0;
+  if (t == MGS_EFC_EQUALITY) {
+    if (et[id] == MGS_EQ_CONNECT) v = biw[2 * eo1[id]] + biw[2 * eo2[id]];
+    else if (et[id] == MGS_EQ_WELD) v = biw[2 * eo1[id] + (k > 2)] + biw[2 * eo2[id] + (k > 2)];
+    else {
+      v = diw[jd[eo1[id]]];
+      if (eo2[id] >= 0) v = v + diw[jd[eo2[id]]];
     }
-    d.scratch[r] = v;   // efc_diagApprox, consumed by row_params
+  } else if (t == MGS_EFC_FRICTION) {
+    v = diw[id];
+  } else if (t == MGS_EFC_LIMIT) {
+    v = diw[jd[id]];
+  } else {
+    int b1 = gbody[d.con_g1[id]], b2 = gbody[d.con_g2[id]];
+    v = (k < 3) ? biw[2 * b1] + biw[2 * b2] : biw[2 * b1 + 1] + biw[2 * b2 + 1];
   }
+  d.scratch[r] = v;   // efc_diagApprox, consumed by row_params
 }
 
 // Build J rows (into the G slots), then per row: velocity, J.qacc_smooth,
@@ -1664,30 +1670,22 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   }
   wsync();
   PT(10);
-  if (lane == 0) {
-    diag_approx(md, d, ne);
-    const double *eqsr = DA(md, eq_solref), *eqsi = DA(md, eq_solimp);
-    for (int r = 0; r < ints[8]; r++) {
-      int e = d.efc_con[r];
-      row_params(md, d, r, 1, eqsr + 2 * e, eqsi + 5 * e, nullptr, 0);
-    }
-    const double *dsr = DA(md, dof_solref), *dsi = DA(md, dof_solimp);
-    for (int r = ints[9]; r < ints[10]; r++) {
-      int k = d.efc_con[r];
-      row_params(md, d, r, 1, dsr + 2 * k, dsi + 5 * k, nullptr, 0);
-    }
-    const double *jsr = DA(md, jnt_solref), *jsi = DA(md, jnt_solimp);
-    for (int r = ints[11]; r < ints[12]; r++) {
-      int j = d.efc_con[r];
-      row_params(md, d, r, 1, jsr + 2 * j, jsi + 5 * j, nullptr, 0);
-    }
-    const double *psr = DA(md, pair_solref), *psi = DA(md, pair_solimp);
-    for (int r = ints[6]; r < ints[7];) {
-      int c = d.efc_con[r];
-      int p = d.con_pair[c];
-      int dim = d.efc_dim[r];
-      row_params(md, d, r, dim, psr + 2 * p, psi + 5 * p, d.con_mu + 5 * c, 1);
-      r += dim;
+  // diagApprox then impedance / reference acceleration, lanes over rows (blocks
+  // by their leading row); each lane writes only its own rows
+  for (int r = lane; r < ne; r += WAVE) diag_approx_row(md, d, r);
+  wsync();
+  for (int r = lane; r < ne; r += WAVE) {
+    int t = d.efc_type[r], id = d.efc_con[r];
+    if (t == MGS_EFC_EQUALITY) {
+      row_params(md, d, r, 1, DA(md, eq_solref) + 2 * id, DA(md, eq_solimp) + 5 * id, nullptr, 0);
+    } else if (t == MGS_EFC_FRICTION) {
+      row_params(md, d, r, 1, DA(md, dof_solref) + 2 * id, DA(md, dof_solimp) + 5 * id, nullptr, 0);
+    } else if (t == MGS_EFC_LIMIT) {
+      row_params(md, d, r, 1, DA(md, jnt_solref) + 2 * id, DA(md, jnt_solimp) + 5 * id, nullptr, 0);
+    } else if (efc_lead(d, r)) {
+      int p = d.con_pair[id];
+      row_params(md, d, r, d.efc_dim[r], DA(md, pair_solref) + 2 * p, DA(md, pair_solimp) + 5 * p,
+                 d.con_mu + 5 * id, 1);
     }
   }
   wsync();
@@ -2081,30 +2079,35 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
   }
 }
 
+// qacc = qacc_smooth + L^-T D^-1/2 u ; qfrc_constraint = L D^1/2 u, lane i owns
+// dof i: backward substitution column by column (k descending, as the oracle),
+// the L-multiply row by row (k ascending), broadcasts by v_readlane.
+template <int NV>
 DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
-  int nv = md.m.nv, lane = lane_id();
-  // qacc = qacc_smooth + L^-T D^-1/2 u ; qfrc_constraint = L D^1/2 u   (lane 0)
-  if (lane < nv) d.tmp2[lane] = u;
-  wsync();
-  if (lane == 0) {
-    double* z = d.tmp;
-    for (int i = nv - 1; i >= 0; i--) {
-      double s = d.tmp2[i] * d.isD[i];
-      for (int k = i + 1; k < nv; k++) s = s - d.M[k * nv + i] * z[k];
-      z[i] = s;
-    }
-    double* t = d.scratch;
-    for (int i = 0; i < nv; i++) t[i] = d.tmp2[i] * d.sD[i];
-    for (int i = 0; i < nv; i++) {
-      double s = t[i];
-      for (int k = 0; k < i; k++) s = s + d.M[i * nv + k] * t[k];
-      d.qfrc_constraint[i] = s;
-      d.qacc_ws[i] = d.qacc_smooth[i] + z[i];   // qacc, kept as next step's warmstart
-    }
+  int lane = lane_id();
+  int li = lane < NV ? lane : 0;
+  double Lr[NV], Lc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) { Lr[k] = d.M[li * NV + k]; Lc[k] = d.M[k * NV + li]; }
+  double z = u * d.isD[li];
+#pragma unroll
+  for (int k = NV - 1; k >= 0; k--) {
+    double zk = readlane_d(z, k);
+    if (lane < k) z = z - Lc[k] * zk;
+  }
+  double t = u * d.sD[li];
+  double q = t;
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    double tk = readlane_d(t, k);
+    if (lane > k) q = q + Lr[k] * tk;
+  }
+  if (lane < NV) {
+    d.qfrc_constraint[lane] = q;
+    d.qacc_ws[lane] = d.qacc_smooth[lane] + z;   // qacc, kept as next step's warmstart
   }
   wsync();
 }
-
 
 // ---------------------------------------------------------------------------
 // Newton solver on the primal (MuJoCo mj_solNewton restated; oracle
@@ -2488,7 +2491,7 @@ DEVI void solve(const Mdl& md, Dat& d) {
   PT(16);
   noslip(md, d, scale, fr0, fr1, u);
   PT(17);
-  finalize_solution(md, d, u);
+  finalize_solution<NV>(md, d, u);
   PT(18);
 }
 
@@ -2524,14 +2527,18 @@ DEVI void integrate(const Mdl& md, Dat& d) {
   // recompute M (it was factored in place), then MI = M - dt*qDeriv
   crb(md, d);
   PT(19);
-  if (lane == 0) {
-    for (int i = 0; i < nv * nv; i++) d.qDeriv[i] = 0.0;
+  // M - dt * qDeriv, lane i forms row i of qDeriv (-damping on the diagonal,
+  // then each active affine actuator's mom_i (mom_j dv) in actuator order) and
+  // applies it straight to M (the oracle's element expressions)
+  if (lane < nv) {
     const double* damp = DA(md, dof_damping);
-    for (int k = 0; k < nv; k++) d.qDeriv[k * nv + k] = -damp[k];
     const int32_t *gtype = IA(md, actuator_gaintype), *btype = IA(md, actuator_biastype);
     const int32_t* flim = IA(md, actuator_forcelimited);
     const double *gain = DA(md, actuator_gainprm), *bias = DA(md, actuator_biasprm);
     const double* frange = DA(md, actuator_forcerange);
+    double q[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) q[j] = (j == lane) ? -damp[lane] : 0.0;
     for (int u = 0; u < md.m.nu; u++) {
       double f = d.act_force[u];
       if (flim[u] && (f <= frange[2 * u] || f >= frange[2 * u + 1])) continue;
@@ -2540,14 +2547,14 @@ DEVI void integrate(const Mdl& md, Dat& d) {
       if (gtype[u] == MGS_GAIN_AFFINE) dv = dv + gain[3 * u + 2] * d.ctrl[u];
       if (dv == 0.0) continue;
       const double* mom = d.act_moment + u * nv;
-      for (int i = 0; i < nv; i++) {
-        if (mom[i] == 0.0) continue;
-        for (int j = 0; j < nv; j++) d.qDeriv[i * nv + j] = d.qDeriv[i * nv + j] + mom[i] * (mom[j] * dv);
-      }
+      double mi = mom[lane];
+      if (mi == 0.0) continue;
+#pragma unroll
+      for (int j = 0; j < NV; j++) q[j] = q[j] + mi * (mom[j] * dv);
     }
+#pragma unroll
+    for (int j = 0; j < NV; j++) d.M[lane * NV + j] = d.M[lane * NV + j] - dt * q[j];
   }
-  wsync();
-  for (int i = lane; i < nv * nv; i += WAVE) d.M[i] = d.M[i] - dt * d.qDeriv[i];
   wsync();
   PT(20);
   ldl_factor<NV>(d.M, d.Dv, d.Dinv);

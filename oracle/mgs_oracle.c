@@ -1704,7 +1704,7 @@ static void finalize_solution(const Mdl* md, Dat* d) {
   double z[128];
   for (int i = nv - 1; i >= 0; i--) {
     double s = d->w[i] * d->isD[i];
-    for (int k = i + 1; k < nv; k++) s = s - d->L[k * nv + i] * z[k];
+    for (int k = nv - 1; k > i; k--) s = s - d->L[k * nv + i] * z[k];   /* k descending (kernel order) */
     z[i] = s;
   }
   double t[128];
