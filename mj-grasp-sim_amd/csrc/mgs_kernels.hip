@@ -727,25 +727,25 @@ DEVI void sup_dpp_level(SupAcc& a, int sel) {
   }
   sup_take(a, ob, oi);
 }
-// reduce and return the winning local-frame vertex (uniform)
-DEVI void sup_finish(SupAcc& a, double* v) {
-  // lanes keep their own best vertex; the wave winner's lane holds it
-  double lb = a.best;
-  int li = a.bi;
-  sup_dpp_level(a, 0);
-  sup_dpp_level(a, 1);
-  sup_dpp_level(a, 2);
-  sup_dpp_level(a, 3);
-  double b0 = readlane_d(a.best, 0), b1 = readlane_d(a.best, 16), b2 = readlane_d(a.best, 32),
-         b3 = readlane_d(a.best, 48);
-  int i0 = __builtin_amdgcn_readlane(a.bi, 0), i1 = __builtin_amdgcn_readlane(a.bi, 16),
-      i2 = __builtin_amdgcn_readlane(a.bi, 32), i3 = __builtin_amdgcn_readlane(a.bi, 48);
+// reduce and return the winning local-frame vertex (uniform).  Only lanes
+// < min(n, 64) hold candidates, so the reduction stops at the smallest power of
+// two covering them (8-vertex boxes: three DPP levels and one readlane).
+DEVI void sup_finish(SupAcc& a, double* v, int n) {
+  int P = n < WAVE ? next_pow2(n) : WAVE;
+  if (P > 1) sup_dpp_level(a, 0);
+  if (P > 2) sup_dpp_level(a, 1);
+  if (P > 4) sup_dpp_level(a, 2);
+  if (P > 8) sup_dpp_level(a, 3);
   SupAcc u;
-  u.best = b0; u.bi = i0;
-  sup_take(u, b1, i1);
-  sup_take(u, b2, i2);
-  sup_take(u, b3, i3);
-  (void)lb; (void)li;
+  u.best = readlane_d(a.best, 0);
+  u.bi = __builtin_amdgcn_readlane(a.bi, 0);
+  if (P > 16) {
+    sup_take(u, readlane_d(a.best, 16), __builtin_amdgcn_readlane(a.bi, 16));
+    if (P > 32) {
+      sup_take(u, readlane_d(a.best, 32), __builtin_amdgcn_readlane(a.bi, 32));
+      sup_take(u, readlane_d(a.best, 48), __builtin_amdgcn_readlane(a.bi, 48));
+    }
+  }
   int bi = (u.bi == 0x7fffffff) ? 0 : u.bi;
   int wl = bi & (WAVE - 1);
   v[0] = readlane_d(a.vx, wl);
@@ -754,50 +754,68 @@ DEVI void sup_finish(SupAcc& a, double* v) {
   a.bi = bi;
 }
 
-// supports of geom g1 along dir and geom g2 along -dir in one pass (two
-// independent reductions interleaved); results in world frame
-DEVI void support_pair(const Mdl& md, const Dat& d, int g1, int g2, const double* dir, double* out1,
-                       double* out2) {
+// Per-pair narrowphase context: both geoms' poses in registers (uniform) and,
+// for hulls of at most 64 vertices, this lane's vertex (lane i holds vertex i)
+// so the support mappings of a small hull never touch memory.
+struct PairCtx {
+  int n1, n2;
+  const double *V1, *V2;
+  double R1[9], R2[9], x1[3], x2[3];
+  double c1[3], c2[3];
+};
+DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   int lane = lane_id();
   const int32_t *ghull = IA(md, geom_hullid), *hadr = IA(md, hull_vertadr), *hnum = IA(md, hull_vertnum);
   int h1 = ghull[g1], h2 = ghull[g2];
-  int n1 = hnum[h1], n2 = hnum[h2];
-  const double* V1 = DA(md, hull_vert) + 3 * hadr[h1];
-  const double* V2 = DA(md, hull_vert) + 3 * hadr[h2];
-  const double* R1 = d.geom_xmat + 9 * g1;
-  const double* R2 = d.geom_xmat + 9 * g2;
+  c.n1 = hnum[h1];
+  c.n2 = hnum[h2];
+  c.V1 = DA(md, hull_vert) + 3 * hadr[h1];
+  c.V2 = DA(md, hull_vert) + 3 * hadr[h2];
+  for (int k = 0; k < 9; k++) { c.R1[k] = d.geom_xmat[9 * g1 + k]; c.R2[k] = d.geom_xmat[9 * g2 + k]; }
+  for (int k = 0; k < 3; k++) { c.x1[k] = d.geom_xpos[3 * g1 + k]; c.x2[k] = d.geom_xpos[3 * g2 + k]; }
+  int i1 = (lane < c.n1) ? lane : 0, i2 = (lane < c.n2) ? lane : 0;
+  for (int k = 0; k < 3; k++) { c.c1[k] = c.V1[3 * i1 + k]; c.c2[k] = c.V2[3 * i2 + k]; }
+}
+
+DEVI void sup_scan(SupAcc& a, const double* V, int n, const double* cached, const double* dl) {
+  int lane = lane_id();
+  if (n <= WAVE) {
+    if (lane < n) {
+      double sc = (cached[0] * dl[0] + cached[1] * dl[1]) + cached[2] * dl[2];
+      if (sc > a.best) { a.best = sc; a.bi = lane; a.vx = cached[0]; a.vy = cached[1]; a.vz = cached[2]; }
+    }
+  } else {
+    for (int i = lane; i < n; i += WAVE) {
+      double x = V[3 * i], y = V[3 * i + 1], z = V[3 * i + 2];
+      double sc = (x * dl[0] + y * dl[1]) + z * dl[2];
+      if (sc > a.best) { a.best = sc; a.bi = i; a.vx = x; a.vy = y; a.vz = z; }
+    }
+  }
+}
+
+// supports of g1 along dir and g2 along -dir (world frame), oracle support_geom()
+DEVI void support_pair(const PairCtx& c, const double* dir, double* out1, double* out2) {
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
   double dl1[3], dl2[3];
-  mulmtv3(dl1, R1, dir);
-  mulmtv3(dl2, R2, nd);
+  mulmtv3(dl1, c.R1, dir);
+  mulmtv3(dl2, c.R2, nd);
   SupAcc a1, a2;
   sup_init(a1);
   sup_init(a2);
-  int nmax = n1 > n2 ? n1 : n2;
-  for (int i = lane; i < nmax; i += WAVE) {
-    if (i < n1) {
-      double x = V1[3 * i], y = V1[3 * i + 1], z = V1[3 * i + 2];
-      double sc = (x * dl1[0] + y * dl1[1]) + z * dl1[2];
-      if (sc > a1.best) { a1.best = sc; a1.bi = i; a1.vx = x; a1.vy = y; a1.vz = z; }
-    }
-    if (i < n2) {
-      double x = V2[3 * i], y = V2[3 * i + 1], z = V2[3 * i + 2];
-      double sc = (x * dl2[0] + y * dl2[1]) + z * dl2[2];
-      if (sc > a2.best) { a2.best = sc; a2.bi = i; a2.vx = x; a2.vy = y; a2.vz = z; }
-    }
-  }
+  sup_scan(a1, c.V1, c.n1, c.c1, dl1);
+  sup_scan(a2, c.V2, c.n2, c.c2, dl2);
   double v1[3], v2[3], t[3];
-  sup_finish(a1, v1);
-  sup_finish(a2, v2);
-  mulmv3(t, R1, v1);
-  add3(out1, d.geom_xpos + 3 * g1, t);
-  mulmv3(t, R2, v2);
-  add3(out2, d.geom_xpos + 3 * g2, t);
+  sup_finish(a1, v1, c.n1);
+  sup_finish(a2, v2, c.n2);
+  mulmv3(t, c.R1, v1);
+  add3(out1, c.x1, t);
+  mulmv3(t, c.R2, v2);
+  add3(out2, c.x2, t);
 }
 
-DEVI void mink_support(const Mdl& md, const Dat& d, int g1, int g2, const double* dir, SupPt* p) {
+DEVI void mink_support(const PairCtx& c, const double* dir, SupPt* p) {
   PT(4);
-  support_pair(md, d, g1, g2, dir, p->a, p->b);
+  support_pair(c, dir, p->a, p->b);
   sub3(p->v, p->a, p->b);
   PT(22);
 }
@@ -835,7 +853,8 @@ DEVI int portal_choose(const SupPt& p0, const SupPt& p1, const SupPt& p2, const 
     else p3 = p4;                                     \
   } while (0)
 
-DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n, double* depth, double* pos) {
+DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1, int g2, double* n, double* depth,
+                         double* pos) {
   const double tol = md.m.mpr_tolerance;
   const int32_t* ghull = IA(md, geom_hullid);
   const double* HC = DA(md, hull_center);
@@ -849,7 +868,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
   if (p0.v[0] == 0.0 && p0.v[1] == 0.0 && p0.v[2] == 0.0) p0.v[0] = 1e-9;
   dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
   normalize3(dir);
-  mink_support(md, d, g1, g2, dir, &p1);
+  mink_support(pc, dir, &p1);
   if (dot3(p1.v, dir) <= 0.0) return 0;
   cross3(dir, p0.v, p1.v);
   if (dot3(dir, dir) < 1e-30) {
@@ -861,7 +880,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
     return 1;
   }
   normalize3(dir);
-  mink_support(md, d, g1, g2, dir, &p2);
+  mink_support(pc, dir, &p2);
   if (dot3(p2.v, dir) <= 0.0) return 0;
   {
     double e1[3], e2[3];
@@ -876,7 +895,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
   }
   int it;
   for (it = 0; it < K_MPR_MAXIT; it++) {
-    mink_support(md, d, g1, g2, dir, &p3);
+    mink_support(pc, dir, &p3);
     if (dot3(p3.v, dir) <= 0.0) return 0;
     double c[3];
     int cont = 0;
@@ -897,7 +916,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
   for (it = 0; it < K_MPR_MAXIT; it++) {
     portal_normal(dir, &p1, &p2, &p3);
     if (dot3(dir, p1.v) >= 0.0) break;
-    mink_support(md, d, g1, g2, dir, &p4);
+    mink_support(pc, dir, &p4);
     if (dot3(p4.v, dir) < 0.0) return 0;
     if (portal_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) return 0;
     PORTAL_EXPAND(p0, p1, p2, p3, p4);
@@ -905,7 +924,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, int g1, int g2, double* n,
   if (it == K_MPR_MAXIT) return 0;
   for (it = 0;; it++) {
     portal_normal(dir, &p1, &p2, &p3);
-    mink_support(md, d, g1, g2, dir, &p4);
+    mink_support(pc, dir, &p4);
     if (it >= K_MPR_MAXIT || portal_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) {
       double dep = dot3(dir, p1.v);
       if (!(dep > 0.0)) return 0;
@@ -943,56 +962,75 @@ DEVI void make_frame(const double* n, double* t1, double* t2) {
 }
 
 // feature extraction: wave max over heights, then ballot compaction in vertex
-// order of the vertices within tol of the extreme; out[] written to LDS.
-DEVI int feature(const Mdl& md, const Dat& d, int g, const double* n, const double* t1, const double* t2,
-                       int sign, double tol, P2* out, double* ext) {
+// feature extraction on geom 1 or 2 of the pair (oracle feature()): extreme of
+// the signed height along n over the hull (wave reduction sized to the hull),
+// then, if collect, the vertices within tol of it, compacted with a ballot in
+// vertex order (<= K_MAXF) into out[] (LDS).  Small hulls use the lane-cached
+// vertex of the pair context.
+DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1, const double* t2, int sign,
+                 double tol, int collect, P2* out, double* ext) {
   int lane = lane_id();
-  int h = IA(md, geom_hullid)[g];
-  int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
-  const double* V = DA(md, hull_vert) + 3 * adr;
-  const double* R = d.geom_xmat + 9 * g;
-  const double* x = d.geom_xpos + 3 * g;
+  const double* R = which == 1 ? c.R1 : c.R2;
+  const double* x = which == 1 ? c.x1 : c.x2;
+  const double* V = which == 1 ? c.V1 : c.V2;
+  const double* cv = which == 1 ? c.c1 : c.c2;
+  int num = which == 1 ? c.n1 : c.n2;
   double nl[3];
   mulmtv3(nl, R, n);
   double base = dot3(x, n);
   double best = (sign > 0) ? -INFINITY : INFINITY;
-  for (int i = lane; i < num; i += WAVE) {
-    double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
-    if (sign > 0 ? (s > best) : (s < best)) best = s;
+  if (num <= WAVE) {
+    if (lane < num) best = base + ((cv[0] * nl[0] + cv[1] * nl[1]) + cv[2] * nl[2]);
+  } else {
+    for (int i = lane; i < num; i += WAVE) {
+      double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
+      if (sign > 0 ? (s > best) : (s < best)) best = s;
+    }
   }
-  // extreme over the wave: DPP inside 16-lane rows, then the four row values
+  int P = num < WAVE ? next_pow2(num) : WAVE;
 #pragma unroll
   for (int sel = 0; sel < 4; sel++) {
-    double ob = dpp_d(best, sel);
-    if (sign > 0 ? (ob > best) : (ob < best)) best = ob;
+    if (P > (1 << sel)) {
+      double ob = dpp_d(best, sel);
+      if (sign > 0 ? (ob > best) : (ob < best)) best = ob;
+    }
   }
   {
-    double r1 = readlane_d(best, 16), r2 = readlane_d(best, 32), r3 = readlane_d(best, 48);
-    best = readlane_d(best, 0);
-    if (sign > 0 ? (r1 > best) : (r1 < best)) best = r1;
-    if (sign > 0 ? (r2 > best) : (r2 < best)) best = r2;
-    if (sign > 0 ? (r3 > best) : (r3 < best)) best = r3;
+    double b0 = readlane_d(best, 0);
+    if (P > 16) {
+      double r1 = readlane_d(best, 16);
+      if (sign > 0 ? (r1 > b0) : (r1 < b0)) b0 = r1;
+      if (P > 32) {
+        double r2 = readlane_d(best, 32), r3 = readlane_d(best, 48);
+        if (sign > 0 ? (r2 > b0) : (r2 < b0)) b0 = r2;
+        if (sign > 0 ? (r3 > b0) : (r3 < b0)) b0 = r3;
+      }
+    }
+    best = b0;
   }
   *ext = best;
+  if (!collect) return 0;
   double lim = (sign > 0) ? best - tol : best + tol;
   int cnt = 0;
   for (int c0 = 0; c0 < num && cnt < K_MAXF; c0 += WAVE) {
     int i = c0 + lane;
-    double s = 0.0;
+    double s = 0.0, vx = 0.0, vy = 0.0, vz = 0.0;
     int pred = 0;
     if (i < num) {
-      s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
+      if (num <= WAVE) { vx = cv[0]; vy = cv[1]; vz = cv[2]; }
+      else { vx = V[3 * i]; vy = V[3 * i + 1]; vz = V[3 * i + 2]; }
+      s = base + ((vx * nl[0] + vy * nl[1]) + vz * nl[2]);
       pred = sign > 0 ? (s >= lim) : (s <= lim);
     }
     unsigned long long mask = __ballot(pred);
     int before = __popcll(mask & ((1ull << lane) - 1ull));
     int pos = cnt + before;
     if (pred && pos < K_MAXF) {
-      double t[3], P[3];
-      mulmv3(t, R, V + 3 * i);
-      add3(P, x, t);
-      out[pos].x = dot3(P, t1);
-      out[pos].y = dot3(P, t2);
+      double vv[3] = {vx, vy, vz}, t[3], Pw[3];
+      mulmv3(t, R, vv);
+      add3(Pw, x, t);
+      out[pos].x = dot3(Pw, t1);
+      out[pos].y = dot3(Pw, t2);
       out[pos].h = s;
     }
     cnt += __popcll(mask);
@@ -1117,7 +1155,9 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   int lane = lane_id();
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
   double n[3], depth, mpos[3];
-  int hit = mpr_penetration(md, d, g1, g2, n, &depth, mpos);
+  PairCtx pc;
+  pair_ctx(md, d, g1, g2, pc);
+  int hit = mpr_penetration(md, d, pc, g1, g2, n, &depth, mpos);
   PT(4);
   if (!hit) return;
   double t1[3], t2[3];
@@ -1130,13 +1170,15 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   P2* pts = d.poly + 5 * K_MAXPOLY;
   double* dep = d.pdep;
   double s1, s2;
-  int na = feature(md, d, g1, n, t1, t2, +1, 0.0, fa, &s1);
-  int nb = feature(md, d, g2, n, t1, t2, -1, 0.0, fb, &s2);
+  // first pass: only the extremes are used (the oracle's first feature() pass
+  // output is overwritten by the second)
+  feature(pc, 1, n, t1, t2, +1, 0.0, 0, fa, &s1);
+  feature(pc, 2, n, t1, t2, -1, 0.0, 0, fb, &s2);
   double dn = s1 - s2;
   if (!(dn > 0.0)) return;
   double tol = dn + K_FEAT_EPS;
-  na = feature(md, d, g1, n, t1, t2, +1, tol, fa, &s1);
-  nb = feature(md, d, g2, n, t1, t2, -1, tol, fb, &s2);
+  int na = feature(pc, 1, n, t1, t2, +1, tol, 1, fa, &s1);
+  int nb = feature(pc, 2, n, t1, t2, -1, tol, 1, fb, &s2);
   if (lane == 0) {
     int refB = (nb >= na);
     int nr = refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly);
