@@ -124,6 +124,9 @@ typedef struct mgs_model_desc {
   int32_t i_body_lastdof;   /* last dof in the body's kinematic chain, -1 if none */
   int32_t i_body_dofmask;   /* 2: bit d set if dof d moves the body (dofs 0-31, 32-63) */
   int32_t i_body_depth;     /* tree depth (world 0); entry [nbody] = max depth */
+  int32_t i_body_childadr;  /* first entry of the body's children in body_child */
+  int32_t i_body_childnum;  /* number of children */
+  int32_t i_body_child;     /* children grouped by parent, decreasing body index */
   /* body arrays: double */
   int32_t d_body_pos;       /* 3 */
   int32_t d_body_quat;      /* 4 */

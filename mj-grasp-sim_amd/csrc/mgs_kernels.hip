@@ -371,7 +371,7 @@ DEVI void kinematics(const Mdl& md, Dat& d) {
 template <int W>
 DEVI void accumulate_up(const Mdl& md, double* arr, int with_world) {
   int lane = lane_id(), nb = md.m.nbody;
-  const int32_t *depth = IA(md, body_depth), *parent = IA(md, body_parentid);
+  const int32_t* depth = IA(md, body_depth);
   int maxd = max_depth(md);
   int myd = (lane < nb) ? depth[lane] : -1;
   for (int L = maxd; L >= 1; L--) {
@@ -379,11 +379,12 @@ DEVI void accumulate_up(const Mdl& md, double* arr, int with_world) {
       double acc[W];
 #pragma unroll
       for (int k = 0; k < W; k++) acc[k] = arr[W * lane + k];
-      for (int c = nb - 1; c > lane; c--) {
-        if (parent[c] == lane) {
+      const int32_t* kids = IA(md, body_child) + IA(md, body_childadr)[lane];
+      int nk = IA(md, body_childnum)[lane];
+      for (int q = 0; q < nk; q++) {   // children in decreasing body index
+        int c = kids[q];
 #pragma unroll
-          for (int k = 0; k < W; k++) acc[k] = acc[k] + arr[W * c + k];
-        }
+        for (int k = 0; k < W; k++) acc[k] = acc[k] + arr[W * c + k];
       }
 #pragma unroll
       for (int k = 0; k < W; k++) arr[W * lane + k] = acc[k];
@@ -1536,6 +1537,7 @@ DEVI void diag_approx_row(const Mdl& md, Dat& d, int r) {
 
 // Build J rows (into the G slots), then per row: velocity, J.qacc_smooth,
 // whitened row G = D^-1/2 L^-1 J^T in place, A = G.G; impedance; blocks.
+template <int NV>
 DEVI void make_constraints(const Mdl& md, Dat& d) {
   int nv = md.m.nv, lane = lane_id();
   int* ints = d.ints;
@@ -1696,19 +1698,28 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   PT(9);
   int ne = uni(d.NEFC);
   // per row (lanes over rows): vel, J.qacc_smooth, G in place, A
+  // (the row lives in registers for the triangular solve)
   for (int r = lane; r < ne; r += WAVE) {
-    double* Gr = d.G + r * nv;
+    double* Gr = d.G + r * NV;
+    double g[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) g[k] = Gr[k];
     double v = 0.0, bj = 0.0;
-    for (int k = 0; k < nv; k++) v = v + Gr[k] * d.qvel[k];
-    for (int k = 0; k < nv; k++) bj = bj + Gr[k] * d.qacc_smooth[k];
+#pragma unroll
+    for (int k = 0; k < NV; k++) v = v + g[k] * d.qvel[k];
+#pragma unroll
+    for (int k = 0; k < NV; k++) bj = bj + g[k] * d.qacc_smooth[k];
     d.efc_vel[r] = v;
     d.efc_b[r] = bj;
-    for (int i = 0; i < nv; i++) {
-      double s = Gr[i];
-      for (int k = 0; k < i; k++) s = s - d.M[i * nv + k] * Gr[k];
-      Gr[i] = s;
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+      double s = g[i];
+#pragma unroll
+      for (int k = 0; k < i; k++) s = s - d.M[i * NV + k] * g[k];
+      g[i] = s;
     }
-    for (int i = 0; i < nv; i++) Gr[i] = Gr[i] * d.isD[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) Gr[i] = g[i] * d.isD[i];
   }
   wsync();
   PT(10);
@@ -2558,7 +2569,7 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
   if (lane < nv) d.qfrc_smooth[lane] = (d.qfrc_passive[lane] - d.qfrc_bias[lane]) + d.qfrc_actuator[lane];
   wsync();
   ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
-  make_constraints(md, d);
+  make_constraints<NV>(md, d);
   solve<NV>(md, d);
 }
 
@@ -2739,7 +2750,7 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       wsync();
       ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
       PT(8);
-      make_constraints(md, d);
+      make_constraints<NV>(md, d);
       solve<NV>(md, d);
       integrate<NV>(md, d); PT(21);
 #else

@@ -1042,6 +1042,11 @@ class CompiledModel:
             depth[b] = depth[self.body_parentid[b]] + 1
         depth[self.nbody] = depth[:self.nbody].max()
         put_i("body_depth", depth)
+        kids = [[c for c in range(self.nbody - 1, 0, -1) if self.body_parentid[c] == b] for b in range(self.nbody)]
+        adr = np.cumsum([0] + [len(k) for k in kids])[:-1]
+        put_i("body_childadr", adr)
+        put_i("body_childnum", [len(k) for k in kids])
+        put_i("body_child", [c for k in kids for c in k] or [0])
         for n in ["body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia",
                   "body_invweight0", "dof_invweight0"]:
             put_d(n, getattr(self, n))
