@@ -2276,14 +2276,19 @@ DEVI double tree_rows(double v0, double v1, int ne) {
 }
 
 // jar = G w - aref; forces, zones, cone Hessians into LDS; returns total cost
+template <int NV>
 DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P) {
-  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
-  double q = (lane < nv) ? w[lane] - d.nw0[lane] : 0.0;
+  int ne = uni(d.NEFC), lane = lane_id();
+  double q = (lane < NV) ? w[lane] - d.nw0[lane] : 0.0;
   double gauss = 0.5 * tree_sum(q * q, P);
+  double wr[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) wr[k] = w[k];
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Gr = d.G + r * nv;
+    const double* Gr = d.G + r * NV;
     double s = 0.0;
-    for (int k = 0; k < nv; k++) s = s + Gr[k] * w[k];
+#pragma unroll
+    for (int k = 0; k < NV; k++) s = s + Gr[k] * wr[k];
     d.efc_jar[r] = s - d.efc_aref[r];
   }
   wsync();
@@ -2318,11 +2323,23 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P) {
 }
 
 // g = (w - w0) - G^T f   (lanes over dofs, rows summed in order)
+template <int NV>
 DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
-  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
-  if (lane < nv) {
+  int ne = uni(d.NEFC), lane = lane_id();
+  if (lane < NV) {
     double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d.G[r * nv + lane] * d.efc_f[r];
+    int r = 0;
+    // rows in order, four loads in flight per step
+    for (; r + 4 <= ne; r += 4) {
+      double g0 = d.G[r * NV + lane], g1 = d.G[(r + 1) * NV + lane], g2 = d.G[(r + 2) * NV + lane],
+             g3 = d.G[(r + 3) * NV + lane];
+      double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
+      s = s + g0 * f0;
+      s = s + g1 * f1;
+      s = s + g2 * f2;
+      s = s + g3 * f3;
+    }
+    for (; r < ne; r++) s = s + d.G[r * NV + lane] * d.efc_f[r];
     d.ng[lane] = (w[lane] - d.nw0[lane]) - s;
   }
   wsync();
@@ -2384,20 +2401,29 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     d.efc_Dr[r] = 1.0 / d.efc_R[r];
   }
   // w0 = W(qacc_smooth), w = W(qacc_ws)   (lane i: s_i = a_i + sum_{k>i} L_ki a_k)
-  if (lane < nv) {
-    double s = d.qacc_smooth[lane], s2 = d.qacc_ws[lane];
-    for (int k = lane + 1; k < nv; k++) s = s + d.M[k * nv + lane] * d.qacc_smooth[k];
-    for (int k = lane + 1; k < nv; k++) s2 = s2 + d.M[k * nv + lane] * d.qacc_ws[k];
-    d.nw0[lane] = s * d.sD[lane];
-    d.nw[lane] = s2 * d.sD[lane];
+  {
+    int li = lane < NV ? lane : 0;
+    double s = d.qacc_smooth[li], s2 = d.qacc_ws[li];
+#pragma unroll
+    for (int k = 1; k < NV; k++) {
+      double l = d.M[k * NV + li];
+      if (k > lane) {
+        s = s + l * d.qacc_smooth[k];
+        s2 = s2 + l * d.qacc_ws[k];
+      }
+    }
+    if (lane < NV) {
+      d.nw0[lane] = s * d.sD[lane];
+      d.nw[lane] = s2 * d.sD[lane];
+    }
   }
   wsync();
   double C = 0.0;
   if (ne > 0) {
-    double cws = newton_eval(md, d, d.nw, P);
-    double c0 = newton_eval(md, d, d.nw0, P);
+    double cws = newton_eval<NV>(md, d, d.nw, P);
+    double c0 = newton_eval<NV>(md, d, d.nw0, P);
     if (cws < c0) {
-      C = newton_eval(md, d, d.nw, P);
+      C = newton_eval<NV>(md, d, d.nw, P);
     } else {
       if (lane < nv) d.nw[lane] = d.nw0[lane];
       C = c0;
@@ -2407,7 +2433,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     if (lane < nv) d.nw[lane] = d.nw0[lane];
     wsync();
   }
-  newton_grad(md, d, d.nw);
+  newton_grad<NV>(md, d, d.nw);
   PT(12);
   int npair = (nv * (nv + 1)) / 2;
   int it;
@@ -2472,11 +2498,17 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     ldl_solve<NV>(d.nH, d.tmp2, d.ng, d.ndir);
     if (lane < nv) d.ndir[lane] = -d.ndir[lane];
     wsync();
-    for (int r = lane; r < ne; r += WAVE) {
-      const double* Gr = d.G + r * nv;
-      double s = 0.0;
-      for (int k = 0; k < nv; k++) s = s + Gr[k] * d.ndir[k];
-      d.efc_jv[r] = s;
+    {
+      double dr[NV];
+#pragma unroll
+      for (int k = 0; k < NV; k++) dr[k] = d.ndir[k];
+      for (int r = lane; r < ne; r += WAVE) {
+        const double* Gr = d.G + r * NV;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NV; k++) s = s + Gr[k] * dr[k];
+        d.efc_jv[r] = s;
+      }
     }
     wsync();
     PT(14);
@@ -2505,8 +2537,8 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     if (!(alpha > 0.0)) { it++; break; }
     if (lane < nv) d.nw[lane] = d.nw[lane] + alpha * dl;
     wsync();
-    double Cn = newton_eval(md, d, d.nw, P);
-    newton_grad(md, d, d.nw);
+    double Cn = newton_eval<NV>(md, d, d.nw, P);
+    newton_grad<NV>(md, d, d.nw);
     double improvement = scale * (C - Cn);
     C = Cn;
     double gl = (lane < nv) ? d.ng[lane] : 0.0;
@@ -2519,9 +2551,19 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   fr0 = (lane < ne) ? d.efc_f[lane] : 0.0;
   fr1 = (lane + WAVE < ne) ? d.efc_f[lane + WAVE] : 0.0;
   u = 0.0;
-  if (lane < nv) {
+  if (lane < NV) {
     double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d.G[r * nv + lane] * d.efc_f[r];
+    int r = 0;
+    for (; r + 4 <= ne; r += 4) {
+      double g0 = d.G[r * NV + lane], g1 = d.G[(r + 1) * NV + lane], g2 = d.G[(r + 2) * NV + lane],
+             g3 = d.G[(r + 3) * NV + lane];
+      double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
+      s = s + g0 * f0;
+      s = s + g1 * f1;
+      s = s + g2 * f2;
+      s = s + g3 * f3;
+    }
+    for (; r < ne; r++) s = s + d.G[r * NV + lane] * d.efc_f[r];
     u = s;
   }
 }
