@@ -2177,8 +2177,7 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
 // evaluate the block led by row r at violations jr[] (registers, dim <= 4):
 // forces f[], zone, cone Hessian hb[a*4+b] (if want_hb); returns cost
 DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const double* jr, double* f, int& st,
-                     double* hb,
-                     bool want_hb) {
+                     double* hb, bool want_hb, double* cq = nullptr) {
   if (t == MGS_EFC_EQUALITY) {
     double Dr = d.efc_Dr[r];
     f[0] = -jr[0] * Dr;
@@ -2244,6 +2243,12 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
       f[a] = y[a] * isr[a];
       c = c + y[a] * y[a];
     }
+  }
+  if (cq && st == ST_CONE) {
+    cq[0] = 1.0 / (1.0 + mup * mup);
+    cq[1] = (mup * yn) / tn;
+#pragma unroll
+    for (int a = 1; a < 4; a++) cq[1 + a] = z[a] / tn;
   }
   if (want_hb && st == ST_CONE) {
     double k1 = 1.0 / (1.0 + mup * mup);
@@ -2355,14 +2360,14 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
     if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
       int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
-      double jr[4], jv[4], f[4], hb[16];
+      double jr[4], jv[4], f[4], hb[16], cq[5];
       int st = ST_OFF;
 #pragma unroll
       for (int a = 0; a < 4; a++) {
         jv[a] = (a < dim) ? d.efc_jv[r + a] : 0.0;
         jr[a] = (a < dim) ? d.efc_jar[r + a] + alpha * jv[a] : 0.0;
       }
-      row_eval(md, d, r, t, dim, jr, f, st, hb, true);
+      row_eval(md, d, r, t, dim, jr, f, st, hb, false, cq);
       double s1 = 0.0, s2 = 0.0;
       if (dim == 1) {
         s1 = -f[0] * jv[0];
@@ -2376,11 +2381,21 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
           for (int a = 0; a < 4; a++)
             if (a < dim) s2 = s2 + (jv[a] * d.efc_Dr[r + a]) * jv[a];
         } else if (st == ST_CONE) {
+          // jv' hb jv in closed form (oracle ls_eval)
+          double mup = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
+          double u[4];
 #pragma unroll
-          for (int a = 0; a < 4; a++)
+          for (int a = 0; a < 4; a++) u[a] = (a < dim) ? jv[a] * d.efc_isR[r + a] : 0.0;
+          double vu = u[0], eu = 0.0, uu = 0.0;
 #pragma unroll
-            for (int b = 0; b < 4; b++)
-              if (a < dim && b < dim) s2 = s2 + (jv[a] * hb[a * 4 + b]) * jv[b];
+          for (int a = 1; a < 4; a++) {
+            if (a < dim) {
+              vu = vu + (mup * cq[1 + a]) * u[a];
+              eu = eu + cq[1 + a] * u[a];
+              uu = uu + u[a] * u[a];
+            }
+          }
+          s2 = (cq[0] * vu) * vu + cq[1] * (uu - eu * eu);
         }
       }
       c1[h] = s1;
@@ -2420,14 +2435,16 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   wsync();
   double C = 0.0;
   if (ne > 0) {
-    double cws = newton_eval<NV>(md, d, d.nw, P);
+    // (oracle: evaluate warmstart, smooth, keep the cheaper; evaluating the
+    // smooth point first leaves the warmstart's rows current in the common case)
     double c0 = newton_eval<NV>(md, d, d.nw0, P);
+    double cws = newton_eval<NV>(md, d, d.nw, P);
     if (cws < c0) {
-      C = newton_eval<NV>(md, d, d.nw, P);
+      C = cws;
     } else {
       if (lane < nv) d.nw[lane] = d.nw0[lane];
-      C = c0;
       wsync();
+      C = newton_eval<NV>(md, d, d.nw, P);
     }
   } else {
     if (lane < nv) d.nw[lane] = d.nw0[lane];

@@ -1745,7 +1745,7 @@ static double tree_rows(const double* v, int ne) {
 
 /* evaluate row r (or the block starting at r) at violations jr[];
  * writes forces f[], returns cost; state per row; hb = Hessian block (dim x dim) for cones */
-static double row_eval(const Dat* d, int r, const double* jr, double* f, int* st, double* hb) {
+static double row_eval(const Dat* d, int r, const double* jr, double* f, int* st, double* hb, double* cq) {
   int t = d->efc_type[r];
   if (t == MGS_EFC_EQUALITY) {
     double Dr = d->efc_Dr[r];
@@ -1803,6 +1803,12 @@ static double row_eval(const Dat* d, int r, const double* jr, double* f, int* st
     st[a] = zone;
     c = c + y[a] * y[a];
   }
+  if (cq && zone == ST_CONE) {
+    /* cone curvature: k1 = 1/(1+mu'^2), k2 = mu' yn / |z_t|, e = z_t / |z_t| */
+    cq[0] = 1.0 / (1.0 + mup * mup);
+    cq[1] = (mup * yn) / tn;
+    for (int a = 1; a < dim; a++) cq[1 + a] = z[a] / tn;
+  }
   if (hb && zone == ST_CONE) {
     double k1 = 1.0 / (1.0 + mup * mup);
     double k2 = (mup * yn) / tn;
@@ -1834,7 +1840,7 @@ static double newton_eval(const Mdl* md, Dat* d, const double* w, const double* 
   }
   for (int r = 0; r < ne;) {
     int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
-    cr[r] = row_eval(d, r, d->efc_jar + r, d->efc_f + r, d->efc_state + r, d->efc_hb + 36 * r);
+    cr[r] = row_eval(d, r, d->efc_jar + r, d->efc_f + r, d->efc_state + r, d->efc_hb + 36 * r, NULL);
     for (int a = 1; a < dim; a++) cr[r + a] = 0.0;
     r += dim;
   }
@@ -1855,10 +1861,10 @@ static void ls_eval(const Dat* d, double alpha, double A1, double A2, double* d1
   double c1[256], c2[256];
   for (int r = 0; r < ne;) {
     int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
-    double jr[6], f[6], hb[36];
+    double jr[6], f[6], cq[8];
     int st[6];
     for (int a = 0; a < dim; a++) jr[a] = d->efc_jar[r + a] + alpha * d->efc_jv[r + a];
-    row_eval(d, r, jr, f, st, hb);
+    row_eval(d, r, jr, f, st, NULL, cq);
     double s1 = 0.0, s2 = 0.0;
     if (dim == 1) {
       s1 = -f[0] * d->efc_jv[r];
@@ -1868,8 +1874,18 @@ static void ls_eval(const Dat* d, double alpha, double A1, double A2, double* d1
       if (st[0] == ST_QUAD) {
         for (int a = 0; a < dim; a++) s2 = s2 + (d->efc_jv[r + a] * d->efc_Dr[r + a]) * d->efc_jv[r + a];
       } else if (st[0] == ST_CONE) {
-        for (int a = 0; a < dim; a++)
-          for (int b = 0; b < dim; b++) s2 = s2 + (d->efc_jv[r + a] * hb[a * dim + b]) * d->efc_jv[r + b];
+        /* jv' hb jv in closed form: u_a = jv_a / sqrt(R_a),
+         * s2 = k1 (v.u)^2 + k2 (|u_t|^2 - (e.u_t)^2),  v = (1, mu' e) */
+        double mup = d->efc_mup[r];
+        double u[6];
+        for (int a = 0; a < dim; a++) u[a] = d->efc_jv[r + a] * d->efc_isR[r + a];
+        double vu = u[0], eu = 0.0, uu = 0.0;
+        for (int a = 1; a < dim; a++) {
+          vu = vu + (mup * cq[1 + a]) * u[a];
+          eu = eu + cq[1 + a] * u[a];
+          uu = uu + u[a] * u[a];
+        }
+        s2 = (cq[0] * vu) * vu + cq[1] * (uu - eu * eu);
       }
     }
     c1[r] = s1;
