@@ -522,21 +522,24 @@ DEVI void crb(const Mdl& md, Dat& d) {
 // register rows and their loops are fully static.
 template <int NV>
 DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
+  // right-looking: after pivot j is scaled, every later column c takes its
+  // update r_i[c] -= l_ij (l_cj d_j) at once.  Each entry receives the same
+  // products in the same ascending-pivot order as the oracle's left-looking
+  // loop (l_ij w with w = l_cj d_j; the diagonal w l_jj commutes), so the
+  // factor is bit-identical while the pivot chain shrinks to one column.
   int lane = lane_id();
 #pragma unroll
   for (int j = 0; j < NV; j++) {
     double dj = readlane_d(r[j], j);
-    double sj = r[j];
-#pragma unroll
-    for (int k = 0; k < j; k++) {
-      double l = readlane_d(r[k], j);
-      double w = l * Dv[k];
-      dj = dj - w * l;
-      sj = sj - r[k] * w;
-    }
     double inv = 1.0 / dj;
-    if (lane > j) r[j] = sj * inv;
+    if (lane > j) r[j] = r[j] * inv;
     if (lane == 0) { Dv[j] = dj; Dinv[j] = inv; }
+    double v = r[j] * dj;   // lane c: l_cj d_j
+#pragma unroll
+    for (int c = j + 1; c < NV; c++) {
+      double w = readlane_d(v, c);
+      r[c] = r[c] - r[j] * w;
+    }
   }
 }
 template <int NV>
@@ -2406,6 +2409,110 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
   *d2 = A2 + tree_rows(c2[0], c2[1], ne);
 }
 
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// Newton Hessian (see solve_newton): per-row weights into the (idle) nH
+// region, then the lower tiles of G' X by v_mfma_f64_16x16x4, written to nH
+// as full rows of H = I + G' W G (upper entries left unwritten).
+template <int NV>
+DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
+  constexpr int NT = (NV + 15) / 16;
+  int lane = lane_id();
+  // weight table: wt[4r..4r+3] = w_a, wi[r] = lead * 8 + nd (exact in f64)
+  double* wt = d.nH;
+  double* wi = d.nH + 4 * md.m.nefc_max;
+  for (int r = lane; r < ne; r += WAVE) {
+    int t = d.efc_type[r];
+    int st = d.efc_state[r];
+    double w0 = 0.0, w1 = 0.0, w2 = 0.0, w3 = 0.0;
+    int lead = r, nd = 0;
+    if (st == ST_QUAD) {
+      w0 = d.efc_Dr[r];
+      nd = 1;
+    } else if (st == ST_CONE && t == MGS_EFC_CONTACT) {
+      int c = d.efc_con[r], dim = d.efc_dim[r];
+      int bp = 0;
+      for (int q = 1; q < 4; q++)
+        if (r - q >= 0 && bp == q - 1 && d.efc_type[r - q] == MGS_EFC_CONTACT && d.efc_con[r - q] == c) bp = q;
+      const double* hb = d.con_hb + 16 * c + bp;
+      lead = r - bp;
+      nd = dim;
+      w0 = hb[0];
+      w1 = (dim > 1) ? hb[dim] : 0.0;
+      w2 = (dim > 2) ? hb[2 * dim] : 0.0;
+      w3 = (dim > 3) ? hb[3 * dim] : 0.0;
+    }
+    wt[4 * r] = w0; wt[4 * r + 1] = w1; wt[4 * r + 2] = w2; wt[4 * r + 3] = w3;
+    wi[r] = (double)(lead * 8 + nd);
+  }
+  wsync();
+  int cl = lane & 15, rg = lane >> 4;
+  v4d acc[NT * (NT + 1) / 2];
+#pragma unroll
+  for (int q = 0; q < NT * (NT + 1) / 2; q++) acc[q] = (v4d){0.0, 0.0, 0.0, 0.0};
+  int ks = (ne + 3) >> 2;
+  for (int s = 0; s < ks; s++) {
+    int r = 4 * s + rg;
+    bool valid = r < ne;
+    int rr = valid ? r : 0;
+    double gv[NT], x[NT];
+    const double* Gr = d.G + rr * NV;
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      int c = cl + 16 * t;
+      double v = Gr[c < NV ? c : 0];
+      gv[t] = (valid && c < NV) ? v : 0.0;
+    }
+    const double* wr = wt + 4 * rr;
+    double w[4] = {wr[0], wr[1], wr[2], wr[3]};
+    int info = (int)wi[rr];
+    int lead = info >> 3, nd = valid ? (info & 7) : 0;
+    bool multi = __ballot(nd > 1) != 0ull;
+    if (!multi) {
+#pragma unroll
+      for (int t = 0; t < NT; t++) x[t] = (nd == 1) ? 0.0 + gv[t] * w[0] : 0.0;
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        int c = cl + 16 * t;
+        int cc = c < NV ? c : 0;
+        double xs = 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+          int aa = a < nd ? a : 0;
+          double tv = xs + d.G[(lead + aa) * NV + cc] * w[a];
+          xs = (a < nd) ? tv : xs;
+        }
+        x[t] = (c < NV) ? xs : 0.0;
+      }
+    }
+    // tile (tj, ti), tj <= ti: D[j][i] += G_rj X_ri
+    int q = 0;
+#pragma unroll
+    for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+      for (int tj = 0; tj <= ti; tj++) {
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[tj], x[ti], acc[q], 0, 0, 0);
+        q++;
+      }
+  }
+  wsync();   // the weight table is dead; H overwrites the region
+  int q = 0;
+#pragma unroll
+  for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+    for (int tj = 0; tj <= ti; tj++) {
+      int i = cl + 16 * ti;
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        int j = rg + 4 * g + 16 * tj;
+        if (i < NV && j <= i) d.nH[i * NV + j] = (i == j ? 1.0 : 0.0) + acc[q][g];
+      }
+      q++;
+    }
+  wsync();
+}
+
 template <int NV>
 DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
@@ -2455,60 +2562,22 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   int npair = (nv * (nv + 1)) / 2;
   int it;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
-    // Hessian I + G' h G: lane i accumulates row i (j <= i) in registers over the
-    // row blocks in order (quad rows: (G_ri Dr) G_rj; cone blocks: x_b = sum_a
-    // G_{a,i} hb_ab, then x_b G_bj), then factors it in place (register LDL).
+    // Hessian I + G' W G on the matrix cores.  W is block diagonal (Dr on quad
+    // rows, the cone Hessian on cone blocks, 0 on inactive rows); X = W G row
+    // by row (x = 0.0 + sum_a G_{lead+a,i} w_a), then H_ij = (i == j) +
+    // sum_r G_rj X_ri as v_mfma_f64_16x16x4 k-steps over 4 rows at a time: an
+    // fma chain over the rows in ascending order, which the oracle restates.
+    // Lane l takes row 4s + (l >> 4) of k-step s and column (l & 15) + 16 t.
+    hessian_mfma<NV>(md, d, ne);
+    PT(23);
     {
+      int li = lane < NV ? lane : 0;
       double hr[NV];
 #pragma unroll
-      for (int j = 0; j < NV; j++) hr[j] = 0.0;
-      int li = lane < nv ? lane : 0;
-      // row metadata for all rows in registers (lane r holds row r / r + 64), read
-      // per row with v_readlane: no LDS round trip on the loop-control path
-      int meta0 = 0, meta1 = 0;
-      if (lane < ne) {
-        int t = d.efc_type[lane];
-        int dm = (t == MGS_EFC_CONTACT) ? d.efc_dim[lane] : 1;
-        meta0 = dm | (d.efc_state[lane] << 4) | (d.efc_con[lane] << 8);
-      }
-      if (lane + WAVE < ne) {
-        int rr = lane + WAVE;
-        int t = d.efc_type[rr];
-        int dm = (t == MGS_EFC_CONTACT) ? d.efc_dim[rr] : 1;
-        meta1 = dm | (d.efc_state[rr] << 4) | (d.efc_con[rr] << 8);
-      }
-      for (int r = 0; r < ne;) {
-        int m = (r < WAVE) ? __builtin_amdgcn_readlane(meta0, r) : __builtin_amdgcn_readlane(meta1, r - WAVE);
-        int dim = m & 15, st = (m >> 4) & 15, con = m >> 8;
-        if (dim > 1 && st == ST_CONE) {
-          const double* hb = d.con_hb + 16 * con;
-          for (int b = 0; b < dim; b++) {
-            double x = 0.0;
-            for (int a = 0; a < dim; a++) x = x + d.G[(r + a) * nv + li] * hb[a * dim + b];
-            const double* Gb = d.G + (r + b) * nv;
-            double g[NV];
-#pragma unroll
-            for (int j = 0; j < NV; j++) g[j] = Gb[j];
-#pragma unroll
-            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * g[j];
-          }
-        } else if (st == ST_QUAD) {
-          for (int a = 0; a < dim; a++) {
-            const double* Ga = d.G + (r + a) * nv;
-            double g[NV];
-#pragma unroll
-            for (int j = 0; j < NV; j++) g[j] = Ga[j];
-            double x = Ga[li] * d.efc_Dr[r + a];
-#pragma unroll
-            for (int j = 0; j < NV; j++) hr[j] = hr[j] + x * g[j];
-          }
-        }
-        r += dim;
-      }
-      asm volatile("; HESS_END");
-#pragma unroll
-      for (int j = 0; j < NV; j++) hr[j] = (j == lane ? 1.0 : 0.0) + hr[j];
+      for (int k = 0; k < NV; k++) hr[k] = d.nH[li * NV + k];
+      PT(24);
       ldl_factor_regs<NV>(hr, d.tmp, d.tmp2);
+      PT(25);
       store_lower<NV>(d.nH, hr);
     }
     PT(13);

@@ -74,7 +74,7 @@ typedef struct {
   int nefc;
   double *J, *K, *efc_pos, *efc_margin, *efc_vel, *efc_aref, *efc_R, *efc_A, *efc_b, *efc_f;
   double *efc_mu, *efc_blk, *efc_hb, *efc_dA, *efc_floss, *efc_AR, *efc_ARinv, *efc_Ainv;
-  double *efc_Dr, *efc_sqR, *efc_isR, *efc_mup, *efc_jar, *efc_jv;
+  double *efc_Dr, *efc_sqR, *efc_isR, *efc_mup, *efc_jar, *efc_jv, *hX;
   int* efc_state;
   double *Dv, *sD, *isD;
   int *efc_type, *efc_dim, *efc_con;
@@ -261,7 +261,7 @@ static Dat* dat_alloc(const Mdl* md) {
   TAKE(efc_aref, ne); TAKE(efc_R, ne); TAKE(efc_A, ne); TAKE(efc_b, ne); TAKE(efc_f, ne);
   TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_hb, 36 * ne); TAKE(efc_dA, ne); TAKE(efc_floss, ne); TAKE(w, nv);
   TAKE(efc_AR, ne); TAKE(efc_ARinv, ne); TAKE(efc_Ainv, ne); TAKE(Dv, nv); TAKE(sD, nv); TAKE(isD, nv);
-  TAKE(efc_Dr, ne); TAKE(efc_sqR, ne); TAKE(efc_isR, ne); TAKE(efc_mup, ne); TAKE(efc_jar, ne); TAKE(efc_jv, ne);
+  TAKE(efc_Dr, ne); TAKE(efc_sqR, ne); TAKE(efc_isR, ne); TAKE(efc_mup, ne); TAKE(efc_jar, ne); TAKE(efc_jv, ne); TAKE(hX, ne * nv);
 #undef TAKE
   if (pass == 0) base = (double*)calloc(tot, sizeof(double));
   }
@@ -1937,27 +1937,39 @@ static void solve_newton(const Mdl* md, Dat* d) {
   newton_grad(d, nv, w, w0, g);
   int it = 0;
   for (it = 0; it < m->iterations && ne > 0; it++) {
-    /* Hessian I + G' h G (lower triangle then mirrored), blocks in row order */
+    /* Hessian I + G' W G with W block diagonal: Dr on quad rows, the cone
+       Hessian block on cone blocks, 0 on inactive rows.  X = W G row by row
+       (x = 0.0 + sum_a G_{lead+a,i} w_a), then H_ij = (i == j) + an fma chain
+       over the rows in ascending order of G_rj X_ri: the kernel computes the
+       sum with v_mfma_f64_16x16x4 k-steps, which round once per row (probed
+       bit-exactly on MI355X, tools/probes/mfma_f64_check.py). */
+    for (int r = 0; r < ne; r++) {
+      int t = d->efc_type[r], st = d->efc_state[r];
+      double wv[4] = {0.0, 0.0, 0.0, 0.0};
+      int lead = r, nd = 0;
+      if (st == ST_QUAD) {
+        wv[0] = d->efc_Dr[r];
+        nd = 1;
+      } else if (st == ST_CONE && t == MGS_EFC_CONTACT) {
+        lead = r;
+        while (lead > 0 && d->efc_type[lead - 1] == MGS_EFC_CONTACT && d->efc_con[lead - 1] == d->efc_con[r] &&
+               r - lead < 3)
+          lead--;
+        int dim = d->efc_dim[r], bp = r - lead;
+        const double* hb = d->efc_hb + 36 * lead;
+        for (int a = 0; a < dim; a++) wv[a] = hb[a * dim + bp];
+        nd = dim;
+      }
+      for (int i = 0; i < nv; i++) {
+        double x = 0.0;
+        for (int a = 0; a < nd; a++) x = x + d->K[(size_t)(lead + a) * nv + i] * wv[a];
+        d->hX[(size_t)r * nv + i] = x;
+      }
+    }
     for (int i = 0; i < nv; i++)
       for (int j = 0; j <= i; j++) {
         double s = 0.0;
-        for (int r = 0; r < ne;) {
-          int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
-          int st = d->efc_state[r];
-          if (dim > 1 && st == ST_CONE) {
-            /* x_b = sum_a G_{r+a,i} hb_ab, then s += x_b G_{r+b,j} (the kernel's per-lane order) */
-            const double* hb = d->efc_hb + 36 * r;
-            for (int b = 0; b < dim; b++) {
-              double x = 0.0;
-              for (int a = 0; a < dim; a++) x = x + d->K[(size_t)(r + a) * nv + i] * hb[a * dim + b];
-              s = s + x * d->K[(size_t)(r + b) * nv + j];
-            }
-          } else if (st == ST_QUAD) {
-            for (int a = 0; a < dim; a++)
-              s = s + (d->K[(size_t)(r + a) * nv + i] * d->efc_Dr[r + a]) * d->K[(size_t)(r + a) * nv + j];
-          }
-          r += dim;
-        }
+        for (int r = 0; r < ne; r++) s = fma(d->K[(size_t)r * nv + j], d->hX[(size_t)r * nv + i], s);
         H[i * nv + j] = (i == j ? 1.0 : 0.0) + s;
         H[j * nv + i] = H[i * nv + j];
       }
