@@ -384,8 +384,8 @@ int mgs_tree_probe(const double* a, const double* c, int n, int nb, double* out)
 // diagnostic build only: read and clear the stage timers (s_memtime ticks)
 int mgs_prof_read(unsigned long long* out) {
 #ifdef MGS_PROFILE
-  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 32));
-  unsigned long long z[32] = {0};
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 64));
+  unsigned long long z[64] = {0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
   return MGS_OK;
 #else

@@ -82,19 +82,21 @@ DEVI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // Diagnostic stage timers (built only with -DMGS_PROFILE; never in the product build)
 #ifdef MGS_PROFILE
-__device__ unsigned long long g_prof[32];
+__device__ unsigned long long g_prof[64];
 // per-workgroup accumulators in static LDS; PT(k) at wave-uniform points only
-__shared__ unsigned long long s_prof[33];
+__shared__ unsigned long long s_prof[65];
 #define PT(k) do { unsigned long long _n = __builtin_amdgcn_s_memtime(); \
-    if (__lane_id() == 0) { s_prof[k] += _n - s_prof[32]; s_prof[32] = _n; } } while (0)
-#define PROF_DECL if (__lane_id() == 0) { for (int _k = 0; _k < 32; _k++) s_prof[_k] = 0; \
-    s_prof[32] = __builtin_amdgcn_s_memtime(); }
+    if (__lane_id() == 0) { s_prof[k] += _n - s_prof[64]; s_prof[64] = _n; } } while (0)
+#define PROF_DECL if (__lane_id() == 0) { for (int _k = 0; _k < 64; _k++) s_prof[_k] = 0; \
+    s_prof[64] = __builtin_amdgcn_s_memtime(); }
 #define PROF(k) PT(k)
-#define PROF_FLUSH if (lane_id() == 0) for (int _k = 0; _k < 32; _k++) atomicAdd(&g_prof[_k], s_prof[_k]);
+#define PCNT(k, v) do { if (__lane_id() == 0) s_prof[k] += (v); } while (0)
+#define PROF_FLUSH if (lane_id() == 0) for (int _k = 0; _k < 64; _k++) atomicAdd(&g_prof[_k], s_prof[_k]);
 #else
 #define PT(k)
 #define PROF_DECL
 #define PROF(k)
+#define PCNT(k, v)
 #define PROF_FLUSH
 #endif
 DEVI void wsync() { __syncthreads(); }
@@ -591,9 +593,11 @@ DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double
   wsync();
 }
 
-// actuation (lane 0)
+// actuation (oracle actuation()), lanes over dofs: each lane builds its entry of
+// every moment row (tendon wraps in order), the actuator length / velocity are
+// the oracle's sequential sums evaluated uniformly, forces applied per dof.
 DEVI void actuation(const Mdl& md, Dat& d) {
-  int nv = md.m.nv;
+  int nv = md.m.nv, lane = lane_id();
   const int32_t *trntype = IA(md, actuator_trntype), *trnid = IA(md, actuator_trnid);
   const int32_t *gtype = IA(md, actuator_gaintype), *btype = IA(md, actuator_biastype);
   const int32_t *clim = IA(md, actuator_ctrllimited), *flim = IA(md, actuator_forcelimited);
@@ -604,28 +608,27 @@ DEVI void actuation(const Mdl& md, Dat& d) {
   const int32_t *wdof = IA(md, wrap_dofid), *wq = IA(md, wrap_qposadr);
   const double* wcoef = DA(md, wrap_coef);
   const int32_t *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
-  for (int k = 0; k < nv; k++) d.qfrc_actuator[k] = 0.0;
+  double qfa = 0.0;
   for (int u = 0; u < md.m.nu; u++) {
     double* mom = d.act_moment + u * nv;
-    for (int k = 0; k < nv; k++) mom[k] = 0.0;
-    double len;
+    double m = 0.0, len;
     if (trntype[u] == MGS_TRN_JOINT) {
       int j = trnid[u];
       len = d.qpos[jq[j]] * gear[u];
-      mom[jd[j]] = gear[u];
+      if (lane == jd[j]) m = gear[u];
     } else {
       int t = trnid[u];
       double tl = 0.0;
       for (int w = tadr[t]; w < tadr[t] + tnum[t]; w++) {
         tl = tl + wcoef[w] * d.qpos[wq[w]];
-        mom[wdof[w]] = mom[wdof[w]] + wcoef[w] * gear[u];
+        if (lane == wdof[w]) m = m + wcoef[w] * gear[u];
       }
       len = tl * gear[u];
     }
+    if (lane < nv) mom[lane] = m;
+    wsync();
     double vel = 0.0;
     for (int k = 0; k < nv; k++) vel = vel + mom[k] * d.qvel[k];
-    d.act_length[u] = len;
-    d.act_vel[u] = vel;
     double c = d.ctrl[u];
     if (clim[u]) {
       if (c < crange[2 * u]) c = crange[2 * u];
@@ -639,9 +642,10 @@ DEVI void actuation(const Mdl& md, Dat& d) {
       if (f < frange[2 * u]) f = frange[2 * u];
       if (f > frange[2 * u + 1]) f = frange[2 * u + 1];
     }
-    d.act_force[u] = f;
-    for (int k = 0; k < nv; k++) d.qfrc_actuator[k] = d.qfrc_actuator[k] + mom[k] * f;
+    if (lane == 0) { d.act_length[u] = len; d.act_vel[u] = vel; d.act_force[u] = f; }
+    qfa = qfa + m * f;
   }
+  if (lane < nv) d.qfrc_actuator[lane] = qfa;
 }
 
 // passive forces (oracle passive()), one dof per lane
@@ -781,19 +785,35 @@ DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   for (int k = 0; k < 3; k++) { c.c1[k] = c.V1[3 * i1 + k]; c.c2[k] = c.V2[3 * i2 + k]; }
 }
 
-DEVI void sup_scan(SupAcc& a, const double* V, int n, const double* cached, const double* dl) {
+DEVI void sup_cached(SupAcc& a, int n, const double* cached, const double* dl) {
   int lane = lane_id();
-  if (n <= WAVE) {
-    if (lane < n) {
-      double sc = (cached[0] * dl[0] + cached[1] * dl[1]) + cached[2] * dl[2];
-      if (sc > a.best) { a.best = sc; a.bi = lane; a.vx = cached[0]; a.vy = cached[1]; a.vz = cached[2]; }
-    }
-  } else {
-    for (int i = lane; i < n; i += WAVE) {
-      double x = V[3 * i], y = V[3 * i + 1], z = V[3 * i + 2];
-      double sc = (x * dl[0] + y * dl[1]) + z * dl[2];
-      if (sc > a.best) { a.best = sc; a.bi = i; a.vx = x; a.vy = y; a.vz = z; }
-    }
+  if (lane < n) {
+    double sc = (cached[0] * dl[0] + cached[1] * dl[1]) + cached[2] * dl[2];
+    if (sc > a.best) { a.best = sc; a.bi = lane; a.vx = cached[0]; a.vy = cached[1]; a.vz = cached[2]; }
+  }
+}
+// vertices [base, base + SUP_CH * 64) of a large hull: every load issued before
+// the first compare, so a round costs one memory latency, not one per vertex
+// stride; each lane still visits its vertices in ascending order (strict >,
+// ties keep the smaller index)
+#define SUP_CH 4
+struct SupChunk { double x[SUP_CH], y[SUP_CH], z[SUP_CH]; };
+DEVI void sup_load(SupChunk& c, const double* V, int n, int base) {
+  int lane = lane_id();
+#pragma unroll
+  for (int u = 0; u < SUP_CH; u++) {
+    int i = base + u * WAVE + lane;
+    int ii = i < n ? i : 0;
+    c.x[u] = V[3 * ii]; c.y[u] = V[3 * ii + 1]; c.z[u] = V[3 * ii + 2];
+  }
+}
+DEVI void sup_take_chunk(SupAcc& a, const SupChunk& c, int n, int base, const double* dl) {
+  int lane = lane_id();
+#pragma unroll
+  for (int u = 0; u < SUP_CH; u++) {
+    int i = base + u * WAVE + lane;
+    double sc = (c.x[u] * dl[0] + c.y[u] * dl[1]) + c.z[u] * dl[2];
+    if (i < n && sc > a.best) { a.best = sc; a.bi = i; a.vx = c.x[u]; a.vy = c.y[u]; a.vz = c.z[u]; }
   }
 }
 
@@ -806,8 +826,21 @@ DEVI void support_pair(const PairCtx& c, const double* dir, double* out1, double
   SupAcc a1, a2;
   sup_init(a1);
   sup_init(a2);
-  sup_scan(a1, c.V1, c.n1, c.c1, dl1);
-  sup_scan(a2, c.V2, c.n2, c.c2, dl2);
+  if (c.n1 <= WAVE) sup_cached(a1, c.n1, c.c1, dl1);
+  if (c.n2 <= WAVE) sup_cached(a2, c.n2, c.c2, dl2);
+  int big1 = c.n1 > WAVE, big2 = c.n2 > WAVE;
+  if (big1 | big2) {
+    int nmax = big1 ? c.n1 : 0;
+    if (big2 && c.n2 > nmax) nmax = c.n2;
+    for (int base = 0; base < nmax; base += SUP_CH * WAVE) {
+      SupChunk k1, k2;
+      int t1 = big1 && base < c.n1, t2 = big2 && base < c.n2;
+      if (t1) sup_load(k1, c.V1, c.n1, base);
+      if (t2) sup_load(k2, c.V2, c.n2, base);
+      if (t1) sup_take_chunk(a1, k1, c.n1, base, dl1);
+      if (t2) sup_take_chunk(a2, k2, c.n2, base, dl2);
+    }
+  }
   double v1[3], v2[3], t[3];
   sup_finish(a1, v1, c.n1);
   sup_finish(a2, v2, c.n2);
@@ -819,6 +852,8 @@ DEVI void support_pair(const PairCtx& c, const double* dir, double* out1, double
 
 DEVI void mink_support(const PairCtx& c, const double* dir, SupPt* p) {
   PT(4);
+  PCNT(28, 1);
+  PCNT(29, (c.n1 > WAVE) + (c.n2 > WAVE));
   support_pair(c, dir, p->a, p->b);
   sub3(p->v, p->a, p->b);
   PT(22);
@@ -986,9 +1021,15 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
   if (num <= WAVE) {
     if (lane < num) best = base + ((cv[0] * nl[0] + cv[1] * nl[1]) + cv[2] * nl[2]);
   } else {
-    for (int i = lane; i < num; i += WAVE) {
-      double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
-      if (sign > 0 ? (s > best) : (s < best)) best = s;
+    for (int b0 = 0; b0 < num; b0 += SUP_CH * WAVE) {
+      SupChunk k;
+      sup_load(k, V, num, b0);
+#pragma unroll
+      for (int u = 0; u < SUP_CH; u++) {
+        int i = b0 + u * WAVE + lane;
+        double s = base + ((k.x[u] * nl[0] + k.y[u] * nl[1]) + k.z[u] * nl[2]);
+        if (i < num && (sign > 0 ? (s > best) : (s < best))) best = s;
+      }
     }
   }
   int P = num < WAVE ? next_pow2(num) : WAVE;
@@ -1163,6 +1204,9 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   pair_ctx(md, d, g1, g2, pc);
   int hit = mpr_penetration(md, d, pc, g1, g2, n, &depth, mpos);
   PT(4);
+  PCNT(26, 1);
+  PCNT(27, hit);
+  PCNT(30, (pc.n1 > WAVE) + (pc.n2 > WAVE));
   if (!hit) return;
   double t1[3], t2[3];
   make_frame(n, t1, t2);
@@ -1627,39 +1671,63 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       wsync();
     }
   }
-  if (lane == 0) {
-    ints[8] = d.NEFC;
+  PT(31);
+  // dof friction-loss rows, then joint-limit rows (lower bound before upper),
+  // in the oracle's order: lanes over dofs / joints, ballot prefixes place the
+  // rows, rows past nefc_max are dropped with the overflow flag (add_row)
+  {
+    int ne0 = uni(d.NEFC);
     const double* floss = DA(md, dof_frictionloss);
-    ints[9] = d.NEFC;
-    for (int k = 0; k < nv; k++) {
-      if (floss[k] > 0.0) {
-        int r = add_row(md, d, MGS_EFC_FRICTION, 0.0, 0.0, 1, k);
-        if (r < 0) break;
-        for (int c = 0; c < nv; c++) J[r * nv + c] = 0.0;
-        J[r * nv + k] = 1.0;
-      }
+    int hasf = (lane < nv) && floss[lane] > 0.0;
+    unsigned long long mf = __ballot(hasf);
+    unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
+    int nf = __popcll(mf);
+    int rf = ne0 + __popcll(mf & lt);
+    if (hasf && rf < md.m.nefc_max) {
+      d.efc_type[rf] = MGS_EFC_FRICTION; d.efc_pos[rf] = 0.0; d.efc_margin[rf] = 0.0;
+      d.efc_dim[rf] = 1; d.efc_con[rf] = lane;
     }
-    ints[10] = d.NEFC;
+    int ne1 = ne0 + nf;
+    if (ne1 > md.m.nefc_max) ne1 = md.m.nefc_max;
     const int32_t *lim = IA(md, jnt_limited), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
     const double *range = DA(md, jnt_range), *jmargin = DA(md, jnt_margin);
-    ints[11] = d.NEFC;
-    for (int j = 0; j < md.m.njnt; j++) {
-      if (!lim[j]) continue;
-      double q = d.qpos[jq[j]];
-      double dlo = q - range[2 * j], dhi = range[2 * j + 1] - q;
-      if (dlo < jmargin[j]) {
-        int r = add_row(md, d, MGS_EFC_LIMIT, dlo, jmargin[j], 1, j);
-        if (r >= 0) { for (int c = 0; c < nv; c++) J[r * nv + c] = 0.0; J[r * nv + jd[j]] = 1.0; }
-      }
-      if (dhi < jmargin[j]) {
-        int r = add_row(md, d, MGS_EFC_LIMIT, dhi, jmargin[j], 1, j);
-        if (r >= 0) { for (int c = 0; c < nv; c++) J[r * nv + c] = 0.0; J[r * nv + jd[j]] = -1.0; }
-      }
+    int lo = 0, hi = 0;
+    double dlo = 0.0, dhi = 0.0, jm = 0.0;
+    if (lane < md.m.njnt && lim[lane]) {
+      double q = d.qpos[jq[lane]];
+      dlo = q - range[2 * lane];
+      dhi = range[2 * lane + 1] - q;
+      jm = jmargin[lane];
+      lo = dlo < jm;
+      hi = dhi < jm;
     }
-    ints[12] = d.NEFC;
-    ints[6] = d.NEFC;
+    unsigned long long ml = __ballot(lo), mh = __ballot(hi);
+    int nl = __popcll(ml) + __popcll(mh);
+    int rl = ne1 + __popcll(ml & lt) + __popcll(mh & lt);
+    int rh = rl + lo;
+    if (lo && rl < md.m.nefc_max) {
+      d.efc_type[rl] = MGS_EFC_LIMIT; d.efc_pos[rl] = dlo; d.efc_margin[rl] = jm; d.efc_dim[rl] = 1; d.efc_con[rl] = lane;
+    }
+    if (hi && rh < md.m.nefc_max) {
+      d.efc_type[rh] = MGS_EFC_LIMIT; d.efc_pos[rh] = dhi; d.efc_margin[rh] = jm; d.efc_dim[rh] = 1; d.efc_con[rh] = lane;
+    }
+    int ne2 = ne1 + nl;
+    int ovf = ne0 + nf > md.m.nefc_max || ne2 > md.m.nefc_max;
+    if (ne2 > md.m.nefc_max) ne2 = md.m.nefc_max;
+    // J rows [ne0, ne2): zeros, then the unit entries
+    for (int e = lane; e < (ne2 - ne0) * NV; e += WAVE) J[ne0 * NV + e] = 0.0;
+    wsync();
+    if (hasf && rf < md.m.nefc_max) J[rf * NV + lane] = 1.0;
+    if (lo && rl < md.m.nefc_max) J[rl * NV + jd[lane]] = 1.0;
+    if (hi && rh < md.m.nefc_max) J[rh * NV + jd[lane]] = -1.0;
+    if (lane == 0) {
+      ints[8] = ne0; ints[9] = ne0; ints[10] = ne1; ints[11] = ne1; ints[12] = ne2; ints[6] = ne2;
+      d.NEFC = ne2;
+      if (ovf) d.OVERFLOW |= 2;
+    }
   }
   wsync();
+  PT(32);
   const int32_t *gbody = IA(md, geom_bodyid), *pcd = IA(md, pair_condim);
   const double *pfr = DA(md, pair_friction), *pmar = DA(md, pair_margin);
   int ncon = uni(d.NCON);
@@ -2691,7 +2759,7 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
     d.sD[k] = sd;
     d.isD[k] = 1.0 / sd;
   }
-  if (lane == 0) actuation(md, d);
+  actuation(md, d);
   passive(md, d);
   rne(md, d);
   if (lane < nv) d.qfrc_smooth[lane] = (d.qfrc_passive[lane] - d.qfrc_bias[lane]) + d.qfrc_actuator[lane];
@@ -2871,9 +2939,12 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       ldl_factor<NV>(d.M, d.Dv, d.Dinv);
       for (int k = lane; k < md.m.nv; k += WAVE) { double sd = sqrt(d.Dv[k]); d.sD[k] = sd; d.isD[k] = 1.0 / sd; }
       wsync(); PT(7);
-      if (lane == 0) actuation(md, d);
+      actuation(md, d);
+      wsync(); PT(33);
       passive(md, d);
+      wsync(); PT(34);
       rne(md, d);
+      PT(35);
       if (lane < md.m.nv) d.qfrc_smooth[lane] = (d.qfrc_passive[lane] - d.qfrc_bias[lane]) + d.qfrc_actuator[lane];
       wsync();
       ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);

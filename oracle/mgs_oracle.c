@@ -623,6 +623,7 @@ static void rne(const Mdl* md, Dat* d) {
 typedef struct { double v[3], a[3], b[3]; } SupPt;
 
 /* support point of geom g along world direction dir; returns vertex index */
+static long g_sup_calls;   /* diagnostics: support calls (single-threaded use) */
 static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, double* out) {
   int h = IA(md, geom_hullid)[g];
   int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
@@ -643,6 +644,7 @@ static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, d
 }
 
 static void mink_support(const Mdl* md, const Dat* d, int g1, int g2, const double* dir, SupPt* p) {
+  g_sup_calls++;
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
   support_geom(md, d, g1, dir, p->a);
   support_geom(md, d, g2, nd, p->b);
@@ -1051,6 +1053,9 @@ OBB_FN int obb_separated(const double* R1, const double* x1, const double* b1, c
   return 0;
 }
 
+/* diagnostics (single-threaded use only): broadphase passes / hits per pair */
+static long g_pair_bp[256], g_pair_hit[256], g_pair_sup[256];
+long* oracle_pair_counters(void) { static long buf[768]; for (int i = 0; i < 256; i++) { buf[i] = g_pair_bp[i]; buf[256 + i] = g_pair_hit[i]; buf[512 + i] = g_pair_sup[i]; g_pair_bp[i] = g_pair_hit[i] = g_pair_sup[i] = 0; } return buf; }
 static void collision(const Mdl* md, Dat* d) {
   const mgs_model_desc* m = md->m;
   const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
@@ -1075,7 +1080,14 @@ static void collision(const Mdl* md, Dat* d) {
     if (ov && obb_separated(d->geom_xmat + 9 * g[0], d->geom_xpos + 3 * g[0], aabb + 6 * g[0],
                             d->geom_xmat + 9 * g[1], d->geom_xpos + 3 * g[1], aabb + 6 * g[1], pm[p]))
       ov = 0;
-    if (ov) collide_pair(md, d, p);
+    if (ov) {
+      if (p < 256) g_pair_bp[p]++;
+      int n0 = d->ncon;
+      long s0 = g_sup_calls;
+      collide_pair(md, d, p);
+      if (p < 256) g_pair_sup[p] += g_sup_calls - s0;
+      if (p < 256 && d->ncon > n0) g_pair_hit[p]++;
+    }
   }
 }
 

@@ -146,15 +146,35 @@ __global__ void probe(unsigned long long* out, double* buf) {
   REP100(asm volatile("s_add_u32 %0, %0, 3" : "+s"(sv));)
   t1 = __builtin_amdgcn_s_memtime(); out[k++] = t1 - t0;
   i0 += sv;
+  // 22: 20 dependent global loads (pointer chase, L1/L2-resident 2 KB buffer)
+  {
+    int gi = lane & 7;
+    const int* gb = (const int*)(buf + 256);
+    t0 = __builtin_amdgcn_s_memtime();
+    for (int j = 0; j < 20; j++) { gi = gb[gi]; asm volatile("" : "+v"(gi)); }
+    t1 = __builtin_amdgcn_s_memtime(); out[k++] = t1 - t0;
+    i0 += gi;
+  }
+  // 23: 20 dependent global loads, uniform address (scalar-loadable) via volatile vector path
+  {
+    int gi = 0;
+    const int* gb = (const int*)(buf + 256);
+    t0 = __builtin_amdgcn_s_memtime();
+    for (int j = 0; j < 20; j++) { gi = __builtin_amdgcn_readfirstlane(gb[gi + (lane & 0)]); }
+    t1 = __builtin_amdgcn_s_memtime(); out[k++] = t1 - t0;
+    i0 += gi;
+  }
   if (lane == 0) out[31] = (unsigned long long)(a + a1 + a2 + a3 + a4 + a5 + a6 + a7 + c + q + sq + i0 + i1 + i2 + i3 + idx + acc[0]);
   buf[lane] = a + b;
 }
 
 int main() {
   unsigned long long* d_out; double* d_buf;
-  hipMalloc(&d_out, 32 * 8); hipMalloc(&d_buf, 256 * 8);
+  hipMalloc(&d_out, 32 * 8); hipMalloc(&d_buf, 2048 * 8);
   double h[256]; for (int i = 0; i < 256; i++) h[i] = 1.0 + 1e-3 * i;
   hipMemcpy(d_buf, h, sizeof(h), hipMemcpyHostToDevice);
+  int hi[512]; for (int i = 0; i < 512; i++) hi[i] = (i * 37 + 11) % 64;
+  hipMemcpy(d_buf + 256, hi, sizeof(hi), hipMemcpyHostToDevice);
   for (int it = 0; it < 2; it++) {
     hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, d_out, d_buf);
     hipDeviceSynchronize();
@@ -167,7 +187,7 @@ int main() {
                          "100 dep v_mul_f64", "100 indep v_add_u32", "20 dep ds_read_b64", "100 readlane x2 + add_f64",
                          "100 dep v_rcp_f64", "10 dep f64 div", "10 dep f64 sqrt", "100 indep ds_read_b64", "100 dep v_cndmask", "100 indep readlane_b32", "50 ds_read_b128 bcast",
                          "100 ds_read_b64 per-lane", "100 ds_write_b64", "100 ds_bpermute_b32", "100 dep dpp mov",
-                         "100 dep s_add_u32"};
-  for (int i = 2; i < 22; i++) printf("%-28s %6llu ticks  (%.1f per op)\n", names[i], o[i], o[i] / (i == 8 ? 20.0 : (i == 11 || i == 12) ? 10.0 : i == 16 ? 50.0 : 100.0));
+                         "100 dep s_add_u32", "20 dep global loads", "20 dep global (readfirstlane)"};
+  for (int i = 2; i < 24; i++) printf("%-28s %6llu ticks  (%.1f per op)\n", names[i], o[i], o[i] / (i == 8 || i == 22 || i == 23 ? 20.0 : (i == 11 || i == 12) ? 10.0 : i == 16 ? 50.0 : 100.0));
   return 0;
 }

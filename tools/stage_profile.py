@@ -23,16 +23,18 @@ plan = env.rollout_plan(poses[idx], J[idx], nstep_lift=h['nstep_lift'], shake_st
                         close_steps=h['close_steps'], lift_check_every=h['lift_check_every'])
 L = E.load_library()
 L.mgs_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 32)()
+buf = (ctypes.c_ulonglong * 64)()
 L.mgs_prof_read(buf)
 r = env.engine.rollout(plan)
 L.mgs_prof_read(buf)
-v = np.array(buf[:26], dtype=np.float64)
+v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64)])
+cnt = np.array(buf[26:31], dtype=np.float64)
 names = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll: MPR', 'coll: feature+clip',
          'crb', 'ldl(M)', 'act+passive+rne+smooth', 'con: J rows', 'con: G transform', 'con: params+blocks',
          'newton: setup', 'newton: hessian', 'newton: ldl+solve+jv', 'newton: linesearch', 'newton: eval+grad',
          'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: MPR support calls',
-         'newton: H accumulate', 'newton: H to rows', 'newton: H factor']
+         'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
+         'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne']
 tot = v.sum()
 print('N=%d collision-free candidates, kernel %.1f ms, labels %d, mean iters/step %.1f, overflow %d' % (
     len(idx), r['kernel_ms'], r['label'].sum(), r['stats'][:, 3].sum() / max(1, r['stats'][:, 3].size) / 200, (r['stats'][:, 2] != 0).sum()))
@@ -40,3 +42,7 @@ for n_, x in zip(names, v):
     print('%-28s %6.1f%%  %.3g ticks' % (n_, 100 * x / tot, x))
 steps = len(idx) * 200
 print('ticks per candidate-step: %.0f' % (tot / steps))
+
+steps_exec = r['stats'][:, 3].size and None
+print('per candidate-step (all %d steps counted): narrowphase pairs %.2f, hits %.2f, support calls %.2f, big-hull support scans %.2f, big-hull pairs %.2f' % (
+    steps, cnt[0] / steps, cnt[1] / steps, cnt[2] / steps, cnt[3] / steps, cnt[4] / steps))
