@@ -54,7 +54,8 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   us[U_comacc] = 4 * nb;
   us[U_cvel] = 6 * nb; us[U_cacc] = 6 * nb; us[U_cfrc] = 6 * nb; us[U_cdof_dot] = 6 * nv;
   us[U_qfrc_bias] = nv; us[U_qfrc_passive] = nv; us[U_qfrc_actuator] = nv;
-  us[U_G] = ne * nv; us[U_aref] = ne;
+  us[U_G] = ne * (nv + 0);   // row stride: GS in the kernel
+  us[U_aref] = ne;
   us[U_scratch] = (2 * ne > nv ? 2 * ne : nv);
   // {vel, pos, margin} (make_constraints) | Newton Hessian, which may run on into
   // the scratch slot (scratch is idle while the Hessian is live)

@@ -31,6 +31,9 @@
 #define K_MPR_MAXIT 64
 #define K_FEAT_EPS 1e-5
 #define WAVE 64
+// row stride of the constraint matrix G (doubles).  An odd stride (NV + 1) makes
+// row walks bank-conflict free but measured no faster and costs 680 B of LDS
+#define GS (NV + 0)
 #define DEVI __device__ __attribute__((always_inline)) inline
 
 struct P2 { double x, y, h; };
@@ -67,6 +70,7 @@ struct Dat {
   // Newton solver workspace (U region, after the constraint stage views)
   double *efc_jar, *efc_jv, *efc_f, *efc_Dr, *efc_isR, *nH, *nw, *nw0, *ng, *ndir, *con_hb;
   int *con_pair, *con_g1, *con_g2, *efc_type, *efc_dim, *efc_con, *efc_state, *ints;
+  int gs;   // row stride of G (nv + 1)
 };
 // ints[]: 0 ncon, 1 nefc, 2 overflow, 3 iters, 6 cr0, 7 cr1, 8 neq rows, 9 fr0, 10 fr1, 11 lr0, 12 lr1
 #define NCON ints[0]
@@ -1411,6 +1415,7 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   BU(qDeriv, U_qDeriv);
 #undef BU
   d.con_hb = d.con_blk;   // Newton cone Hessians reuse the contact-block slots
+  d.gs = l.nv + 0;
   int* ib = (int*)(s + l.o[L_ints]);
   d.ints = ib;
   int ncmax = l.ncon_max, nemax = l.nefc_max;
@@ -1425,7 +1430,7 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
 
 // A_rr = G_r . G_r in the oracle's order (its efc_A)
 DEVI double row_sqnorm(const Dat& d, int r, int nv) {
-  const double* Gr = d.G + r * nv;
+  const double* Gr = d.G + r * d.gs;
   double a = 0.0;
   for (int k = 0; k < nv; k++) a = a + Gr[k] * Gr[k];
   return a;
@@ -1620,7 +1625,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       jac_col(md, d, b1, p1, col, cjp1, cjr1);
       jac_col(md, d, b2, p2, col, cjp2, cjr2);
       if (lane < nv)
-        for (int k = 0; k < 3; k++) J[(r0 + k) * nv + lane] = cjp1[k] - cjp2[k];
+        for (int k = 0; k < 3; k++) J[(r0 + k) * d.gs + lane] = cjp1[k] - cjp2[k];
       if (et[e] == MGS_EQ_WELD) {
         double q1r[4], q2c[4], qe[4];
         quatmul(q1r, d.xquat + 4 * b1, data + 3);
@@ -1638,7 +1643,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
           double t1q[4], t2q[4];
           quatmul(t1q, q2c, ax);
           quatmul(t2q, t1q, q1r);
-          for (int k = 0; k < 3; k++) J[(rr + k) * nv + lane] = (0.5 * t2q[1 + k]) * ts;
+          for (int k = 0; k < 3; k++) J[(rr + k) * d.gs + lane] = (0.5 * t2q[1 + k]) * ts;
         }
       }
       wsync();
@@ -1662,11 +1667,11 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       wsync();
       if (d.OVERFLOW & 2) break;
       int r = d.NEFC - 1;
-      for (int c = lane; c < nv; c += WAVE) J[r * nv + c] = 0.0;
+      for (int c = lane; c < nv; c += WAVE) J[r * d.gs + c] = 0.0;
       wsync();
       if (lane == 0) {
-        J[r * nv + jd[j1]] = 1.0;
-        if (j2 >= 0) J[r * nv + jd[j2]] = J[r * nv + jd[j2]] - deriv;
+        J[r * d.gs + jd[j1]] = 1.0;
+        if (j2 >= 0) J[r * d.gs + jd[j2]] = J[r * d.gs + jd[j2]] - deriv;
       }
       wsync();
     }
@@ -1715,11 +1720,11 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     int ovf = ne0 + nf > md.m.nefc_max || ne2 > md.m.nefc_max;
     if (ne2 > md.m.nefc_max) ne2 = md.m.nefc_max;
     // J rows [ne0, ne2): zeros, then the unit entries
-    for (int e = lane; e < (ne2 - ne0) * NV; e += WAVE) J[ne0 * NV + e] = 0.0;
+    for (int e = lane; e < (ne2 - ne0) * GS; e += WAVE) J[ne0 * GS + e] = 0.0;
     wsync();
-    if (hasf && rf < md.m.nefc_max) J[rf * NV + lane] = 1.0;
-    if (lo && rl < md.m.nefc_max) J[rl * NV + jd[lane]] = 1.0;
-    if (hi && rh < md.m.nefc_max) J[rh * NV + jd[lane]] = -1.0;
+    if (hasf && rf < md.m.nefc_max) J[rf * GS + lane] = 1.0;
+    if (lo && rl < md.m.nefc_max) J[rl * GS + jd[lane]] = 1.0;
+    if (hi && rh < md.m.nefc_max) J[rh * GS + jd[lane]] = -1.0;
     if (lane == 0) {
       ints[8] = ne0; ints[9] = ne0; ints[10] = ne1; ints[11] = ne1; ints[12] = ne2; ints[6] = ne2;
       d.NEFC = ne2;
@@ -1755,10 +1760,10 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       jac_col(md, d, b2, pt, col, cjp2, cjr2);
       if (lane < nv) {
         double dp[3] = {cjp2[0] - cjp1[0], cjp2[1] - cjp1[1], cjp2[2] - cjp1[2]};
-        for (int j = 0; j < dim && j < 3; j++) J[(r + j) * nv + col] = dot3(fr + 3 * j, dp);
+        for (int j = 0; j < dim && j < 3; j++) J[(r + j) * d.gs + col] = dot3(fr + 3 * j, dp);
         if (dim >= 4) {
           double dr[3] = {cjr2[0] - cjr1[0], cjr2[1] - cjr1[1], cjr2[2] - cjr1[2]};
-          J[(r + 3) * nv + col] = dot3(fr, dr);
+          J[(r + 3) * d.gs + col] = dot3(fr, dr);
         }
       }
     }
@@ -1771,7 +1776,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   // per row (lanes over rows): vel, J.qacc_smooth, G in place, A
   // (the row lives in registers for the triangular solve)
   for (int r = lane; r < ne; r += WAVE) {
-    double* Gr = d.G + r * NV;
+    double* Gr = d.G + r * GS;
     double g[NV];
 #pragma unroll
     for (int k = 0; k < NV; k++) g[k] = Gr[k];
@@ -1828,8 +1833,8 @@ DEVI void contact_blocks(const Mdl& md, Dat& d) {
     double* blk = d.con_blk + BLKSTRIDE * uni(d.efc_con[r]);
     for (int e = lane; e < dim * dim; e += WAVE) {
       int i = e / dim, j = e % dim;
-      const double* Gi = d.G + (r + i) * nv;
-      const double* Gj = d.G + (r + j) * nv;
+      const double* Gi = d.G + (r + i) * d.gs;
+      const double* Gj = d.G + (r + j) * d.gs;
       double a = 0.0;
       for (int k = 0; k < nv; k++) a = a + Gi[k] * Gj[k];
       blk[i * dim + j] = a;
@@ -1934,7 +1939,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
   const double* mu = d.con_mu + 5 * c;
 #pragma unroll
   for (int i = 0; i < DIM; i++) {
-    g[i] = (lane < nv) ? d.G[(r + i) * nv + lane] : 0.0;
+    g[i] = (lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
     double jw = tree_sum(g[i] * u, P);
     old[i] = getf(fr0, fr1, r + i);
     res[i] = noslip ? (jw + d.efc_b[r + i]) : ((jw + d.efc_R[r + i] * old[i]) + d.efc_b[r + i]);
@@ -2086,7 +2091,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
   double* fl = d.scratch;                 // f staging (ne)
   double* terms = d.scratch + md.m.nefc_max;
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Gr = d.G + r * nv;
+    const double* Gr = d.G + r * d.gs;
     double jar = 0.0;
     for (int k = 0; k < nv; k++) jar = jar + Gr[k] * d.tmp[k];
     jar = jar - d.efc_aref[r];
@@ -2105,13 +2110,13 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
   u = 0.0;
   if (lane < nv) {
     double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d.G[r * nv + lane] * fl[r];
+    for (int r = 0; r < ne; r++) s = s + d.G[r * d.gs + lane] * fl[r];
     u = s;
     d.tmp2[lane] = s;
   }
   wsync();
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Gr = d.G + r * nv;
+    const double* Gr = d.G + r * d.gs;
     double jw = 0.0;
     for (int k = 0; k < nv; k++) jw = jw + Gr[k] * d.tmp2[k];
     terms[r] = fl[r] * ((0.5 * (jw + d.efc_R[r] * fl[r])) + d.efc_b[r]);
@@ -2131,7 +2136,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
       int t = uni(d.efc_type[r]);
       int dim = uni(d.efc_dim[r]);
       if (t != MGS_EFC_CONTACT || dim == 1) {
-        double g = (lane < nv) ? d.G[r * nv + lane] : 0.0;
+        double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
         double jw = tree_sum(g * u, P);
         double fo = getf(fr0, fr1, r);
         double res = (jw + d.efc_R[r] * fo) + d.efc_b[r];
@@ -2164,6 +2169,7 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   for (int ns = 0; ns < md.m.noslip_iterations && ne > 0; ns++) {
+    PCNT(38, 1);
     double improvement = 0.0;
     // the noslip cost drops the regulariser: count its removal at iteration 0
     if (ns == 0)
@@ -2175,7 +2181,7 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
       int t = uni(d.efc_type[r]);
       int dim = uni(d.efc_dim[r]);
       if (t == MGS_EFC_FRICTION) {
-        double g = (lane < nv) ? d.G[r * nv + lane] : 0.0;
+        double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
         double res = tree_sum(g * u, P) + d.efc_b[r];
         double fo = getf(fr0, fr1, r);
         double Arr = row_sqnorm(d, r, nv);
@@ -2248,7 +2254,7 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
 // evaluate the block led by row r at violations jr[] (registers, dim <= 4):
 // forces f[], zone, cone Hessian hb[a*4+b] (if want_hb); returns cost
 DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const double* jr, double* f, int& st,
-                     double* hb, bool want_hb, double* cq = nullptr) {
+                     double* hb, bool want_hb, double mup, double k1, double* cq = nullptr) {
   if (t == MGS_EFC_EQUALITY) {
     double Dr = d.efc_Dr[r];
     f[0] = -jr[0] * Dr;
@@ -2277,8 +2283,8 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
     f[0] = y * isr;
     return y * z - 0.5 * (y * y);
   }
-  // mu' = mu0 / sqrt(impratio) (oracle efc_mup)
-  double mup = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
+  // mup = mu0 / sqrt(impratio), k1 = 1 / (1 + mup^2): per-block constants of the
+  // solve (oracle efc_mup, efc_k1), held in registers by the caller
   double z[4], y[4], isr[4];
 #pragma unroll
   for (int a = 0; a < 4; a++) {
@@ -2290,7 +2296,7 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
   for (int a = 1; a < 4; a++)
     if (a < dim) t2 = t2 + z[a] * z[a];
   double tn = sqrt(t2);
-  double yn = 0.0;
+  double yn = 0.0, itn = 0.0, sc = 0.0;
   if (tn <= mup * z[0]) {
     st = ST_QUAD;
 #pragma unroll
@@ -2301,9 +2307,10 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
     for (int a = 0; a < 4; a++) y[a] = 0.0;
   } else {
     st = ST_CONE;
-    yn = (z[0] + mup * tn) / (1.0 + mup * mup);
+    yn = (z[0] + mup * tn) * k1;
+    itn = 1.0 / tn;
+    sc = (mup * yn) * itn;
     y[0] = yn;
-    double sc = (mup * yn) / tn;
 #pragma unroll
     for (int a = 1; a < 4; a++) y[a] = sc * z[a];
   }
@@ -2316,19 +2323,18 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
     }
   }
   if (cq && st == ST_CONE) {
-    cq[0] = 1.0 / (1.0 + mup * mup);
-    cq[1] = (mup * yn) / tn;
+    cq[0] = k1;
+    cq[1] = sc;
 #pragma unroll
-    for (int a = 1; a < 4; a++) cq[1 + a] = z[a] / tn;
+    for (int a = 1; a < 4; a++) cq[1 + a] = z[a] * itn;
   }
   if (want_hb && st == ST_CONE) {
-    double k1 = 1.0 / (1.0 + mup * mup);
-    double k2 = (mup * yn) / tn;
+    double k2 = sc;
     double v[4], e[4];
     v[0] = 1.0;
     e[0] = 0.0;
 #pragma unroll
-    for (int a = 1; a < 4; a++) { e[a] = z[a] / tn; v[a] = mup * e[a]; }
+    for (int a = 1; a < 4; a++) { e[a] = z[a] * itn; v[a] = mup * e[a]; }
 #pragma unroll
     for (int a = 0; a < 4; a++)
 #pragma unroll
@@ -2353,15 +2359,16 @@ DEVI double tree_rows(double v0, double v1, int ne) {
 
 // jar = G w - aref; forces, zones, cone Hessians into LDS; returns total cost
 template <int NV>
-DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P) {
+DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const double* mupR, const double* k1R) {
   int ne = uni(d.NEFC), lane = lane_id();
+  PCNT(37, 1);
   double q = (lane < NV) ? w[lane] - d.nw0[lane] : 0.0;
   double gauss = 0.5 * tree_sum(q * q, P);
   double wr[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) wr[k] = w[k];
   for (int r = lane; r < ne; r += WAVE) {
-    const double* Gr = d.G + r * NV;
+    const double* Gr = d.G + r * GS;
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < NV; k++) s = s + Gr[k] * wr[k];
@@ -2379,7 +2386,7 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P) {
       int st = ST_OFF;
 #pragma unroll
       for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
-      cr[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true);
+      cr[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true, mupR[h], k1R[h]);
 #pragma unroll
       for (int a = 0; a < 4; a++)
         if (a < dim) { d.efc_f[r + a] = f[a]; d.efc_state[r + a] = st; }
@@ -2407,23 +2414,25 @@ DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
     int r = 0;
     // rows in order, four loads in flight per step
     for (; r + 4 <= ne; r += 4) {
-      double g0 = d.G[r * NV + lane], g1 = d.G[(r + 1) * NV + lane], g2 = d.G[(r + 2) * NV + lane],
-             g3 = d.G[(r + 3) * NV + lane];
+      double g0 = d.G[r * GS + lane], g1 = d.G[(r + 1) * GS + lane], g2 = d.G[(r + 2) * GS + lane],
+             g3 = d.G[(r + 3) * GS + lane];
       double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
       s = s + g0 * f0;
       s = s + g1 * f1;
       s = s + g2 * f2;
       s = s + g3 * f3;
     }
-    for (; r < ne; r++) s = s + d.G[r * NV + lane] * d.efc_f[r];
+    for (; r < ne; r++) s = s + d.G[r * GS + lane] * d.efc_f[r];
     d.ng[lane] = (w[lane] - d.nw0[lane]) - s;
   }
   wsync();
 }
 
 // cost derivatives along the search direction at step alpha
-DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, double A2, double* d1, double* d2) {
+DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, double A2, double* d1, double* d2,
+                  const double* mupR, const double* k1R) {
   int lane = lane_id();
+  PCNT(36, 1);
   double c1[2] = {0.0, 0.0}, c2[2] = {0.0, 0.0};
 #pragma unroll
   for (int h = 0; h < 2; h++) {
@@ -2438,7 +2447,7 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
         jv[a] = (a < dim) ? d.efc_jv[r + a] : 0.0;
         jr[a] = (a < dim) ? d.efc_jar[r + a] + alpha * jv[a] : 0.0;
       }
-      row_eval(md, d, r, t, dim, jr, f, st, hb, false, cq);
+      row_eval(md, d, r, t, dim, jr, f, st, hb, false, mupR[h], k1R[h], cq);
       double s1 = 0.0, s2 = 0.0;
       if (dim == 1) {
         s1 = -f[0] * jv[0];
@@ -2453,7 +2462,7 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
             if (a < dim) s2 = s2 + (jv[a] * d.efc_Dr[r + a]) * jv[a];
         } else if (st == ST_CONE) {
           // jv' hb jv in closed form (oracle ls_eval)
-          double mup = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
+          double mup = mupR[h];
           double u[4];
 #pragma unroll
           for (int a = 0; a < 4; a++) u[a] = (a < dim) ? jv[a] * d.efc_isR[r + a] : 0.0;
@@ -2524,7 +2533,7 @@ DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
     bool valid = r < ne;
     int rr = valid ? r : 0;
     double gv[NT], x[NT];
-    const double* Gr = d.G + rr * NV;
+    const double* Gr = d.G + rr * GS;
 #pragma unroll
     for (int t = 0; t < NT; t++) {
       int c = cl + 16 * t;
@@ -2548,7 +2557,7 @@ DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
 #pragma unroll
         for (int a = 0; a < 4; a++) {
           int aa = a < nd ? a : 0;
-          double tv = xs + d.G[(lead + aa) * NV + cc] * w[a];
+          double tv = xs + d.G[(lead + aa) * GS + cc] * w[a];
           xs = (a < nd) ? tv : xs;
         }
         x[t] = (c < NV) ? xs : 0.0;
@@ -2581,6 +2590,133 @@ DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
   wsync();
 }
 
+// Line-search rows in registers: lane r holds block-leader row r (rows >= 64
+// take the LDS path of ls_eval).  Loaded once per Newton iteration, so each
+// evaluation along the direction is register arithmetic plus two reductions;
+// the expressions are row_eval()'s and ls_eval()'s (oracle ls_eval), per kind.
+struct LsRow {
+  int kind, dim;   // kind: 0 none, 1 equality, 2 limit / frictionless contact, 3 friction, 4 cone block
+  double jar[4], jv[4], isr[4], Dr[4];
+  double mup, k1, lim;
+};
+DEVI void ls_row_load(const Mdl& md, const Dat& d, int r, int ne, double mup, double k1, LsRow& L) {
+  L.kind = 0;
+  L.dim = 1;
+  L.mup = mup;
+  L.k1 = k1;
+  L.lim = 0.0;
+#pragma unroll
+  for (int a = 0; a < 4; a++) { L.jar[a] = 0.0; L.jv[a] = 0.0; L.isr[a] = 0.0; L.Dr[a] = 0.0; }
+  if (r < ne && efc_lead(d, r)) {
+    int t = d.efc_type[r];
+    int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
+    L.dim = dim;
+    L.kind = (t == MGS_EFC_EQUALITY) ? 1 : (t == MGS_EFC_FRICTION) ? 3 : (dim == 1) ? 2 : 4;
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+      if (a < dim) {
+        L.jar[a] = d.efc_jar[r + a];
+        L.jv[a] = d.efc_jv[r + a];
+        L.isr[a] = d.efc_isR[r + a];
+        L.Dr[a] = d.efc_Dr[r + a];
+      }
+    }
+    if (L.kind == 3) L.lim = row_floss(md, d, r) * sqrt(d.efc_R[r]);
+  }
+}
+DEVI void ls_row(const LsRow& L, double alpha, double& s1o, double& s2o) {
+  double s1 = 0.0, s2 = 0.0;
+  double jr0 = L.jar[0] + alpha * L.jv[0];
+  if (L.kind == 1 || L.kind == 2) {
+    double f0 = 0.0;
+    bool quad = (L.kind == 1) || (jr0 < 0.0);
+    if (quad) f0 = -jr0 * L.Dr[0];
+    s1 = -f0 * L.jv[0];
+    if (quad) s2 = (L.jv[0] * L.Dr[0]) * L.jv[0];
+  } else if (L.kind == 3) {
+    double z = -jr0 * L.isr[0];
+    double y = z;
+    bool quad = true;
+    if (z > L.lim) { y = L.lim; quad = false; }
+    else if (z < -L.lim) { y = -L.lim; quad = false; }
+    double f0 = y * L.isr[0];
+    s1 = -f0 * L.jv[0];
+    if (quad) s2 = (L.jv[0] * L.Dr[0]) * L.jv[0];
+  } else if (L.kind == 4) {
+    int dim = L.dim;
+    double mup = L.mup;
+    double z[4], y[4];
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+      double jr = (a < dim) ? L.jar[a] + alpha * L.jv[a] : 0.0;
+      z[a] = (a < dim) ? -jr * L.isr[a] : 0.0;
+    }
+    double t2 = 0.0;
+#pragma unroll
+    for (int a = 1; a < 4; a++)
+      if (a < dim) t2 = t2 + z[a] * z[a];
+    double tn = sqrt(t2);
+    int st;
+    double yn = 0.0, itn = 0.0, sc = 0.0;
+    if (tn <= mup * z[0]) {
+      st = ST_QUAD;
+#pragma unroll
+      for (int a = 0; a < 4; a++) y[a] = z[a];
+    } else if (mup * tn <= -z[0]) {
+      st = ST_OFF;
+#pragma unroll
+      for (int a = 0; a < 4; a++) y[a] = 0.0;
+    } else {
+      st = ST_CONE;
+      yn = (z[0] + mup * tn) * L.k1;
+      itn = 1.0 / tn;
+      sc = (mup * yn) * itn;
+      y[0] = yn;
+#pragma unroll
+      for (int a = 1; a < 4; a++) y[a] = sc * z[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+      if (a < dim) s1 = s1 - (y[a] * L.isr[a]) * L.jv[a];
+    if (st == ST_QUAD) {
+#pragma unroll
+      for (int a = 0; a < 4; a++)
+        if (a < dim) s2 = s2 + (L.jv[a] * L.Dr[a]) * L.jv[a];
+    } else if (st == ST_CONE) {
+      double u[4];
+#pragma unroll
+      for (int a = 0; a < 4; a++) u[a] = (a < dim) ? L.jv[a] * L.isr[a] : 0.0;
+      double vu = u[0], eu = 0.0, uu = 0.0;
+#pragma unroll
+      for (int a = 1; a < 4; a++) {
+        if (a < dim) {
+          double e = z[a] * itn;
+          vu = vu + (mup * e) * u[a];
+          eu = eu + e * u[a];
+          uu = uu + u[a] * u[a];
+        }
+      }
+      s2 = (L.k1 * vu) * vu + sc * (uu - eu * eu);
+    }
+  }
+  s1o = s1;
+  s2o = s2;
+}
+// ls_eval with the first 64 rows from registers
+DEVI void ls_eval_fast(const Mdl& md, const Dat& d, int ne, const LsRow& L, double alpha, double A1, double A2,
+                       double* d1, double* d2, const double* mupR, const double* k1R) {
+  PCNT(36, 1);
+  double c1[2] = {0.0, 0.0}, c2[2] = {0.0, 0.0};
+  ls_row(L, alpha, c1[0], c2[0]);
+  if (ne > WAVE) {
+    LsRow L1;
+    ls_row_load(md, d, lane_id() + WAVE, ne, mupR[1], k1R[1], L1);
+    ls_row(L1, alpha, c1[1], c2[1]);
+  }
+  *d1 = (A1 + alpha * A2) + tree_rows(c1[0], c1[1], ne);
+  *d2 = A2 + tree_rows(c2[0], c2[1], ne);
+}
+
 template <int NV>
 DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
@@ -2589,6 +2725,17 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     double sq = sqrt(d.efc_R[r]);
     d.efc_isR[r] = 1.0 / sq;
     d.efc_Dr[r] = 1.0 / d.efc_R[r];
+  }
+  // per-block cone constants of this solve, rows lane and lane + 64
+  double mupR[2] = {0.0, 0.0}, k1R[2] = {0.0, 0.0};
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    int r = lane + h * WAVE;
+    if (r < ne && d.efc_type[r] == MGS_EFC_CONTACT && d.efc_dim[r] > 1) {
+      double mup = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
+      mupR[h] = mup;
+      k1R[h] = 1.0 / (1.0 + mup * mup);
+    }
   }
   // w0 = W(qacc_smooth), w = W(qacc_ws)   (lane i: s_i = a_i + sum_{k>i} L_ki a_k)
   {
@@ -2612,14 +2759,14 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   if (ne > 0) {
     // (oracle: evaluate warmstart, smooth, keep the cheaper; evaluating the
     // smooth point first leaves the warmstart's rows current in the common case)
-    double c0 = newton_eval<NV>(md, d, d.nw0, P);
-    double cws = newton_eval<NV>(md, d, d.nw, P);
+    double c0 = newton_eval<NV>(md, d, d.nw0, P, mupR, k1R);
+    double cws = newton_eval<NV>(md, d, d.nw, P, mupR, k1R);
     if (cws < c0) {
       C = cws;
     } else {
       if (lane < nv) d.nw[lane] = d.nw0[lane];
       wsync();
-      C = newton_eval<NV>(md, d, d.nw, P);
+      C = newton_eval<NV>(md, d, d.nw, P, mupR, k1R);
     }
   } else {
     if (lane < nv) d.nw[lane] = d.nw0[lane];
@@ -2657,7 +2804,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
 #pragma unroll
       for (int k = 0; k < NV; k++) dr[k] = d.ndir[k];
       for (int r = lane; r < ne; r += WAVE) {
-        const double* Gr = d.G + r * NV;
+        const double* Gr = d.G + r * GS;
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < NV; k++) s = s + Gr[k] * dr[k];
@@ -2671,14 +2818,16 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     double A1 = tree_sum(q * dl, P);
     double A2 = tree_sum(dl * dl, P);
     double p0, q0, alpha = 0.0;
-    ls_eval(md, d, ne, 0.0, A1, A2, &p0, &q0);
+    LsRow LR;
+    ls_row_load(md, d, lane, ne, mupR[0], k1R[0], LR);
+    ls_eval_fast(md, d, ne, LR, 0.0, A1, A2, &p0, &q0, mupR, k1R);
     if (p0 < 0.0) {
       double lo = 0.0, hi = 0.0;
       int hi_ok = 0;
       alpha = -p0 / q0;
       for (int ls = 0; ls < md.m.ls_iterations; ls++) {
         double pp, qq;
-        ls_eval(md, d, ne, alpha, A1, A2, &pp, &qq);
+        ls_eval_fast(md, d, ne, LR, alpha, A1, A2, &pp, &qq, mupR, k1R);
         if (fabs(pp) < md.m.ls_tolerance * (-p0)) break;
         if (pp < 0.0) lo = alpha;
         else { hi = alpha; hi_ok = 1; }
@@ -2691,7 +2840,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     if (!(alpha > 0.0)) { it++; break; }
     if (lane < nv) d.nw[lane] = d.nw[lane] + alpha * dl;
     wsync();
-    double Cn = newton_eval<NV>(md, d, d.nw, P);
+    double Cn = newton_eval<NV>(md, d, d.nw, P, mupR, k1R);
     newton_grad<NV>(md, d, d.nw);
     double improvement = scale * (C - Cn);
     C = Cn;
@@ -2709,15 +2858,15 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     double s = 0.0;
     int r = 0;
     for (; r + 4 <= ne; r += 4) {
-      double g0 = d.G[r * NV + lane], g1 = d.G[(r + 1) * NV + lane], g2 = d.G[(r + 2) * NV + lane],
-             g3 = d.G[(r + 3) * NV + lane];
+      double g0 = d.G[r * GS + lane], g1 = d.G[(r + 1) * GS + lane], g2 = d.G[(r + 2) * GS + lane],
+             g3 = d.G[(r + 3) * GS + lane];
       double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
       s = s + g0 * f0;
       s = s + g1 * f1;
       s = s + g2 * f2;
       s = s + g3 * f3;
     }
-    for (; r < ne; r++) s = s + d.G[r * NV + lane] * d.efc_f[r];
+    for (; r < ne; r++) s = s + d.G[r * GS + lane] * d.efc_f[r];
     u = s;
   }
 }

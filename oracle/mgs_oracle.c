@@ -74,7 +74,7 @@ typedef struct {
   int nefc;
   double *J, *K, *efc_pos, *efc_margin, *efc_vel, *efc_aref, *efc_R, *efc_A, *efc_b, *efc_f;
   double *efc_mu, *efc_blk, *efc_hb, *efc_dA, *efc_floss, *efc_AR, *efc_ARinv, *efc_Ainv;
-  double *efc_Dr, *efc_sqR, *efc_isR, *efc_mup, *efc_jar, *efc_jv, *hX;
+  double *efc_Dr, *efc_sqR, *efc_isR, *efc_mup, *efc_k1, *efc_jar, *efc_jv, *hX;
   int* efc_state;
   double *Dv, *sD, *isD;
   int *efc_type, *efc_dim, *efc_con;
@@ -261,7 +261,7 @@ static Dat* dat_alloc(const Mdl* md) {
   TAKE(efc_aref, ne); TAKE(efc_R, ne); TAKE(efc_A, ne); TAKE(efc_b, ne); TAKE(efc_f, ne);
   TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_hb, 36 * ne); TAKE(efc_dA, ne); TAKE(efc_floss, ne); TAKE(w, nv);
   TAKE(efc_AR, ne); TAKE(efc_ARinv, ne); TAKE(efc_Ainv, ne); TAKE(Dv, nv); TAKE(sD, nv); TAKE(isD, nv);
-  TAKE(efc_Dr, ne); TAKE(efc_sqR, ne); TAKE(efc_isR, ne); TAKE(efc_mup, ne); TAKE(efc_jar, ne); TAKE(efc_jv, ne); TAKE(hX, ne * nv);
+  TAKE(efc_Dr, ne); TAKE(efc_sqR, ne); TAKE(efc_isR, ne); TAKE(efc_mup, ne); TAKE(efc_k1, ne); TAKE(efc_jar, ne); TAKE(efc_jv, ne); TAKE(hX, ne * nv);
 #undef TAKE
   if (pass == 0) base = (double*)calloc(tot, sizeof(double));
   }
@@ -1795,7 +1795,7 @@ static double row_eval(const Dat* d, int r, const double* jr, double* f, int* st
   for (int a = 1; a < dim; a++) t2 = t2 + z[a] * z[a];
   double tn = sqrt(t2);
   int zone;
-  double yn = 0.0;
+  double yn = 0.0, itn = 0.0, sc = 0.0;
   if (tn <= mup * z[0]) {
     zone = ST_QUAD;
     for (int a = 0; a < dim; a++) y[a] = z[a];
@@ -1804,10 +1804,12 @@ static double row_eval(const Dat* d, int r, const double* jr, double* f, int* st
     for (int a = 0; a < dim; a++) y[a] = 0.0;
   } else {
     zone = ST_CONE;
-    yn = (z[0] + mup * tn) / (1.0 + mup * mup);
+    /* k1 = 1 / (1 + mu'^2) per block; one reciprocal of |z_t| per evaluation */
+    yn = (z[0] + mup * tn) * d->efc_k1[r];
+    itn = 1.0 / tn;
+    sc = (mup * yn) * itn;
     y[0] = yn;
-    double s = (mup * yn) / tn;
-    for (int a = 1; a < dim; a++) y[a] = s * z[a];
+    for (int a = 1; a < dim; a++) y[a] = sc * z[a];
   }
   double c = 0.0;
   for (int a = 0; a < dim; a++) {
@@ -1817,17 +1819,17 @@ static double row_eval(const Dat* d, int r, const double* jr, double* f, int* st
   }
   if (cq && zone == ST_CONE) {
     /* cone curvature: k1 = 1/(1+mu'^2), k2 = mu' yn / |z_t|, e = z_t / |z_t| */
-    cq[0] = 1.0 / (1.0 + mup * mup);
-    cq[1] = (mup * yn) / tn;
-    for (int a = 1; a < dim; a++) cq[1 + a] = z[a] / tn;
+    cq[0] = d->efc_k1[r];
+    cq[1] = sc;
+    for (int a = 1; a < dim; a++) cq[1 + a] = z[a] * itn;
   }
   if (hb && zone == ST_CONE) {
-    double k1 = 1.0 / (1.0 + mup * mup);
-    double k2 = (mup * yn) / tn;
+    double k1 = d->efc_k1[r];
+    double k2 = sc;
     double v[6], e[6];
     v[0] = 1.0;
     e[0] = 0.0;
-    for (int a = 1; a < dim; a++) { e[a] = z[a] / tn; v[a] = mup * e[a]; }
+    for (int a = 1; a < dim; a++) { e[a] = z[a] * itn; v[a] = mup * e[a]; }
     for (int a = 0; a < dim; a++)
       for (int b = 0; b < dim; b++) {
         double P = (k1 * v[a]) * v[b];
@@ -1925,7 +1927,11 @@ static void solve_newton(const Mdl* md, Dat* d) {
   }
   for (int r = 0; r < ne;) {
     int dim = (d->efc_type[r] == MGS_EFC_CONTACT) ? d->efc_dim[r] : 1;
-    if (dim > 1) d->efc_mup[r] = d->efc_mu[5 * r] / sqrt(m->impratio);
+    if (dim > 1) {
+      double mup = d->efc_mu[5 * r] / sqrt(m->impratio);
+      d->efc_mup[r] = mup;
+      d->efc_k1[r] = 1.0 / (1.0 + mup * mup);
+    }
     r += dim;
   }
   /* whitened smooth and warmstart accelerations: W(a)_i = sD_i (a_i + sum_{k>i} L_ki a_k) */

@@ -46,3 +46,5 @@ print('ticks per candidate-step: %.0f' % (tot / steps))
 steps_exec = r['stats'][:, 3].size and None
 print('per candidate-step (all %d steps counted): narrowphase pairs %.2f, hits %.2f, support calls %.2f, big-hull support scans %.2f, big-hull pairs %.2f' % (
     steps, cnt[0] / steps, cnt[1] / steps, cnt[2] / steps, cnt[3] / steps, cnt[4] / steps))
+cnt2 = np.array(buf[36:39], dtype=np.float64)
+print('per candidate-step: ls_eval calls %.2f, newton_eval calls %.2f, noslip sweeps %.2f' % tuple(cnt2 / steps))
