@@ -544,7 +544,7 @@ DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
 #pragma unroll
     for (int c = j + 1; c < NV; c++) {
       double w = readlane_d(v, c);
-      r[c] = r[c] - r[j] * w;
+      r[c] = __builtin_fma(-r[j], w, r[c]);
     }
   }
 }
@@ -584,13 +584,13 @@ DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     double yk = readlane_d(acc, k);
-    if (lane > k) acc = acc - Lr[k] * yk;
+    if (lane > k) acc = __builtin_fma(-Lr[k], yk, acc);
   }
   acc = acc * Dinv[li];
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
     double xk = readlane_d(acc, k);
-    if (lane < k) acc = acc - Lc[k] * xk;
+    if (lane < k) acc = __builtin_fma(-Lc[k], xk, acc);
   }
   wsync();
   if (lane < NV) x[lane] = acc;
@@ -860,7 +860,7 @@ DEVI void mink_support(const PairCtx& c, const double* dir, SupPt* p) {
   PCNT(29, (c.n1 > WAVE) + (c.n2 > WAVE));
   support_pair(c, dir, p->a, p->b);
   sub3(p->v, p->a, p->b);
-  PT(22);
+  if (c.n1 > WAVE || c.n2 > WAVE) PT(39); else PT(22);
 }
 
 DEVI void portal_normal(double* n, const SupPt* p1, const SupPt* p2, const SupPt* p3) {
@@ -1231,6 +1231,7 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   double tol = dn + K_FEAT_EPS;
   int na = feature(pc, 1, n, t1, t2, +1, tol, 1, fa, &s1);
   int nb = feature(pc, 2, n, t1, t2, -1, tol, 1, fb, &s2);
+  PT(40);
   if (lane == 0) {
     int refB = (nb >= na);
     int nr = refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly);
@@ -1285,7 +1286,7 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
     }
   }
   wsync();
-  PT(5);
+  PT(41);
 }
 
 #define OBB_FN DEVI
@@ -1791,7 +1792,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     for (int i = 0; i < NV; i++) {
       double s = g[i];
 #pragma unroll
-      for (int k = 0; k < i; k++) s = s - d.M[i * NV + k] * g[k];
+      for (int k = 0; k < i; k++) s = __builtin_fma(-d.M[i * NV + k], g[k], s);
       g[i] = s;
     }
 #pragma unroll
@@ -2223,14 +2224,14 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
     double zk = readlane_d(z, k);
-    if (lane < k) z = z - Lc[k] * zk;
+    if (lane < k) z = __builtin_fma(-Lc[k], zk, z);
   }
   double t = u * d.sD[li];
   double q = t;
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     double tk = readlane_d(t, k);
-    if (lane > k) q = q + Lr[k] * tk;
+    if (lane > k) q = __builtin_fma(Lr[k], tk, q);
   }
   if (lane < NV) {
     d.qfrc_constraint[lane] = q;
@@ -2371,7 +2372,7 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const dou
     const double* Gr = d.G + r * GS;
     double s = 0.0;
 #pragma unroll
-    for (int k = 0; k < NV; k++) s = s + Gr[k] * wr[k];
+    for (int k = 0; k < NV; k++) s = __builtin_fma(Gr[k], wr[k], s);
     d.efc_jar[r] = s - d.efc_aref[r];
   }
   wsync();
@@ -2417,12 +2418,12 @@ DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
       double g0 = d.G[r * GS + lane], g1 = d.G[(r + 1) * GS + lane], g2 = d.G[(r + 2) * GS + lane],
              g3 = d.G[(r + 3) * GS + lane];
       double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
-      s = s + g0 * f0;
-      s = s + g1 * f1;
-      s = s + g2 * f2;
-      s = s + g3 * f3;
+      s = __builtin_fma(g0, f0, s);
+      s = __builtin_fma(g1, f1, s);
+      s = __builtin_fma(g2, f2, s);
+      s = __builtin_fma(g3, f3, s);
     }
-    for (; r < ne; r++) s = s + d.G[r * GS + lane] * d.efc_f[r];
+    for (; r < ne; r++) s = __builtin_fma(d.G[r * GS + lane], d.efc_f[r], s);
     d.ng[lane] = (w[lane] - d.nw0[lane]) - s;
   }
   wsync();
@@ -2745,8 +2746,8 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     for (int k = 1; k < NV; k++) {
       double l = d.M[k * NV + li];
       if (k > lane) {
-        s = s + l * d.qacc_smooth[k];
-        s2 = s2 + l * d.qacc_ws[k];
+        s = __builtin_fma(l, d.qacc_smooth[k], s);
+        s2 = __builtin_fma(l, d.qacc_ws[k], s2);
       }
     }
     if (lane < NV) {
@@ -2807,7 +2808,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
         const double* Gr = d.G + r * GS;
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < NV; k++) s = s + Gr[k] * dr[k];
+        for (int k = 0; k < NV; k++) s = __builtin_fma(Gr[k], dr[k], s);
         d.efc_jv[r] = s;
       }
     }
@@ -2861,12 +2862,12 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
       double g0 = d.G[r * GS + lane], g1 = d.G[(r + 1) * GS + lane], g2 = d.G[(r + 2) * GS + lane],
              g3 = d.G[(r + 3) * GS + lane];
       double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
-      s = s + g0 * f0;
-      s = s + g1 * f1;
-      s = s + g2 * f2;
-      s = s + g3 * f3;
+      s = __builtin_fma(g0, f0, s);
+      s = __builtin_fma(g1, f1, s);
+      s = __builtin_fma(g2, f2, s);
+      s = __builtin_fma(g3, f3, s);
     }
-    for (; r < ne; r++) s = s + d.G[r * GS + lane] * d.efc_f[r];
+    for (; r < ne; r++) s = __builtin_fma(d.G[r * GS + lane], d.efc_f[r], s);
     u = s;
   }
 }

@@ -489,12 +489,12 @@ static void ldl_factor(int n, const double* A, double* L, double* Dinv, double* 
   for (int j = 0; j < n; j++) {
     for (int k = 0; k < j; k++) W[k] = L[j * n + k] * Dv[k];
     double dj = A[j * n + j];
-    for (int k = 0; k < j; k++) dj = dj - W[k] * L[j * n + k];
+    for (int k = 0; k < j; k++) dj = fma(-W[k], L[j * n + k], dj);
     Dv[j] = dj;
     Dinv[j] = 1.0 / dj;
     for (int i = j + 1; i < n; i++) {
       double s = A[i * n + j];
-      for (int k = 0; k < j; k++) s = s - L[i * n + k] * W[k];
+      for (int k = 0; k < j; k++) s = fma(-L[i * n + k], W[k], s);
       L[i * n + j] = s * Dinv[j];
     }
   }
@@ -503,13 +503,13 @@ static void ldl_solve(int n, const double* L, const double* Dinv, const double* 
   double y[128];
   for (int i = 0; i < n; i++) {
     double s = b[i];
-    for (int k = 0; k < i; k++) s = s - L[i * n + k] * y[k];
+    for (int k = 0; k < i; k++) s = fma(-L[i * n + k], y[k], s);
     y[i] = s;
   }
   /* backward substitution, k descending (the kernel's column order) */
   for (int i = n - 1; i >= 0; i--) {
     double s = y[i] * Dinv[i];
-    for (int k = n - 1; k > i; k--) s = s - L[k * n + i] * x[k];
+    for (int k = n - 1; k > i; k--) s = fma(-L[k * n + i], x[k], s);
     x[i] = s;
   }
 }
@@ -624,6 +624,11 @@ typedef struct { double v[3], a[3], b[3]; } SupPt;
 
 /* support point of geom g along world direction dir; returns vertex index */
 static long g_sup_calls;   /* diagnostics: support calls (single-threaded use) */
+int g_sep_log; long g_sep_n; double g_sep_val[200000]; int g_sep_pair[200000];
+double* oracle_sep_vals(void) { return g_sep_val; }
+int* oracle_sep_pairs(void) { return g_sep_pair; }
+long oracle_sep_count(void) { return g_sep_n; }
+void oracle_sep_enable(int on) { g_sep_log = on; g_sep_n = 0; }
 static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, double* out) {
   int h = IA(md, geom_hullid)[g];
   int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
@@ -699,6 +704,7 @@ static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* 
   dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
   normalize3(dir);
   mink_support(md, d, g1, g2, dir, &p1);
+  if (g_sep_log && g_sep_n < 200000) { g_sep_val[g_sep_n] = dot3(p1.v, dir); g_sep_pair[g_sep_n] = g1 * 64 + g2; g_sep_n++; }
   if (dot3(p1.v, dir) <= 0.0) return 0;
   cross3(dir, p0.v, p1.v);
   if (dot3(dir, dir) < 1e-30) {
@@ -1361,7 +1367,7 @@ static void make_constraints(const Mdl* md, Dat* d) {
     d->efc_b[r] = bj;
     for (int i = 0; i < nv; i++) {
       double s = Jr[i];
-      for (int k = 0; k < i; k++) s = s - d->L[i * nv + k] * Gr[k];
+      for (int k = 0; k < i; k++) s = fma(-d->L[i * nv + k], Gr[k], s);
       Gr[i] = s;
     }
     for (int i = 0; i < nv; i++) Gr[i] = Gr[i] * d->isD[i];
@@ -1716,14 +1722,14 @@ static void finalize_solution(const Mdl* md, Dat* d) {
   double z[128];
   for (int i = nv - 1; i >= 0; i--) {
     double s = d->w[i] * d->isD[i];
-    for (int k = nv - 1; k > i; k--) s = s - d->L[k * nv + i] * z[k];   /* k descending (kernel order) */
+    for (int k = nv - 1; k > i; k--) s = fma(-d->L[k * nv + i], z[k], s);   /* k descending (kernel order) */
     z[i] = s;
   }
   double t[128];
   for (int i = 0; i < nv; i++) t[i] = d->w[i] * d->sD[i];
   for (int i = 0; i < nv; i++) {
     double s = t[i];
-    for (int k = 0; k < i; k++) s = s + d->L[i * nv + k] * t[k];
+    for (int k = 0; k < i; k++) s = fma(d->L[i * nv + k], t[k], s);
     d->qfrc_constraint[i] = s;
     d->qacc[i] = d->qacc_smooth[i] + z[i];
   }
@@ -1849,7 +1855,7 @@ static double newton_eval(const Mdl* md, Dat* d, const double* w, const double* 
   for (int r = 0; r < ne; r++) {
     const double* Gr = d->K + (size_t)r * nv;
     double s = 0.0;
-    for (int k = 0; k < nv; k++) s = s + Gr[k] * w[k];
+    for (int k = 0; k < nv; k++) s = fma(Gr[k], w[k], s);
     d->efc_jar[r] = s - d->efc_aref[r];
   }
   for (int r = 0; r < ne;) {
@@ -1864,7 +1870,7 @@ static double newton_eval(const Mdl* md, Dat* d, const double* w, const double* 
 static void newton_grad(const Dat* d, int nv, const double* w, const double* w0, double* g) {
   for (int k = 0; k < nv; k++) {
     double s = 0.0;
-    for (int r = 0; r < d->nefc; r++) s = s + d->K[(size_t)r * nv + k] * d->efc_f[r];
+    for (int r = 0; r < d->nefc; r++) s = fma(d->K[(size_t)r * nv + k], d->efc_f[r], s);
     g[k] = (w[k] - w0[k]) - s;
   }
 }
@@ -1938,8 +1944,8 @@ static void solve_newton(const Mdl* md, Dat* d) {
   double w0[64], w[64], g[64], dir[64], H[64 * 64], HL[64 * 64], HDinv[64], HDv[64];
   for (int i = 0; i < nv; i++) {
     double s = d->qacc_smooth[i], s2 = d->qacc_ws[i];
-    for (int k = i + 1; k < nv; k++) s = s + d->L[k * nv + i] * d->qacc_smooth[k];
-    for (int k = i + 1; k < nv; k++) s2 = s2 + d->L[k * nv + i] * d->qacc_ws[k];
+    for (int k = i + 1; k < nv; k++) s = fma(d->L[k * nv + i], d->qacc_smooth[k], s);
+    for (int k = i + 1; k < nv; k++) s2 = fma(d->L[k * nv + i], d->qacc_ws[k], s2);
     w0[i] = s * d->sD[i];
     w[i] = s2 * d->sD[i];
   }
@@ -1997,7 +2003,7 @@ static void solve_newton(const Mdl* md, Dat* d) {
     for (int r = 0; r < ne; r++) {
       const double* Gr = d->K + (size_t)r * nv;
       double s = 0.0;
-      for (int k = 0; k < nv; k++) s = s + Gr[k] * dir[k];
+      for (int k = 0; k < nv; k++) s = fma(Gr[k], dir[k], s);
       d->efc_jv[r] = s;
     }
     double q[64];
@@ -2035,7 +2041,7 @@ static void solve_newton(const Mdl* md, Dat* d) {
   /* u = G^T f */
   for (int k = 0; k < nv; k++) {
     double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d->K[(size_t)r * nv + k] * d->efc_f[r];
+    for (int r = 0; r < ne; r++) s = fma(d->K[(size_t)r * nv + k], d->efc_f[r], s);
     d->w[k] = s;
   }
 }

@@ -27,14 +27,14 @@ buf = (ctypes.c_ulonglong * 64)()
 L.mgs_prof_read(buf)
 r = env.engine.rollout(plan)
 L.mgs_prof_read(buf)
-v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64)])
+v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64), np.array(buf[39:42], dtype=np.float64)])
 cnt = np.array(buf[26:31], dtype=np.float64)
 names = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll: MPR', 'coll: feature+clip',
          'crb', 'ldl(M)', 'act+passive+rne+smooth', 'con: J rows', 'con: G transform', 'con: params+blocks',
          'newton: setup', 'newton: hessian', 'newton: ldl+solve+jv', 'newton: linesearch', 'newton: eval+grad',
-         'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: MPR support calls',
+         'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
          'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
-         'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne']
+         'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne', 'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)']
 tot = v.sum()
 print('N=%d collision-free candidates, kernel %.1f ms, labels %d, mean iters/step %.1f, overflow %d' % (
     len(idx), r['kernel_ms'], r['label'].sum(), r['stats'][:, 3].sum() / max(1, r['stats'][:, 3].size) / 200, (r['stats'][:, 2] != 0).sum()))
