@@ -134,3 +134,15 @@ def robotiq_candidates(obj, num, seed=0):
     gen = AntipodalGraspGenerator(obj.obj_file_path, rng=np.random.default_rng(seed))
     H, aux = gen.generate_grasps(num)
     return H.astype(np.float32), np.zeros((num, 8)), aux["width"]
+
+
+def panda_candidates(obj, num, seed=0, gripper=None):
+    """(pose, joints (num,2), width) as gen_grasp_candidates.py:66-71 builds them for
+    the Panda: joints = width_to_joints(_clamp_width(width))."""
+    from mgs.gripper.panda import GripperPanda
+    from mgs.util.geo.transforms import SE3Pose
+    g = gripper if gripper is not None else GripperPanda(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz"))
+    gen = AntipodalGraspGenerator(obj.obj_file_path, rng=np.random.default_rng(seed))
+    H, aux = gen.generate_grasps(num)
+    j1, j2 = g.width_to_joints(g._clamp_width(aux["width"]))
+    return H.astype(np.float32), np.stack([j1, j2], axis=-1), aux["width"]
