@@ -62,7 +62,7 @@ def cpu_baseline(env, poses, joints, h, budget_s, threads):
     """The oracle (C restatement, OpenMP over candidates) on the host cores, on a
     bounded leading sample of the same candidate block; returns a dict."""
     from oracle import oracle as O
-    om = O.OracleModel(env.model)
+    om = O.OracleModel(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max)
     q, mp, mq, _ = env.initial_state(poses, joints)
     # pilot on 256 candidates to size the sample to the time budget
     n_pilot = min(256, len(poses))
@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--solver", default=None, help="override the model's solver (Newton | PGS)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
+    ap.add_argument("--no-escalate", dest="escalate", action="store_false",
+                    help="skip the contact-capacity re-run of overflowed candidates")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -120,7 +123,7 @@ def main():
 
     grip = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz"))
     obj = get_object("003_cracker_box")
-    env = GravitylessObjectGrasping(grip, obj, device=local)
+    env = GravitylessObjectGrasping(grip, obj, device=local, ncon_max=args.ncon_max)
     if args.solver:
         env.model.options["solver"] = args.solver
     h = HORIZONS[args.horizon]
@@ -147,6 +150,12 @@ def main():
     d_stats = torch.zeros((N, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
+    # contact-capacity escalation (GravitylessObjectGrasping.rollout): candidates
+    # whose contacts exceeded ncon_max at some step are re-run with a wider engine,
+    # selected on the device (no host round trip) and merged into the outputs
+    wide = env.engine_for(2 * env.ncon_max) if args.escalate else None
+    w_label, w_fail, w_objq, w_stats = (torch.zeros_like(t) for t in (d_label, d_fail, d_objq, d_stats))
+    d_ovf = torch.zeros(N, dtype=torch.uint8, device=dev)
 
     def step():
         eng.collision_free_device(N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(), d_free.data_ptr(),
@@ -154,6 +163,16 @@ def main():
         eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
                            d_label.data_ptr(), d_fail.data_ptr(), d_objq.data_ptr(), d_stats.data_ptr(),
                            d_active=d_free.data_ptr(), stream=sp)
+        if wide is not None:
+            torch.ne(d_stats[:, 2], 0, out=d_ovf.view(torch.bool))
+            wide.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
+                                w_label.data_ptr(), w_fail.data_ptr(), w_objq.data_ptr(), w_stats.data_ptr(),
+                                d_active=d_ovf.data_ptr(), stream=sp)
+            m = d_ovf.bool()
+            d_label.copy_(torch.where(m, w_label, d_label))
+            d_fail.copy_(torch.where(m, w_fail, d_fail))
+            d_objq.copy_(torch.where(m[:, None], w_objq, d_objq))
+            d_stats.copy_(torch.where(m[:, None], w_stats, d_stats))
 
     for _ in range(args.warmup):
         step()
@@ -161,13 +180,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    roll_ms, coll_ms = [], []
+    roll_ms, coll_ms, wide_ms = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         # per-launch kernel durations (HIP events recorded on this stream by the library)
         roll_ms.append(eng.last_kernel_ms())
         coll_ms.append(eng.last_collision_ms())
+        if wide is not None:
+            wide_ms.append(wide.last_kernel_ms())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -213,7 +234,10 @@ def main():
                    "mean_ncon": float(stats[:, 4].sum() / max(1, steps_exec)),
                    "mean_nefc": float(stats[:, 5].sum() / max(1, steps_exec)),
                    "solver_iters_per_step": float(stats[:, 3].sum() / max(1, steps_exec)),
-                   "overflow_candidates": int((stats[:, 2] != 0).sum())},
+                   "overflow_candidates": int(d_ovf.sum().item()) if wide is not None
+                   else int((stats[:, 2] != 0).sum()),
+                   "escalation_kernel_ms": float(np.mean(wide_ms)) if wide_ms else None,
+                   "still_capped_after_escalation": int((stats[:, 2] != 0).sum()) if wide is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,

@@ -248,6 +248,12 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
                      int device, mgs_model** out);
 void mgs_model_free(mgs_model* model);
 
+/* Per-candidate LDS working set (bytes) the kernels would use for this model
+ * description, i.e. at its ncon_max / nefc_max capacity; host-only (no device
+ * needed).  The host picks the contact/row capacity with it: a CU holds
+ * floor(160 KiB / bytes) candidates in flight. */
+int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes);
+
 /* Device buffers for up to `capacity` candidates. */
 int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out);
 void mgs_batch_close(mgs_batch* batch);

@@ -186,7 +186,10 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
     snprintf(buf, sizeof(buf), "%zu", need);
     return fail(MGS_ECAPACITY, "per-candidate working set %s B exceeds 160 KiB LDS; lower ncon_max", buf);
   }
-  HIPCHK(set_lds_limit(desc->nv, (int)m->lds_bytes));
+  // the attribute is per kernel function, shared by every model of this nv: set it
+  // to the CU's whole LDS so a later, smaller model cannot lower it under an
+  // earlier, wider one (occupancy follows each launch's own dynamic size)
+  HIPCHK(set_lds_limit(desc->nv, 160 * 1024));
   *out = m;
   return MGS_OK;
 }
@@ -397,6 +400,14 @@ int mgs_prof_read(unsigned long long* out) {
 }
 
 int mgs_lds_bytes(mgs_model* m) { return m ? (int)m->lds_bytes : -1; }
+
+int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes) {
+  if (!desc || !out_bytes) return fail(MGS_EINVAL, "mgs_model_lds_bytes: null argument%s");
+  size_t b = 0;
+  make_layout(*desc, &b);
+  *out_bytes = (int64_t)b;
+  return MGS_OK;
+}
 
 int mgs_device_count(void) {
   int n = 0;

@@ -50,10 +50,43 @@ def load_library():
     L.mgs_tree_probe.argtypes = [P(c_d), P(c_d), ctypes.c_int, ctypes.c_int, P(c_d)]
     L.mgs_lds_bytes.argtypes = [vp]
     L.mgs_device_count.restype = ctypes.c_int
+    L.mgs_model_lds_bytes.argtypes = [P(abi.ModelDesc), P(ctypes.c_int64)]
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
         raise EngineError("libmgs_gpu.so ABI version mismatch with include/mgs_gpu.h")
     _lib = L
     return L
+
+
+LDS_PER_CU = 160 * 1024
+
+
+def lds_bytes_for(cm, ncon_max, nefc_max=None):
+    """Per-candidate LDS bytes of the kernels for this model and capacity (host only)."""
+    L = load_library()
+    fields, _, _ = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
+    desc = abi.make_desc(fields)
+    out = ctypes.c_int64()
+    _check(L.mgs_model_lds_bytes(ctypes.byref(desc), ctypes.byref(out)), "mgs_model_lds_bytes")
+    return int(out.value)
+
+
+def auto_capacity(cm, ncon_max=20):
+    """Constraint-row capacity for `ncon_max` contacts that keeps the most
+    candidates in flight per CU: rows are shrunk from the worst case (every
+    contact at the largest condim) down to 3 rows per contact as long as that
+    raises the per-CU occupancy.  Candidates that exceed a capacity are
+    flagged by the kernel and re-run wider (GravitylessObjectGrasping.rollout)."""
+    fields, _, _ = cm.pack(ncon_max=ncon_max)
+    full = int(fields["nefc_max"])
+    fixed = full - ncon_max * (int(cm.pair_condim.max()) if len(cm.pair_condim) else 1)
+    best, best_occ = full, LDS_PER_CU // lds_bytes_for(cm, ncon_max, full)
+    floor = min(full, fixed + 3 * ncon_max)
+    for ne in range(full - 1, floor - 1, -1):
+        occ = LDS_PER_CU // lds_bytes_for(cm, ncon_max, ne)
+        if occ > best_occ:
+            best, best_occ = ne, occ
+            break
+    return ncon_max, best
 
 
 def _check(rc, what):

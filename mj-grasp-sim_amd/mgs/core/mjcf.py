@@ -1092,7 +1092,8 @@ class CompiledModel:
         nlim = int(np.sum(self.jnt_limited))
         maxdim = int(self.pair_condim.max()) if len(self.pair_condim) else 1
         if nefc_max is None:
-            nefc_max = neqrow + nfric + nlim + ncon_max * maxdim
+            # rows are register-held two per lane in the kernels: at most 128
+            nefc_max = min(128, neqrow + nfric + nlim + ncon_max * maxdim)
         o = self.options
         fields.update(
             nq=self.nq, nv=self.nv, nbody=self.nbody, njnt=len(self.jnt_type),

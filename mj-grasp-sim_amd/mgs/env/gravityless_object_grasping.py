@@ -84,6 +84,11 @@ class RolloutPlan:
     def horizon(self):
         return int(sum(self.nsteps))
 
+    def subset(self, idx) -> "RolloutPlan":
+        return RolloutPlan(self.nsteps, self.check_every, self.check_at_end, self.ctrl,
+                           self.qpos_init[idx], self.mocap_quat[idx], self.phase_start[idx],
+                           self.phase_target[idx], self.obj_qposadr)
+
 
 class _SimView:
     """Minimal stand-in for the reference's MjSimulation attributes used by
@@ -96,7 +101,7 @@ class _SimView:
 
 class GravitylessObjectGrasping:
     def __init__(self, gripper: MjShakableOpenCloseGripper, obj: CollisionMeshObject,
-                 device: int = 0, ncon_max: int = 16):
+                 device: int = 0, ncon_max: int = 20, nefc_max: Optional[int] = None):
         self.gripper = gripper
         self.obj = obj
         self.gripper_xml, self.gripper_assets = gripper.to_xml()
@@ -105,6 +110,7 @@ class GravitylessObjectGrasping:
         self.model: CompiledModel = compile_xml(self.model_xml, {**self.gripper_assets, **self.object_assets})
         self.device = device
         self.ncon_max = ncon_max
+        self._nefc_max = nefc_max
         self._engine = None
         self._sim = _SimView(self)
 
@@ -116,11 +122,54 @@ class GravitylessObjectGrasping:
         return self.get_joint_idxs(["{}:joint".format(self.obj.name)])[0]
 
     @property
+    def nefc_max(self) -> int:
+        """Constraint-row capacity of the main engine (default: mgs.core.engine.
+        auto_capacity, the most candidates in flight per CU for ncon_max)."""
+        if self._nefc_max is None:
+            from mgs.core.engine import auto_capacity
+            self._nefc_max = auto_capacity(self.model, self.ncon_max)[1]
+        return self._nefc_max
+
+    @property
+    def capacity(self):
+        return self.ncon_max, self.nefc_max
+
+    @property
     def engine(self):
         if self._engine is None:
             from mgs.core.engine import Engine
-            self._engine = Engine(self.model, device=self.device, ncon_max=self.ncon_max)
+            self._engine = Engine(self.model, device=self.device, ncon_max=self.ncon_max, nefc_max=self.nefc_max)
         return self._engine
+
+    def engine_for(self, ncon_max: int):
+        """Engine with a larger per-candidate contact capacity (overflow re-runs)."""
+        if ncon_max == self.ncon_max:
+            return self.engine
+        if not hasattr(self, "_wide"):
+            self._wide = {}
+        if ncon_max not in self._wide:
+            from mgs.core.engine import Engine
+            self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max)
+        return self._wide[ncon_max]
+
+    def rollout(self, plan: "RolloutPlan", max_ncon: int = 40):
+        """engine.rollout with capacity escalation: MuJoCo has no contact cap, the
+        kernel's per-candidate contact arrays do (ncon_max, LDS-resident).  A
+        candidate that exceeded it at any step (stats[:, 2] != 0) is re-run from
+        its initial state with twice the capacity (constraint rows capped at 128),
+        until none overflows or max_ncon is reached; its results replace the
+        capped run's.  res['overflow'] counts candidates still capped."""
+        res = self.engine.rollout(plan)
+        cap = self.ncon_max
+        ov = np.nonzero(res["stats"][:, 2])[0]
+        while len(ov) and cap < max_ncon:
+            cap = min(2 * cap, max_ncon)
+            sub = self.engine_for(cap).rollout(plan.subset(ov))
+            for k in ("label", "fail_step", "obj_qpos", "stats"):
+                res[k][ov] = sub[k]
+            ov = ov[np.nonzero(sub["stats"][:, 2])[0]]
+        res["overflow"] = len(ov)
+        return res
 
     # -- host-side bookkeeping (exactly the reference's arithmetic) ------------
     def _check_inputs(self, poses, joints, check_width=True):
@@ -209,7 +258,7 @@ class GravitylessObjectGrasping:
             return np.zeros(0, dtype=bool)
         plan = self.rollout_plan(poses, joints, nstep_lift, lift_dist, shake_steps, shake_dist,
                                  close_steps=close_steps, lift_check_every=lift_check_every)
-        res = self.engine.rollout(plan)
+        res = self.rollout(plan)
         labels = apply_enough_stable(res["label"].astype(bool), enough_stable)
         if return_details:
             res["label"] = labels

@@ -37,7 +37,7 @@ def candidates(env):
 @pytest.fixture(scope="session")
 def oracle_model(env):
     from oracle import oracle as O
-    return O.OracleModel(env.model)
+    return O.OracleModel(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max)
 
 
 def plan_for(env, poses, joints, horizon="h200"):

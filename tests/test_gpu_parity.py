@@ -88,7 +88,7 @@ def test_rollout_parity_h200(env, candidates, solver):
     from conftest import plan_for
     from oracle import oracle as O
     e2 = _variant(env, solver=solver)
-    om = O.OracleModel(e2.model)
+    om = O.OracleModel(e2.model, ncon_max=e2.ncon_max, nefc_max=e2.nefc_max)
     poses, J = candidates
     q, mp, mq, _ = e2.initial_state(poses, J)
     idx = np.nonzero(om.collision_free(q, mp, mq, nthreads=8))[0]
@@ -207,3 +207,34 @@ def test_full_size_properties(env, eng, oracle_model):
     ro = oracle_model.rollout(plan_for(env, poses[idx[:k]], J[idx[:k]]), nthreads=8)
     for key in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(r1[key][:k], ro[key]), key
+
+
+def test_contact_capacity_escalation(env):
+    """Candidates whose contacts exceed ncon_max=16 (7 of the seed-0 8192 block)
+    are re-run at ncon_max=32 by GravitylessObjectGrasping.rollout; every result
+    then equals the oracle run at the capacity that held it, and none stays capped."""
+    from conftest import plan_for
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    from oracle import oracle as O
+    e16 = GravitylessObjectGrasping(env.gripper, env.obj, ncon_max=16)
+    H, J, _ = robotiq_candidates(env.obj, 8192, seed=0)
+    P = SE3Pose.from_mat(H)
+    q, mp, mq, _ = e16.initial_state(P, J)
+    idx = np.nonzero(e16.engine.collision_free(q, mp, mq))[0]
+    plan = plan_for(e16, P[idx], J[idx])
+    capped = e16.engine.rollout(plan)
+    ov = np.nonzero(capped["stats"][:, 2])[0]
+    assert len(ov) > 0
+    res = e16.rollout(plan)
+    assert res["overflow"] == 0
+    keep = np.setdiff1d(np.arange(len(idx)), ov)
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(res[k][keep], capped[k][keep]), k
+    ro = O.OracleModel(env.model, ncon_max=32).rollout(plan.subset(ov), nthreads=8)
+    _assert_same({k: res[k][ov] for k in ro}, ro, "escalated")
+    # the default capacity (20 contacts, auto rows) holds all of them
+    assert env.ncon_max == 20
+    r20 = env.rollout(plan.subset(ov))
+    assert not r20["stats"][:, 2].any()

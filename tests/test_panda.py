@@ -33,7 +33,7 @@ def pcand(penv):
 @pytest.fixture(scope="module")
 def pom(penv):
     from oracle import oracle as O
-    return O.OracleModel(penv.model)
+    return O.OracleModel(penv.model, ncon_max=penv.ncon_max, nefc_max=penv.nefc_max)
 
 
 def test_panda_model_sizes(penv):
