@@ -774,6 +774,7 @@ struct PairCtx {
   const double *V1, *V2;
   double R1[9], R2[9], x1[3], x2[3];
   double c1[3], c2[3];
+  double r1, r2;   // rounding radii (sphere / capsule: hull (+) ball), 0 for hulls
 };
 DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   int lane = lane_id();
@@ -787,6 +788,8 @@ DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   for (int k = 0; k < 3; k++) { c.x1[k] = d.geom_xpos[3 * g1 + k]; c.x2[k] = d.geom_xpos[3 * g2 + k]; }
   int i1 = (lane < c.n1) ? lane : 0, i2 = (lane < c.n2) ? lane : 0;
   for (int k = 0; k < 3; k++) { c.c1[k] = c.V1[3 * i1 + k]; c.c2[k] = c.V2[3 * i2 + k]; }
+  c.r1 = DA(md, geom_radius)[g1];
+  c.r2 = DA(md, geom_radius)[g2];
 }
 
 DEVI void sup_cached(SupAcc& a, int n, const double* cached, const double* dl) {
@@ -852,6 +855,9 @@ DEVI void support_pair(const PairCtx& c, const double* dir, double* out1, double
   add3(out1, c.x1, t);
   mulmv3(t, c.R2, v2);
   add3(out2, c.x2, t);
+  // rounded geoms (oracle support_geom): + r * unit direction
+  if (c.r1 > 0.0) { out1[0] = out1[0] + c.r1 * dir[0]; out1[1] = out1[1] + c.r1 * dir[1]; out1[2] = out1[2] + c.r1 * dir[2]; }
+  if (c.r2 > 0.0) { out2[0] = out2[0] + c.r2 * nd[0]; out2[1] = out2[1] + c.r2 * nd[1]; out2[2] = out2[2] + c.r2 * nd[2]; }
 }
 
 DEVI void mink_support(const PairCtx& c, const double* dir, SupPt* p) {
@@ -1018,9 +1024,11 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
   const double* V = which == 1 ? c.V1 : c.V2;
   const double* cv = which == 1 ? c.c1 : c.c2;
   int num = which == 1 ? c.n1 : c.n2;
+  double rr = which == 1 ? c.r1 : c.r2;
   double nl[3];
   mulmtv3(nl, R, n);
   double base = dot3(x, n);
+  if (rr > 0.0) base = (sign > 0) ? base + rr : base - rr;   // rounded: surface = hull (+) ball
   double best = (sign > 0) ? -INFINITY : INFINITY;
   if (num <= WAVE) {
     if (lane < num) best = base + ((cv[0] * nl[0] + cv[1] * nl[1]) + cv[2] * nl[2]);

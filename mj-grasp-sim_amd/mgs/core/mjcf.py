@@ -51,6 +51,7 @@ _JOINT_DEFAULTS = dict(type="hinge", axis="0 0 1", pos="0 0 0", range="0 0",
                        solimpfriction="0.9 0.95 0.001 0.5 2", margin="0", ref="0")
 _EQ_DEFAULTS = dict(solref="0.02 1", solimp="0.9 0.95 0.001 0.5 2", active="true")
 
+CYL_SIDES = 16   # cylinder collision geoms: 32-vertex prisms (a cap fits one contact feature, K_MAXF)
 _JNT_TYPES = {"free": 0, "ball": 1, "slide": 2, "hinge": 3}
 
 
@@ -673,8 +674,23 @@ class Compiler:
                     hull_of_mesh[mname] = len(hulls)
                     hulls.append(self._mesh_hull(mname))
                 hid = hull_of_mesh[mname]
+            elif t in ("sphere", "capsule"):
+                # rounded geoms: a point / a z-segment swept by a ball of radius size[0]
+                s = _f(g["size"], 3)
+                hid = len(hulls)
+                hulls.append(np.zeros((1, 3)) if t == "sphere" else np.array([[0, 0, -s[1]], [0, 0, s[1]]]))
+            elif t == "cylinder":
+                # a CYL_SIDES-sided prism inscribed in the cylinder (vertices on the
+                # true rim): documented approximation of MuJoCo's smooth support
+                s = _f(g["size"], 3)
+                a = 2 * np.pi * np.arange(CYL_SIDES) / CYL_SIDES
+                rim = np.stack([s[0] * np.cos(a), s[0] * np.sin(a)], 1)
+                hid = len(hulls)
+                hulls.append(np.concatenate([np.c_[rim, np.full(CYL_SIDES, -s[1])],
+                                             np.c_[rim, np.full(CYL_SIDES, s[1])]]))
             else:
                 raise MJCFError(f"collision geom type {t} not supported yet")
+            radius = float(_f(g["size"], 3)[0]) if t in ("sphere", "capsule") else 0.0
             side = 0 if partition is None else int(np.sign(gid - partition))
             fr = _fv(g, "friction")
             cgeoms.append(dict(gid=gid, body=bi, hull=hid, pos=gpos, quat=gquat, contype=ct,
@@ -682,7 +698,7 @@ class Compiler:
                                solref=_fv(g, "solref"), solimp=_fv(g, "solimp"),
                                margin=float(g.get("margin", "0")), gap=float(g.get("gap", "0")),
                                priority=int(g.get("priority", "0")), solmix=float(g.get("solmix", "1")),
-                               side=side, name=g.get("name", "")))
+                               side=side, name=g.get("name", ""), radius=radius))
         # --- admissible pairs
         excl = set()
         for b1, b2 in self.excludes:
@@ -869,9 +885,10 @@ class Compiler:
         aabb = []
         for g in cgeoms:
             v = hulls[g["hull"]]
-            lo, hi = v.min(0), v.max(0)
+            lo, hi = v.min(0) - g["radius"], v.max(0) + g["radius"]
             aabb.append(np.concatenate([(lo + hi) / 2, (hi - lo) / 2]))
         cm.geom_aabb = np.array(aabb).reshape(-1, 6)
+        cm.geom_radius = np.array([g["radius"] for g in cgeoms], np.float64)
         cm.hull_vertnum = np.array([len(h) for h in hulls], np.int32)
         cm.hull_vertadr = np.concatenate([[0], np.cumsum(cm.hull_vertnum)[:-1]]).astype(np.int32) if hulls else np.zeros(0, np.int32)
         cm.hull_vert = np.concatenate(hulls).reshape(-1, 3) if hulls else np.zeros((0, 3))
@@ -1062,7 +1079,7 @@ class CompiledModel:
             put_d(n, getattr(self, n))
         for n in ["geom_bodyid", "geom_hullid", "geom_side"]:
             put_i(n, getattr(self, n))
-        for n in ["geom_pos", "geom_quat", "geom_aabb"]:
+        for n in ["geom_pos", "geom_quat", "geom_aabb", "geom_radius"]:
             put_d(n, getattr(self, n))
         put_i("hull_vertadr", self.hull_vertadr)
         put_i("hull_vertnum", self.hull_vertnum)

@@ -67,3 +67,20 @@ class MjShakableOpenCloseGripper(MjGripper):
 
     def open_ctrl(self, sim) -> np.ndarray:
         return np.zeros(sim.model.nu)
+
+
+def fmt32(v) -> str:
+    """space-separated float32-rounded values (MJCF attribute text)."""
+    return " ".join(repr(float(np.float32(x))) if abs(x) > 0 else "0" for x in np.ravel(v))
+
+
+def mesh_inertial_xml(vol, com, inertia, density, offset=(0.0, 0.0, 0.0)) -> str:
+    """<inertial> equal to MuJoCo's mass from one mesh geom at `density`, placed
+    at `offset` in the body frame (geom pos, identity geom orientation)."""
+    from mgs.core.mjcf import mat2quat
+    w, V = np.linalg.eigh(np.asarray(inertia) * density)
+    if np.linalg.det(V) < 0:
+        V[:, 2] = -V[:, 2]
+    pos = np.asarray(com) + np.asarray(offset)
+    return (f'<inertial mass="{float(density * vol)!r}" pos="{fmt32(pos)}" quat="{fmt32(mat2quat(V))}" '
+            f'diaginertia="{fmt32(w)}"/>')

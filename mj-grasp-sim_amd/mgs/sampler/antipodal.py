@@ -146,3 +146,13 @@ def panda_candidates(obj, num, seed=0, gripper=None):
     H, aux = gen.generate_grasps(num)
     j1, j2 = g.width_to_joints(g._clamp_width(aux["width"]))
     return H.astype(np.float32), np.stack([j1, j2], axis=-1), aux["width"]
+
+
+def hand_candidates(obj, num, gripper, seed=0):
+    """Antipodal contact frames with the hand's open joint configuration, for
+    dexterous hands whose own sampler (the reference's JAX contact sampler,
+    mgs/sampler/contact.py) is out of scope here: (pose, joints (num, nj), width)."""
+    gen = AntipodalGraspGenerator(obj.obj_file_path, rng=np.random.default_rng(seed))
+    H, aux = gen.generate_grasps(num)
+    J = np.tile(np.asarray(gripper.open_ctrl(None), np.float64), (num, 1))
+    return H.astype(np.float32), J, aux["width"]

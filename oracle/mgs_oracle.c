@@ -645,6 +645,9 @@ static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, d
   double t[3];
   mulmv3(t, R, V + 3 * bi);
   add3(out, d->geom_xpos + 3 * g, t);
+  /* rounded geoms (sphere, capsule): hull (+) ball; dir is a unit vector */
+  double r = DA(md, geom_radius)[g];
+  if (r > 0.0) { out[0] = out[0] + r * dir[0]; out[1] = out[1] + r * dir[1]; out[2] = out[2] + r * dir[2]; }
   return bi;
 }
 
@@ -814,6 +817,8 @@ static int feature(const Mdl* md, const Dat* d, int g, const double* n, const do
   double nl[3];
   mulmtv3(nl, R, n);
   double base = dot3(x, n);
+  double r = DA(md, geom_radius)[g];
+  if (r > 0.0) base = (sign > 0) ? base + r : base - r;   /* rounded: surface = hull (+) ball */
   double best = (sign > 0) ? -INFINITY : INFINITY;
   for (int i = 0; i < num; i++) {
     double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
