@@ -101,9 +101,9 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
 }  // namespace
 
 // dof counts with a compiled kernel instantiation (Panda + free object = 14,
-// Allegro + free object = 28,
+// Allegro + free object = 28, Shadow + free object = 34,
 // Robotiq 2F-85 + free object = 20)
-#define MGS_NV_LIST(X) X(14) X(20) X(28)
+#define MGS_NV_LIST(X) X(14) X(20) X(28) X(34)
 
 static bool nv_supported(int nv) {
   switch (nv) {

@@ -68,6 +68,10 @@ class MjShakableOpenCloseGripper(MjGripper):
     def open_ctrl(self, sim) -> np.ndarray:
         return np.zeros(sim.model.nu)
 
+    def open_joints(self) -> np.ndarray:
+        """actuated-joint values of the open hand (order of get_actuator_joint_names)."""
+        return np.asarray(self.open_ctrl(None), dtype=np.float64)
+
 
 def fmt32(v) -> str:
     """space-separated float32-rounded values (MJCF attribute text)."""

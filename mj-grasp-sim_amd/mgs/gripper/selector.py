@@ -5,10 +5,12 @@ from mgs.gripper.base import MjShakableOpenCloseGripper
 from mgs.gripper.allegro import GripperAllegro
 from mgs.gripper.panda import GripperPanda
 from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+from mgs.gripper.shadow import GripperShadowRight
 from mgs.util.geo.transforms import SE3Pose
 
 _GRIPPERS = {"Robotiq2f85Gripper": GripperRobotiq2f85, "PandaGripper": GripperPanda,
-             "AllegroGripper": GripperAllegro}
+             "AllegroGripper": GripperAllegro,
+             "ShadowHand": GripperShadowRight}
 
 
 def get_gripper(cfg, default_pose=None) -> MjShakableOpenCloseGripper:

@@ -154,5 +154,10 @@ def hand_candidates(obj, num, gripper, seed=0):
     mgs/sampler/contact.py) is out of scope here: (pose, joints (num, nj), width)."""
     gen = AntipodalGraspGenerator(obj.obj_file_path, rng=np.random.default_rng(seed))
     H, aux = gen.generate_grasps(num)
-    J = np.tile(np.asarray(gripper.open_ctrl(None), np.float64), (num, 1))
+    site = getattr(gripper, "grasp_site", None)
+    if site is not None:
+        # hands whose base frame is the wrist (identity base-to-contact): put the
+        # hand's grasp site, not the wrist, on the antipodal centre
+        H[:, :3, 3] -= H[:, :3, :3] @ np.asarray(site)
+    J = np.tile(gripper.open_joints(), (num, 1))
     return H.astype(np.float32), J, aux["width"]
