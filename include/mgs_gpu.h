@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 4
+#define MGS_ABI_VERSION 5
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -159,6 +159,8 @@ typedef struct mgs_model_desc {
   int32_t d_dof_solref;     /* 2 */
   int32_t d_dof_solimp;     /* 5 */
   int32_t d_qpos0;          /* nq */
+  int32_t d_qvel0;          /* nv: initial qvel of every candidate (0; a clutter scene's env_state) */
+  int32_t d_qacc_ws0;       /* nv: initial qacc_warmstart (0; a clutter scene's env_state) */
   int32_t d_qpos_spring;    /* nq */
   /* collision geoms */
   int32_t i_geom_bodyid;
@@ -255,6 +257,12 @@ void mgs_model_free(mgs_model* model);
  * needed).  The host picks the contact/row capacity with it: a CU holds
  * floor(160 KiB / bytes) candidates in flight. */
 int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes);
+
+/* Capacity limits of this library build: constraint rows per candidate
+ * (libmgs_gpu.so 128, libmgs_gpu_wide.so 256) and whether a kernel is
+ * instantiated for a dof count (1/0). */
+int mgs_max_rows(void);
+int mgs_supports_nv(int nv);
 
 /* Device buffers for up to `capacity` candidates. */
 int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out);

@@ -7,6 +7,10 @@
 #include <string>
 #include <vector>
 
+#ifdef MGS_WIDE
+#define MGS_RPL 4
+#define MGS_G_GLOBAL 1
+#endif
 #include "mgs_kernels.hip"
 
 namespace {
@@ -54,7 +58,11 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   us[U_comacc] = 4 * nb;
   us[U_cvel] = 6 * nb; us[U_cacc] = 6 * nb; us[U_cfrc] = 6 * nb; us[U_cdof_dot] = 6 * nv;
   us[U_qfrc_bias] = nv; us[U_qfrc_passive] = nv; us[U_qfrc_actuator] = nv;
+#ifdef MGS_G_GLOBAL
+  us[U_G] = 0;               // G in HBM (batch buffer), see bind()
+#else
   us[U_G] = ne * (nv + 0);   // row stride: GS in the kernel
+#endif
   us[U_aref] = ne;
   us[U_scratch] = (2 * ne > nv ? 2 * ne : nv);
   // {vel, pos, margin} (make_constraints) | Newton Hessian, which may run on into
@@ -100,10 +108,16 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
 }
 }  // namespace
 
-// dof counts with a compiled kernel instantiation (Panda + free object = 14,
-// Allegro + free object = 28, Shadow + free object = 34,
-// Robotiq 2F-85 + free object = 20)
+// dof counts with a compiled kernel instantiation.  Main library: Panda +
+// free object = 14, Robotiq 2F-85 + free object = 20, Allegro + free object =
+// 28, Shadow + free object = 34.  Wide library (MGS_WIDE: 4 rows per lane, G in
+// HBM) for clutter piles of 5 free objects: Panda 38, Robotiq 44, Allegro 52,
+// Shadow 58.
+#ifdef MGS_WIDE
+#define MGS_NV_LIST(X) X(38) X(44) X(52) X(58)
+#else
 #define MGS_NV_LIST(X) X(14) X(20) X(28) X(34)
+#endif
 
 static bool nv_supported(int nv) {
   switch (nv) {
@@ -145,6 +159,8 @@ struct mgs_batch {
   double *d_qpos, *d_mpos, *d_mquat, *d_ps, *d_pt, *d_objq;
   uint8_t *d_label, *d_free;
   int32_t *d_fail, *d_stats;
+  double* d_G;      // MGS_G_GLOBAL: per-candidate constraint rows (HBM)
+  size_t g_elems;
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
@@ -162,7 +178,8 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
     return fail(MGS_EINVAL, "only elliptic cones and implicitfast are supported%s");
   if (desc->nu > 32) return fail(MGS_EINVAL, "at most 32 actuators%s");
   if (desc->nmocap > 1) return fail(MGS_EINVAL, "at most one mocap body%s");
-  if (desc->nefc_max > 128) return fail(MGS_EINVAL, "nefc_max must be <= 128%s");
+  if (desc->nefc_max > 64 * MGS_RPL) return fail(MGS_EINVAL, "nefc_max exceeds this library's rows (mgs_max_rows)%s");
+  if (desc->nv > 64) return fail(MGS_EINVAL, "nv must be <= 64 (lanes over dofs)%s");
   for (int p = 0; p < desc->npair; p++) {
     int cd = ibuf[desc->i_pair_condim + p];
     if (cd != 1 && cd != 3 && cd != 4) return fail(MGS_EINVAL, "condim must be 1, 3 or 4%s");
@@ -236,11 +253,31 @@ void mgs_batch_close(mgs_batch* b) {
   if (!b) return;
   hipFree(b->d_qpos); hipFree(b->d_mpos); hipFree(b->d_mquat); hipFree(b->d_ps); hipFree(b->d_pt);
   hipFree(b->d_objq); hipFree(b->d_label); hipFree(b->d_free); hipFree(b->d_fail); hipFree(b->d_stats);
+  if (b->d_G) hipFree(b->d_G);
   if (b->e0) hipEventDestroy(b->e0);
   if (b->e1) hipEventDestroy(b->e1);
   if (b->e2) hipEventDestroy(b->e2);
   if (b->e3) hipEventDestroy(b->e3);
   delete b;
+}
+
+// the layout a launch over n candidates uses: in the wide library the G rows of
+// every candidate live in a batch-owned HBM buffer, grown on demand
+static int launch_layout(mgs_batch* b, int n, Lay* lay) {
+  *lay = b->m->lay;
+  lay->gmem = nullptr;
+#ifdef MGS_G_GLOBAL
+  size_t need = (size_t)n * (size_t)b->m->desc.nefc_max * (size_t)b->m->desc.nv;
+  if (need > b->g_elems) {
+    if (b->d_G) HIPCHK(hipFree(b->d_G));
+    b->d_G = nullptr;
+    b->g_elems = 0;
+    if (hipMalloc(&b->d_G, need * sizeof(double)) != hipSuccess) return fail(MGS_ENOMEM, "G buffer allocation failed%s");
+    b->g_elems = need;
+  }
+  lay->gmem = b->d_G;
+#endif
+  return MGS_OK;
 }
 
 static Mdl device_model(const mgs_model* m) {
@@ -261,9 +298,12 @@ int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, co
   HIPCHK(hipSetDevice(b->m->device));
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
+  Lay lay;
+  int lrc = launch_layout(b, n, &lay);
+  if (lrc) return lrc;
   HIPCHK(hipEventRecord(b->e2, st));
 #define MGS_LAUNCH_COLL(NV_) hipLaunchKernelGGL(mgs_collision_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
-      md.I, md.D, b->m->lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free)
+      md.I, md.D, lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free)
   switch (md.m.nv) {
 #define MGS_CASE(NV_) case NV_: MGS_LAUNCH_COLL(NV_); break;
     MGS_NV_LIST(MGS_CASE)
@@ -301,9 +341,12 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
   HIPCHK(hipSetDevice(b->m->device));
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
+  Lay lay;
+  int lrc = launch_layout(b, n, &lay);
+  if (lrc) return lrc;
   HIPCHK(hipEventRecord(b->e0, st));
 #define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
-      md.I, md.D, b->m->lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
+      md.I, md.D, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
       d_fail_step, d_obj_qpos, d_stats)
   switch (md.m.nv) {
 #define MGS_CASE(NV_) case NV_: MGS_LAUNCH_ROLL(NV_); break;
@@ -401,6 +444,10 @@ int mgs_prof_read(unsigned long long* out) {
 }
 
 int mgs_lds_bytes(mgs_model* m) { return m ? (int)m->lds_bytes : -1; }
+
+int mgs_max_rows(void) { return 64 * MGS_RPL; }
+
+int mgs_supports_nv(int nv) { return nv_supported(nv) ? 1 : 0; }
 
 int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes) {
   if (!desc || !out_bytes) return fail(MGS_EINVAL, "mgs_model_lds_bytes: null argument%s");

@@ -78,6 +78,9 @@ struct Dat {
 #define OVERFLOW ints[2]
 #define ITERS ints[3]
 #define BLKSTRIDE 16
+#ifndef MGS_RPL
+#define MGS_RPL 2   // constraint rows per lane (nefc_max <= 64 * MGS_RPL)
+#endif
 
 DEVI int lane_id() { return (int)__lane_id(); }
 // values that are uniform across the wave but come from LDS: move to SGPRs so
@@ -1399,6 +1402,7 @@ struct Lay {
   int u[U_COUNT];   // offsets relative to o[L_U]
   int ncon_max, nefc_max, nv;
   int total_doubles;
+  double* gmem;     // MGS_G_GLOBAL: per-candidate G rows in HBM (nefc_max * nv doubles each)
 };
 
 DEVI void bind(Dat& d, double* s, const Lay& l) {
@@ -1418,7 +1422,14 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   BU(xanchor, U_xanchor); BU(xaxis, U_xaxis); BU(subtree_mass, U_subtree_mass); BU(comacc, U_comacc);
   BU(crb, U_crb); BU(cvel, U_cvel); BU(cacc, U_cacc); BU(cfrc, U_cfrc); BU(cdof_dot, U_cdof_dot);
   BU(qfrc_bias, U_qfrc_bias); BU(qfrc_passive, U_qfrc_passive); BU(qfrc_actuator, U_qfrc_actuator);
-  BU(G, U_G); BU(efc_aref, U_aref); BU(efc_vel, U_vel); BU(efc_pos, U_pos); BU(efc_margin, U_margin);
+#ifdef MGS_G_GLOBAL
+  // wide library (clutter piles): G = D^-1/2 L^-1 J' is too large for LDS at
+  // nefc_max 256 x nv 58; it lives in this candidate's HBM slice (L2-cached)
+  d.G = l.gmem + (size_t)blockIdx.x * (size_t)l.nefc_max * (size_t)l.nv;
+#else
+  BU(G, U_G);
+#endif
+  BU(efc_aref, U_aref); BU(efc_vel, U_vel); BU(efc_pos, U_pos); BU(efc_margin, U_margin);
   BU(nH, U_nH); BU(scratch, U_scratch); BU(efc_jar, U_jar); BU(efc_jv, U_jv); BU(efc_f, U_f);
   BU(efc_Dr, U_Dr); BU(efc_isR, U_isR); BU(nw, U_nw); BU(nw0, U_nw0); BU(ng, U_ng); BU(ndir, U_ndir);
   BU(qDeriv, U_qDeriv);
@@ -1929,19 +1940,32 @@ DEVI void qcqp3(const double* A, const double* b, const double* mu, double r, do
   }
 }
 
-// forces live in registers: lane l holds f[l] (fr0) and f[l + 64] (fr1)
-DEVI double getf(double fr0, double fr1, int r) {
-  return r < WAVE ? readlane_d(fr0, r) : readlane_d(fr1, r - WAVE);
+// forces live in registers: lane l holds f[l + 64 h] in F.v[h], h < MGS_RPL
+// (rows per lane: 2 in the main library, 4 in the wide one for clutter piles)
+struct Frc {
+  double v[MGS_RPL];
+};
+DEVI double getf(const Frc& F, int r) {
+  double out = 0.0;
+#pragma unroll
+  for (int h = 0; h < MGS_RPL; h++)
+    if ((r >> 6) == h) out = readlane_d(F.v[h], r & (WAVE - 1));
+  return out;
 }
-DEVI void setf(double& fr0, double& fr1, int r, double v, int lane) {
-  if (r < WAVE) fr0 = (lane == r) ? v : fr0;
-  else fr1 = (lane == r - WAVE) ? v : fr1;
+DEVI void setf(Frc& F, int r, double v, int lane) {
+#pragma unroll
+  for (int h = 0; h < MGS_RPL; h++)
+    if ((r >> 6) == h) F.v[h] = (lane == (r & (WAVE - 1))) ? v : F.v[h];
+}
+// registers <- efc_f (rows >= ne: 0)
+DEVI void load_frc(Frc& F, const double* f, int ne, int lane) {
+#pragma unroll
+  for (int h = 0; h < MGS_RPL; h++) F.v[h] = (lane + h * WAVE < ne) ? f[lane + h * WAVE] : 0.0;
 }
 
 // one PGS update of the contact block starting at row r with DIM rows
 template <int DIM>
-DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u, double& fr0,
-                                              double& fr1, int noslip) {
+DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u, Frc& F, int noslip) {
   double g[DIM], res[DIM], old[DIM], nw[DIM];
   const int c = uni(d.efc_con[r]);
   const double* blk = d.con_blk + BLKSTRIDE * c;
@@ -1950,7 +1974,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
   for (int i = 0; i < DIM; i++) {
     g[i] = (lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
     double jw = tree_sum(g[i] * u, P);
-    old[i] = getf(fr0, fr1, r + i);
+    old[i] = getf(F, r + i);
     res[i] = noslip ? (jw + d.efc_b[r + i]) : ((jw + d.efc_R[r + i] * old[i]) + d.efc_b[r + i]);
   }
   double Ab[DIM * DIM];
@@ -2005,7 +2029,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
     for (int i = 0; i < DIM; i++) s = s + g[i] * del[i];
     if (lane < nv) u = s;
 #pragma unroll
-    for (int i = 0; i < DIM; i++) setf(fr0, fr1, r + i, nw[i], lane);
+    for (int i = 0; i < DIM; i++) setf(F, r + i, nw[i], lane);
   } else {
     // friction dims only, normal fixed, A without R
     const int NF = DIM - 1;
@@ -2048,7 +2072,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
     for (int i = 0; i < NF; i++) s = s + g[1 + i] * del[i];
     if (lane < nv) u = s;
 #pragma unroll
-    for (int i = 0; i < NF; i++) setf(fr0, fr1, r + 1 + i, nw[1 + i], lane);
+    for (int i = 0; i < NF; i++) setf(F, r + 1 + i, nw[1 + i], lane);
   }
   return dc;
 }
@@ -2085,7 +2109,7 @@ DEVI void project_block_lds(const Mdl& md, const Dat& d, int r, double* f) {
   }
 }
 
-DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
+DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   // warmstart: hws = D^1/2 L^T qacc_ws (lane 0), f_r by lanes over rows, block projection
@@ -2133,10 +2157,11 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
   wsync();
   double cw = 0.0;
   for (int r = 0; r < ne; r++) cw = cw + terms[r];
-  fr0 = (lane < ne) ? fl[lane] : 0.0;
-  fr1 = (lane + WAVE < ne) ? fl[lane + WAVE] : 0.0;
+  load_frc(F, fl, ne, lane);
   if (!(cw < 0.0)) {
-    fr0 = 0.0; fr1 = 0.0; u = 0.0;
+#pragma unroll
+    for (int h = 0; h < MGS_RPL; h++) F.v[h] = 0.0;
+    u = 0.0;
   }
   int it;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
@@ -2147,7 +2172,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
       if (t != MGS_EFC_CONTACT || dim == 1) {
         double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
         double jw = tree_sum(g * u, P);
-        double fo = getf(fr0, fr1, r);
+        double fo = getf(F, r);
         double res = (jw + d.efc_R[r] * fo) + d.efc_b[r];
         double AR = row_sqnorm(d, r, nv) + d.efc_R[r];
         double fnew[1] = {fo - res * (1.0 / AR)};
@@ -2157,14 +2182,14 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
         if (delta != 0.0) {
           double s = u + g * delta;
           if (lane < nv) u = s;
-          setf(fr0, fr1, r, fnew[0], lane);
+          setf(F, r, fnew[0], lane);
         }
         r += 1;
       } else if (dim == 3) {
-        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, fr0, fr1, 0);
+        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 0);
         r += 3;
       } else {
-        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, fr0, fr1, 0);
+        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 0);
         r += 4;
       }
     }
@@ -2174,7 +2199,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, double& fr0, double& fr
 }
 
 // noslip post-pass (both solvers): friction dims only, unregularised, normals fixed
-DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
+DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   for (int ns = 0; ns < md.m.noslip_iterations && ne > 0; ns++) {
@@ -2183,7 +2208,7 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
     // the noslip cost drops the regulariser: count its removal at iteration 0
     if (ns == 0)
       for (int r = 0; r < ne; r++) {
-        double f = getf(fr0, fr1, r);
+        double f = getf(F, r);
         improvement = improvement + ((0.5 * f) * f) * d.efc_R[r];
       }
     for (int r = 0; r < ne;) {
@@ -2192,7 +2217,7 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
       if (t == MGS_EFC_FRICTION) {
         double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
         double res = tree_sum(g * u, P) + d.efc_b[r];
-        double fo = getf(fr0, fr1, r);
+        double fo = getf(F, r);
         double Arr = row_sqnorm(d, r, nv);
         double fnew[1] = {fo - res * (1.0 / Arr)};
         project_scalar(t, row_floss(md, d, r), fnew);
@@ -2201,14 +2226,14 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, 
         if (delta != 0.0) {
           double s = u + g * delta;
           if (lane < nv) u = s;
-          setf(fr0, fr1, r, fnew[0], lane);
+          setf(F, r, fnew[0], lane);
         }
         r += 1;
       } else if (t == MGS_EFC_CONTACT && dim == 3) {
-        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, fr0, fr1, 1);
+        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1);
         r += 3;
       } else if (t == MGS_EFC_CONTACT && dim == 4) {
-        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, fr0, fr1, 1);
+        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1);
         r += 4;
       } else {
         r += (t == MGS_EFC_CONTACT) ? dim : 1;
@@ -2356,12 +2381,16 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
   return 0.5 * c;
 }
 
-// sum over rows in the oracle's tree_rows order: leaf l = v[l] + v[l + 64]
-DEVI double tree_rows(double v0, double v1, int ne) {
+// sum over rows in the oracle's tree_rows order: leaf l = ((v[l] + v[l + 64]) +
+// v[l + 128]) + v[l + 192], rows past ne left out
+DEVI double tree_rows(const double (&v)[MGS_RPL], int ne) {
   int n = ne < WAVE ? ne : WAVE;
   if (n <= 0) return 0.0;
   int lane = lane_id();
-  double leaf = (lane + WAVE < ne) ? v0 + v1 : v0;
+  double leaf = v[0];
+#pragma unroll
+  for (int h = 1; h < MGS_RPL; h++)
+    if (lane + h * WAVE < ne) leaf = leaf + v[h];
   if (lane >= n) leaf = 0.0;
   return tree_sum(leaf, next_pow2(n));
 }
@@ -2384,9 +2413,10 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const dou
     d.efc_jar[r] = s - d.efc_aref[r];
   }
   wsync();
-  double cr[2] = {0.0, 0.0};
+  double cr[MGS_RPL];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
+  for (int h = 0; h < MGS_RPL; h++) {
+    cr[h] = 0.0;
     int r = lane + h * WAVE;
     if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
@@ -2409,7 +2439,7 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const dou
       }
     }
   }
-  double tot = gauss + tree_rows(cr[0], cr[1], ne);
+  double tot = gauss + tree_rows(cr, ne);
   wsync();
   return tot;
 }
@@ -2442,9 +2472,11 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
                   const double* mupR, const double* k1R) {
   int lane = lane_id();
   PCNT(36, 1);
-  double c1[2] = {0.0, 0.0}, c2[2] = {0.0, 0.0};
+  double c1[MGS_RPL], c2[MGS_RPL];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
+  for (int h = 0; h < MGS_RPL; h++) {
+    c1[h] = 0.0;
+    c2[h] = 0.0;
     int r = lane + h * WAVE;
     if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
@@ -2491,8 +2523,8 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
       c2[h] = s2;
     }
   }
-  *d1 = (A1 + alpha * A2) + tree_rows(c1[0], c1[1], ne);
-  *d2 = A2 + tree_rows(c2[0], c2[1], ne);
+  *d1 = (A1 + alpha * A2) + tree_rows(c1, ne);
+  *d2 = A2 + tree_rows(c2, ne);
 }
 
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -2715,19 +2747,24 @@ DEVI void ls_row(const LsRow& L, double alpha, double& s1o, double& s2o) {
 DEVI void ls_eval_fast(const Mdl& md, const Dat& d, int ne, const LsRow& L, double alpha, double A1, double A2,
                        double* d1, double* d2, const double* mupR, const double* k1R) {
   PCNT(36, 1);
-  double c1[2] = {0.0, 0.0}, c2[2] = {0.0, 0.0};
+  double c1[MGS_RPL], c2[MGS_RPL];
+#pragma unroll
+  for (int h = 0; h < MGS_RPL; h++) { c1[h] = 0.0; c2[h] = 0.0; }
   ls_row(L, alpha, c1[0], c2[0]);
-  if (ne > WAVE) {
-    LsRow L1;
-    ls_row_load(md, d, lane_id() + WAVE, ne, mupR[1], k1R[1], L1);
-    ls_row(L1, alpha, c1[1], c2[1]);
+#pragma unroll
+  for (int h = 1; h < MGS_RPL; h++) {
+    if (ne > h * WAVE) {
+      LsRow L1;
+      ls_row_load(md, d, lane_id() + h * WAVE, ne, mupR[h], k1R[h], L1);
+      ls_row(L1, alpha, c1[h], c2[h]);
+    }
   }
-  *d1 = (A1 + alpha * A2) + tree_rows(c1[0], c1[1], ne);
-  *d2 = A2 + tree_rows(c2[0], c2[1], ne);
+  *d1 = (A1 + alpha * A2) + tree_rows(c1, ne);
+  *d2 = A2 + tree_rows(c2, ne);
 }
 
 template <int NV>
-DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double& fr1, double& u) {
+DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   for (int r = lane; r < ne; r += WAVE) {
@@ -2736,9 +2773,11 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
     d.efc_Dr[r] = 1.0 / d.efc_R[r];
   }
   // per-block cone constants of this solve, rows lane and lane + 64
-  double mupR[2] = {0.0, 0.0}, k1R[2] = {0.0, 0.0};
+  double mupR[MGS_RPL], k1R[MGS_RPL];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
+  for (int h = 0; h < MGS_RPL; h++) {
+    mupR[h] = 0.0;
+    k1R[h] = 0.0;
     int r = lane + h * WAVE;
     if (r < ne && d.efc_type[r] == MGS_EFC_CONTACT && d.efc_dim[r] > 1) {
       double mup = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
@@ -2860,8 +2899,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, double& fr0, double&
   }
   if (lane == 0) d.ITERS += it;
   // forces to registers, u = G^T f
-  fr0 = (lane < ne) ? d.efc_f[lane] : 0.0;
-  fr1 = (lane + WAVE < ne) ? d.efc_f[lane + WAVE] : 0.0;
+  load_frc(F, d.efc_f, ne, lane);
   u = 0.0;
   if (lane < NV) {
     double s = 0.0;
@@ -2887,16 +2925,17 @@ DEVI void solve(const Mdl& md, Dat& d) {
   for (int k = 0; k < nv; k++) meaninertia = meaninertia + d.M[k * nv + k];
   meaninertia = meaninertia / (double)nv;
   double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
-  double fr0, fr1, u;
+  Frc F;
+  double u;
   if (md.m.solver == 0) {
     contact_blocks(md, d);
-    solve_pgs(md, d, scale, fr0, fr1, u);
+    solve_pgs(md, d, scale, F, u);
   } else {
-    solve_newton<NV>(md, d, scale, fr0, fr1, u);
+    solve_newton<NV>(md, d, scale, F, u);
     if (md.m.noslip_iterations > 0) contact_blocks(md, d);   // overwrites the cone Hessians
   }
   PT(16);
-  noslip(md, d, scale, fr0, fr1, u);
+  noslip(md, d, scale, F, u);
   PT(17);
   finalize_solution<NV>(md, d, u);
   PT(18);
@@ -3007,7 +3046,7 @@ DEVI int obj_contact(const Mdl& md, const Dat& d) {
 DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mpos, const double* mquat) {
   int lane = lane_id();
   for (int k = lane; k < md.m.nq; k += WAVE) d.qpos[k] = qpos_init[k];
-  for (int k = lane; k < md.m.nv; k += WAVE) { d.qvel[k] = 0.0; d.qacc_ws[k] = 0.0; }
+  for (int k = lane; k < md.m.nv; k += WAVE) { d.qvel[k] = DA(md, qvel0)[k]; d.qacc_ws[k] = DA(md, qacc_ws0)[k]; }
   if (lane == 0) {
     for (int u = 0; u < (md.m.nu > 0 ? md.m.nu : 1); u++) d.ctrl[u] = 0.0;
     for (int k = 0; k < 3; k++) d.mocap_pos[k] = mpos ? mpos[k] : 0.0;

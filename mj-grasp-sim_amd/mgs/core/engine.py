@@ -14,21 +14,25 @@ import numpy as np
 from mgs.core import abi
 from mgs.core.abi import ptr
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libmgs_gpu.so")
-_lib = None
+LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmgs_gpu.so")
+# same C-ABI, built with 4 constraint rows per lane and G in HBM (MGS_WIDE) for
+# the clutter piles' dof counts and row counts
+LIB_WIDE_PATH = os.path.join(LIB_DIR, "libmgs_gpu_wide.so")
+_libs = {}
 
 
 class EngineError(RuntimeError):
     pass
 
 
-def load_library():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.isfile(LIB_PATH):
-        raise EngineError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-    L = ctypes.CDLL(LIB_PATH)
+def load_library(wide: bool = False):
+    path = LIB_WIDE_PATH if wide else LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.isfile(path):
+        raise EngineError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
     P = ctypes.POINTER
     c_i, c_d, c_u8, vp = ctypes.c_int32, ctypes.c_double, ctypes.c_uint8, ctypes.c_void_p
     L.mgs_abi_version.restype = ctypes.c_int
@@ -51,10 +55,25 @@ def load_library():
     L.mgs_lds_bytes.argtypes = [vp]
     L.mgs_device_count.restype = ctypes.c_int
     L.mgs_model_lds_bytes.argtypes = [P(abi.ModelDesc), P(ctypes.c_int64)]
+    L.mgs_max_rows.restype = ctypes.c_int
+    L.mgs_supports_nv.argtypes = [ctypes.c_int]
+    L.mgs_supports_nv.restype = ctypes.c_int
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
-        raise EngineError("libmgs_gpu.so ABI version mismatch with include/mgs_gpu.h")
-    _lib = L
+        raise EngineError(f"{os.path.basename(path)} ABI version mismatch with include/mgs_gpu.h")
+    _libs[path] = L
     return L
+
+
+def library_for(nv: int, nefc_max: int):
+    """the library build whose kernels hold this model: the main one when it has
+    a kernel for nv and enough constraint rows, else the wide one."""
+    L = load_library()
+    if L.mgs_supports_nv(nv) and nefc_max <= L.mgs_max_rows():
+        return L
+    W = load_library(wide=True)
+    if W.mgs_supports_nv(nv) and nefc_max <= W.mgs_max_rows():
+        return W
+    raise EngineError(f"no kernel instantiated for nv={nv} with {nefc_max} constraint rows (MGS_NV_LIST)")
 
 
 LDS_PER_CU = 160 * 1024
@@ -62,8 +81,8 @@ LDS_PER_CU = 160 * 1024
 
 def lds_bytes_for(cm, ncon_max, nefc_max=None):
     """Per-candidate LDS bytes of the kernels for this model and capacity (host only)."""
-    L = load_library()
     fields, _, _ = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
+    L = library_for(cm.nv, int(fields["nefc_max"]))
     desc = abi.make_desc(fields)
     out = ctypes.c_int64()
     _check(L.mgs_model_lds_bytes(ctypes.byref(desc), ctypes.byref(out)), "mgs_model_lds_bytes")
@@ -89,9 +108,9 @@ def auto_capacity(cm, ncon_max=20):
     return ncon_max, best
 
 
-def _check(rc, what):
+def _check(rc, what, lib=None):
     if rc != 0:
-        msg = load_library().mgs_last_error().decode(errors="replace")
+        msg = (lib or load_library()).mgs_last_error().decode(errors="replace")
         raise EngineError(f"{what} failed ({rc}): {msg}")
 
 
@@ -99,19 +118,22 @@ class Engine:
     """One compiled model resident on one GPU plus a reusable batch."""
 
     def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None):
-        self.lib = load_library()
+        fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
+        self.lib = library_for(cm.nv, int(fields["nefc_max"]))
         if self.lib.mgs_device_count() <= device:
             raise EngineError("no HIP device visible for the MI355X engine")
-        fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
         self.desc = abi.make_desc(fields)
         self.cm = cm
         self.device = device
         self._model = ctypes.c_void_p()
-        _check(self.lib.mgs_model_create(ctypes.byref(self.desc), ptr(self._ib, ctypes.c_int32),
+        self._ck(self.lib.mgs_model_create(ctypes.byref(self.desc), ptr(self._ib, ctypes.c_int32),
                                          ptr(self._db, ctypes.c_double), device, ctypes.byref(self._model)),
                "mgs_model_create")
         self._batch = ctypes.c_void_p()
         self._cap = 0
+
+    def _ck(self, rc, what):
+        _check(rc, what, self.lib)
 
     def close(self):
         if self._batch:
@@ -133,7 +155,7 @@ class Engine:
                 self.lib.mgs_batch_close(self._batch)
             cap = max(n, 256)
             self._batch = ctypes.c_void_p()
-            _check(self.lib.mgs_batch_open(self._model, cap, ctypes.byref(self._batch)), "mgs_batch_open")
+            self._ck(self.lib.mgs_batch_open(self._model, cap, ctypes.byref(self._batch)), "mgs_batch_open")
             self._cap = cap
         return self._batch
 
@@ -146,7 +168,7 @@ class Engine:
         q = np.ascontiguousarray(qpos, np.float64)
         mp = np.ascontiguousarray(mocap_pos, np.float64)
         mq = np.ascontiguousarray(mocap_quat, np.float64)
-        _check(self.lib.mgs_collision_free(self.batch(n), n, ptr(q, ctypes.c_double), ptr(mp, ctypes.c_double),
+        self._ck(self.lib.mgs_collision_free(self.batch(n), n, ptr(q, ctypes.c_double), ptr(mp, ctypes.c_double),
                                            ptr(mq, ctypes.c_double), pr, ptr(out, ctypes.c_uint8)),
                "mgs_collision_free")
         return out.astype(bool)
@@ -166,7 +188,7 @@ class Engine:
         mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
         ps = np.ascontiguousarray(plan.phase_start, np.float64)
         pt = np.ascontiguousarray(plan.phase_target, np.float64)
-        _check(self.lib.mgs_rollout(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
+        self._ck(self.lib.mgs_rollout(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
                                     ptr(mq, ctypes.c_double), ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double),
                                     ctypes.byref(out)), "mgs_rollout")
         return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats,
@@ -175,14 +197,14 @@ class Engine:
     def collision_free_device(self, n, d_qpos, d_mpos, d_mquat, d_out, predicate="any", stream=None):
         """Asynchronous launch on device pointers (ints) with inputs resident in HBM."""
         pr = abi.MGS["MGS_PRED_ANY_CONTACT"] if predicate == "any" else abi.MGS["MGS_PRED_PARTITION"]
-        _check(self.lib.mgs_collision_free_device(self.batch(1), n, d_qpos, d_mpos, d_mquat, pr, d_out, stream),
+        self._ck(self.lib.mgs_collision_free_device(self.batch(1), n, d_qpos, d_mpos, d_mquat, pr, d_out, stream),
                "mgs_collision_free_device")
 
     def rollout_device(self, sched, n, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats,
                        d_active=None, stream=None):
         """Asynchronous launch on device pointers (ints) with inputs resident in HBM;
         d_active (optional) masks out collision-mask rejects."""
-        _check(self.lib.mgs_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps, d_pt,
+        self._ck(self.lib.mgs_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps, d_pt,
                                            d_active, d_label, d_fail, d_objq, d_stats, stream),
                "mgs_rollout_device")
 

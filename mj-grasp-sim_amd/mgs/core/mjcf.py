@@ -1077,6 +1077,12 @@ class CompiledModel:
         for n in ["dof_armature", "dof_damping", "dof_frictionloss", "dof_solref", "dof_solimp",
                   "qpos0", "qpos_spring"]:
             put_d(n, getattr(self, n))
+        # initial velocity state shared by every candidate (mj_resetData: zeros;
+        # ClutterTableEnv: the scene's env_state, clutter_table.py:290-291)
+        put_d("qvel0", getattr(self, "qvel0", None) if getattr(self, "qvel0", None) is not None
+              else np.zeros(self.nv))
+        put_d("qacc_ws0", getattr(self, "qacc_ws0", None) if getattr(self, "qacc_ws0", None) is not None
+              else np.zeros(self.nv))
         for n in ["geom_bodyid", "geom_hullid", "geom_side"]:
             put_i(n, getattr(self, n))
         for n in ["geom_pos", "geom_quat", "geom_aabb", "geom_radius"]:

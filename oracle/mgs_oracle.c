@@ -1751,12 +1751,19 @@ static void finalize_solution(const Mdl* md, Dat* d) {
  * isotropic second-order cone |y_t| <= mu' y_n, mu' = mu0/sqrt(impratio)
  * (MuJoCo's "mu = friction[0]/sqrt(impratio)").  Reductions over dofs use
  * tree_dot (lanes over dofs), reductions over rows use tree_rows (lanes over
- * rows, rows >= 64 pre-added to row - 64). */
+ * rows, rows >= 64 pre-added to row mod 64 in ascending order). */
 static double tree_rows(const double* v, int ne) {
   double leaf[64], one[64];
   int n = ne < 64 ? ne : 64;
   if (n <= 0) return 0.0;
-  for (int k = 0; k < n; k++) { leaf[k] = (k + 64 < ne) ? v[k] + v[k + 64] : v[k]; one[k] = 1.0; }
+  for (int k = 0; k < n; k++) {
+    /* lane k holds rows k, k + 64, k + 128, k + 192 (kernel Frc): summed in that order */
+    double s = v[k];
+    for (int h = 1; h < 4; h++)
+      if (k + 64 * h < ne) s = s + v[k + 64 * h];
+    leaf[k] = s;
+    one[k] = 1.0;
+  }
   /* tree_dot multiplies by 1.0: exact */
   return tree_dot(leaf, one, n);
 }
@@ -2155,8 +2162,8 @@ static int obj_contact(const Mdl* md, const Dat* d) {
 static void reset(const Mdl* md, Dat* d, const double* qpos_init, const double* mpos, const double* mquat) {
   const mgs_model_desc* m = md->m;
   memcpy(d->qpos, qpos_init, sizeof(double) * m->nq);
-  memset(d->qvel, 0, sizeof(double) * m->nv);
-  memset(d->qacc_ws, 0, sizeof(double) * m->nv);
+  memcpy(d->qvel, DA(md, qvel0), sizeof(double) * m->nv);
+  memcpy(d->qacc_ws, DA(md, qacc_ws0), sizeof(double) * m->nv);
   memset(d->ctrl, 0, sizeof(double) * (m->nu > 0 ? m->nu : 1));
   for (int k = 0; k < 3; k++) d->mocap_pos[k] = mpos ? mpos[k] : 0.0;
   for (int k = 0; k < 4; k++) d->mocap_quat[k] = mquat[k];
