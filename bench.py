@@ -133,7 +133,8 @@ def main():
     qpos, mpos, mquat, _ = env.initial_state(poses, J)
     plan = env.rollout_plan(poses, J, nstep_lift=h["nstep_lift"], shake_steps=h["shake_steps"],
                             close_steps=h["close_steps"], lift_check_every=h["lift_check_every"])
-    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                                  check_offset=getattr(plan, "check_offset", None))
     horizon = plan.horizon
     eng = env.engine
     dev = torch.device("cuda", local)

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 5
+#define MGS_ABI_VERSION 6
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -79,7 +79,10 @@ extern "C" {
 
 /* predicate for the collision pre-filter */
 #define MGS_PRED_ANY_CONTACT 0     /* data.ncon != 0            (gravityless :306-307) */
-#define MGS_PRED_PARTITION 1       /* gripper geom vs geom past the partition (clutter) */
+#define MGS_PRED_PARTITION 1       /* gripper geom vs geom past the partition (gravityless
+                                      check_contact_with_object :309-320; clutter check_gripper_contact) */
+#define MGS_PRED_PARTITION_INCL 2  /* gripper geom vs the partition geom or past it
+                                      (clutter check_gripper_collision, clutter_table.py:237-252) */
 
 typedef struct mgs_model_desc {
   /* sizes */
@@ -218,8 +221,9 @@ typedef struct mgs_model_desc {
  * During phase p, step t (0-based) the mocap position is
  *     start + (target - start) * (t / nsteps)          (per component, fp64)
  * with per-candidate start/target given to mgs_rollout; ctrl is held at
- * ctrl[p*32 .. p*32+nu).  After step t, if check_every > 0 and t > 0 and
- * t % check_every == 0, the gripper-object contact predicate is evaluated on
+ * ctrl[p*32 .. p*32+nu).  After step t, if check_every > 0 and t + off > 0 and
+ * (t + off) % check_every == 0 (off = check_offset[p]), the gripper-object
+ * contact predicate is evaluated on
  * the contacts of that step; if check_at_end, it is evaluated after the last
  * step.  The first failed check ends the candidate with label 0.            */
 #define MGS_MAX_PHASES 8
@@ -229,6 +233,8 @@ typedef struct mgs_schedule {
   int32_t nsteps[MGS_MAX_PHASES];
   int32_t check_every[MGS_MAX_PHASES];
   int32_t check_at_end[MGS_MAX_PHASES];
+  int32_t check_offset[MGS_MAX_PHASES];  /* check after step t if (t + off) > 0 and (t + off) % check_every == 0:
+                                            0 = gravityless lift (:216), 1 = clutter lift ((t+1) % 100, :313) */
   double ctrl[MGS_MAX_PHASES * 32];
 } mgs_schedule;
 

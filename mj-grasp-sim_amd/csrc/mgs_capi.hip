@@ -293,7 +293,7 @@ int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, co
   if (!b || n < 0) return fail(MGS_EINVAL, "mgs_collision_free_device: bad argument%s");
   if (n == 0) return MGS_OK;
   if (!d_qpos_init || !d_mocap_pos || !d_mocap_quat || !d_out_free) return fail(MGS_EINVAL, "null argument%s");
-  if (predicate != MGS_PRED_ANY_CONTACT && predicate != MGS_PRED_PARTITION)
+  if (predicate != MGS_PRED_ANY_CONTACT && predicate != MGS_PRED_PARTITION && predicate != MGS_PRED_PARTITION_INCL)
     return fail(MGS_EINVAL, "unknown contact predicate%s");
   HIPCHK(hipSetDevice(b->m->device));
   hipStream_t st = (hipStream_t)stream;

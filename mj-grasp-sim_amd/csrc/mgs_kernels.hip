@@ -3043,6 +3043,17 @@ DEVI int obj_contact(const Mdl& md, const Dat& d) {
   return 0;
 }
 
+// clutter collision predicate: a gripper geom against the table or any geom past it
+DEVI int obj_contact_incl(const Mdl& md, const Dat& d) {
+  const int32_t* side = IA(md, geom_side);
+  int ncon = uni(d.NCON);
+  for (int c = 0; c < ncon; c++) {
+    int s1 = side[d.con_g1[c]], s2 = side[d.con_g2[c]];
+    if ((s1 < 0 && s2 >= 0) || (s1 >= 0 && s2 < 0)) return 1;
+  }
+  return 0;
+}
+
 DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mpos, const double* mquat) {
   int lane = lane_id();
   for (int k = lane; k < md.m.nq; k += WAVE) d.qpos[k] = qpos_init[k];
@@ -3076,7 +3087,8 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   reset(md, d, qpos_init + (size_t)i * md.m.nq, mocap_pos + 3 * i, mocap_quat + 4 * i);
   forward<NV>(md, d, 0);
   if (lane_id() == 0) {
-    int hit = (predicate == MGS_PRED_ANY_CONTACT) ? (d.NCON != 0) : obj_contact(md, d);
+    int hit = (predicate == MGS_PRED_ANY_CONTACT) ? (d.NCON != 0)
+              : (predicate == MGS_PRED_PARTITION_INCL) ? obj_contact_incl(md, d) : obj_contact(md, d);
     out[i] = (uint8_t)(hit ? 0 : 1);
   }
 }
@@ -3158,7 +3170,8 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       sumcon += uni(d.NCON);
       sumefc += uni(d.NEFC);
       int ce = sc.check_every[p];
-      if (ce > 0 && t > 0 && (t % ce) == 0 && !obj_contact(md, d)) { ok = 0; fstep = gstep; }
+      int tc = t + sc.check_offset[p];
+      if (ce > 0 && tc > 0 && (tc % ce) == 0 && !obj_contact(md, d)) { ok = 0; fstep = gstep; }
       gstep++;
     }
     if (ok && sc.check_at_end[p] && !obj_contact(md, d)) { ok = 0; fstep = gstep - 1; }

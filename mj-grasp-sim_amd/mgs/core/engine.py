@@ -164,7 +164,7 @@ class Engine:
         out = np.zeros(n, np.uint8)
         if n == 0:
             return out.astype(bool)
-        pr = abi.MGS["MGS_PRED_ANY_CONTACT"] if predicate == "any" else abi.MGS["MGS_PRED_PARTITION"]
+        pr = abi.predicate_code(predicate)
         q = np.ascontiguousarray(qpos, np.float64)
         mp = np.ascontiguousarray(mocap_pos, np.float64)
         mq = np.ascontiguousarray(mocap_quat, np.float64)
@@ -175,7 +175,8 @@ class Engine:
 
     def rollout(self, plan):
         n = len(plan.qpos_init)
-        sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+        sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                                  check_offset=getattr(plan, "check_offset", None))
         label = np.zeros(n, np.uint8)
         fail = np.zeros(n, np.int32)
         objq = np.zeros((n, 7), np.float64)
@@ -196,7 +197,7 @@ class Engine:
 
     def collision_free_device(self, n, d_qpos, d_mpos, d_mquat, d_out, predicate="any", stream=None):
         """Asynchronous launch on device pointers (ints) with inputs resident in HBM."""
-        pr = abi.MGS["MGS_PRED_ANY_CONTACT"] if predicate == "any" else abi.MGS["MGS_PRED_PARTITION"]
+        pr = abi.predicate_code(predicate)
         self._ck(self.lib.mgs_collision_free_device(self.batch(1), n, d_qpos, d_mpos, d_mquat, pr, d_out, stream),
                "mgs_collision_free_device")
 

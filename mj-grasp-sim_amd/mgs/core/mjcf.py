@@ -650,7 +650,7 @@ class Compiler:
                 allgeoms.append((bi, g))
         partition = None
         for gid, (bi, g) in enumerate(allgeoms):
-            if g.get("name") == "geom:ground" or g.get("name") == "table":
+            if g.get("name") in ("geom:ground", "geom:table", "table"):
                 partition = gid
         cgeoms = []
         hulls = []

@@ -79,6 +79,7 @@ class RolloutPlan:
     phase_start: np.ndarray    # (n, nphase, 3)
     phase_target: np.ndarray   # (n, nphase, 3)
     obj_qposadr: int
+    check_offset: Optional[List[int]] = None    # per phase, see mgs_schedule (0 when None)
 
     @property
     def horizon(self):
@@ -87,7 +88,7 @@ class RolloutPlan:
     def subset(self, idx) -> "RolloutPlan":
         return RolloutPlan(self.nsteps, self.check_every, self.check_at_end, self.ctrl,
                            self.qpos_init[idx], self.mocap_quat[idx], self.phase_start[idx],
-                           self.phase_target[idx], self.obj_qposadr)
+                           self.phase_target[idx], self.obj_qposadr, self.check_offset)
 
 
 class _SimView:

@@ -2159,6 +2159,16 @@ static int obj_contact(const Mdl* md, const Dat* d) {
   return 0;
 }
 
+/* clutter_table.py:237-252: a gripper geom against the table or past it */
+static int obj_contact_incl(const Mdl* md, const Dat* d) {
+  const int32_t* side = IA(md, geom_side);
+  for (int c = 0; c < d->ncon; c++) {
+    int s1 = side[d->con_g1[c]], s2 = side[d->con_g2[c]];
+    if ((s1 < 0 && s2 >= 0) || (s1 >= 0 && s2 < 0)) return 1;
+  }
+  return 0;
+}
+
 static void reset(const Mdl* md, Dat* d, const double* qpos_init, const double* mpos, const double* mquat) {
   const mgs_model_desc* m = md->m;
   memcpy(d->qpos, qpos_init, sizeof(double) * m->nq);
@@ -2188,7 +2198,8 @@ int oracle_collision_free(const mgs_model_desc* desc, const int32_t* I, const do
     for (int i = 0; i < n; i++) {
       reset(&md, d, qpos_init + (size_t)i * desc->nq, mocap_pos + 3 * i, mocap_quat + 4 * i);
       forward(&md, d, 0);
-      int hit = (predicate == MGS_PRED_ANY_CONTACT) ? (d->ncon != 0) : obj_contact(&md, d);
+      int hit = (predicate == MGS_PRED_ANY_CONTACT) ? (d->ncon != 0)
+                : (predicate == MGS_PRED_PARTITION_INCL) ? obj_contact_incl(&md, d) : obj_contact(&md, d);
       out[i] = (uint8_t)(hit ? 0 : 1);
     }
     dat_free(d);
@@ -2224,7 +2235,8 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
           sumcon += d->ncon;
           sumefc += d->nefc;
           int ce = sc->check_every[p];
-          if (ce > 0 && t > 0 && (t % ce) == 0 && !obj_contact(&md, d)) { ok = 0; fstep = gstep; }
+          int tc = t + sc->check_offset[p];
+          if (ce > 0 && tc > 0 && (tc % ce) == 0 && !obj_contact(&md, d)) { ok = 0; fstep = gstep; }
           gstep++;
         }
         if (ok && sc->check_at_end[p] && !obj_contact(&md, d)) { ok = 0; fstep = gstep - 1; }
@@ -2240,6 +2252,32 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
     }
     dat_free(d);
   }
+  return 0;
+}
+
+/* Free simulation (scene settling, gen_clutter restatement): nsteps with a
+ * fixed mocap and ctrl from qpos_init and the model's initial velocity state;
+ * after every step qvel is clipped to [-vclip, vclip] when vclip > 0
+ * (clutter_table.py:215-221).  Returns the final qpos, qvel, qacc_warmstart. */
+int oracle_simulate(const mgs_model_desc* desc, const int32_t* I, const double* D, const double* qpos_init,
+                    const double* mocap_pos, const double* mocap_quat, const double* ctrl, int nsteps,
+                    double vclip, double* qpos_out, double* qvel_out, double* qacc_ws_out) {
+  Mdl md = {desc, I, D};
+  Dat* d = dat_alloc(&md);
+  reset(&md, d, qpos_init, mocap_pos, mocap_quat);
+  for (int u = 0; u < desc->nu; u++) d->ctrl[u] = ctrl[u];
+  for (int t = 0; t < nsteps; t++) {
+    step(&md, d);
+    if (vclip > 0.0)
+      for (int k = 0; k < desc->nv; k++) {
+        if (d->qvel[k] > vclip) d->qvel[k] = vclip;
+        if (d->qvel[k] < -vclip) d->qvel[k] = -vclip;
+      }
+  }
+  memcpy(qpos_out, d->qpos, sizeof(double) * desc->nq);
+  memcpy(qvel_out, d->qvel, sizeof(double) * desc->nv);
+  memcpy(qacc_ws_out, d->qacc_ws, sizeof(double) * desc->nv);
+  dat_free(d);
   return 0;
 }
 

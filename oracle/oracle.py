@@ -60,7 +60,7 @@ class OracleModel:
     def collision_free(self, qpos, mocap_pos, mocap_quat, predicate="any", nthreads=1):
         n = len(qpos)
         out = np.zeros(n, np.uint8)
-        pr = abi.MGS["MGS_PRED_ANY_CONTACT"] if predicate == "any" else abi.MGS["MGS_PRED_PARTITION"]
+        pr = abi.predicate_code(predicate)
         q = np.ascontiguousarray(qpos, np.float64)
         mp = np.ascontiguousarray(mocap_pos, np.float64)
         mq = np.ascontiguousarray(mocap_quat, np.float64)
@@ -70,7 +70,8 @@ class OracleModel:
 
     def rollout(self, plan, nthreads=1):
         n = len(plan.qpos_init)
-        sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+        sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                                  check_offset=getattr(plan, "check_offset", None))
         label = np.zeros(n, np.uint8)
         fail = np.zeros(n, np.int32)
         objq = np.zeros((n, 7), np.float64)
@@ -94,6 +95,18 @@ class OracleModel:
         lib().oracle_trace(*self._args(), *[ptr(a, ctypes.c_double) for a in args], nsteps,
                            ptr(tr, ctypes.c_double), ptr(nc, ctypes.c_int32), ptr(qv, ctypes.c_double))
         return tr, nc, qv
+
+    def simulate(self, qpos, mocap_pos, mocap_quat, ctrl, nsteps, vclip=0.0):
+        """free simulation from qpos and the model's qvel0 / qacc_ws0; returns the
+        final (qpos, qvel, qacc_warmstart)."""
+        q = np.zeros(self.cm.nq)
+        v = np.zeros(self.cm.nv)
+        w = np.zeros(self.cm.nv)
+        args = [np.ascontiguousarray(a, np.float64) for a in (qpos, mocap_pos, mocap_quat, ctrl)]
+        lib().oracle_simulate(*self._args(), *[ptr(a, ctypes.c_double) for a in args], int(nsteps),
+                              ctypes.c_double(vclip), ptr(q, ctypes.c_double), ptr(v, ctypes.c_double),
+                              ptr(w, ctypes.c_double))
+        return q, v, w
 
     def contacts(self, qpos, mocap_pos, mocap_quat, maxc=64):
         pos = np.zeros((maxc, 3)); fr = np.zeros((maxc, 9)); dist = np.zeros(maxc); g = np.zeros((maxc, 2), np.int32)

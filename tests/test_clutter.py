@@ -1,0 +1,121 @@
+"""ClutterTableEnv: grasp_collision_mask and
+grasp_stable_mask over a settled 5-object pile (tests/golden/clutter_scene.npz,
+made by tests/golden/make_clutter_scene.py on the oracle).
+
+CPU: the scene-dict / integration-state round trip, the reference's host rules
+(in-bounds box :344-354, the inclusive collision predicate vs the strict lift
+predicate :237-270, the (t + 1) % 100 lift cadence :313), and that the oracle's
+lifted grasps hold objects.  GPU: both methods bit-exact against the oracle
+through the wide library (4 constraint rows per lane, G rows in HBM)."""
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SCENE = os.path.join(HERE, "golden", "clutter_scene.npz")
+
+
+@pytest.fixture(scope="module")
+def cenv():
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_clutter_scene import make_env
+    z = np.load(SCENE)
+    env = make_env()
+    env.set_state(z["state"])
+    return env
+
+
+@pytest.fixture(scope="module")
+def ccand(cenv):
+    """antipodal Robotiq grasps of every object in its own frame, posed by the
+    settled object pose (gen_scene.py:59-66: o2w @ pose)."""
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    H, J = [], []
+    for k, o in enumerate(cenv.objects):
+        h, j, _ = robotiq_candidates(o, 48, seed=k)
+        o2w = cenv.get_obj_pose(o.name)
+        H.append((o2w @ SE3Pose.from_mat(h)).to_mat())
+        J.append(j)
+    return SE3Pose.from_mat(np.concatenate(H).astype(np.float32)), np.concatenate(J)
+
+
+def test_state_layout_and_dict_roundtrip(cenv):
+    from mgs.env.clutter_table import ClutterTableEnv
+    cm = cenv.model
+    # reference layout: gripper (22 -> 15 qpos) + camera free joint + 5 objects
+    assert cenv.ref_nq == cm.nq + 7 and cenv.ref_nv == cm.nv + 6
+    assert cm.nv == 14 + 6 * 5
+    s = cenv.get_state()
+    assert s.shape == (cenv.state_size(),)
+    d = cenv.to_dict()
+    e2 = ClutterTableEnv.from_dict(d)
+    assert np.array_equal(e2.get_state(), s)
+    assert cm.geom_names.index("geom:table") < cm.geom_names.index("geom:camera")
+
+
+def test_collision_mask_rules(cenv, ccand):
+    from oracle import oracle as O
+    poses, J = ccand
+    p = poses.pos
+    inb = (np.abs(p[:, 0]) < 0.25) & (np.abs(p[:, 1]) < 0.25) & (p[:, 2] > 0) & (p[:, 2] < 1)
+    q, mp, mq = cenv._initial_qpos(poses, J, cenv.get_state())
+    om = O.OracleModel(cenv.model, ncon_max=cenv.ncon_max, nefc_max=256)
+    incl = om.collision_free(q, mp, mq, predicate="partition_incl", nthreads=8)
+    strict = om.collision_free(q, mp, mq, predicate="partition", nthreads=8)
+    anyc = om.collision_free(q, mp, mq, predicate="any", nthreads=8)
+    # gripper-table contacts count as collisions for the mask, not for the lift check
+    assert np.all(incl <= strict) and np.all(anyc <= incl)
+    assert 0 < (incl & inb).sum() < len(inb)
+
+
+def test_stable_plan_cadence(cenv, ccand):
+    poses, J = ccand
+    plan = cenv.stable_plan(poses[:2], J[:2], cenv.get_state())
+    assert plan.nsteps == [3000, 3000] and plan.check_every == [0, 100] and plan.check_offset == [0, 1]
+    assert np.allclose(plan.phase_target[:, 1, 2] - plan.phase_start[:, 1, 2], 0.3)
+    assert plan.check_at_end == [0, 0]
+
+
+def test_oracle_stable_grasps_hold(cenv, ccand):
+    from oracle import oracle as O
+    poses, J = ccand
+    st = cenv.get_state()
+    q, mp, mq = cenv._initial_qpos(poses, J, st)
+    om = O.OracleModel(cenv.model_for(st), ncon_max=cenv.ncon_max, nefc_max=256)
+    free = om.collision_free(q, mp, mq, predicate="partition_incl", nthreads=8)
+    idx = np.nonzero(free)[0][:12]
+    plan = cenv.stable_plan(poses[idx], J[idx], st, nstep_lift=600, close_steps=600)
+    r = om.rollout(plan, nthreads=8)
+    assert len(idx) == 12 and r["label"].sum() >= 4
+    assert np.all(np.isin(r["fail_step"][~r["label"]], 600 + np.arange(99, 600, 100)))
+
+
+@pytest.mark.gpu
+def test_clutter_gpu_parity(cenv, ccand):
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+    from oracle import oracle as O
+    poses, J = ccand
+    st = cenv.get_state()
+    eng = cenv.engine_for_state(st)
+    om = O.OracleModel(cenv.model_for(st), ncon_max=cenv.ncon_max, nefc_max=eng.desc.nefc_max)
+    mask = cenv.grasp_collision_mask(poses, J)
+    p = poses.pos
+    inb = (np.abs(p[:, 0]) < 0.25) & (np.abs(p[:, 1]) < 0.25) & (p[:, 2] > 0) & (p[:, 2] < 1)
+    q, mp, mq = cenv._initial_qpos(poses, J, st)
+    ref = om.collision_free(q, mp, mq, predicate="partition_incl", nthreads=8) & inb
+    assert np.array_equal(mask, ref)
+    idx = np.nonzero(mask)[0][:24]
+    plan = cenv.stable_plan(poses[idx], J[idx], st, nstep_lift=600, close_steps=600)
+    rg, ro = eng.rollout(plan), om.rollout(plan, nthreads=8)
+    for k in ("label", "fail_step", "stats"):
+        assert np.array_equal(rg[k], ro[k]), k
+    lab = cenv.grasp_stable_mask(poses[idx], J[idx], st, nstep_lift=600, close_steps=600, enough_stable=3)
+    assert lab.sum() == min(3, int(ro["label"].sum()))

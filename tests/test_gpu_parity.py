@@ -156,7 +156,8 @@ def test_device_entry_with_active_mask(env, eng, candidates, oracle_model):
     poses, J = candidates
     q, mp, mq, _ = env.initial_state(poses, J)
     plan = plan_for(env, poses, J)
-    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                                  check_offset=getattr(plan, "check_offset", None))
     n = len(q)
     dev = torch.device("cuda", 0)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
