@@ -153,10 +153,12 @@ def main():
     sp = stream.cuda_stream
     # contact-capacity escalation (GravitylessObjectGrasping.rollout): candidates
     # whose contacts exceeded ncon_max at some step are re-run with a wider engine,
-    # selected on the device (no host round trip) and merged into the outputs
+    # selected on the device and merged into the outputs; a one-byte host check
+    # skips the launch when nothing overflowed (the usual case)
     wide = env.engine_for(2 * env.ncon_max) if args.escalate else None
     w_label, w_fail, w_objq, w_stats = (torch.zeros_like(t) for t in (d_label, d_fail, d_objq, d_stats))
     d_ovf = torch.zeros(N, dtype=torch.uint8, device=dev)
+    n_wide = [0]
 
     def step():
         eng.collision_free_device(N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(), d_free.data_ptr(),
@@ -164,8 +166,12 @@ def main():
         eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
                            d_label.data_ptr(), d_fail.data_ptr(), d_objq.data_ptr(), d_stats.data_ptr(),
                            d_active=d_free.data_ptr(), stream=sp)
+        n_wide[0] = 0
         if wide is not None:
             torch.ne(d_stats[:, 2], 0, out=d_ovf.view(torch.bool))
+            if not bool(d_ovf.any()):
+                return
+            n_wide[0] = 1
             wide.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
                                 w_label.data_ptr(), w_fail.data_ptr(), w_objq.data_ptr(), w_stats.data_ptr(),
                                 d_active=d_ovf.data_ptr(), stream=sp)
@@ -188,7 +194,7 @@ def main():
         # per-launch kernel durations (HIP events recorded on this stream by the library)
         roll_ms.append(eng.last_kernel_ms())
         coll_ms.append(eng.last_collision_ms())
-        if wide is not None:
+        if n_wide[0]:
             wide_ms.append(wide.last_kernel_ms())
     torch.cuda.synchronize(dev)
     if world > 1:

@@ -1,0 +1,58 @@
+"""Summarise a tools/prof_r01.sh output directory into profiles/:
+
+  profiles/r01_rocprof_kernel_stats.csv   kernel-trace --stats of the bench command
+  profiles/r01_pmc_{fetch,write,sq}.csv   the rollout kernel's counter rows
+  profiles/pmc_rollout.json               HBM bytes per launch (FETCH_SIZE x 2, the
+                                          gfx950 half-count correction of
+                                          MI355X_MICROARCH.md, + WRITE_SIZE; KiB) and
+                                          per executed candidate-step, SQ totals
+  profiles/r01_bench.json                 the bench line of the same run
+
+    python tools/pmc_summary.py gpurun_out/r01d
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def rows(path, kernel="mgs_rollout_kernel"):
+    with open(path) as f:
+        return [r for r in csv.DictReader(f) if kernel in r["Kernel_Name"]]
+
+
+def main(d):
+    shutil.copy(os.path.join(d, "trace", "bench_kernel_stats.csv"), os.path.join(PROF, "r01_rocprof_kernel_stats.csv"))
+    shutil.copy(os.path.join(d, "bench.json"), os.path.join(PROF, "r01_bench.json"))
+    out = {"source": "rocprofv3 --kernel-trace --pmc <counters> (separate passes) on `python3 bench.py --steps 1 "
+                     "--warmup 0 --cpu-budget 0` (tools/prof_r01.sh)",
+           "kernel": "mgs_rollout_kernel<20>"}
+    sums = {}
+    for name in ("fetch", "write", "sq"):
+        p = os.path.join(d, f"pmc_{name}", "pmc_counter_collection.csv")
+        rr = rows(p)
+        with open(os.path.join(PROF, f"r01_pmc_{name}.csv"), "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(rr[0].keys()))
+            w.writeheader()
+            w.writerows(rr)
+        for r in rr:
+            sums[r["Counter_Name"]] = sums.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    with open(os.path.join(d, "pmc_fetch.json")) as f:
+        steps = json.loads(f.read().strip().splitlines()[-1])["detail"]["executed_candidate_steps"]
+    hbm = (2.0 * sums["FETCH_SIZE"] + sums["WRITE_SIZE"]) * 1024.0
+    out.update(fetch_size_kb_raw=sums["FETCH_SIZE"], write_size_kb_raw=sums["WRITE_SIZE"],
+               hbm_bytes_per_launch_corrected=hbm,
+               correction="FETCH_SIZE x 2 (gfx950 half-count, MI355X_MICROARCH.md), WRITE_SIZE as reported; both KiB",
+               executed_candidate_steps=steps, hbm_bytes_per_candidate_step=hbm / steps,
+               sq={k: v for k, v in sums.items() if k.startswith("SQ_")})
+    with open(os.path.join(PROF, "pmc_rollout.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
