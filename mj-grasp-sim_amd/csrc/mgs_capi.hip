@@ -128,6 +128,13 @@ static bool nv_supported(int nv) {
   }
 }
 
+// static LDS of the kernels (the diagnostic stage timers of the MGS_PROFILE build)
+#ifdef MGS_PROFILE
+#define MGS_STATIC_LDS (65 * 8)
+#else
+#define MGS_STATIC_LDS 0
+#endif
+
 static hipError_t set_lds_limit(int nv, int bytes) {
   switch (nv) {
 #define MGS_CASE(NV_)                                                                                      \
@@ -197,7 +204,7 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
   HIPCHK(hipMemcpy(m->dI, ibuf, sizeof(int32_t) * desc->isize, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(m->dD, dbuf, sizeof(double) * desc->dsize, hipMemcpyHostToDevice));
   m->lay = make_layout(*desc, &m->lds_bytes);
-  if (m->lds_bytes > 160 * 1024) {
+  if (m->lds_bytes > 160 * 1024 - MGS_STATIC_LDS) {
     size_t need = m->lds_bytes;
     mgs_model_free(m);
     char buf[64];
@@ -207,7 +214,7 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
   // the attribute is per kernel function, shared by every model of this nv: set it
   // to the CU's whole LDS so a later, smaller model cannot lower it under an
   // earlier, wider one (occupancy follows each launch's own dynamic size)
-  HIPCHK(set_lds_limit(desc->nv, 160 * 1024));
+  HIPCHK(set_lds_limit(desc->nv, 160 * 1024 - MGS_STATIC_LDS));
   *out = m;
   return MGS_OK;
 }

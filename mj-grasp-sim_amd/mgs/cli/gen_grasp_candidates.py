@@ -1,0 +1,43 @@
+"""python -m mgs.cli.gen_grasp_candidates gripper=<cfg> id=<k> num_grasps=<n>
+(reference: mgs/cli/gen_grasp_candidates.py:16-83).
+
+Antipodal candidates (mgs.sampler.antipodal) written to
+$MGS_OUTPUT_DIR/<gripper>/<object>/candidates.npz.  Parallel grippers get the
+reference's joints (Panda: width_to_joints(_clamp_width(w)), :66-71; Robotiq:
+open = zeros); the dexterous hands, whose reference sampler is the JAX contact
+sampler (out of scope), get their open configuration."""
+import os
+
+import numpy as np
+
+from mgs.cli._common import grasp_dir, object_id
+from mgs.cli._hydra import main
+from mgs.gripper.selector import get_gripper
+from mgs.obj.selector import get_object
+from mgs.sampler import antipodal
+
+
+def candidates(gripper, obj, num, seed):
+    name = type(gripper).__name__
+    if name == "GripperPanda":
+        return antipodal.panda_candidates(obj, num, seed=seed, gripper=gripper)[:2]
+    if name == "GripperRobotiq2f85":
+        return antipodal.robotiq_candidates(obj, num, seed=seed)[:2]
+    return antipodal.hand_candidates(obj, num, gripper, seed=seed)[:2]
+
+
+@main("gen_grasp_candidates")
+def run(cfg):
+    print(f"Generating grasp candidates for gripper: {cfg.gripper.name}")
+    oid = object_id(cfg)
+    obj = get_object(oid)
+    gripper = get_gripper(cfg.gripper)
+    out = grasp_dir(cfg, oid, "MGS_OUTPUT_DIR")
+    os.makedirs(out, exist_ok=True)
+    H, J = candidates(gripper, obj, int(cfg.get("num_grasps", 10000)), int(cfg.get("seed", 0)))
+    np.savez(os.path.join(out, "candidates.npz"), pose=H, joints=J)
+    print("Done!", os.path.join(out, "candidates.npz"))
+
+
+if __name__ == "__main__":
+    run()
