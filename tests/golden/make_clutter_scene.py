@@ -27,6 +27,8 @@ for p in (REPO, os.path.join(REPO, "mj-grasp-sim_amd")):
 OBJECT_IDS = ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange", "061_foam_brick"]
 GRIPPER = "Robotiq2f85Gripper"
 OUT = os.path.join(HERE, "clutter_scene.npz")
+# `python make_clutter_scene.py ShadowHand` -> clutter_scene_shadow.npz (config C5's gripper)
+OUTS = {"Robotiq2f85Gripper": OUT, "ShadowHand": os.path.join(HERE, "clutter_scene_shadow.npz")}
 
 
 def make_env(gripper_name=GRIPPER, object_ids=OBJECT_IDS):
@@ -89,7 +91,8 @@ def env_expand(env, ref_vec, reduced, which):
 
 
 def main():
-    env = make_env()
+    gname = sys.argv[1] if len(sys.argv) > 1 else GRIPPER
+    env = make_env(gname)
     rng = np.random.default_rng(0)
     state = settle(env, rng)
     env.set_state(state)
@@ -98,8 +101,8 @@ def main():
     q0, q1 = env.split_state(state)["qpos"], env.split_state(s2)["qpos"]
     drift = max(np.abs(q1[qs][:3] - q0[qs][:3]).sum() for _, qs, _ in env._obj_slices())
     print("object z:", [round(float(q0[qs][2]), 4) for _, qs, _ in env._obj_slices()], "drift", drift)
-    np.savez(OUT, state=state, object_ids=np.array(OBJECT_IDS), gripper=np.array(GRIPPER), drift=drift)
-    print("wrote", OUT, state.shape)
+    np.savez(OUTS[gname], state=state, object_ids=np.array(OBJECT_IDS), gripper=np.array(gname), drift=drift)
+    print("wrote", OUTS[gname], state.shape)
 
 
 def settle_more(env, state, n):

@@ -1,0 +1,130 @@
+"""Secondary BASELINE.json configurations on one MI355X (bench.py keeps the
+headline C2 line).  One JSON line per configuration:
+
+  c3  Franka Panda over the (synthetic) YCB set, 16384 candidates per object
+  c4  Allegro on object stand-ins (GSO is not shipped), 32768 candidates
+      (the whole 8-GPU job on one GPU; per-GPU share = 4096)
+  c5  Shadow Hand on a settled 5-object clutter pile (tests/golden/
+      clutter_scene_shadow.npz): collision mask + 3000-step close + 3000-step
+      lift per candidate (the reference's grasp_stable_mask schedule)
+
+Timing: wall clock of the env API calls (collision mask + stability rollout,
+host buffers, PCIe included), and the kernels' own HIP-event durations.
+Horizons: c3/c4 use h200 (bench.py's), c5 the reference's clutter schedule
+(scaled down with --c5-steps for a bounded run).
+
+    python tools/bench_configs.py [c3 c4 c5] [--c5-steps 600]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "mj-grasp-sim_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+import numpy as np  # noqa: E402
+
+
+def gravityless(gripper_name, object_ids, n, horizon="h200"):
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, HORIZONS
+    from mgs.gripper.selector import get_gripper
+    from mgs.obj.selector import get_object
+    from mgs.sampler import antipodal
+    from mgs.util.geo.transforms import SE3Pose
+    h = HORIZONS[horizon]
+    tot_n = tot_t = tot_k = 0.0
+    per = []
+    for oid in object_ids:
+        g = get_gripper({"name": gripper_name})
+        env = GravitylessObjectGrasping(g, get_object(oid))
+        if gripper_name == "PandaGripper":
+            H, J, _ = antipodal.panda_candidates(env.obj, n, seed=0, gripper=g)
+        else:
+            H, J, _ = antipodal.hand_candidates(env.obj, n, g, seed=0)
+        P = SE3Pose.from_mat(H)
+        env.grasp_collision_mask(P[:64], J[:64])          # warm up (model upload, code objects)
+        t0 = time.perf_counter()
+        mask = env.grasp_collision_mask(P, J)
+        km = env.engine.last_collision_ms()
+        idx = np.nonzero(mask)[0]
+        res = env.grasp_stability_evaluation_from_joints(P[idx], J[idx], nstep_lift=h["nstep_lift"],
+                                                         shake_steps=h["shake_steps"],
+                                                         close_steps=h["close_steps"],
+                                                         lift_check_every=h["lift_check_every"],
+                                                         return_details=True) if len(idx) else None
+        dt = time.perf_counter() - t0
+        kr = res["kernel_ms"] if res is not None else 0.0
+        per.append(dict(object=oid, candidates=n, collision_free=int(mask.sum()),
+                        stable=int(res["label"].sum()) if res is not None else 0, seconds=dt,
+                        kernel_ms=km + kr))
+        tot_n += n
+        tot_t += dt
+        tot_k += (km + kr) * 1e-3
+    return dict(value=tot_n / tot_t, kernel_only=tot_n / tot_k, objects=per)
+
+
+def clutter(n_per_obj, steps):
+    from make_clutter_scene import make_env
+    from mgs.sampler.antipodal import hand_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    z = np.load(os.path.join(ROOT, "tests", "golden", "clutter_scene_shadow.npz"))
+    env = make_env("ShadowHand")
+    env.set_state(z["state"])
+    H, J = [], []
+    for k, o in enumerate(env.objects):
+        h, j, _ = hand_candidates(o, n_per_obj, env.gripper, seed=k)
+        H.append((env.get_obj_pose(o.name) @ SE3Pose.from_mat(h)).to_mat())
+        J.append(j)
+    P = SE3Pose.from_mat(np.concatenate(H).astype(np.float32))
+    J = np.concatenate(J)
+    st = env.get_state()
+    env.grasp_collision_mask(P[:8], J[:8])
+    t0 = time.perf_counter()
+    mask = env.grasp_collision_mask(P, J)
+    idx = np.nonzero(mask)[0]
+    res = env.grasp_stable_mask(P[idx], J[idx], st, nstep_lift=steps, close_steps=steps, return_details=True)
+    dt = time.perf_counter() - t0
+    eng = env.engine_for_state(st)
+    return dict(value=len(P) / dt, candidates=len(P), collision_free=int(mask.sum()),
+                stable=int(res["label"].sum()), seconds=dt, rollout_kernel_ms=res["kernel_ms"],
+                overflow_rerun=int((res["stats"][:, 2] != 0).sum()), steps_per_phase=steps,
+                nv=int(env.model.nv), nefc_max=int(eng.desc.nefc_max), library=os.path.basename(
+                    "libmgs_gpu_wide.so" if eng.desc.nefc_max > 128 else "libmgs_gpu.so"),
+                mean_ncon=float(res["stats"][:, 4].sum() / max(1, (2 * steps) * len(idx))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c3", "c4", "c5"])
+    ap.add_argument("--c5-steps", type=int, default=600)
+    ap.add_argument("--c5-per-object", type=int, default=256)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.init()
+    from mgs.obj.ycb import ObjectYCB
+    ycb = ObjectYCB.all_object_ids()
+    for c in a.configs:
+        if c == "c3":
+            r = gravityless("PandaGripper", ycb, 16384)
+            out = dict(config="c3", workload=f"Franka Panda x {len(ycb)} synthetic YCB objects, 16384 candidates/object,"
+                                             " mask + h200 rollout", unit="candidates/s", **r)
+        elif c == "c4":
+            r = gravityless("AllegroGripper", ["017_orange"], 32768)
+            out = dict(config="c4", workload="Allegro x 017_orange stand-in (GSO absent), 32768 candidates on one GPU,"
+                                             " mask + h200 rollout", unit="candidates/s", **r)
+        elif c == "c5":
+            r = clutter(a.c5_per_object, a.c5_steps)
+            out = dict(config="c5", workload=f"Shadow Hand x settled 5-object pile, {r['candidates']} candidates, "
+                                             f"mask + close {a.c5_steps} + lift {a.c5_steps} (reference: 3000 + 3000)",
+                       unit="candidates/s", **r)
+        else:
+            raise SystemExit(f"unknown config {c}")
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
