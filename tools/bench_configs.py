@@ -92,8 +92,7 @@ def clutter(n_per_obj, steps):
     return dict(value=len(P) / dt, candidates=len(P), collision_free=int(mask.sum()),
                 stable=int(res["label"].sum()), seconds=dt, rollout_kernel_ms=res["kernel_ms"],
                 overflow_rerun=int((res["stats"][:, 2] != 0).sum()), steps_per_phase=steps,
-                nv=int(env.model.nv), nefc_max=int(eng.desc.nefc_max), library=os.path.basename(
-                    "libmgs_gpu_wide.so" if eng.desc.nefc_max > 128 else "libmgs_gpu.so"),
+                nv=int(env.model.nv), nefc_max=int(eng.desc.nefc_max), library=os.path.basename(eng.lib._name),
                 mean_ncon=float(res["stats"][:, 4].sum() / max(1, (2 * steps) * len(idx))))
 
 
