@@ -306,6 +306,18 @@ int mgs_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n,
                        const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step,
                        double* d_obj_qpos, int32_t* d_stats, void* stream);
 
+/* Antipodal candidate ray casting (AntipodalGraspGenerator.generate_grasps,
+ * mgs/sampler/antipodal.py:96-172, trimesh intersects_location): for each of
+ * n surface points, cast dir and -dir from origin through the ntri triangles
+ * (tri: ntri * 9, vertices v0 v1 v2), keep hits at distance >= eps, and return
+ * the k-th, k = min(floor(u_choice * count), count - 1), in the order (+dir hits
+ * by triangle index, -dir hits by triangle index).  out_nvalid[i] = count (0:
+ * the caller applies the reference's random-offset fallback).  Host pointers;
+ * synchronous on `device`; kernel_ms (may be NULL) = kernel duration. */
+int mgs_antipodal_contacts(int device, const double* tri, int ntri, int n, const double* origin,
+                           const double* dir, const double* u_choice, double eps, double* out_second,
+                           int32_t* out_nvalid, double* kernel_ms);
+
 /* Duration (ms) of the last rollout kernel launch, measured with HIP events
  * on the launch stream (waits for it). */
 double mgs_last_kernel_ms(mgs_batch* batch);

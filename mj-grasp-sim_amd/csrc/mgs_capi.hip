@@ -12,6 +12,7 @@
 #define MGS_G_GLOBAL 1
 #endif
 #include "mgs_kernels.hip"
+#include "mgs_sampler.hip"
 
 namespace {
 thread_local std::string g_err;
@@ -451,6 +452,53 @@ int mgs_prof_read(unsigned long long* out) {
 }
 
 int mgs_lds_bytes(mgs_model* m) { return m ? (int)m->lds_bytes : -1; }
+
+int mgs_antipodal_contacts(int device, const double* tri, int ntri, int n, const double* origin,
+                           const double* dir, const double* u_choice, double eps, double* out_second,
+                           int32_t* out_nvalid, double* kernel_ms) {
+  if (n < 0 || ntri < 0) return fail(MGS_EINVAL, "mgs_antipodal_contacts: negative size%s");
+  if (n == 0) return MGS_OK;
+  if (!tri || !origin || !dir || !u_choice || !out_second || !out_nvalid)
+    return fail(MGS_EINVAL, "mgs_antipodal_contacts: null argument%s");
+  HIPCHK(hipSetDevice(device));
+  double *dT = nullptr, *dO = nullptr, *dD = nullptr, *dU = nullptr, *dS = nullptr;
+  int32_t* dN = nullptr;
+  size_t nt = (size_t)(ntri > 0 ? ntri : 1) * 9;
+  bool ok = hipMalloc(&dT, nt * sizeof(double)) == hipSuccess && hipMalloc(&dO, 3 * n * sizeof(double)) == hipSuccess &&
+            hipMalloc(&dD, 3 * n * sizeof(double)) == hipSuccess && hipMalloc(&dU, n * sizeof(double)) == hipSuccess &&
+            hipMalloc(&dS, 3 * n * sizeof(double)) == hipSuccess && hipMalloc(&dN, n * sizeof(int32_t)) == hipSuccess;
+  int rc = MGS_OK;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (!ok) {
+    rc = fail(MGS_ENOMEM, "device allocation failed%s");
+  } else {
+    if (ntri > 0) hipMemcpy(dT, tri, (size_t)ntri * 9 * sizeof(double), hipMemcpyHostToDevice);
+    hipMemcpy(dO, origin, 3 * n * sizeof(double), hipMemcpyHostToDevice);
+    hipMemcpy(dD, dir, 3 * n * sizeof(double), hipMemcpyHostToDevice);
+    hipMemcpy(dU, u_choice, n * sizeof(double), hipMemcpyHostToDevice);
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, nullptr);
+    hipLaunchKernelGGL(mgs_antipodal_kernel, dim3((n + 255) / 256), dim3(256), 0, nullptr, dT, ntri, n, dO, dD, dU,
+                       eps, dS, dN);
+    hipEventRecord(e1, nullptr);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e != hipSuccess) {
+      rc = fail(MGS_EHIP, "HIP error: %s", hipGetErrorString(e));
+    } else {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (kernel_ms) *kernel_ms = ms;
+      hipMemcpy(out_second, dS, 3 * n * sizeof(double), hipMemcpyDeviceToHost);
+      hipMemcpy(out_nvalid, dN, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    }
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipFree(dT); hipFree(dO); hipFree(dD); hipFree(dU); hipFree(dS); hipFree(dN);
+  return rc;
+}
 
 int mgs_max_rows(void) { return 64 * MGS_RPL; }
 

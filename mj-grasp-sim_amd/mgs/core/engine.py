@@ -56,6 +56,8 @@ def load_library(wide: bool = False):
     L.mgs_device_count.restype = ctypes.c_int
     L.mgs_model_lds_bytes.argtypes = [P(abi.ModelDesc), P(ctypes.c_int64)]
     L.mgs_max_rows.restype = ctypes.c_int
+    L.mgs_antipodal_contacts.argtypes = [ctypes.c_int, P(c_d), ctypes.c_int, ctypes.c_int, P(c_d), P(c_d), P(c_d),
+                                         c_d, P(c_d), P(c_i), P(c_d)]
     L.mgs_supports_nv.argtypes = [ctypes.c_int]
     L.mgs_supports_nv.restype = ctypes.c_int
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
@@ -217,6 +219,27 @@ class Engine:
 
     def last_kernel_ms(self):
         return self.lib.mgs_last_kernel_ms(self._batch)
+
+
+def antipodal_contacts(tri, origin, direction, u_choice, eps, device=0):
+    """GPU ray casting of the antipodal sampler (mgs_antipodal_contacts):
+    returns (second contact (n,3), valid-hit count (n,), kernel ms)."""
+    L = load_library()
+    if L.mgs_device_count() <= device:
+        raise EngineError("no HIP device visible for the MI355X engine")
+    tri = np.ascontiguousarray(tri, np.float64).reshape(-1, 9)
+    o = np.ascontiguousarray(origin, np.float64).reshape(-1, 3)
+    d = np.ascontiguousarray(direction, np.float64).reshape(-1, 3)
+    u = np.ascontiguousarray(u_choice, np.float64).reshape(-1)
+    n = len(o)
+    sec = np.zeros((n, 3))
+    cnt = np.zeros(n, np.int32)
+    ms = ctypes.c_double(0.0)
+    _check(L.mgs_antipodal_contacts(device, ptr(tri, ctypes.c_double), len(tri), n, ptr(o, ctypes.c_double),
+                                    ptr(d, ctypes.c_double), ptr(u, ctypes.c_double), float(eps),
+                                    ptr(sec, ctypes.c_double), ptr(cnt, ctypes.c_int32), ctypes.byref(ms)),
+           "mgs_antipodal_contacts", L)
+    return sec, cnt, ms.value
 
 
 def tree_probe(a, c, n):

@@ -107,6 +107,49 @@ class AntipodalGraspGenerator:
         widths = np.maximum(np.linalg.norm(two - one, axis=1), 0) * self.scale
         return H, {"width": widths}
 
+    def draw(self, num: int, kappa: float = 10.0):
+        """All random inputs of one batch, drawn vectorised up front (the device
+        path): surface points (area-weighted face, uniform barycentric), von
+        Mises-Fisher directions around the inward normal (Wood's exact 3-D
+        sampler), the hit-choice uniforms and the fallback offsets."""
+        rng = self.rng
+        tri = self.verts[self.faces]
+        cr = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+        area = 0.5 * np.linalg.norm(cr, axis=1)
+        normals = cr / np.maximum(np.linalg.norm(cr, axis=1, keepdims=True), 1e-30)
+        fidx = rng.choice(len(tri), size=num, p=area / area.sum())
+        r1, r2 = rng.random((2, num, 1))
+        s1 = np.sqrt(r1)
+        pts = (1 - s1) * tri[fidx, 0] + s1 * (1 - r2) * tri[fidx, 1] + s1 * r2 * tri[fidx, 2]
+        mu = -normals[fidx]
+        xi = rng.random(num)
+        w = 1.0 + np.log(xi + (1.0 - xi) * np.exp(-2.0 * kappa)) / kappa
+        v = rng.standard_normal((num, 3))
+        v -= np.sum(v * mu, axis=1, keepdims=True) * mu
+        v /= np.maximum(np.linalg.norm(v, axis=1, keepdims=True), 1e-30)
+        dirs = w[:, None] * mu + np.sqrt(np.maximum(1.0 - w * w, 0.0))[:, None] * v
+        dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+        return dict(tri=tri, points=pts, dirs=dirs, u=rng.random(num),
+                    offset=rng.uniform(-0.05, 0.05, size=(num, 3)))
+
+    def finish(self, one, two, rng):
+        H = self.define_gripper_pose(one, two, rng)
+        H[..., :3, 3] = self.denormalize_points(H[..., :3, 3])
+        widths = np.maximum(np.linalg.norm(two - one, axis=1), 0) * self.scale
+        return H, {"width": widths}
+
+    def generate_grasps_device(self, num: int, kappa: float = 10.0, eps: float = 1e-5, device: int = 0):
+        """generate_grasps with the ray casting of every point on the MI355X
+        (mgs_antipodal_contacts): one batch, no per-point host loop."""
+        from mgs.core.engine import antipodal_contacts
+        self.normalize_load()
+        r = self.draw(num, kappa)
+        sec, cnt, ms = antipodal_contacts(r["tri"], r["points"], r["dirs"], r["u"], eps, device=device)
+        two = np.where((cnt > 0)[:, None], sec, r["points"] + r["offset"])
+        H, aux = self.finish(r["points"], two, self.rng)
+        aux.update(kernel_ms=ms, hits=cnt)
+        return H, aux
+
     @staticmethod
     def define_gripper_pose(c1, c2, rng):
         n = len(c1)

@@ -2281,6 +2281,73 @@ int oracle_simulate(const mgs_model_desc* desc, const int32_t* I, const double* 
   return 0;
 }
 
+/* Antipodal ray casting (mgs_antipodal_contacts, csrc/mgs_sampler.hip; the
+ * reference's trimesh intersects_location in antipodal.py:117-145): Moller-
+ * Trumbore per triangle, valid hits at distance >= eps, the k-th valid hit,
+ * k = min(floor(u * count), count - 1), +dir hits before -dir hits. */
+static int o_ray_tri(const double* o, const double* d, const double* T, double* tout) {
+  double e1[3], e2[3], p[3], tv[3], q[3];
+  for (int k = 0; k < 3; k++) { e1[k] = T[3 + k] - T[k]; e2[k] = T[6 + k] - T[k]; }
+  p[0] = d[1] * e2[2] - d[2] * e2[1];
+  p[1] = d[2] * e2[0] - d[0] * e2[2];
+  p[2] = d[0] * e2[1] - d[1] * e2[0];
+  double det = (e1[0] * p[0] + e1[1] * p[1]) + e1[2] * p[2];
+  if (!(fabs(det) > 1e-12)) return 0;
+  double inv = 1.0 / det;
+  for (int k = 0; k < 3; k++) tv[k] = o[k] - T[k];
+  double u = ((tv[0] * p[0] + tv[1] * p[1]) + tv[2] * p[2]) * inv;
+  q[0] = tv[1] * e1[2] - tv[2] * e1[1];
+  q[1] = tv[2] * e1[0] - tv[0] * e1[2];
+  q[2] = tv[0] * e1[1] - tv[1] * e1[0];
+  double w = ((q[0] * d[0] + q[1] * d[1]) + q[2] * d[2]) * inv;
+  double t = ((e2[0] * q[0] + e2[1] * q[1]) + e2[2] * q[2]) * inv;
+  if (u >= 0.0 && w >= 0.0 && u + w <= 1.0 && t > 0.0) { *tout = t; return 1; }
+  return 0;
+}
+
+static int o_ray_valid(const double* o, const double* d, double t, double eps, double* loc) {
+  double s = 0.0;
+  for (int k = 0; k < 3; k++) {
+    loc[k] = o[k] + t * d[k];
+    double r = loc[k] - o[k];
+    s = s + r * r;
+  }
+  return sqrt(s) >= eps;
+}
+
+int oracle_antipodal_contacts(const double* tri, int ntri, int n, const double* origin, const double* dir,
+                              const double* u_choice, double eps, double* out_second, int32_t* out_nvalid,
+                              int nthreads) {
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+  for (int i = 0; i < n; i++) {
+    const double* o = origin + 3 * i;
+    double dp[3] = {dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]}, dm[3] = {-dp[0], -dp[1], -dp[2]};
+    int cnt[2] = {0, 0};
+    for (int s = 0; s < 2; s++)
+      for (int j = 0; j < ntri; j++) {
+        double t, loc[3];
+        if (o_ray_tri(o, s ? dm : dp, tri + 9 * j, &t) && o_ray_valid(o, s ? dm : dp, t, eps, loc)) cnt[s]++;
+      }
+    int total = cnt[0] + cnt[1];
+    double sel[3] = {0, 0, 0};
+    if (total > 0) {
+      double fk = floor(u_choice[i] * (double)total);
+      int kth = fk < (double)(total - 1) ? (int)fk : total - 1;
+      int s = kth < cnt[0] ? 0 : 1, kk = s ? kth - cnt[0] : kth, seen = 0;
+      for (int j = 0; j < ntri && seen <= kk; j++) {
+        double t, loc[3];
+        if (o_ray_tri(o, s ? dm : dp, tri + 9 * j, &t) && o_ray_valid(o, s ? dm : dp, t, eps, loc)) {
+          if (seen == kk) { sel[0] = loc[0]; sel[1] = loc[1]; sel[2] = loc[2]; }
+          seen++;
+        }
+      }
+    }
+    out_nvalid[i] = total;
+    for (int k = 0; k < 3; k++) out_second[3 * i + k] = sel[k];
+  }
+  return 0;
+}
+
 /* Debug/KAT helper: run nsteps with a fixed mocap and ctrl from an initial
  * state, recording qpos after every step (nsteps * nq) and ncon per step. */
 int oracle_trace(const mgs_model_desc* desc, const int32_t* I, const double* D, const double* qpos_init,

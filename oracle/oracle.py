@@ -118,6 +118,25 @@ class OracleModel:
         return n, pos[:k], fr[:k], dist[:k], g[:k]
 
 
+def antipodal_contacts(tri, origin, direction, u_choice, eps, nthreads=8):
+    """CPU restatement of mgs_antipodal_contacts (checker)."""
+    tri = np.ascontiguousarray(tri, np.float64).reshape(-1, 9)
+    o = np.ascontiguousarray(origin, np.float64).reshape(-1, 3)
+    d = np.ascontiguousarray(direction, np.float64).reshape(-1, 3)
+    u = np.ascontiguousarray(u_choice, np.float64).reshape(-1)
+    n = len(o)
+    sec = np.zeros((n, 3))
+    cnt = np.zeros(n, np.int32)
+    L = lib()
+    L.oracle_antipodal_contacts.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int] + \
+        [ctypes.POINTER(ctypes.c_double)] * 3 + [ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+                                                 ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
+    L.oracle_antipodal_contacts(ptr(tri, ctypes.c_double), len(tri), n, ptr(o, ctypes.c_double),
+                                ptr(d, ctypes.c_double), ptr(u, ctypes.c_double), float(eps),
+                                ptr(sec, ctypes.c_double), ptr(cnt, ctypes.c_int32), nthreads)
+    return sec, cnt
+
+
 def sincos(x):
     x = np.ascontiguousarray(x, np.float64)
     s = np.zeros_like(x)
