@@ -17,13 +17,28 @@ from mgs.obj.selector import get_object
 from mgs.sampler import antipodal
 
 
-def candidates(gripper, obj, num, seed):
+def candidates(gripper, obj, num, seed, sampler="device"):
+    """(pose float32 (num,4,4), joints) for `gripper`; sampler "device" casts the
+    rays on the GPU (generate_grasps_device), "host" is the numpy restatement."""
     name = type(gripper).__name__
+    if sampler == "host":
+        if name == "GripperPanda":
+            return antipodal.panda_candidates(obj, num, seed=seed, gripper=gripper)[:2]
+        if name == "GripperRobotiq2f85":
+            return antipodal.robotiq_candidates(obj, num, seed=seed)[:2]
+        return antipodal.hand_candidates(obj, num, gripper, seed=seed)[:2]
+    gen = antipodal.AntipodalGraspGenerator(obj.obj_file_path, rng=np.random.default_rng(seed))
+    H, aux = gen.generate_grasps_device(num)
+    H = H.astype(np.float32)
     if name == "GripperPanda":
-        return antipodal.panda_candidates(obj, num, seed=seed, gripper=gripper)[:2]
+        j1, j2 = gripper.width_to_joints(gripper._clamp_width(aux["width"]))
+        return H, np.stack([j1, j2], axis=-1)
     if name == "GripperRobotiq2f85":
-        return antipodal.robotiq_candidates(obj, num, seed=seed)[:2]
-    return antipodal.hand_candidates(obj, num, gripper, seed=seed)[:2]
+        return H, np.zeros((num, 8))
+    site = getattr(gripper, "grasp_site", None)
+    if site is not None:
+        H[:, :3, 3] -= H[:, :3, :3] @ np.asarray(site, np.float32)
+    return H, np.tile(gripper.open_joints(), (num, 1))
 
 
 @main("gen_grasp_candidates")
@@ -34,7 +49,8 @@ def run(cfg):
     gripper = get_gripper(cfg.gripper)
     out = grasp_dir(cfg, oid, "MGS_OUTPUT_DIR")
     os.makedirs(out, exist_ok=True)
-    H, J = candidates(gripper, obj, int(cfg.get("num_grasps", 10000)), int(cfg.get("seed", 0)))
+    H, J = candidates(gripper, obj, int(cfg.get("num_grasps", 10000)), int(cfg.get("seed", 0)),
+                      cfg.get("sampler", "device"))
     np.savez(os.path.join(out, "candidates.npz"), pose=H, joints=J)
     print("Done!", os.path.join(out, "candidates.npz"))
 

@@ -27,7 +27,8 @@ def run(cfg):
     out = grasp_dir(cfg, oid, "MGS_OUTPUT_DIR")
     os.makedirs(out, exist_ok=True)
     t0 = time.perf_counter()
-    H, J = candidates(gripper, obj, int(cfg.get("num_grasps", 8192)), int(cfg.get("seed", 0)))
+    H, J = candidates(gripper, obj, int(cfg.get("num_grasps", 8192)), int(cfg.get("seed", 0)),
+                      cfg.get("sampler", "device"))
     np.savez(os.path.join(out, "candidates.npz"), pose=H, joints=J)
     t1 = time.perf_counter()
     env = GravitylessObjectGrasping(gripper, obj)

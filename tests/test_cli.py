@@ -19,7 +19,7 @@ def test_compose_defaults_and_overrides():
 def test_gen_grasp_candidates_file_format(tmp_path, monkeypatch):
     from mgs.cli import gen_grasp_candidates
     monkeypatch.setenv("MGS_OUTPUT_DIR", str(tmp_path))
-    gen_grasp_candidates.run(["gripper=panda", "id=0", "num_grasps=32"])
+    gen_grasp_candidates.run(["gripper=panda", "id=0", "num_grasps=32", "sampler=host"])
     z = np.load(tmp_path / "PandaGripper" / "003_cracker_box" / "candidates.npz")
     assert z["pose"].shape == (32, 4, 4) and z["pose"].dtype == np.float32
     assert z["joints"].shape == (32, 2)
@@ -43,7 +43,7 @@ def test_gen_grasps_and_filter_to_stable(tmp_path, monkeypatch):
     from oracle import oracle as O
     monkeypatch.setenv("MGS_OUTPUT_DIR", str(tmp_path))
     monkeypatch.setenv("MGS_INPUT_DIR", str(tmp_path))
-    gen_grasps.run(["id=0", "num_grasps=256", "horizon=h200", "enough_stable=20"])
+    gen_grasps.run(["id=0", "num_grasps=256", "horizon=h200", "enough_stable=20"])    # device sampler
     d = tmp_path / "Robotiq2f85Gripper" / "003_cracker_box"
     cand = np.load(d / "candidates.npz")
     stable = np.load(d / "stable_grasps.npz")

@@ -25,6 +25,7 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "mj-grasp-sim_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import numpy as np  # noqa: E402
 
@@ -96,9 +97,38 @@ def clutter(n_per_obj, steps):
                 mean_ncon=float(res["stats"][:, 4].sum() / max(1, (2 * steps) * len(idx))))
 
 
+def sampler(n=8192, subdiv=5):
+    """Antipodal candidate ray casting on a 20480-face icosphere (a YCB-scale
+    mesh): device kernel vs the C restatement on 16 host threads."""
+    import tempfile
+    from make_synthetic_ycb_mesh import icosphere_obj
+    from mgs.core.engine import antipodal_contacts
+    from mgs.sampler.antipodal import AntipodalGraspGenerator
+    from oracle import oracle as O
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "sphere.obj")
+        with open(path, "w") as f:
+            f.write(icosphere_obj(0.04, subdiv))
+        g = AntipodalGraspGenerator(path, rng=np.random.default_rng(0))
+        g.normalize_load()
+        r = g.draw(n)
+    antipodal_contacts(r["tri"], r["points"][:256], r["dirs"][:256], r["u"][:256], 1e-5)   # warm-up
+    t0 = time.perf_counter()
+    sg, cg, ms = antipodal_contacts(r["tri"], r["points"], r["dirs"], r["u"], 1e-5)
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    so, co = O.antipodal_contacts(r["tri"], r["points"], r["dirs"], r["u"], 1e-5, nthreads=16)
+    dc = time.perf_counter() - t1
+    tests = 2 * 2 * n * len(r["tri"])          # two rays, two sweeps
+    return dict(value=n / (ms * 1e-3), unit="candidate points/s (kernel)", points=n, triangles=len(r["tri"]),
+                kernel_ms=ms, wall_ms=dt * 1e3, ray_triangle_tests_per_s=tests / (ms * 1e-3),
+                cpu_baseline=dict(value=n / dc, cores=16, kind="port", seconds=dc),
+                bit_exact=bool(np.array_equal(sg, so) and np.array_equal(cg, co)))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("configs", nargs="*", default=["c3", "c4", "c5"])
+    ap.add_argument("configs", nargs="*", default=["c3", "c4", "c5", "sampler"])
     ap.add_argument("--c5-steps", type=int, default=600)
     ap.add_argument("--c5-per-object", type=int, default=256)
     a = ap.parse_args()
@@ -120,6 +150,9 @@ def main():
             out = dict(config="c5", workload=f"Shadow Hand x settled 5-object pile, {r['candidates']} candidates, "
                                              f"mask + close {a.c5_steps} + lift {a.c5_steps} (reference: 3000 + 3000)",
                        unit="candidates/s", **r)
+        elif c == "sampler":
+            out = dict(config="sampler", workload="antipodal ray casting, 8192 points x 20480-face icosphere",
+                       **sampler())
         else:
             raise SystemExit(f"unknown config {c}")
         print(json.dumps(out), flush=True)
