@@ -81,6 +81,14 @@ struct Dat {
 #ifndef MGS_RPL
 #define MGS_RPL 2   // constraint rows per lane (nefc_max <= 64 * MGS_RPL)
 #endif
+// NV-long operand rows of the triangular solves / G products held in registers
+// (main build) or read from LDS at each use (wide build: nv up to 58 would
+// spill them to scratch).  Same values either way.
+#ifdef MGS_WIDE
+#define MGS_REG_ROWS 0
+#else
+#define MGS_REG_ROWS 1
+#endif
 
 DEVI int lane_id() { return (int)__lane_id(); }
 // values that are uniform across the wave but come from LDS: move to SGPRs so
@@ -580,21 +588,30 @@ template <int NV>
 DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double* x) {
   int lane = lane_id();
   int li = lane < NV ? lane : 0;
+#if MGS_REG_ROWS
   double Lr[NV], Lc[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) { Lr[k] = L[li * NV + k]; Lc[k] = L[k * NV + li]; }
+#define LS_LR(k) Lr[k]
+#define LS_LC(k) Lc[k]
+#else
+#define LS_LR(k) L[li * NV + (k)]
+#define LS_LC(k) L[(k) * NV + li]
+#endif
   double acc = b[li];
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     double yk = readlane_d(acc, k);
-    if (lane > k) acc = __builtin_fma(-Lr[k], yk, acc);
+    if (lane > k) acc = __builtin_fma(-LS_LR(k), yk, acc);
   }
   acc = acc * Dinv[li];
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
     double xk = readlane_d(acc, k);
-    if (lane < k) acc = __builtin_fma(-Lc[k], xk, acc);
+    if (lane < k) acc = __builtin_fma(-LS_LC(k), xk, acc);
   }
+#undef LS_LR
+#undef LS_LC
   wsync();
   if (lane < NV) x[lane] = acc;
   wsync();
@@ -2250,22 +2267,31 @@ template <int NV>
 DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
   int lane = lane_id();
   int li = lane < NV ? lane : 0;
+#if MGS_REG_ROWS
   double Lr[NV], Lc[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) { Lr[k] = d.M[li * NV + k]; Lc[k] = d.M[k * NV + li]; }
+#define FS_LR(k) Lr[k]
+#define FS_LC(k) Lc[k]
+#else
+#define FS_LR(k) d.M[li * NV + (k)]
+#define FS_LC(k) d.M[(k) * NV + li]
+#endif
   double z = u * d.isD[li];
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
     double zk = readlane_d(z, k);
-    if (lane < k) z = __builtin_fma(-Lc[k], zk, z);
+    if (lane < k) z = __builtin_fma(-FS_LC(k), zk, z);
   }
   double t = u * d.sD[li];
   double q = t;
 #pragma unroll
   for (int k = 0; k < NV; k++) {
     double tk = readlane_d(t, k);
-    if (lane > k) q = __builtin_fma(Lr[k], tk, q);
+    if (lane > k) q = __builtin_fma(FS_LR(k), tk, q);
   }
+#undef FS_LR
+#undef FS_LC
   if (lane < NV) {
     d.qfrc_constraint[lane] = q;
     d.qacc_ws[lane] = d.qacc_smooth[lane] + z;   // qacc, kept as next step's warmstart
@@ -2402,9 +2428,13 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const dou
   PCNT(37, 1);
   double q = (lane < NV) ? w[lane] - d.nw0[lane] : 0.0;
   double gauss = 0.5 * tree_sum(q * q, P);
+#if MGS_REG_ROWS
   double wr[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) wr[k] = w[k];
+#else
+  const double* wr = w;
+#endif
   for (int r = lane; r < ne; r += WAVE) {
     const double* Gr = d.G + r * GS;
     double s = 0.0;
@@ -2848,9 +2878,13 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     if (lane < nv) d.ndir[lane] = -d.ndir[lane];
     wsync();
     {
+#if MGS_REG_ROWS
       double dr[NV];
 #pragma unroll
       for (int k = 0; k < NV; k++) dr[k] = d.ndir[k];
+#else
+      const double* dr = d.ndir;
+#endif
       for (int r = lane; r < ne; r += WAVE) {
         const double* Gr = d.G + r * GS;
         double s = 0.0;

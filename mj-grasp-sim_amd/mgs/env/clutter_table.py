@@ -94,7 +94,7 @@ def _frozen_object_xml(xml_bytes: bytes, qpos7) -> bytes:
 
 class ClutterTableEnv:
     def __init__(self, gripper, objects: list, scene_randomization=True, device: int = 0,
-                 ncon_max: int = 48, nefc_max: Optional[int] = None):
+                 ncon_max: int = 96, nefc_max: Optional[int] = None):
         self.gripper = gripper
         self.objects = list(objects)
         self.object_names = [o.name for o in self.objects]
@@ -337,7 +337,7 @@ class ClutterTableEnv:
                            phase_target=np.ascontiguousarray(np.stack([mp, target_lift], 1)),
                            obj_qposadr=-1, check_offset=[0, 1])
 
-    def rollout(self, plan: RolloutPlan, env_state, max_ncon: int = 96):
+    def rollout(self, plan: RolloutPlan, env_state, max_ncon: int = 128):
         """engine rollout with contact-capacity escalation (see
         GravitylessObjectGrasping.rollout)."""
         res = self.engine_for_state(env_state).rollout(plan)
