@@ -120,6 +120,16 @@ class Engine:
     """One compiled model resident on one GPU plus a reusable batch."""
 
     def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None):
+        if nefc_max is None:
+            # worst-case rows, capped at what a library with a kernel for this nv holds
+            full = int(cm.pack(ncon_max=ncon_max)[0]["nefc_max"])
+            main, wide = load_library(), None
+            if os.path.isfile(LIB_WIDE_PATH):
+                wide = load_library(wide=True)
+            if main.mgs_supports_nv(cm.nv) and (full <= main.mgs_max_rows() or not (wide and wide.mgs_supports_nv(cm.nv))):
+                nefc_max = min(full, main.mgs_max_rows())
+            else:
+                nefc_max = min(full, wide.mgs_max_rows() if wide else full)
         fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
         self.lib = library_for(cm.nv, int(fields["nefc_max"]))
         if self.lib.mgs_device_count() <= device:

@@ -1115,8 +1115,9 @@ class CompiledModel:
         nlim = int(np.sum(self.jnt_limited))
         maxdim = int(self.pair_condim.max()) if len(self.pair_condim) else 1
         if nefc_max is None:
-            # rows are register-held two per lane in the kernels: at most 128
-            nefc_max = min(128, neqrow + nfric + nlim + ncon_max * maxdim)
+            # worst case (every contact at the largest condim); the kernels hold
+            # 2 (main build) or 4 (wide build) rows per lane: at most 256
+            nefc_max = min(256, neqrow + nfric + nlim + ncon_max * maxdim)
         o = self.options
         fields.update(
             nq=self.nq, nv=self.nv, nbody=self.nbody, njnt=len(self.jnt_type),

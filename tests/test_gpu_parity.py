@@ -233,7 +233,8 @@ def test_contact_capacity_escalation(env):
     keep = np.setdiff1d(np.arange(len(idx)), ov)
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(res[k][keep], capped[k][keep]), k
-    ro = O.OracleModel(env.model, ncon_max=32).rollout(plan.subset(ov), nthreads=8)
+    ro = O.OracleModel(env.model, ncon_max=32, nefc_max=e16.engine_for(32).desc.nefc_max).rollout(
+        plan.subset(ov), nthreads=8)
     _assert_same({k: res[k][ov] for k in ro}, ro, "escalated")
     # the default capacity (20 contacts, auto rows) holds all of them
     assert env.ncon_max == 20

@@ -84,6 +84,7 @@ def test_shadow_gpu_parity(senv, scand):
     res = senv.rollout(plan)
     ov = np.nonzero(rg["stats"][:, 2])[0]
     if len(ov):
-        ow = O.OracleModel(senv.model, ncon_max=40).rollout(plan.subset(ov), nthreads=8)
+        ow = O.OracleModel(senv.model, ncon_max=40, nefc_max=senv.engine_for(40).desc.nefc_max).rollout(
+            plan.subset(ov), nthreads=8)
         for k in ("label", "fail_step", "obj_qpos", "stats"):
             assert np.array_equal(res[k][ov], ow[k]), k
