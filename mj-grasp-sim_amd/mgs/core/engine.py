@@ -91,6 +91,17 @@ def lds_bytes_for(cm, ncon_max, nefc_max=None):
     return int(out.value)
 
 
+def default_rows(cm, worst: int) -> int:
+    """worst-case constraint rows, capped at what the library that will hold
+    this model provides (the main one when it has a kernel for nv and the rows
+    fit, else the wide one)."""
+    main = load_library()
+    wide = load_library(wide=True) if os.path.isfile(LIB_WIDE_PATH) else None
+    if main.mgs_supports_nv(cm.nv) and (worst <= main.mgs_max_rows() or not (wide and wide.mgs_supports_nv(cm.nv))):
+        return min(worst, main.mgs_max_rows())
+    return min(worst, wide.mgs_max_rows()) if wide else worst
+
+
 def auto_capacity(cm, ncon_max=20):
     """Constraint-row capacity for `ncon_max` contacts that keeps the most
     candidates in flight per CU: rows are shrunk from the worst case (every
@@ -98,8 +109,9 @@ def auto_capacity(cm, ncon_max=20):
     raises the per-CU occupancy.  Candidates that exceed a capacity are
     flagged by the kernel and re-run wider (GravitylessObjectGrasping.rollout)."""
     fields, _, _ = cm.pack(ncon_max=ncon_max)
-    full = int(fields["nefc_max"])
-    fixed = full - ncon_max * (int(cm.pair_condim.max()) if len(cm.pair_condim) else 1)
+    worst = int(fields["nefc_max"])
+    fixed = worst - ncon_max * (int(cm.pair_condim.max()) if len(cm.pair_condim) else 1)
+    full = default_rows(cm, worst)
     best, best_occ = full, LDS_PER_CU // lds_bytes_for(cm, ncon_max, full)
     floor = min(full, fixed + 3 * ncon_max)
     for ne in range(full - 1, floor - 1, -1):
@@ -121,15 +133,7 @@ class Engine:
 
     def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None):
         if nefc_max is None:
-            # worst-case rows, capped at what a library with a kernel for this nv holds
-            full = int(cm.pack(ncon_max=ncon_max)[0]["nefc_max"])
-            main, wide = load_library(), None
-            if os.path.isfile(LIB_WIDE_PATH):
-                wide = load_library(wide=True)
-            if main.mgs_supports_nv(cm.nv) and (full <= main.mgs_max_rows() or not (wide and wide.mgs_supports_nv(cm.nv))):
-                nefc_max = min(full, main.mgs_max_rows())
-            else:
-                nefc_max = min(full, wide.mgs_max_rows() if wide else full)
+            nefc_max = default_rows(cm, int(cm.pack(ncon_max=ncon_max)[0]["nefc_max"]))
         fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
         self.lib = library_for(cm.nv, int(fields["nefc_max"]))
         if self.lib.mgs_device_count() <= device:
