@@ -80,3 +80,19 @@ def test_plan_layout(env, candidates):
     assert plan.phase_start.shape == (5, 5, 3) and plan.phase_target.shape == (5, 5, 3)
     # left shake restarts from the pre-right position (gravityless_object_grasping.py:264-272)
     assert np.array_equal(plan.phase_start[:, 4], plan.phase_start[:, 3])
+
+
+def test_gso_loader_format():
+    """ObjectGSO (reference mgs/obj/gso.py:28-160): GoogleScannedObjects/<id>/ with
+    info.yml, model.obj as the sampling mesh, same include body as YCB."""
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    from mgs.gripper.selector import get_gripper
+    from mgs.obj.gso import ObjectGSO
+    from mgs.obj.selector import get_object
+    o = get_object("Synthetic_Mug_Body", name="mug")
+    assert isinstance(o, ObjectGSO) and o.obj_file_path.endswith("GoogleScannedObjects/Synthetic_Mug_Body/model.obj")
+    env = GravitylessObjectGrasping(get_gripper({"name": "PandaGripper"}), o)
+    cm = env.model
+    assert cm.jnt_names[-1] == "mug:joint" and cm.nv == 14
+    g = cm.geom_names.index("geom:ground")
+    assert len(cm.geom_names) == g + 2 and cm.pair_condim.max() == 4

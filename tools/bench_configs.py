@@ -2,7 +2,7 @@
 headline C2 line).  One JSON line per configuration:
 
   c3  Franka Panda over the (synthetic) YCB set, 16384 candidates per object
-  c4  Allegro on object stand-ins (GSO is not shipped), 32768 candidates
+  c4  Allegro on a GSO-format object stand-in (GSO is not shipped), 32768 candidates
       (the whole 8-GPU job on one GPU; per-GPU share = 4096)
   c5  Shadow Hand on a settled 5-object clutter pile (tests/golden/
       clutter_scene_shadow.npz): collision mask + 3000-step close + 3000-step
@@ -142,9 +142,9 @@ def main():
             out = dict(config="c3", workload=f"Franka Panda x {len(ycb)} synthetic YCB objects, 16384 candidates/object,"
                                              " mask + h200 rollout", unit="candidates/s", **r)
         elif c == "c4":
-            r = gravityless("AllegroGripper", ["017_orange"], 32768)
-            out = dict(config="c4", workload="Allegro x 017_orange stand-in (GSO absent), 32768 candidates on one GPU,"
-                                             " mask + h200 rollout", unit="candidates/s", **r)
+            r = gravityless("AllegroGripper", ["Synthetic_Mug_Body"], 32768)
+            out = dict(config="c4", workload="Allegro x GSO-format stand-in (Synthetic_Mug_Body), 32768 candidates on "
+                                             "one GPU, mask + h200 rollout", unit="candidates/s", **r)
         elif c == "c5":
             r = clutter(a.c5_per_object, a.c5_steps)
             out = dict(config="c5", workload=f"Shadow Hand x settled 5-object pile, {r['candidates']} candidates, "

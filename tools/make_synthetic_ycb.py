@@ -31,6 +31,10 @@ OBJECTS = {
 }
 
 
+# GSO stand-in: a 24-gon mug-sized cylinder r 0.04, h 0.09 m, 0.3 kg
+GSO_OBJECTS = {"Synthetic_Mug_Body": dict(cyl=(0.04, 0.045, 24), weight=0.3)}
+
+
 def convex_obj(verts, title):
     """OBJ text of the convex hull of `verts` with outward-oriented triangles."""
     import numpy as np
@@ -110,6 +114,17 @@ def main():
             yaml.safe_dump(info, fh, sort_keys=False)
     with open(os.path.join(ROOT, "..", "fast_eta_objects.txt"), "w") as fh:
         fh.write("\n".join(OBJECTS) + "\n")
+    # one Google-Scanned-Objects-format stand-in (model.obj; reference gso.py:50-52)
+    for oid, spec in GSO_OBJECTS.items():
+        d = os.path.join(ROOT, "..", "GoogleScannedObjects", oid)
+        os.makedirs(d, exist_ok=True)
+        body = convex_obj(cylinder_verts(*spec["cyl"]), "cylinder")
+        open(os.path.join(d, "model.obj"), "w").write(body)
+        open(os.path.join(d, "collision_0.obj"), "w").write(body)
+        info = dict(original_file="model.obj", submesh_files=["collision_0.obj"], submesh_props=[1.0],
+                    weight=spec["weight"], material_map="texture.png", synthetic=True)
+        with open(os.path.join(d, "info.yml"), "w") as fh:
+            yaml.safe_dump(info, fh, sort_keys=False)
     return 0
 
 
