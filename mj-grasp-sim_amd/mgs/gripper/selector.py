@@ -19,3 +19,11 @@ def get_gripper(cfg, default_pose=None) -> MjShakableOpenCloseGripper:
     if name not in _GRIPPERS:
         raise ValueError(f"Unknown gripper: {name}")
     return _GRIPPERS[name](pose)
+
+
+def gripper_class(class_name: str):
+    """gripper class by its Python class name (scene files store it)."""
+    for cls in _GRIPPERS.values():
+        if cls.__name__ == class_name:
+            return cls
+    raise ValueError(f"Unknown gripper class: {class_name}")

@@ -119,3 +119,44 @@ def test_clutter_gpu_parity(cenv, ccand):
         assert np.array_equal(rg[k], ro[k]), k
     lab = cenv.grasp_stable_mask(poses[idx], J[idx], st, nstep_lift=600, close_steps=600, enough_stable=3)
     assert lab.sum() == min(3, int(ro["label"].sum()))
+
+
+def test_scene_file_roundtrip(cenv, tmp_path):
+    from mgs.env.selector import get_env_from_dict, load_scene, save_scene
+    save_scene(tmp_path / "scene.npz", cenv.to_dict())
+    sd = load_scene(tmp_path / "scene.npz")
+    e2 = get_env_from_dict({"name": "ClutterTable"}, sd)
+    assert np.array_equal(e2.get_state(), cenv.get_state())
+    assert e2.object_names == cenv.object_names and type(e2.gripper) is type(cenv.gripper)
+
+
+@pytest.mark.gpu
+def test_eval_grasps_cli(cenv, ccand, tmp_path, monkeypatch):
+    """eval_grasps.py:13-82 on a scene directory: success rate = stable / all."""
+    from mgs.cli import eval_grasps
+    from mgs.env.selector import save_scene
+    from oracle import oracle as O
+    poses, J = ccand
+    d = tmp_path / "Robotiq2f85Gripper" / "scene_000"
+    d.mkdir(parents=True)
+    save_scene(d / "scene.npz", cenv.to_dict())
+    sel = np.arange(0, len(J), 4)
+    np.savez(d / "inference_grasps.npz", pose=poses[sel].to_mat(), joints=J[sel])
+    monkeypatch.setenv("MGS_INPUT_DIR", str(tmp_path))
+    eval_grasps.run(["id=0", "lift_steps=300"])
+    import json
+    res = json.load(open(d / "grasp_evaluation.json"))
+    # oracle: the same pipeline (inverse b2c, then the env's own b2c, mask, stable)
+    from mgs.util.geo.transforms import SE3Pose
+    b2c_inv = cenv.gripper.base_to_contact_transform().inverse().to_mat()
+    P = SE3Pose.from_mat(np.einsum("nij,jk->nik", poses[sel].to_mat(), b2c_inv))
+    st = cenv.get_state()
+    eng = cenv.engine_for_state(st)
+    om = O.OracleModel(cenv.model_for(st), ncon_max=cenv.ncon_max, nefc_max=eng.desc.nefc_max)
+    q, mp, mq = cenv._initial_qpos(P, J[sel], st)
+    p = P.pos
+    inb = (np.abs(p[:, 0]) < 0.25) & (np.abs(p[:, 1]) < 0.25) & (p[:, 2] > 0) & (p[:, 2] < 1)
+    free = om.collision_free(q, mp, mq, predicate="partition_incl", nthreads=8) & inb
+    idx = np.nonzero(free)[0]
+    lab = om.rollout(cenv.stable_plan(P[idx], J[sel][idx], st, nstep_lift=300, close_steps=300), nthreads=8)["label"]
+    assert res["success_rate"] == pytest.approx(lab.sum() / len(sel)) and res["num_objects"] == 5
