@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 6
+#define MGS_ABI_VERSION 7
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -236,6 +236,8 @@ typedef struct mgs_schedule {
   int32_t check_offset[MGS_MAX_PHASES];  /* check after step t if (t + off) > 0 and (t + off) % check_every == 0:
                                             0 = gravityless lift (:216), 1 = clutter lift ((t+1) % 100, :313) */
   double ctrl[MGS_MAX_PHASES * 32];
+  double vclip;          /* > 0: clip every qvel entry to [-vclip, vclip] after each step
+                            (ClutterTableEnv.gen_clutter, clutter_table.py:215-221); 0 = off */
 } mgs_schedule;
 
 /* per-candidate rollout outputs */
@@ -317,6 +319,24 @@ int mgs_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n,
 int mgs_antipodal_contacts(int device, const double* tri, int ntri, int n, const double* origin,
                            const double* dir, const double* u_choice, double eps, double* out_second,
                            int32_t* out_nvalid, double* kernel_ms);
+
+/* Free simulation of n states (scene settling: ClutterTableEnv.gen_clutter /
+ * is_stable / settle, clutter_table.py:157-222): the rollout loop of `sched`
+ * with its contact checks ignored (a free simulation never stops early),
+ * starting from qpos_init (n * nq) and, when vstate_init is not NULL,
+ * per-state qvel and qacc_warmstart (n * 2nv: qvel then warmstart; NULL = the
+ * model's qvel0 / qacc_ws0).  state_out receives n * (nq + 2nv): final qpos,
+ * qvel, qacc_warmstart.  stats (may be NULL): n * MGS_NSTATS as in
+ * mgs_rollout_out; stats[i * MGS_NSTATS + 2] != 0 means state i exceeded the
+ * contact / row capacity at some step and should be re-run wider.  Host
+ * pointers (mgs_simulate) or device pointers on a stream (mgs_simulate_device,
+ * n <= the batch capacity). */
+int mgs_simulate(mgs_batch* batch, const mgs_schedule* sched, int n, const double* qpos_init,
+                 const double* vstate_init, const double* mocap_quat, const double* phase_start,
+                 const double* phase_target, double* state_out, int32_t* stats);
+int mgs_simulate_device(mgs_batch* batch, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                        const double* d_vstate_init, const double* d_mocap_quat, const double* d_phase_start,
+                        const double* d_phase_target, double* d_state_out, int32_t* d_stats, void* stream);
 
 /* Duration (ms) of the last rollout kernel launch, measured with HIP events
  * on the launch stream (waits for it). */

@@ -339,10 +339,10 @@ int mgs_collision_free(mgs_batch* b, int n, const double* qpos_init, const doubl
   return MGS_OK;
 }
 
-int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
-                       const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
-                       const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
-                       int32_t* d_stats, void* stream) {
+static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                          const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
+                          const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
+                          int32_t* d_stats, const double* d_vstate, double* d_state_out, void* stream) {
   if (!b || !sched || n < 0) return fail(MGS_EINVAL, "mgs_rollout_device: bad argument%s");
   if (sched->nphase < 1 || sched->nphase > MGS_MAX_PHASES) return fail(MGS_EINVAL, "bad phase count%s");
   if (n == 0) return MGS_OK;
@@ -355,7 +355,7 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
   HIPCHK(hipEventRecord(b->e0, st));
 #define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
       md.I, md.D, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
-      d_fail_step, d_obj_qpos, d_stats)
+      d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out)
   switch (md.m.nv) {
 #define MGS_CASE(NV_) case NV_: MGS_LAUNCH_ROLL(NV_); break;
     MGS_NV_LIST(MGS_CASE)
@@ -365,6 +365,59 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->e1, st));
   return MGS_OK;
+}
+
+int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                       const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
+                       const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
+                       int32_t* d_stats, void* stream) {
+  return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
+                        d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream);
+}
+
+int mgs_simulate_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                        const double* d_vstate_init, const double* d_mocap_quat, const double* d_phase_start,
+                        const double* d_phase_target, double* d_state_out, int32_t* d_stats, void* stream) {
+  if (!b || !sched || !d_state_out || n < 0 || n > b->cap) return fail(MGS_EINVAL, "mgs_simulate_device: bad argument%s");
+  mgs_schedule s = *sched;   // no contact checks: a free simulation never stops early
+  for (int p = 0; p < MGS_MAX_PHASES; p++) { s.check_every[p] = 0; s.check_at_end[p] = 0; }
+  return launch_rollout(b, &s, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, nullptr, b->d_label,
+                        b->d_fail, b->d_objq, d_stats ? d_stats : b->d_stats, d_vstate_init, d_state_out, stream);
+}
+
+int mgs_simulate(mgs_batch* b, const mgs_schedule* sched, int n, const double* qpos_init,
+                 const double* vstate_init, const double* mocap_quat, const double* phase_start,
+                 const double* phase_target, double* state_out, int32_t* stats) {
+  if (!b || !sched || n < 0 || n > b->cap) return fail(MGS_EINVAL, "mgs_simulate: bad argument%s");
+  if (n == 0) return MGS_OK;
+  if (!qpos_init || !mocap_quat || !phase_start || !phase_target || !state_out)
+    return fail(MGS_EINVAL, "mgs_simulate: null argument%s");
+  const mgs_model_desc& d = b->m->desc;
+  int np = sched->nphase;
+  HIPCHK(hipSetDevice(b->m->device));
+  double *dv = nullptr, *ds = nullptr;
+  size_t nst = (size_t)n * (d.nq + 2 * d.nv);
+  if (hipMalloc(&ds, nst * sizeof(double)) != hipSuccess) return fail(MGS_ENOMEM, "state buffer allocation failed%s");
+  if (vstate_init && hipMalloc(&dv, (size_t)n * 2 * d.nv * sizeof(double)) != hipSuccess) {
+    hipFree(ds);
+    return fail(MGS_ENOMEM, "state buffer allocation failed%s");
+  }
+  int rc = MGS_OK;
+  if (hipMemcpy(b->d_qpos, qpos_init, sizeof(double) * n * d.nq, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(b->d_mquat, mocap_quat, sizeof(double) * n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(b->d_ps, phase_start, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(b->d_pt, phase_target, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice) != hipSuccess ||
+      (dv && hipMemcpy(dv, vstate_init, (size_t)n * 2 * d.nv * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
+    rc = fail(MGS_EHIP, "host to device copy failed%s");
+  if (!rc) rc = mgs_simulate_device(b, sched, n, b->d_qpos, dv, b->d_mquat, b->d_ps, b->d_pt, ds, nullptr, nullptr);
+  if (!rc && hipMemcpy(state_out, ds, nst * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(MGS_EHIP, "device to host copy failed%s");
+  if (!rc && stats &&
+      hipMemcpy(stats, b->d_stats, sizeof(int32_t) * n * MGS_NSTATS, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(MGS_EHIP, "device to host copy failed%s");
+  hipFree(ds);
+  if (dv) hipFree(dv);
+  return rc;
 }
 
 double mgs_last_collision_ms(mgs_batch* b) {

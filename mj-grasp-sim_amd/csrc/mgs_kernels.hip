@@ -3088,10 +3088,14 @@ DEVI int obj_contact_incl(const Mdl& md, const Dat& d) {
   return 0;
 }
 
-DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mpos, const double* mquat) {
+DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mpos, const double* mquat,
+                const double* vstate = nullptr) {
   int lane = lane_id();
+  int nv = md.m.nv;
+  const double* v0 = vstate ? vstate : DA(md, qvel0);
+  const double* w0 = vstate ? vstate + nv : DA(md, qacc_ws0);
   for (int k = lane; k < md.m.nq; k += WAVE) d.qpos[k] = qpos_init[k];
-  for (int k = lane; k < md.m.nv; k += WAVE) { d.qvel[k] = DA(md, qvel0)[k]; d.qacc_ws[k] = DA(md, qacc_ws0)[k]; }
+  for (int k = lane; k < nv; k += WAVE) { d.qvel[k] = v0[k]; d.qacc_ws[k] = w0[k]; }
   if (lane == 0) {
     for (int u = 0; u < (md.m.nu > 0 ? md.m.nu : 1); u++) d.ctrl[u] = 0.0;
     for (int k = 0; k < 3; k++) d.mocap_pos[k] = mpos ? mpos[k] : 0.0;
@@ -3134,7 +3138,8 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
                    const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
                    const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
                    uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
-                   int32_t* __restrict__ stats) {
+                   int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
+                   double* __restrict__ state_out) {
   extern __shared__ double smem[];
   Mdl md = mdarg;
   md.I = mI;
@@ -3159,7 +3164,8 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
   int np = sc.nphase;
   const double* ps = phase_start + (size_t)i * np * 3;
   const double* pt = phase_target + (size_t)i * np * 3;
-  reset(md, d, qpos_init + (size_t)i * md.m.nq, ps, mocap_quat + 4 * i);
+  reset(md, d, qpos_init + (size_t)i * md.m.nq, ps, mocap_quat + 4 * i,
+        vstate_init ? vstate_init + (size_t)i * 2 * md.m.nv : nullptr);
   int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
   PROF_DECL
   for (int p = 0; p < np && ok; p++) {
@@ -3204,6 +3210,15 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       sumcon += uni(d.NCON);
       sumefc += uni(d.NEFC);
       int ce = sc.check_every[p];
+      if (sc.vclip > 0.0) {
+        for (int k = lane; k < md.m.nv; k += WAVE) {
+          double v = d.qvel[k];
+          if (v > sc.vclip) v = sc.vclip;
+          if (v < -sc.vclip) v = -sc.vclip;
+          d.qvel[k] = v;
+        }
+        wsync();
+      }
       int tc = t + sc.check_offset[p];
       if (ce > 0 && tc > 0 && (tc % ce) == 0 && !obj_contact(md, d)) { ok = 0; fstep = gstep; }
       gstep++;
@@ -3219,6 +3234,12 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
     }
   }
   if (obj_qpos && sc.obj_qposadr >= 0 && lane < 7) obj_qpos[7 * i + lane] = d.qpos[sc.obj_qposadr + lane];
+  if (state_out) {
+    int nq = md.m.nq, nv = md.m.nv;
+    double* so = state_out + (size_t)i * (nq + 2 * nv);
+    for (int k = lane; k < nq; k += WAVE) so[k] = d.qpos[k];
+    for (int k = lane; k < nv; k += WAVE) { so[nq + k] = d.qvel[k]; so[nq + nv + k] = d.qacc_ws[k]; }
+  }
   PROF_FLUSH
 }
 

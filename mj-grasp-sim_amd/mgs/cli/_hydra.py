@@ -77,7 +77,24 @@ def compose(config_name: str, overrides: Optional[List[str]] = None, config_dir:
         for q in parts[:-1]:
             node = node.setdefault(q, {})
         node[parts[-1]] = v
+    _resolve(cfg, cfg)
     return cfg
+
+
+def _resolve(node, root):
+    """`${key}` / `${a.b}` interpolation of whole string values (omegaconf's
+    basic form); unknown keys are left as written."""
+    for k, v in list(node.items()):
+        if isinstance(v, dict):
+            _resolve(v, root)
+        elif isinstance(v, str) and v.startswith("${") and v.endswith("}"):
+            ref = root
+            for q in v[2:-1].split("."):
+                if not isinstance(ref, dict) or q not in ref:
+                    break
+                ref = ref[q]
+            else:
+                node[k] = ref
 
 
 def main(config_name: str) -> Callable:

@@ -58,6 +58,9 @@ def load_library(wide: bool = False):
     L.mgs_max_rows.restype = ctypes.c_int
     L.mgs_antipodal_contacts.argtypes = [ctypes.c_int, P(c_d), ctypes.c_int, ctypes.c_int, P(c_d), P(c_d), P(c_d),
                                          c_d, P(c_d), P(c_i), P(c_d)]
+    L.mgs_simulate.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
+                               P(c_i)]
+    L.mgs_simulate_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mgs_supports_nv.argtypes = [ctypes.c_int]
     L.mgs_supports_nv.restype = ctypes.c_int
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
@@ -210,6 +213,32 @@ class Engine:
                                     ctypes.byref(out)), "mgs_rollout")
         return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats,
                     kernel_ms=self.lib.mgs_last_kernel_ms(self._batch))
+
+    def simulate(self, plan, vstate=None, vclip=0.0):
+        """Free simulation (mgs_simulate): final qpos, qvel, qacc_warmstart and stats
+        of every state.  vstate (n, 2nv): initial qvel | qacc_warmstart per state
+        (None: the model's qvel0 / qacc_ws0); vclip > 0 clips qvel after each step."""
+        n = len(plan.qpos_init)
+        nq, nv = self.cm.nq, self.cm.nv
+        out = np.zeros((n, nq + 2 * nv))
+        stats = np.zeros((n, abi.MGS["MGS_NSTATS"]), np.int32)
+        if n:
+            npz = [0] * len(plan.nsteps)
+            sched = abi.make_schedule(plan.nsteps, npz, npz, plan.ctrl, -1, vclip=vclip)
+            q = np.ascontiguousarray(plan.qpos_init, np.float64)
+            mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
+            ps = np.ascontiguousarray(plan.phase_start, np.float64)
+            pt = np.ascontiguousarray(plan.phase_target, np.float64)
+            vs = None
+            if vstate is not None:
+                vs = np.ascontiguousarray(vstate, np.float64)
+                if vs.shape != (n, 2 * nv):
+                    raise ValueError(f"vstate has shape {vs.shape}, expected {(n, 2 * nv)}")
+            self._ck(self.lib.mgs_simulate(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
+                                         None if vs is None else ptr(vs, ctypes.c_double), ptr(mq, ctypes.c_double),
+                                         ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double),
+                                         ptr(out, ctypes.c_double), ptr(stats, ctypes.c_int32)), "mgs_simulate")
+        return dict(qpos=out[:, :nq], qvel=out[:, nq:nq + nv], qacc_warmstart=out[:, nq + nv:], stats=stats)
 
     def collision_free_device(self, n, d_qpos, d_mpos, d_mquat, d_out, predicate="any", stream=None):
         """Asynchronous launch on device pointers (ints) with inputs resident in HBM."""

@@ -366,3 +366,125 @@ class ClutterTableEnv:
             res["label"] = labels
             return res
         return labels
+
+    # -- scene generation (:155-222), many scenes at once -----------------------
+    def _expand(self, ref_vec, reduced, which):
+        """compiled-model qpos / qvel -> the reference layout (the camera and removed
+        objects keep their ref_vec entries)."""
+        out = np.array(ref_vec, dtype=np.float64).copy()
+        h = self._gripper_nq if which == "q" else self._gripper_nv
+        out[:h] = reduced[:h]
+        o = h
+        for name, qs, vs in self._obj_slices():
+            if name in self.removed:
+                continue
+            sl = qs if which == "q" else vs
+            w = sl.stop - sl.start
+            out[sl] = reduced[o:o + w]
+            o += w
+        return out
+
+    def free_plan(self, states, nsteps: int):
+        """RolloutPlan of a free simulation of integration states (rows of
+        `states`): ctrl and mocap held at the first state's, plus the per-state
+        initial (qvel | qacc_warmstart) in the compiled model's layout."""
+        parts = [self.split_state(s) for s in states]
+        q = np.stack([self._reduce(p["qpos"], "q") for p in parts])
+        vs = np.stack([np.concatenate([self._reduce(p["qvel"], "v"), self._reduce(p["qacc_warmstart"], "v")])
+                       for p in parts])
+        mp = np.ascontiguousarray(np.stack([p["mocap_pos"] for p in parts])[:, None, :])
+        mq = np.ascontiguousarray(np.stack([p["mocap_quat"] for p in parts]))
+        plan = RolloutPlan(nsteps=[int(nsteps)], check_every=[0], check_at_end=[0],
+                           ctrl=[np.array(parts[0]["ctrl"], np.float64)], qpos_init=q, mocap_quat=mq,
+                           phase_start=mp, phase_target=mp.copy(), obj_qposadr=-1)
+        return plan, vs
+
+    def apply_free(self, states, res, nsteps: int):
+        """write a free simulation's final (qpos, qvel, qacc_warmstart) back into
+        the states; time advances by nsteps timesteps, added one at a time as
+        mj_step does."""
+        out = np.array(states, dtype=np.float64, copy=True)
+        dt = float(self.model_for(out[0]).options["timestep"])
+        t = out[:, 0].copy()
+        for _ in range(int(nsteps)):
+            t += dt
+        for i in range(len(out)):
+            p = dict(self.split_state(out[i]))
+            p = dict(p, time=t[i:i + 1], qpos=self._expand(p["qpos"], res["qpos"][i], "q"),
+                     qvel=self._expand(p["qvel"], res["qvel"][i], "v"),
+                     qacc_warmstart=self._expand(p["qacc_warmstart"], res["qacc_warmstart"][i], "v"))
+            out[i] = self.join_state(p)
+        return out
+
+    def simulate_states(self, states, nsteps: int, vclip: float = 0.0, max_ncon: int = 128):
+        """advance integration states by `nsteps` mj_step each, all at once on the
+        GPU (mgs_simulate; one wave per state).  vclip > 0 clips every qvel entry
+        to +-vclip after each step.  States that exceed the contact capacity are
+        re-run at twice the capacity (as GravitylessObjectGrasping.rollout);
+        `last_overflow` counts those still over at max_ncon."""
+        states = np.atleast_2d(np.asarray(states, dtype=np.float64))
+        if len(states) == 0 or nsteps <= 0:
+            return states.copy()
+        plan, vs = self.free_plan(states, nsteps)
+        res = self.engine_for_state(states[0]).simulate(plan, vstate=vs, vclip=vclip)
+        cap = self.ncon_max
+        ov = np.nonzero(res["stats"][:, 2])[0]
+        while len(ov) and cap < max_ncon:
+            cap = min(2 * cap, max_ncon)
+            sub = self.engine_for_state(states[0], ncon_max=cap).simulate(plan.subset(ov), vstate=vs[ov],
+                                                                          vclip=vclip)
+            for k in res:
+                res[k][ov] = sub[k]
+            ov = ov[np.nonzero(sub["stats"][:, 2])[0]]
+        self.last_overflow = len(ov)
+        return self.apply_free(states, res, nsteps)
+
+    def gen_clutter_states(self, n_scenes: int, rng=None, steps_each: int = 900, steps_final: int = 9000,
+                           vclip: float = 50.0):
+        """gen_clutter (:197-222) for n_scenes piles at once: one random drop pose
+        per scene at (0, 0, 0.8) (scipy Rotation.random), shared by its objects;
+        each object in turn is placed there with every qvel zeroed and
+        `steps_each` steps run, then `steps_final` steps settle the pile; qvel is
+        clipped to +-vclip after every step (the reference clips before the next
+        step: the same trajectory, except that the final qvel is clipped too).
+        Returns the (n_scenes, state_size) integration states."""
+        from scipy.spatial.transform import Rotation
+        rng = np.random.default_rng(rng)
+        xyzw = Rotation.random(int(n_scenes), random_state=rng).as_quat().reshape(-1, 4)
+        drop = np.concatenate([np.tile([0.0, 0.0, 0.8], (len(xyzw), 1)), xyzw[:, [3, 0, 1, 2]]], axis=1)
+        states = np.tile(self._state, (len(xyzw), 1))
+        q0, v0 = 1, 1 + self.ref_nq
+        for _, qs, _ in self._obj_slices():
+            states[:, q0 + qs.start:q0 + qs.stop] = drop
+            states[:, v0:v0 + self.ref_nv] = 0.0
+            states = self.simulate_states(states, steps_each, vclip)
+        return self.simulate_states(states, steps_final, vclip)
+
+    def gen_clutter(self, rng=None, **kw):
+        """clutter_table.py:197-222 on this env's state."""
+        self._state = self.gen_clutter_states(1, rng, **kw)[0]
+
+    def settle(self):
+        """clutter_table.py:157-158: 10000 free steps."""
+        self._state = self.simulate_states(self._state, 10000)[0]
+
+    def is_stable_states(self, states, rounds: int = 10, steps: int = 100, tol: float = 5e-3):
+        """is_stable (:160-195) for many states: `rounds` x `steps` free steps, per
+        object the summed |position change| of every chunk; a state is stable if
+        the largest sum is < tol.  Returns (stable, largest sum, advanced states)."""
+        states = np.atleast_2d(np.asarray(states, dtype=np.float64))
+        delta = np.zeros((len(states), len(self.object_names)))
+        for _ in range(rounds):
+            new = self.simulate_states(states, steps)
+            for k, (_, qs, _) in enumerate(self._obj_slices()):
+                a = 1 + qs.start
+                delta[:, k] += np.sum(np.abs(new[:, a:a + 3] - states[:, a:a + 3]), axis=1)
+            states = new
+        mx = np.max(delta, axis=1, initial=0.0)
+        return mx < tol, mx, states
+
+    def is_stable(self) -> bool:
+        """clutter_table.py:160-195 (advances this env's state like the reference)."""
+        ok, _, st = self.is_stable_states(self._state)
+        self._state = st[0]
+        return bool(ok[0])

@@ -2207,13 +2207,15 @@ int oracle_collision_free(const mgs_model_desc* desc, const int32_t* I, const do
   return 0;
 }
 
-int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D,
-                   const mgs_schedule* sc, int n, const double* qpos_init,
-                   const double* mocap_quat, const double* phase_start, const double* phase_target,
-                   uint8_t* label, int32_t* fail_step, double* obj_qpos, int32_t* stats, int nthreads) {
+static void rollout_batch(const mgs_model_desc* desc, const int32_t* I, const double* D,
+                          const mgs_schedule* sc, int n, const double* qpos_init,
+                          const double* mocap_quat, const double* phase_start, const double* phase_target,
+                          uint8_t* label, int32_t* fail_step, double* obj_qpos, int32_t* stats,
+                          const double* vstate_init, double* state_out, int nthreads) {
   Mdl md = {desc, I, D};
   int np = sc->nphase;
   int obj_qposadr = sc->obj_qposadr;
+  int nq = desc->nq, nv = desc->nv;
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
   {
     Dat* d = dat_alloc(&md);
@@ -2221,7 +2223,11 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
     for (int i = 0; i < n; i++) {
       const double* ps = phase_start + (size_t)i * np * 3;
       const double* pt = phase_target + (size_t)i * np * 3;
-      reset(&md, d, qpos_init + (size_t)i * desc->nq, ps, mocap_quat + 4 * i);
+      reset(&md, d, qpos_init + (size_t)i * nq, ps, mocap_quat + 4 * i);
+      if (vstate_init) {
+        memcpy(d->qvel, vstate_init + (size_t)i * 2 * nv, sizeof(double) * nv);
+        memcpy(d->qacc_ws, vstate_init + (size_t)i * 2 * nv + nv, sizeof(double) * nv);
+      }
       int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
       for (int p = 0; p < np && ok; p++) {
         for (int u = 0; u < desc->nu; u++) d->ctrl[u] = sc->ctrl[p * 32 + u];
@@ -2234,6 +2240,11 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
           if (d->nefc > maxefc) maxefc = d->nefc;
           sumcon += d->ncon;
           sumefc += d->nefc;
+          if (sc->vclip > 0.0)
+            for (int k = 0; k < nv; k++) {
+              if (d->qvel[k] > sc->vclip) d->qvel[k] = sc->vclip;
+              if (d->qvel[k] < -sc->vclip) d->qvel[k] = -sc->vclip;
+            }
           int ce = sc->check_every[p];
           int tc = t + sc->check_offset[p];
           if (ce > 0 && tc > 0 && (tc % ce) == 0 && !obj_contact(&md, d)) { ok = 0; fstep = gstep; }
@@ -2241,7 +2252,7 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
         }
         if (ok && sc->check_at_end[p] && !obj_contact(&md, d)) { ok = 0; fstep = gstep - 1; }
       }
-      label[i] = (uint8_t)ok;
+      if (label) label[i] = (uint8_t)ok;
       if (fail_step) fail_step[i] = fstep;
       if (obj_qpos && obj_qposadr >= 0)
         for (int k = 0; k < 7; k++) obj_qpos[7 * i + k] = d->qpos[obj_qposadr + k];
@@ -2249,35 +2260,36 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
         int32_t* st = stats + MGS_NSTATS * i;
         st[0] = maxcon; st[1] = maxefc; st[2] = d->overflow; st[3] = d->iters; st[4] = sumcon; st[5] = sumefc;
       }
+      if (state_out) {
+        double* so = state_out + (size_t)i * (nq + 2 * nv);
+        memcpy(so, d->qpos, sizeof(double) * nq);
+        memcpy(so + nq, d->qvel, sizeof(double) * nv);
+        memcpy(so + nq + nv, d->qacc_ws, sizeof(double) * nv);
+      }
     }
     dat_free(d);
   }
+}
+
+int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D,
+                   const mgs_schedule* sc, int n, const double* qpos_init,
+                   const double* mocap_quat, const double* phase_start, const double* phase_target,
+                   uint8_t* label, int32_t* fail_step, double* obj_qpos, int32_t* stats, int nthreads) {
+  rollout_batch(desc, I, D, sc, n, qpos_init, mocap_quat, phase_start, phase_target, label, fail_step, obj_qpos,
+                stats, NULL, NULL, nthreads);
   return 0;
 }
 
-/* Free simulation (scene settling, gen_clutter restatement): nsteps with a
- * fixed mocap and ctrl from qpos_init and the model's initial velocity state;
- * after every step qvel is clipped to [-vclip, vclip] when vclip > 0
- * (clutter_table.py:215-221).  Returns the final qpos, qvel, qacc_warmstart. */
-int oracle_simulate(const mgs_model_desc* desc, const int32_t* I, const double* D, const double* qpos_init,
-                    const double* mocap_pos, const double* mocap_quat, const double* ctrl, int nsteps,
-                    double vclip, double* qpos_out, double* qvel_out, double* qacc_ws_out) {
-  Mdl md = {desc, I, D};
-  Dat* d = dat_alloc(&md);
-  reset(&md, d, qpos_init, mocap_pos, mocap_quat);
-  for (int u = 0; u < desc->nu; u++) d->ctrl[u] = ctrl[u];
-  for (int t = 0; t < nsteps; t++) {
-    step(&md, d);
-    if (vclip > 0.0)
-      for (int k = 0; k < desc->nv; k++) {
-        if (d->qvel[k] > vclip) d->qvel[k] = vclip;
-        if (d->qvel[k] < -vclip) d->qvel[k] = -vclip;
-      }
-  }
-  memcpy(qpos_out, d->qpos, sizeof(double) * desc->nq);
-  memcpy(qvel_out, d->qvel, sizeof(double) * desc->nv);
-  memcpy(qacc_ws_out, d->qacc_ws, sizeof(double) * desc->nv);
-  dat_free(d);
+/* mgs_simulate restated: the rollout loop from per-state (qpos, qvel, warmstart),
+ * final state out (n * (nq + 2nv)) */
+int oracle_simulate_batch(const mgs_model_desc* desc, const int32_t* I, const double* D,
+                          const mgs_schedule* sc, int n, const double* qpos_init, const double* vstate_init,
+                          const double* mocap_quat, const double* phase_start, const double* phase_target,
+                          double* state_out, int32_t* stats, int nthreads) {
+  mgs_schedule s = *sc;   /* no contact checks: a free simulation never stops early */
+  for (int p = 0; p < MGS_MAX_PHASES; p++) { s.check_every[p] = 0; s.check_at_end[p] = 0; }
+  rollout_batch(desc, I, D, &s, n, qpos_init, mocap_quat, phase_start, phase_target, NULL, NULL, NULL, stats,
+                vstate_init, state_out, nthreads);
   return 0;
 }
 

@@ -86,6 +86,26 @@ class OracleModel:
                              ptr(stats, ctypes.c_int32), nthreads)
         return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats)
 
+    def simulate_batch(self, plan, vstate=None, vclip=0.0, nthreads=1):
+        """mgs_simulate restated: final qpos, qvel, qacc_warmstart and stats of every state."""
+        n = len(plan.qpos_init)
+        cm = self.cm
+        sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                                  check_offset=getattr(plan, "check_offset", None), vclip=vclip)
+        out = np.zeros((n, cm.nq + 2 * cm.nv))
+        stats = np.zeros((n, abi.MGS["MGS_NSTATS"]), np.int32)
+        q = np.ascontiguousarray(plan.qpos_init, np.float64)
+        mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
+        ps = np.ascontiguousarray(plan.phase_start, np.float64)
+        pt = np.ascontiguousarray(plan.phase_target, np.float64)
+        vs = None if vstate is None else np.ascontiguousarray(vstate, np.float64)
+        lib().oracle_simulate_batch(*self._args(), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
+                                    None if vs is None else ptr(vs, ctypes.c_double), ptr(mq, ctypes.c_double),
+                                    ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double), ptr(out, ctypes.c_double),
+                                    ptr(stats, ctypes.c_int32), nthreads)
+        nq, nv = cm.nq, cm.nv
+        return dict(qpos=out[:, :nq], qvel=out[:, nq:nq + nv], qacc_warmstart=out[:, nq + nv:], stats=stats)
+
     def trace(self, qpos, mocap_pos, mocap_quat, ctrl, nsteps):
         nq = self.cm.nq
         tr = np.zeros((nsteps, nq))
@@ -99,14 +119,15 @@ class OracleModel:
     def simulate(self, qpos, mocap_pos, mocap_quat, ctrl, nsteps, vclip=0.0):
         """free simulation from qpos and the model's qvel0 / qacc_ws0; returns the
         final (qpos, qvel, qacc_warmstart)."""
-        q = np.zeros(self.cm.nq)
-        v = np.zeros(self.cm.nv)
-        w = np.zeros(self.cm.nv)
-        args = [np.ascontiguousarray(a, np.float64) for a in (qpos, mocap_pos, mocap_quat, ctrl)]
-        lib().oracle_simulate(*self._args(), *[ptr(a, ctypes.c_double) for a in args], int(nsteps),
-                              ctypes.c_double(vclip), ptr(q, ctypes.c_double), ptr(v, ctypes.c_double),
-                              ptr(w, ctypes.c_double))
-        return q, v, w
+        from types import SimpleNamespace
+        mp = np.asarray(mocap_pos, np.float64).reshape(1, 1, 3)
+        plan = SimpleNamespace(nsteps=[int(nsteps)], check_every=[0], check_at_end=[0],
+                               ctrl=[np.asarray(ctrl, np.float64)], obj_qposadr=-1, check_offset=None,
+                               qpos_init=np.asarray(qpos, np.float64).reshape(1, -1),
+                               mocap_quat=np.asarray(mocap_quat, np.float64).reshape(1, 4),
+                               phase_start=mp, phase_target=mp)
+        r = self.simulate_batch(plan, vclip=vclip)
+        return r["qpos"][0], r["qvel"][0], r["qacc_warmstart"][0]
 
     def contacts(self, qpos, mocap_pos, mocap_quat, maxc=64):
         pos = np.zeros((maxc, 3)); fr = np.zeros((maxc, 9)); dist = np.zeros(maxc); g = np.zeros((maxc, 2), np.int32)

@@ -3,48 +3,78 @@ import sys, os, ctypes
 import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'mj-grasp-sim_amd'))
 import mgs.core.engine as E
-E.LIB_PATH = E.LIB_PATH.replace('libmgs_gpu.so', 'libmgs_gpu_prof.so')
-from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
-from mgs.obj.selector import get_object
-from mgs.util.geo.transforms import SE3Pose
-from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, HORIZONS
-from mgs.sampler.antipodal import robotiq_candidates
-grip = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1, 0, 0, 0]), 'wxyz'))
-obj = get_object('003_cracker_box')
-env = GravitylessObjectGrasping(grip, obj)
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-H, J, W = robotiq_candidates(obj, 4 * N, seed=2)
-poses = SE3Pose.from_mat(H)
-q, mp, mq, _ = env.initial_state(poses, J)
-free = env.engine.collision_free(q, mp, mq)
-idx = np.nonzero(free)[0][:N]
-h = HORIZONS['h200']
-plan = env.rollout_plan(poses[idx], J[idx], nstep_lift=h['nstep_lift'], shake_steps=h['shake_steps'],
-                        close_steps=h['close_steps'], lift_check_every=h['lift_check_every'])
-L = E.load_library()
-L.mgs_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 64)()
-L.mgs_prof_read(buf)
-r = env.engine.rollout(plan)
-L.mgs_prof_read(buf)
-v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64), np.array(buf[39:42], dtype=np.float64)])
-cnt = np.array(buf[26:31], dtype=np.float64)
-names = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll: MPR', 'coll: feature+clip',
+
+NAMES = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll: MPR', 'coll: feature+clip',
          'crb', 'ldl(M)', 'act+passive+rne+smooth', 'con: J rows', 'con: G transform', 'con: params+blocks',
          'newton: setup', 'newton: hessian', 'newton: ldl+solve+jv', 'newton: linesearch', 'newton: eval+grad',
          'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
          'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
-         'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne', 'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)']
-tot = v.sum()
-print('N=%d collision-free candidates, kernel %.1f ms, labels %d, mean iters/step %.1f, overflow %d' % (
-    len(idx), r['kernel_ms'], r['label'].sum(), r['stats'][:, 3].sum() / max(1, r['stats'][:, 3].size) / 200, (r['stats'][:, 2] != 0).sum()))
-for n_, x in zip(names, v):
-    print('%-28s %6.1f%%  %.3g ticks' % (n_, 100 * x / tot, x))
-steps = len(idx) * 200
-print('ticks per candidate-step: %.0f' % (tot / steps))
+         'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne',
+         'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)']
 
-steps_exec = r['stats'][:, 3].size and None
-print('per candidate-step (all %d steps counted): narrowphase pairs %.2f, hits %.2f, support calls %.2f, big-hull support scans %.2f, big-hull pairs %.2f' % (
-    steps, cnt[0] / steps, cnt[1] / steps, cnt[2] / steps, cnt[3] / steps, cnt[4] / steps))
-cnt2 = np.array(buf[36:39], dtype=np.float64)
-print('per candidate-step: ls_eval calls %.2f, newton_eval calls %.2f, noslip sweeps %.2f' % tuple(cnt2 / steps))
+
+def report(buf, r, ncand, horizon):
+    v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64),
+                        np.array(buf[39:42], dtype=np.float64)])
+    cnt = np.array(buf[26:31], dtype=np.float64)
+    tot = v.sum()
+    print('N=%d candidates, kernel %.1f ms, labels %d, overflow %d' % (
+        ncand, r['kernel_ms'], r['label'].sum(), (r['stats'][:, 2] != 0).sum()))
+    for n_, x in zip(NAMES, v):
+        print('%-28s %6.1f%%  %.3g ticks' % (n_, 100 * x / tot, x))
+    steps = ncand * horizon
+    print('ticks per candidate-step: %.0f' % (tot / steps))
+    print('per candidate-step: narrowphase pairs %.2f, hits %.2f, support calls %.2f, big-hull scans %.2f, '
+          'big-hull pairs %.2f' % tuple(cnt / steps))
+
+
+def main():
+    E.LIB_PATH = E.LIB_PATH.replace('libmgs_gpu.so', 'libmgs_gpu_prof.so')
+    from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+    from mgs.obj.selector import get_object
+    from mgs.util.geo.transforms import SE3Pose
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, HORIZONS
+    from mgs.sampler.antipodal import robotiq_candidates
+    grip = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1, 0, 0, 0]), 'wxyz'))
+    obj = get_object('003_cracker_box')
+    env = GravitylessObjectGrasping(grip, obj)
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    H, J, W = robotiq_candidates(obj, 4 * N, seed=2)
+    poses = SE3Pose.from_mat(H)
+    q, mp, mq, _ = env.initial_state(poses, J)
+    free = env.engine.collision_free(q, mp, mq)
+    idx = np.nonzero(free)[0][:N]
+    h = HORIZONS['h200']
+    plan = env.rollout_plan(poses[idx], J[idx], nstep_lift=h['nstep_lift'], shake_steps=h['shake_steps'],
+                            close_steps=h['close_steps'], lift_check_every=h['lift_check_every'])
+    L = E.load_library()
+    L.mgs_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    buf = (ctypes.c_ulonglong * 64)()
+    L.mgs_prof_read(buf)
+    r = env.engine.rollout(plan)
+    L.mgs_prof_read(buf)
+    v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64), np.array(buf[39:42], dtype=np.float64)])
+    cnt = np.array(buf[26:31], dtype=np.float64)
+    names = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll: MPR', 'coll: feature+clip',
+             'crb', 'ldl(M)', 'act+passive+rne+smooth', 'con: J rows', 'con: G transform', 'con: params+blocks',
+             'newton: setup', 'newton: hessian', 'newton: ldl+solve+jv', 'newton: linesearch', 'newton: eval+grad',
+             'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
+             'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
+             'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne', 'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)']
+    tot = v.sum()
+    print('N=%d collision-free candidates, kernel %.1f ms, labels %d, mean iters/step %.1f, overflow %d' % (
+        len(idx), r['kernel_ms'], r['label'].sum(), r['stats'][:, 3].sum() / max(1, r['stats'][:, 3].size) / 200, (r['stats'][:, 2] != 0).sum()))
+    for n_, x in zip(names, v):
+        print('%-28s %6.1f%%  %.3g ticks' % (n_, 100 * x / tot, x))
+    steps = len(idx) * 200
+    print('ticks per candidate-step: %.0f' % (tot / steps))
+
+    steps_exec = r['stats'][:, 3].size and None
+    print('per candidate-step (all %d steps counted): narrowphase pairs %.2f, hits %.2f, support calls %.2f, big-hull support scans %.2f, big-hull pairs %.2f' % (
+        steps, cnt[0] / steps, cnt[1] / steps, cnt[2] / steps, cnt[3] / steps, cnt[4] / steps))
+    cnt2 = np.array(buf[36:39], dtype=np.float64)
+    print('per candidate-step: ls_eval calls %.2f, newton_eval calls %.2f, noslip sweeps %.2f' % tuple(cnt2 / steps))
+
+
+if __name__ == "__main__":
+    main()
