@@ -97,6 +97,40 @@ def clutter(n_per_obj, steps):
                 mean_ncon=float(res["stats"][:, 4].sum() / max(1, (2 * steps) * len(idx))))
 
 
+def scenes(n=256, steps_each=900, steps_final=9000, cpu_states=16, cpu_steps=200):
+    """gen_clutter (clutter_table.py:197-222) + is_stable (:160-195) for n Robotiq
+    piles of 5 fast-subset objects at once (mgs_simulate, one wave per pile), at
+    the reference's 5 x 900 + 9000 steps.  CPU: the oracle on 16 host threads,
+    cpu_states of the settled piles advanced cpu_steps free steps."""
+    from mgs.env.clutter_table import ClutterTableEnv
+    from mgs.gripper.selector import get_gripper
+    from mgs.obj.selector import get_objects
+    from mgs.util.geo.transforms import SE3Pose
+    from oracle import oracle as O
+    grip = get_gripper({"name": "Robotiq2f85Gripper"},
+                       default_pose=SE3Pose(np.array([5.0, 5.0, 1.0]), np.array([1.0, 0, 0, 0]), "wxyz"))
+    objs = get_objects({"name": "Fast_Data_Subset", "num_objects": 5}, 0)
+    env = ClutterTableEnv(grip, objs, scene_randomization=False)
+    env.gen_clutter_states(4, np.random.default_rng(1), steps_each=10, steps_final=10)     # warm-up
+    t0 = time.perf_counter()
+    st = env.gen_clutter_states(n, np.random.default_rng(0), steps_each, steps_final)
+    t1 = time.perf_counter()
+    ok, mx, _ = env.is_stable_states(st)
+    t2 = time.perf_counter()
+    steps = len(objs) * steps_each + steps_final
+    plan, vs = env.free_plan(st[:cpu_states], cpu_steps)
+    eng = env.engine_for_state(st[0])
+    om = O.OracleModel(env.model_for(st[0]), ncon_max=env.ncon_max, nefc_max=eng.desc.nefc_max)
+    t3 = time.perf_counter()
+    om.simulate_batch(plan, vstate=vs, nthreads=16)
+    dc = time.perf_counter() - t3
+    return dict(value=n / (t2 - t0), unit="settled + checked piles/s", piles=n, stable=int(ok.sum()),
+                gen_clutter_s=t1 - t0, is_stable_s=t2 - t1, pile_steps_per_s=n * (steps + 1000) / (t2 - t0),
+                nv=int(env.model.nv), overflow_after_escalation=int(env.last_overflow),
+                cpu_baseline=dict(value=cpu_states * cpu_steps / dc, unit="pile-steps/s", cores=16, kind="port",
+                                  sample=f"{cpu_states} settled piles x {cpu_steps} free steps"))
+
+
 def sampler(n=8192, subdiv=5):
     """Antipodal candidate ray casting on a 20480-face icosphere (a YCB-scale
     mesh): device kernel vs the C restatement on 16 host threads."""
@@ -150,6 +184,9 @@ def main():
             out = dict(config="c5", workload=f"Shadow Hand x settled 5-object pile, {r['candidates']} candidates, "
                                              f"mask + close {a.c5_steps} + lift {a.c5_steps} (reference: 3000 + 3000)",
                        unit="candidates/s", **r)
+        elif c == "scenes":
+            out = dict(config="scenes", workload="gen_clutter + is_stable, 256 Robotiq piles of 5 fast-subset objects, "
+                                                 "5 x 900 + 9000 + 1000 steps", **scenes())
         elif c == "sampler":
             out = dict(config="sampler", workload="antipodal ray casting, 8192 points x 20480-face icosphere",
                        **sampler())
