@@ -165,6 +165,7 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c3", "c4", "c5", "sampler"])
     ap.add_argument("--c5-steps", type=int, default=600)
     ap.add_argument("--c5-per-object", type=int, default=256)
+    ap.add_argument("--scene-piles", type=int, default=256)
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -185,8 +186,9 @@ def main():
                                              f"mask + close {a.c5_steps} + lift {a.c5_steps} (reference: 3000 + 3000)",
                        unit="candidates/s", **r)
         elif c == "scenes":
-            out = dict(config="scenes", workload="gen_clutter + is_stable, 256 Robotiq piles of 5 fast-subset objects, "
-                                                 "5 x 900 + 9000 + 1000 steps", **scenes())
+            out = dict(config="scenes", workload=f"gen_clutter + is_stable, {a.scene_piles} Robotiq piles of 5 "
+                                                 "fast-subset objects, 5 x 900 + 9000 + 1000 steps",
+                       **scenes(a.scene_piles))
         elif c == "sampler":
             out = dict(config="sampler", workload="antipodal ray casting, 8192 points x 20480-face icosphere",
                        **sampler())
