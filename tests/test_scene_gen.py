@@ -65,6 +65,64 @@ def test_gen_scene_config():
     assert cfg.only_collision_free is False and cfg.scene_batch == 1
 
 
+class _FakeEnv:
+    """host-logic stand-in for filter_grasps: object 0 at the origin, object 1
+    shifted; every other grasp collides, every third collision-free one holds."""
+    object_names, object_ids = ["a", "b"], ["id_a", "id_b"]
+
+    def get_obj_pose(self, name):
+        from mgs.util.geo.transforms import SE3Pose
+        return SE3Pose(np.array([0.0, 0.0, 0.0] if name == "a" else [1.0, 0.0, 0.0]), np.array([1.0, 0, 0, 0]),
+                       "wxyz")
+
+    def grasp_collision_mask(self, poses, joints):
+        return np.arange(len(poses)) % 2 == 0
+
+    def grasp_stable_mask(self, poses, joints, state, enough_stable=None, **kw):
+        from mgs.env.gravityless_object_grasping import apply_enough_stable
+        return apply_enough_stable(np.arange(len(poses)) % 3 == 0, enough_stable)
+
+
+def test_gen_scene_filter_grasps_host_logic(monkeypatch):
+    """gen_scene.py:48-159 host rules: object-frame grasps posed by the object
+    pose, collision split, enough_stable = min(128, 32 * num_objects), and the
+    reference's unshuffled object indices (fixed by fix_shuffle)."""
+    from mgs.cli import gen_scene
+    from mgs.cli._hydra import compose
+    eye = np.tile(np.eye(4, dtype=np.float32), (6, 1, 1))
+    eye[:, 2, 3] = np.arange(6)
+    monkeypatch.setattr(gen_scene, "get_env_from_dict", lambda cfg, sd: _FakeEnv())
+    monkeypatch.setattr(gen_scene, "get_grasps", lambda g, oid: (eye, np.zeros((6, 1))))
+    scene = {"env_state": {"state": np.zeros(3)}}
+    # 12 grasps, 6 collision-free (3 per object), 2 of them stable: the default
+    # enough_stable = min(128, 32 * 2) = 64 and an explicit 3 both fail
+    cfg = compose("gen_scene", ["num_objects=2", "enough_collision_free=6"])
+    assert cfg.get("enough_stable") is None
+    with pytest.raises(ValueError, match="Not enough stable"):
+        gen_scene.filter_grasps(cfg, scene, rng=0)
+    with pytest.raises(ValueError, match="Not enough stable"):
+        gen_scene.filter_grasps(compose("gen_scene", ["num_objects=2", "enough_collision_free=6",
+                                                      "enough_stable=3"]), scene, rng=0)
+    cfg = compose("gen_scene", ["num_objects=2", "enough_collision_free=6", "enough_stable=1",
+                                "save_collision_grasps=true", "only_collision_free=true"])
+    res, neg = gen_scene.filter_grasps(cfg, scene, rng=0)
+    assert [r["object_id"] for r in res] == ["id_a", "id_b"] and [len(r["pose"]) for r in res] == [3, 3]
+    assert np.allclose(res[1]["pose"][:, 0, 3], 1.0) and np.allclose(res[1]["pose"][:, 2, 3], [0, 2, 4])
+    assert [len(r["pose"]) for r in neg] == [3, 3]
+    with pytest.raises(ValueError, match="Not enough collision free"):
+        gen_scene.filter_grasps(compose("gen_scene", ["enough_collision_free=7"]), scene, rng=0)
+    # the stable pass keeps the reference's unshuffled indices unless fix_shuffle
+    from mgs.env.gravityless_object_grasping import apply_enough_stable
+    base = ["num_objects=2", "enough_collision_free=6", "enough_stable=2"]
+    quirk, _ = gen_scene.filter_grasps(compose("gen_scene", base), scene, rng=0)
+    fixed, _ = gen_scene.filter_grasps(compose("gen_scene", base + ["fix_shuffle=true"]), scene, rng=0)
+    perm = np.random.default_rng(0).permutation(6)
+    idx = np.array([0, 0, 0, 1, 1, 1])
+    stable = apply_enough_stable(np.arange(6) % 3 == 0, 2)
+    assert [r["object_id"] for r in quirk] == [["id_a", "id_b"][i] for i in np.unique(idx[stable])]
+    assert [r["object_id"] for r in fixed] == [["id_a", "id_b"][i] for i in np.unique(idx[perm][stable])]
+
+
 def test_oracle_free_simulation(senv):
     """simulate_batch is the rollout loop with its checks off: vstate = the model's
     qvel0 / qacc_ws0 equals vstate=None, identical states stay identical, vclip
