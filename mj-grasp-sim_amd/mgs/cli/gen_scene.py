@@ -47,7 +47,8 @@ def gen_stable_scene(cfg, rng=None):
     env = get_env(cfg.env, gripper=deepcopy(gripper), obj_list=deepcopy(obj_list))
     states = env.gen_clutter_states(int(cfg.get("scene_batch", 1)), rng,
                                     steps_each=int(cfg.get("steps_each", 900)),
-                                    steps_final=int(cfg.get("steps_final", 9000)))
+                                    steps_final=int(cfg.get("steps_final", 9000)),
+                                    ncon_max=cfg.get("settle_ncon"))
     stable, _, _ = env.is_stable_states(states)
     if not stable.any():
         raise ValueError("Scene unstable")

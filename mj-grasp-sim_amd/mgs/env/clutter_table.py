@@ -416,18 +416,21 @@ class ClutterTableEnv:
             out[i] = self.join_state(p)
         return out
 
-    def simulate_states(self, states, nsteps: int, vclip: float = 0.0, max_ncon: int = 128):
+    def simulate_states(self, states, nsteps: int, vclip: float = 0.0, max_ncon: int = 128,
+                        ncon_max: Optional[int] = None):
         """advance integration states by `nsteps` mj_step each, all at once on the
         GPU (mgs_simulate; one wave per state).  vclip > 0 clips every qvel entry
         to +-vclip after each step.  States that exceed the contact capacity are
         re-run at twice the capacity (as GravitylessObjectGrasping.rollout);
-        `last_overflow` counts those still over at max_ncon."""
+        `last_overflow` counts those still over at max_ncon.  ncon_max (default
+        the env's) sets the starting capacity: a smaller one with auto-sized rows
+        (engine.auto_capacity) keeps more piles in flight per CU."""
         states = np.atleast_2d(np.asarray(states, dtype=np.float64))
         if len(states) == 0 or nsteps <= 0:
             return states.copy()
         plan, vs = self.free_plan(states, nsteps)
-        res = self.engine_for_state(states[0]).simulate(plan, vstate=vs, vclip=vclip)
-        cap = self.ncon_max
+        cap = self.ncon_max if ncon_max is None else int(ncon_max)
+        res = self._sim_engine(states[0], cap).simulate(plan, vstate=vs, vclip=vclip)
         ov = np.nonzero(res["stats"][:, 2])[0]
         while len(ov) and cap < max_ncon:
             cap = min(2 * cap, max_ncon)
@@ -439,8 +442,21 @@ class ClutterTableEnv:
         self.last_overflow = len(ov)
         return self.apply_free(states, res, nsteps)
 
+    def _sim_engine(self, state, ncon_max):
+        """engine for a free simulation starting at capacity ncon_max: the env's own
+        capacity uses engine_for_state; a smaller one gets auto-sized rows."""
+        if ncon_max == self.ncon_max or self._nefc_max is not None:
+            return self.engine_for_state(state, ncon_max=ncon_max)
+        from mgs.core.engine import Engine, auto_capacity
+        cm = self.model_for(state)
+        key = ("sim", ncon_max)
+        if key not in self._engines:
+            self._engines[key] = Engine(cm, device=self.device, ncon_max=ncon_max,
+                                        nefc_max=auto_capacity(cm, ncon_max)[1])
+        return self._engines[key]
+
     def gen_clutter_states(self, n_scenes: int, rng=None, steps_each: int = 900, steps_final: int = 9000,
-                           vclip: float = 50.0):
+                           vclip: float = 50.0, ncon_max: Optional[int] = None):
         """gen_clutter (:197-222) for n_scenes piles at once: one random drop pose
         per scene at (0, 0, 0.8) (scipy Rotation.random), shared by its objects;
         each object in turn is placed there with every qvel zeroed and
@@ -457,8 +473,8 @@ class ClutterTableEnv:
         for _, qs, _ in self._obj_slices():
             states[:, q0 + qs.start:q0 + qs.stop] = drop
             states[:, v0:v0 + self.ref_nv] = 0.0
-            states = self.simulate_states(states, steps_each, vclip)
-        return self.simulate_states(states, steps_final, vclip)
+            states = self.simulate_states(states, steps_each, vclip, ncon_max=ncon_max)
+        return self.simulate_states(states, steps_final, vclip, ncon_max=ncon_max)
 
     def gen_clutter(self, rng=None, **kw):
         """clutter_table.py:197-222 on this env's state."""

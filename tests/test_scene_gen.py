@@ -145,19 +145,20 @@ def test_oracle_free_simulation(senv):
                           senv.split_state(st[0])["qpos"][senv._gripper_nq:senv._gripper_nq + 7])
 
 
-def _oracle_simulate_states(env, states, nsteps, vclip=0.0, max_ncon=128):
+def _oracle_simulate_states(env, states, nsteps, vclip=0.0, max_ncon=128, ncon_max=None):
     """ClutterTableEnv.simulate_states with the oracle in place of mgs_simulate
     (same capacity escalation)."""
     from oracle import oracle as O
     states = np.atleast_2d(states)
     plan, vs = env.free_plan(states, nsteps)
 
-    def run(nc, p, v):
-        eng = env.engine_for_state(states[0], ncon_max=nc)
+    def run(nc, p, v, first=False):
+        eng = env._sim_engine(states[0], nc) if first else env.engine_for_state(states[0], ncon_max=nc)
         om = O.OracleModel(env.model_for(states[0]), ncon_max=nc, nefc_max=eng.desc.nefc_max)
         return om.simulate_batch(p, vstate=v, vclip=vclip, nthreads=8)
 
-    res, cap = run(env.ncon_max, plan, vs), env.ncon_max
+    cap = env.ncon_max if ncon_max is None else ncon_max
+    res = run(cap, plan, vs, first=True)
     ov = np.nonzero(res["stats"][:, 2])[0]
     while len(ov) and cap < max_ncon:
         cap = min(2 * cap, max_ncon)
@@ -195,9 +196,14 @@ def test_gen_clutter_and_is_stable_gpu_vs_oracle():
     env = make_env()
     got = env.gen_clutter_states(2, np.random.default_rng(11), steps_each=80, steps_final=160)
     ref_env = make_env()
-    ref_env.simulate_states = lambda s, n, vclip=0.0: _oracle_simulate_states(env, s, n, vclip)
+    ref_env.simulate_states = lambda s, n, vclip=0.0, ncon_max=None: \
+        _oracle_simulate_states(env, s, n, vclip, ncon_max=ncon_max)
     ref = ref_env.gen_clutter_states(2, np.random.default_rng(11), steps_each=80, steps_final=160)
     assert np.array_equal(got, ref)
+    # a smaller starting capacity (auto-sized rows, escalation on overflow) is exact too
+    got24 = env.gen_clutter_states(2, np.random.default_rng(11), steps_each=80, steps_final=160, ncon_max=24)
+    ref24 = ref_env.gen_clutter_states(2, np.random.default_rng(11), steps_each=80, steps_final=160, ncon_max=24)
+    assert np.array_equal(got24, ref24)
     ok, mx, adv = env.is_stable_states(got, rounds=2, steps=40)
     ok2, mx2, adv2 = ref_env.is_stable_states(ref, rounds=2, steps=40)
     assert np.array_equal(mx, mx2) and np.array_equal(adv, adv2) and np.array_equal(ok, ok2)

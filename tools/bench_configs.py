@@ -97,7 +97,7 @@ def clutter(n_per_obj, steps):
                 mean_ncon=float(res["stats"][:, 4].sum() / max(1, (2 * steps) * len(idx))))
 
 
-def scenes(n=256, steps_each=900, steps_final=9000, cpu_states=16, cpu_steps=200):
+def scenes(n=256, steps_each=900, steps_final=9000, cpu_states=16, cpu_steps=200, ncon=None):
     """gen_clutter (clutter_table.py:197-222) + is_stable (:160-195) for n Robotiq
     piles of 5 fast-subset objects at once (mgs_simulate, one wave per pile), at
     the reference's 5 x 900 + 9000 steps.  CPU: the oracle on 16 host threads,
@@ -113,7 +113,7 @@ def scenes(n=256, steps_each=900, steps_final=9000, cpu_states=16, cpu_steps=200
     env = ClutterTableEnv(grip, objs, scene_randomization=False)
     env.gen_clutter_states(4, np.random.default_rng(1), steps_each=10, steps_final=10)     # warm-up
     t0 = time.perf_counter()
-    st = env.gen_clutter_states(n, np.random.default_rng(0), steps_each, steps_final)
+    st = env.gen_clutter_states(n, np.random.default_rng(0), steps_each, steps_final, ncon_max=ncon)
     t1 = time.perf_counter()
     ok, mx, _ = env.is_stable_states(st)
     t2 = time.perf_counter()
@@ -127,6 +127,7 @@ def scenes(n=256, steps_each=900, steps_final=9000, cpu_states=16, cpu_steps=200
     return dict(value=n / (t2 - t0), unit="settled + checked piles/s", piles=n, stable=int(ok.sum()),
                 gen_clutter_s=t1 - t0, is_stable_s=t2 - t1, pile_steps_per_s=n * (steps + 1000) / (t2 - t0),
                 nv=int(env.model.nv), overflow_after_escalation=int(env.last_overflow),
+                start_capacity=ncon or env.ncon_max,
                 cpu_baseline=dict(value=cpu_states * cpu_steps / dc, unit="pile-steps/s", cores=16, kind="port",
                                   sample=f"{cpu_states} settled piles x {cpu_steps} free steps"))
 
@@ -166,6 +167,7 @@ def main():
     ap.add_argument("--c5-steps", type=int, default=600)
     ap.add_argument("--c5-per-object", type=int, default=256)
     ap.add_argument("--scene-piles", type=int, default=256)
+    ap.add_argument("--scene-ncon", type=int, default=None)
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -188,7 +190,7 @@ def main():
         elif c == "scenes":
             out = dict(config="scenes", workload=f"gen_clutter + is_stable, {a.scene_piles} Robotiq piles of 5 "
                                                  "fast-subset objects, 5 x 900 + 9000 + 1000 steps",
-                       **scenes(a.scene_piles))
+                       **scenes(a.scene_piles, ncon=a.scene_ncon))
         elif c == "sampler":
             out = dict(config="sampler", workload="antipodal ray casting, 8192 points x 20480-face icosphere",
                        **sampler())
