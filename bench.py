@@ -87,6 +87,58 @@ def cpu_baseline(env, poses, joints, h, budget_s, threads):
     return dict(value=n / dt, n=n, seconds=dt, free=free, labels=labels)
 
 
+def host_info():
+    """the CPU the baseline ran on: model name and the cores visible to this process"""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "cpus_visible": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count()}
+
+
+def issue_summary():
+    """latency / issue view of the rollout kernel from the committed PMC pass
+    (profiles/pmc_rollout.json): instructions and wave cycles per executed
+    candidate-step; None if absent"""
+    p = os.path.join(ROOT, "profiles", "pmc_rollout.json")
+    if not os.path.isfile(p):
+        return None
+    with open(p) as f:
+        j = json.load(f)
+    sq, cs = j.get("sq", {}), j.get("executed_candidate_steps")
+    if not sq or not cs:
+        return None
+    out = {k.replace("SQ_", "").lower() + "_per_candidate_step": v / cs for k, v in sq.items()}
+    if "SQ_WAIT_ANY" in sq and "SQ_WAVE_CYCLES" in sq:
+        out["wait_any_frac"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
+    out["source"] = "profiles/pmc_rollout.json (" + j.get("kernel", "") + ")"
+    return out
+
+
+def e2e_api(env, poses, J, h, steps):
+    """the drop-in path as the reference's filter_to_stable calls it
+    (mgs/cli/filter_to_stable.py:39-50): host arrays in, collision mask, then
+    the rollout of the collision-free subset, labels back on the host; host
+    pose processing, schedule building and PCIe copies included"""
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        mask = env.grasp_collision_mask(poses, J)
+        idx = np.nonzero(mask)[0]
+        labels = np.zeros(len(poses), bool)
+        if len(idx):
+            labels[idx] = env.grasp_stability_evaluation_from_joints(
+                poses[idx], J[idx], nstep_lift=h["nstep_lift"], shake_steps=h["shake_steps"],
+                close_steps=h["close_steps"], lift_check_every=h["lift_check_every"])
+        ts.append(time.perf_counter() - t0)
+    return mask, labels, float(np.median(ts))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,12 +148,17 @@ def main():
     ap.add_argument("--horizon", default="h200")
     ap.add_argument("--solver", default=None, help="override the model's solver (Newton | PGS)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: OMP_NUM_THREADS, else the cores this process may run on)")
+    ap.add_argument("--e2e-steps", type=int, default=2,
+                    help="batches timed through the drop-in env API on host arrays (0 = skip)")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
     args = ap.parse_args()
 
+    if args.cpu_threads is None:
+        args.cpu_threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -209,6 +266,15 @@ def main():
     labels = d_label.cpu().numpy().astype(bool)
     fail = d_fail.cpu().numpy()
     stats = d_stats.cpu().numpy()
+    e2e = None
+    if args.e2e_steps > 0:
+        m2, l2, t2 = e2e_api(env, poses, J, h, args.e2e_steps)
+        e2e = {"candidates_per_s": N / t2, "ms_per_batch": t2 * 1e3, "batches": args.e2e_steps,
+               "labels_identical_to_device_run": bool(np.array_equal(m2, free) and np.array_equal(l2, labels)),
+               "what": "env.grasp_collision_mask + grasp_stability_evaluation_from_joints on host arrays "
+                       "(filter_to_stable.py:39-50 call pattern): host SE3 processing, schedule, PCIe "
+                       "copies and the host round trip between mask and rollout included; per rank, "
+                       "median over batches"}
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -236,6 +302,9 @@ def main():
                    "candidates_per_gpu": N, "horizon_steps": horizon, "solver": env.model.options.get("solver"),
                    "parallelism": f"batch split x{world}"},
         "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
+                   "rollouts_per_s": float(free.sum()) * world * args.steps / dt,
+                   "end_to_end_api": e2e,
+                   "issue": issue_summary(),
                    "rollout_kernel_ms": roll_avg, "collision_kernel_ms": float(np.mean(coll_ms)),
                    "executed_candidate_steps": steps_exec,
                    "mean_ncon": float(stats[:, 4].sum() / max(1, steps_exec)),
@@ -257,7 +326,7 @@ def main():
         n = cb["n"]
         agree = bool(np.array_equal(cb["free"], free[:n]) and np.array_equal(cb["labels"], labels[:n]))
         out["cpu_baseline"] = {"value": cb["value"], "unit": "candidates/s", "cores": args.cpu_threads,
-                               "kind": "port",
+                               "kind": "port", "host": host_info(),
                                "sample": f"first {n} of the {N} candidates (mask + h200 rollouts of the "
                                          f"collision-free ones), oracle/ C restatement, OpenMP "
                                          f"{args.cpu_threads} threads, {cb['seconds']:.1f} s",

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 7
+#define MGS_ABI_VERSION 8
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -76,6 +76,10 @@ extern "C" {
 #define MGS_EFC_FRICTION 1
 #define MGS_EFC_LIMIT 2
 #define MGS_EFC_CONTACT 3
+
+/* narrowphase of a geom pair (pair_kind) */
+#define MGS_PAIR_CONVEX 0          /* general convex path: MPR + feature clipping (mjc_Convex role) */
+#define MGS_PAIR_BOXBOX 1          /* box-box separating-axis collider (mjc_BoxBox role) */
 
 /* predicate for the collision pre-filter */
 #define MGS_PRED_ANY_CONTACT 0     /* data.ncon != 0            (gravityless :306-307) */
@@ -183,6 +187,8 @@ typedef struct mgs_model_desc {
   int32_t i_pair_geom1;
   int32_t i_pair_geom2;
   int32_t i_pair_condim;
+  int32_t i_pair_kind;      /* MGS_PAIR_CONVEX (MPR + feature clipping) or MGS_PAIR_BOXBOX
+                               (separating-axis box collider; MuJoCo's mjc_BoxBox role) */
   int32_t d_pair_friction;  /* 5 */
   int32_t d_pair_solref;    /* 2 */
   int32_t d_pair_solimp;    /* 5 */

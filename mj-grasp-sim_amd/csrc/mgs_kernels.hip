@@ -30,6 +30,7 @@
 #define K_MAXPOLY 40
 #define K_MPR_MAXIT 64
 #define K_FEAT_EPS 1e-5
+#define K_BB_MERGE 1e-6     // box-box: merge distance of manifold points, x face half size (oracle BB_MERGE)
 #define WAVE 64
 // row stride of the constraint matrix G (doubles).  An odd stride (NV + 1) makes
 // row walks bank-conflict free but measured no faster and costs 680 B of LDS
@@ -1212,6 +1213,37 @@ DEVI double dist2d(const P2* a, const P2* b) {
   return dx * dx + dy * dy;
 }
 
+// keep <= 4 of np manifold points (oracle select4): the deepest, the farthest
+// from it, the one spanning the largest triangle with those, the one farthest
+// from all three
+DEVI void select4(const P2* pts, const double* dep, int np, int* sel, int* ns) {
+  if (np <= 4) {
+    for (int i = 0; i < np; i++) sel[i] = i;
+    *ns = np;
+    return;
+  }
+  int i0 = 0;
+  for (int i = 1; i < np; i++) if (dep[i] > dep[i0]) i0 = i;
+  int i1 = -1; double bd = -1.0;
+  for (int i = 0; i < np; i++) { if (i == i0) continue; double v = dist2d(&pts[i], &pts[i0]); if (v > bd) { bd = v; i1 = i; } }
+  int i2 = -1; bd = -1.0;
+  for (int i = 0; i < np; i++) {
+    if (i == i0 || i == i1) continue;
+    double v = fabs(cross2(&pts[i0], &pts[i1], &pts[i]));
+    if (v > bd) { bd = v; i2 = i; }
+  }
+  int i3 = -1; bd = -1.0;
+  for (int i = 0; i < np; i++) {
+    if (i == i0 || i == i1 || i == i2) continue;
+    double v0 = dist2d(&pts[i], &pts[i0]), v1 = dist2d(&pts[i], &pts[i1]), v2 = dist2d(&pts[i], &pts[i2]);
+    double v = v0 < v1 ? v0 : v1;
+    v = v < v2 ? v : v2;
+    if (v > bd) { bd = v; i3 = i; }
+  }
+  sel[0] = i0; sel[1] = i1; sel[2] = i2; sel[3] = i3;
+  *ns = 4;
+}
+
 DEVI void add_contact(Dat& d, int ncon_max, int pair, int g1, int g2, const double* pos, const double* n,
                             const double* t1, const double* t2, double dist) {
   if (d.NCON >= ncon_max) { d.OVERFLOW |= 1; return; }
@@ -1276,33 +1308,8 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
     if (np == 0) {
       add_contact(d, ncmax, pair, g1, g2, mpos, n, t1, t2, -dn);
     } else {
-      int sel[4];
-      int ns;
-      if (np <= 4) {
-        for (int i = 0; i < np; i++) sel[i] = i;
-        ns = np;
-      } else {
-        int i0 = 0;
-        for (int i = 1; i < np; i++) if (dep[i] > dep[i0]) i0 = i;
-        int i1 = -1; double bd = -1.0;
-        for (int i = 0; i < np; i++) { if (i == i0) continue; double v = dist2d(&pts[i], &pts[i0]); if (v > bd) { bd = v; i1 = i; } }
-        int i2 = -1; bd = -1.0;
-        for (int i = 0; i < np; i++) {
-          if (i == i0 || i == i1) continue;
-          double v = fabs(cross2(&pts[i0], &pts[i1], &pts[i]));
-          if (v > bd) { bd = v; i2 = i; }
-        }
-        int i3 = -1; bd = -1.0;
-        for (int i = 0; i < np; i++) {
-          if (i == i0 || i == i1 || i == i2) continue;
-          double v0 = dist2d(&pts[i], &pts[i0]), v1 = dist2d(&pts[i], &pts[i1]), v2 = dist2d(&pts[i], &pts[i2]);
-          double v = v0 < v1 ? v0 : v1;
-          v = v < v2 ? v : v2;
-          if (v > bd) { bd = v; i3 = i; }
-        }
-        sel[0] = i0; sel[1] = i1; sel[2] = i2; sel[3] = i3;
-        ns = 4;
-      }
+      int sel[4], ns;
+      select4(pts, dep, np, sel, &ns);
       double sref = refB ? s2 : s1;
       for (int k = 0; k < ns; k++) {
         const P2* p = &pts[sel[k]];
@@ -1315,6 +1322,187 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   }
   wsync();
   PT(41);
+}
+
+// Box-box pair (oracle collide_boxbox; MuJoCo's dedicated mjc_BoxBox collider
+// takes box pairs instead of the convex path).  The 15 separating axes are
+// evaluated one per lane; lane 0 then picks the axis in the oracle's order
+// (box 1 faces, box 2 faces, edge-edge only if shallower by > 5 %) and builds
+// the manifold: the incident face clipped to the reference face rectangle, or
+// one point at the closest points of two edges.
+DEVI int bb_clip(P2* Q, int nq, int axis, double lim, double sgn, P2* buf) {
+  int no = 0;
+  for (int i = 0; i < nq; i++) {
+    const P2* cur = &Q[i];
+    const P2* prv = &Q[(i + nq - 1) % nq];
+    double dc = lim - sgn * (axis ? cur->y : cur->x);
+    double dp = lim - sgn * (axis ? prv->y : prv->x);
+    if (dc >= 0.0) {
+      if (dp < 0.0) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+      buf[no++] = *cur;
+    } else if (dp >= 0.0) {
+      buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+    }
+  }
+  for (int i = 0; i < no; i++) Q[i] = buf[i];
+  return no;
+}
+
+DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
+  int lane = lane_id();
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  const double *R1 = d.geom_xmat + 9 * g1, *R2 = d.geom_xmat + 9 * g2;
+  const double *x1 = d.geom_xpos + 3 * g1, *x2 = d.geom_xpos + 3 * g2;
+  const double *h1 = DA(md, geom_aabb) + 6 * g1 + 3, *h2 = DA(md, geom_aabb) + 6 * g2 + 3;
+  const double margin = DA(md, pair_margin)[pair];
+  double A1[9], A2[9], D[3];
+  for (int k = 0; k < 3; k++)
+    for (int i = 0; i < 3; i++) { A1[3 * k + i] = R1[3 * i + k]; A2[3 * k + i] = R2[3 * i + k]; }
+  sub3(D, x2, x1);
+  // lane q < 15 evaluates axis q: 0-2 box 1 faces, 3-5 box 2 faces, 6-14 edge pairs
+  double s = -INFINITY, L[3] = {0.0, 0.0, 0.0};
+  int valid = 0;
+  if (lane < 3) {
+    const double* Lf = A1 + 3 * lane;
+    double r2 = (h2[0] * fabs(dot3(A2, Lf)) + h2[1] * fabs(dot3(A2 + 3, Lf))) + h2[2] * fabs(dot3(A2 + 6, Lf));
+    s = fabs(dot3(D, Lf)) - (h1[lane] + r2);
+    valid = 1;
+  } else if (lane < 6) {
+    int k = lane - 3;
+    const double* Lf = A2 + 3 * k;
+    double r1 = (h1[0] * fabs(dot3(A1, Lf)) + h1[1] * fabs(dot3(A1 + 3, Lf))) + h1[2] * fabs(dot3(A1 + 6, Lf));
+    s = fabs(dot3(D, Lf)) - (h2[k] + r1);
+    valid = 1;
+  } else if (lane < 15) {
+    int a = (lane - 6) / 3, b = (lane - 6) % 3;
+    cross3(L, A1 + 3 * a, A2 + 3 * b);
+    double ll = sqrt(dot3(L, L));
+    if (!(ll < 1e-6)) {
+      L[0] = L[0] / ll; L[1] = L[1] / ll; L[2] = L[2] / ll;
+      double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));
+      double r2 = (h2[0] * fabs(dot3(A2, L)) + h2[1] * fabs(dot3(A2 + 3, L))) + h2[2] * fabs(dot3(A2 + 6, L));
+      s = fabs(dot3(D, L)) - (r1 + r2);
+      valid = 1;
+    }
+  }
+  if (__ballot(valid && s > margin)) return;     // a separating axis: no contact
+  // lane 0 gathers the 15 values in axis order
+  double sv[15], lx[15], ly[15], lz[15];
+  int vv[15];
+#pragma unroll
+  for (int q = 0; q < 15; q++) {
+    sv[q] = __shfl(s, q);
+    lx[q] = __shfl(L[0], q);
+    ly[q] = __shfl(L[1], q);
+    lz[q] = __shfl(L[2], q);
+    vv[q] = __shfl(valid, q);
+  }
+  if (lane == 0) {
+    double best = -INFINITY;
+    int code = -1;
+    for (int q = 0; q < 6; q++) if (sv[q] > best) { best = sv[q]; code = q; }
+    double ebest = -INFINITY, eL[3] = {0.0, 0.0, 0.0};
+    int ecode = -1;
+    for (int q = 6; q < 15; q++)
+      if (vv[q] && sv[q] > ebest) { ebest = sv[q]; ecode = q - 6; eL[0] = lx[q]; eL[1] = ly[q]; eL[2] = lz[q]; }
+    int ncmax = md.m.ncon_max;
+    double t1[3], t2[3];
+    if (ecode >= 0 && 1.05 * ebest > best) {
+      int a = ecode / 3, b = ecode % 3;
+      double n[3] = {eL[0], eL[1], eL[2]};
+      if (dot3(n, D) < 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+      double e1[3] = {x1[0], x1[1], x1[2]}, e2[3] = {x2[0], x2[1], x2[2]};
+      for (int k = 0; k < 3; k++) {
+        if (k != a) {
+          double sg = dot3(A1 + 3 * k, n) >= 0.0 ? h1[k] : -h1[k];
+          for (int i = 0; i < 3; i++) e1[i] = e1[i] + sg * A1[3 * k + i];
+        }
+        if (k != b) {
+          double sg = dot3(A2 + 3 * k, n) >= 0.0 ? -h2[k] : h2[k];
+          for (int i = 0; i < 3; i++) e2[i] = e2[i] + sg * A2[3 * k + i];
+        }
+      }
+      const double *U = A1 + 3 * a, *V = A2 + 3 * b;
+      double w[3];
+      sub3(w, e1, e2);
+      double bu = dot3(U, V), du = dot3(U, w), ev = dot3(V, w);
+      double den = 1.0 - bu * bu;
+      double ss = (bu * ev - du) / den, tt = (ev - bu * du) / den;
+      if (ss < -h1[a]) ss = -h1[a];
+      if (ss > h1[a]) ss = h1[a];
+      if (tt < -h2[b]) tt = -h2[b];
+      if (tt > h2[b]) tt = h2[b];
+      double pos[3];
+      for (int i = 0; i < 3; i++) pos[i] = 0.5 * ((e1[i] + ss * U[i]) + (e2[i] + tt * V[i]));
+      make_frame(n, t1, t2);
+      add_contact(d, ncmax, pair, g1, g2, pos, n, t1, t2, ebest);
+    } else {
+      int ref1 = code < 3, k = code % 3;
+      const double *RA = ref1 ? A1 : A2, *RB = ref1 ? A2 : A1, *hA = ref1 ? h1 : h2, *hB = ref1 ? h2 : h1;
+      const double *xA = ref1 ? x1 : x2, *xB = ref1 ? x2 : x1;
+      double DAB[3];
+      sub3(DAB, xB, xA);
+      double nr[3] = {RA[3 * k], RA[3 * k + 1], RA[3 * k + 2]};
+      if (dot3(DAB, nr) < 0.0) { nr[0] = -nr[0]; nr[1] = -nr[1]; nr[2] = -nr[2]; }
+      double n[3] = {nr[0], nr[1], nr[2]};
+      if (!ref1) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+      int ku = (k + 1) % 3, kv = (k + 2) % 3;
+      const double *u = RA + 3 * ku, *v = RA + 3 * kv;
+      double cA[3];
+      for (int i = 0; i < 3; i++) cA[i] = xA[i] + hA[k] * nr[i];
+      int j = 0;
+      double bj = fabs(dot3(RB, nr));
+      for (int q = 1; q < 3; q++) { double c = fabs(dot3(RB + 3 * q, nr)); if (c > bj) { bj = c; j = q; } }
+      double sB = dot3(RB + 3 * j, nr) > 0.0 ? -hB[j] : hB[j];
+      int jp = (j + 1) % 3, jq = (j + 2) % 3;
+      P2* poly = d.poly;
+      P2* buf = d.poly + 16;
+      P2* pts = d.poly + 32;
+      double* dep = d.pdep;
+      double deep = INFINITY, deep_c[3] = {0.0, 0.0, 0.0};
+      for (int c = 0; c < 4; c++) {
+        double cp = (c == 0 || c == 3) ? 1.0 : -1.0, cq = (c < 2) ? 1.0 : -1.0;
+        double P[3], rel[3];
+        for (int i = 0; i < 3; i++)
+          P[i] = ((xB[i] + sB * RB[3 * j + i]) + (cp * hB[jp]) * RB[3 * jp + i]) + (cq * hB[jq]) * RB[3 * jq + i];
+        sub3(rel, P, cA);
+        poly[c].x = dot3(rel, u);
+        poly[c].y = dot3(rel, v);
+        poly[c].h = dot3(rel, nr);
+        if (poly[c].h < deep) { deep = poly[c].h; deep_c[0] = P[0]; deep_c[1] = P[1]; deep_c[2] = P[2]; }
+      }
+      int nq = 4;
+      nq = bb_clip(poly, nq, 0, hA[ku], 1.0, buf);
+      if (nq) nq = bb_clip(poly, nq, 0, hA[ku], -1.0, buf);
+      if (nq) nq = bb_clip(poly, nq, 1, hA[kv], 1.0, buf);
+      if (nq) nq = bb_clip(poly, nq, 1, hA[kv], -1.0, buf);
+      double mtol = K_BB_MERGE * (hA[ku] > hA[kv] ? hA[ku] : hA[kv]);
+      mtol = mtol * mtol;
+      int np = 0;
+      for (int i = 0; i < nq; i++) {
+        if (!(poly[i].h < margin)) continue;
+        int dup = 0;
+        for (int q = 0; q < np; q++) if (dist2d(&pts[q], &poly[i]) < mtol) dup = 1;
+        if (!dup) { pts[np] = poly[i]; dep[np] = -poly[i].h; np++; }
+      }
+      make_frame(n, t1, t2);
+      if (np == 0) {
+        double pos[3];
+        for (int i = 0; i < 3; i++) pos[i] = deep_c[i] - (0.5 * deep) * nr[i];
+        add_contact(d, ncmax, pair, g1, g2, pos, n, t1, t2, deep);
+      } else {
+        int sel[4], ns;
+        select4(pts, dep, np, sel, &ns);
+        for (int q = 0; q < ns; q++) {
+          const P2* p = &pts[sel[q]];
+          double pos[3];
+          for (int i = 0; i < 3; i++) pos[i] = ((cA[i] + p->x * u[i]) + p->y * v[i]) + (0.5 * p->h) * nr[i];
+          add_contact(d, ncmax, pair, g1, g2, pos, n, t1, t2, p->h);
+        }
+      }
+    }
+  }
+  wsync();
 }
 
 #define OBB_FN DEVI
@@ -1385,7 +1573,8 @@ DEVI void collision(const Mdl& md, Dat& d) {
     while (mask) {
       int b = __ffsll((long long)mask) - 1;
       mask &= mask - 1ull;
-      collide_pair(md, d, c0 + b);
+      if (IA(md, pair_kind)[c0 + b] == MGS_PAIR_BOXBOX) collide_boxbox(md, d, c0 + b);
+      else collide_pair(md, d, c0 + b);
     }
   }
 }
@@ -3155,8 +3344,9 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       if (stats)
         for (int k = 0; k < MGS_NSTATS; k++) stats[MGS_NSTATS * i + k] = 0;
     }
-    if (obj_qpos && sc.obj_qposadr >= 0 && lane < 7)
-      obj_qpos[7 * i + lane] = qpos_init[(size_t)i * md.m.nq + sc.obj_qposadr + lane];
+    // no object joint reported (obj_qposadr < 0): zeros, as the oracle's output
+    if (obj_qpos && lane < 7)
+      obj_qpos[7 * i + lane] = sc.obj_qposadr >= 0 ? qpos_init[(size_t)i * md.m.nq + sc.obj_qposadr + lane] : 0.0;
     return;
   }
   Dat d;
@@ -3233,7 +3423,7 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       st[0] = maxcon; st[1] = maxefc; st[2] = d.OVERFLOW; st[3] = d.ITERS; st[4] = sumcon; st[5] = sumefc;
     }
   }
-  if (obj_qpos && sc.obj_qposadr >= 0 && lane < 7) obj_qpos[7 * i + lane] = d.qpos[sc.obj_qposadr + lane];
+  if (obj_qpos && lane < 7) obj_qpos[7 * i + lane] = sc.obj_qposadr >= 0 ? d.qpos[sc.obj_qposadr + lane] : 0.0;
   if (state_out) {
     int nq = md.m.nq, nv = md.m.nv;
     double* so = state_out + (size_t)i * (nq + 2 * nv);

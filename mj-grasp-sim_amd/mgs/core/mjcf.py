@@ -51,6 +51,7 @@ _JOINT_DEFAULTS = dict(type="hinge", axis="0 0 1", pos="0 0 0", range="0 0",
                        solimpfriction="0.9 0.95 0.001 0.5 2", margin="0", ref="0")
 _EQ_DEFAULTS = dict(solref="0.02 1", solimp="0.9 0.95 0.001 0.5 2", active="true")
 
+PAIR_CONVEX, PAIR_BOXBOX = 0, 1   # pair_kind: narrowphase used for the pair (mgs_gpu.h MGS_PAIR_*)
 CYL_SIDES = 16   # cylinder collision geoms: 32-vertex prisms (a cap fits one contact feature, K_MAXF)
 _JNT_TYPES = {"free": 0, "ball": 1, "slide": 2, "hinge": 3}
 
@@ -698,7 +699,7 @@ class Compiler:
                                solref=_fv(g, "solref"), solimp=_fv(g, "solimp"),
                                margin=float(g.get("margin", "0")), gap=float(g.get("gap", "0")),
                                priority=int(g.get("priority", "0")), solmix=float(g.get("solmix", "1")),
-                               side=side, name=g.get("name", ""), radius=radius))
+                               side=side, name=g.get("name", ""), radius=radius, type=t))
         # --- admissible pairs
         excl = set()
         for b1, b2 in self.excludes:
@@ -739,7 +740,10 @@ class Compiler:
                     si = mix * g1["solimp"] + (1 - mix) * g2["solimp"]
                 if condim not in (1, 3, 4, 6):
                     raise MJCFError(f"condim {condim} not supported")
-                pairs.append(dict(g1=a, g2=b, condim=condim,
+                # collider: MuJoCo dispatches box-box pairs to its dedicated box
+                # collider (mjc_BoxBox), everything else here to the convex path
+                kind = PAIR_BOXBOX if (g1["type"] == "box" and g2["type"] == "box") else PAIR_CONVEX
+                pairs.append(dict(g1=a, g2=b, condim=condim, kind=kind,
                                   friction=np.array([fr[0], fr[0], fr[1], fr[2], fr[2]]),
                                   solref=np.array(sr), solimp=np.array(si),
                                   margin=max(g1["margin"], g2["margin"]) - max(g1["gap"], g2["gap"])))
@@ -896,6 +900,7 @@ class Compiler:
         cm.pair_geom1 = np.array([p["g1"] for p in pairs], np.int32)
         cm.pair_geom2 = np.array([p["g2"] for p in pairs], np.int32)
         cm.pair_condim = np.array([p["condim"] for p in pairs], np.int32)
+        cm.pair_kind = np.array([p["kind"] for p in pairs], np.int32)
         cm.pair_friction = np.array([p["friction"] for p in pairs]).reshape(-1, 5)
         cm.pair_solref = np.array([p["solref"] for p in pairs]).reshape(-1, 2)
         cm.pair_solimp = np.array([p["solimp"] for p in pairs]).reshape(-1, 5)
@@ -1091,7 +1096,7 @@ class CompiledModel:
         put_i("hull_vertnum", self.hull_vertnum)
         put_d("hull_vert", self.hull_vert)
         put_d("hull_center", self.hull_center)
-        for n in ["pair_geom1", "pair_geom2", "pair_condim"]:
+        for n in ["pair_geom1", "pair_geom2", "pair_condim", "pair_kind"]:
             put_i(n, getattr(self, n))
         for n in ["pair_friction", "pair_solref", "pair_solimp", "pair_margin"]:
             put_d(n, getattr(self, n))

@@ -15,6 +15,18 @@ import numpy as np
 from scipy.spatial.transform import Rotation
 
 
+_PAR_MIN, _PAR_CHUNKS = 2048, 4
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(_PAR_CHUNKS)
+    return _POOL
+
+
 def _wxyz_to_xyzw(q):
     return np.concatenate([q[..., 1:], q[..., :1]], axis=-1)
 
@@ -64,7 +76,15 @@ class SE3Pose:
             raise AssertionError("from_mat expects (...,4,4)")
         if type != "wxyz":
             raise ValueError(type)
-        q = Rotation.from_matrix(mat[..., :3, :3]).as_quat(canonical=False)
+        R = mat[..., :3, :3]
+        if R.ndim == 3 and len(R) >= _PAR_MIN:
+            # scipy orthogonalises every float32 matrix with an SVD (most of the
+            # host time of a large batch); chunks are independent, so a thread
+            # pool over row blocks returns the identical quaternions
+            q = np.concatenate(list(_pool().map(lambda c: Rotation.from_matrix(c).as_quat(canonical=False),
+                                                 np.array_split(R, _PAR_CHUNKS))))
+        else:
+            q = Rotation.from_matrix(R).as_quat(canonical=False)
         return cls(mat[..., :3, 3], _xyzw_to_wxyz(q), type)
 
     def __getitem__(self, idx) -> "SE3Pose":

@@ -42,6 +42,9 @@
 #define O_MAXPOLY 40
 #define O_MPR_MAXIT 64
 #define O_FEAT_EPS 1e-5
+#ifndef BB_MERGE
+#define BB_MERGE 1e-6       /* box-box: merge distance of manifold points, x face half size */
+#endif
 
 /* ------------------------------------------------------------------------ */
 typedef struct {
@@ -943,6 +946,36 @@ static inline double dist2d(const P2* a, const P2* b) {
   return dx * dx + dy * dy;
 }
 
+/* keep <= 4 of np manifold points: the deepest, the farthest from it, the one
+ * spanning the largest triangle with those, the one farthest from all three */
+static void select4(const P2* pts, const double* dep, int np, int* sel, int* ns) {
+  if (np <= 4) {
+    for (int i = 0; i < np; i++) sel[i] = i;
+    *ns = np;
+    return;
+  }
+  int i0 = 0;
+  for (int i = 1; i < np; i++) if (dep[i] > dep[i0]) i0 = i;
+  int i1 = -1; double bd = -1.0;
+  for (int i = 0; i < np; i++) { if (i == i0) continue; double v = dist2d(&pts[i], &pts[i0]); if (v > bd) { bd = v; i1 = i; } }
+  int i2 = -1; bd = -1.0;
+  for (int i = 0; i < np; i++) {
+    if (i == i0 || i == i1) continue;
+    double v = fabs(cross2(&pts[i0], &pts[i1], &pts[i]));
+    if (v > bd) { bd = v; i2 = i; }
+  }
+  int i3 = -1; bd = -1.0;
+  for (int i = 0; i < np; i++) {
+    if (i == i0 || i == i1 || i == i2) continue;
+    double v0 = dist2d(&pts[i], &pts[i0]), v1 = dist2d(&pts[i], &pts[i1]), v2 = dist2d(&pts[i], &pts[i2]);
+    double v = v0 < v1 ? v0 : v1;
+    v = v < v2 ? v : v2;
+    if (v > bd) { bd = v; i3 = i; }
+  }
+  sel[0] = i0; sel[1] = i1; sel[2] = i2; sel[3] = i3;
+  *ns = 4;
+}
+
 static void add_contact(const Mdl* md, Dat* d, int pair, int g1, int g2, const double* pos,
                         const double* n, const double* t1, const double* t2, double dist) {
   if (d->ncon >= d->ncon_max) { d->overflow |= 1; return; }
@@ -995,33 +1028,8 @@ static void collide_pair(const Mdl* md, Dat* d, int pair) {
     add_contact(md, d, pair, g1, g2, mpos, n, t1, t2, dist);
     return;
   }
-  int sel[4];
-  int ns;
-  if (np <= 4) {
-    for (int i = 0; i < np; i++) sel[i] = i;
-    ns = np;
-  } else {
-    int i0 = 0;
-    for (int i = 1; i < np; i++) if (dep[i] > dep[i0]) i0 = i;
-    int i1 = -1; double bd = -1.0;
-    for (int i = 0; i < np; i++) { if (i == i0) continue; double v = dist2d(&pts[i], &pts[i0]); if (v > bd) { bd = v; i1 = i; } }
-    int i2 = -1; bd = -1.0;
-    for (int i = 0; i < np; i++) {
-      if (i == i0 || i == i1) continue;
-      double v = fabs(cross2(&pts[i0], &pts[i1], &pts[i]));
-      if (v > bd) { bd = v; i2 = i; }
-    }
-    int i3 = -1; bd = -1.0;
-    for (int i = 0; i < np; i++) {
-      if (i == i0 || i == i1 || i == i2) continue;
-      double v0 = dist2d(&pts[i], &pts[i0]), v1 = dist2d(&pts[i], &pts[i1]), v2 = dist2d(&pts[i], &pts[i2]);
-      double v = v0 < v1 ? v0 : v1;
-      v = v < v2 ? v : v2;
-      if (v > bd) { bd = v; i3 = i; }
-    }
-    sel[0] = i0; sel[1] = i1; sel[2] = i2; sel[3] = i3;
-    ns = 4;
-  }
+  int sel[4], ns;
+  select4(pts, dep, np, sel, &ns);
   double sref = refB ? s2 : s1;
   for (int k = 0; k < ns; k++) {
     const P2* p = &pts[sel[k]];
@@ -1029,6 +1037,183 @@ static void collide_pair(const Mdl* md, Dat* d, int pair) {
     double pos[3];
     for (int c = 0; c < 3; c++) pos[c] = (p->x * t1[c] + p->y * t2[c]) + hm * n[c];
     add_contact(md, d, pair, g1, g2, pos, n, t1, t2, -dep[sel[k]]);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Box-box: the dedicated collider MuJoCo dispatches box pairs to (mjc_BoxBox,
+ * engine_collision_box.c) instead of the general convex path.  Separating-axis
+ * test over the 3 + 3 face normals and the 9 edge-edge cross products; the axis
+ * of least penetration wins, ties going to box 1's faces, then box 2's, and an
+ * edge-edge axis only when it is shallower than the best face axis by more than
+ * 5 % of the depth (faces are the stable choice for resting boxes).  The face
+ * choice is a deterministic function of the poses, so a symmetric wedge (two
+ * gripper pads closed on each other) keeps one normal instead of flipping
+ * between the two faces as MPR's portal does.
+ * Face axis: the incident face of the other box (the face most anti-parallel
+ * to the normal) is clipped against the reference face rectangle; every clipped
+ * vertex below the reference plane is a contact at the midpoint between the
+ * two surfaces (<= 8; the 4 spanning ones are kept as in collide_pair).
+ * Edge axis: one contact at the closest points of the two edges. */
+static int bb_clip(P2* Q, int nq, int axis, double lim, double sgn) {
+  /* keep sgn * coord <= lim, coord = x (axis 0) or y (axis 1) */
+  P2 buf[16];
+  int no = 0;
+  for (int i = 0; i < nq; i++) {
+    const P2* cur = &Q[i];
+    const P2* prv = &Q[(i + nq - 1) % nq];
+    double dc = lim - sgn * (axis ? cur->y : cur->x);
+    double dp = lim - sgn * (axis ? prv->y : prv->x);
+    if (dc >= 0.0) {
+      if (dp < 0.0) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+      buf[no++] = *cur;
+    } else if (dp >= 0.0) {
+      buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+    }
+  }
+  for (int i = 0; i < no; i++) Q[i] = buf[i];
+  return no;
+}
+
+static void collide_boxbox(const Mdl* md, Dat* d, int pair) {
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  const double *R1 = d->geom_xmat + 9 * g1, *R2 = d->geom_xmat + 9 * g2;
+  const double *x1 = d->geom_xpos + 3 * g1, *x2 = d->geom_xpos + 3 * g2;
+  const double *h1 = DA(md, geom_aabb) + 6 * g1 + 3, *h2 = DA(md, geom_aabb) + 6 * g2 + 3;
+  const double margin = DA(md, pair_margin)[pair];
+  double A1[9], A2[9], D[3];
+  for (int k = 0; k < 3; k++)
+    for (int i = 0; i < 3; i++) { A1[3 * k + i] = R1[3 * i + k]; A2[3 * k + i] = R2[3 * i + k]; }
+  sub3(D, x2, x1);
+  double best = -INFINITY;
+  int code = -1;
+  for (int k = 0; k < 3; k++) {
+    const double* L = A1 + 3 * k;
+    double r2 = (h2[0] * fabs(dot3(A2, L)) + h2[1] * fabs(dot3(A2 + 3, L))) + h2[2] * fabs(dot3(A2 + 6, L));
+    double s = fabs(dot3(D, L)) - (h1[k] + r2);
+    if (s > margin) return;
+    if (s > best) { best = s; code = k; }
+  }
+  for (int k = 0; k < 3; k++) {
+    const double* L = A2 + 3 * k;
+    double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));
+    double s = fabs(dot3(D, L)) - (h2[k] + r1);
+    if (s > margin) return;
+    if (s > best) { best = s; code = 3 + k; }
+  }
+  double ebest = -INFINITY, eL[3] = {0.0, 0.0, 0.0};
+  int ecode = -1;
+  for (int a = 0; a < 3; a++)
+    for (int b = 0; b < 3; b++) {
+      double L[3];
+      cross3(L, A1 + 3 * a, A2 + 3 * b);
+      double ll = sqrt(dot3(L, L));
+      if (ll < 1e-6) continue;      /* (nearly) parallel edges: covered by the face axes */
+      L[0] = L[0] / ll; L[1] = L[1] / ll; L[2] = L[2] / ll;
+      double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));
+      double r2 = (h2[0] * fabs(dot3(A2, L)) + h2[1] * fabs(dot3(A2 + 3, L))) + h2[2] * fabs(dot3(A2 + 6, L));
+      double s = fabs(dot3(D, L)) - (r1 + r2);
+      if (s > margin) return;
+      if (s > ebest) { ebest = s; ecode = 3 * a + b; eL[0] = L[0]; eL[1] = L[1]; eL[2] = L[2]; }
+    }
+  double t1[3], t2[3];
+  if (ecode >= 0 && 1.05 * ebest > best) {
+    /* edge-edge: n from box 1 towards box 2 */
+    int a = ecode / 3, b = ecode % 3;
+    double n[3] = {eL[0], eL[1], eL[2]};
+    if (dot3(n, D) < 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+    double e1[3] = {x1[0], x1[1], x1[2]}, e2[3] = {x2[0], x2[1], x2[2]};
+    for (int k = 0; k < 3; k++) {
+      if (k != a) {
+        double s = dot3(A1 + 3 * k, n) >= 0.0 ? h1[k] : -h1[k];
+        for (int i = 0; i < 3; i++) e1[i] = e1[i] + s * A1[3 * k + i];
+      }
+      if (k != b) {
+        double s = dot3(A2 + 3 * k, n) >= 0.0 ? -h2[k] : h2[k];
+        for (int i = 0; i < 3; i++) e2[i] = e2[i] + s * A2[3 * k + i];
+      }
+    }
+    const double *U = A1 + 3 * a, *V = A2 + 3 * b;
+    double w[3];
+    sub3(w, e1, e2);
+    double bu = dot3(U, V), du = dot3(U, w), ev = dot3(V, w);
+    double den = 1.0 - bu * bu;
+    double s = (bu * ev - du) / den, t = (ev - bu * du) / den;
+    if (s < -h1[a]) s = -h1[a];
+    if (s > h1[a]) s = h1[a];
+    if (t < -h2[b]) t = -h2[b];
+    if (t > h2[b]) t = h2[b];
+    double pos[3];
+    for (int i = 0; i < 3; i++) pos[i] = 0.5 * ((e1[i] + s * U[i]) + (e2[i] + t * V[i]));
+    make_frame(n, t1, t2);
+    add_contact(md, d, pair, g1, g2, pos, n, t1, t2, ebest);
+    return;
+  }
+  /* face: reference box A (code < 3: box 1), incident box B */
+  int ref1 = code < 3, k = code % 3;
+  const double *RA = ref1 ? A1 : A2, *RB = ref1 ? A2 : A1, *hA = ref1 ? h1 : h2, *hB = ref1 ? h2 : h1;
+  const double *xA = ref1 ? x1 : x2, *xB = ref1 ? x2 : x1;
+  double DAB[3];
+  sub3(DAB, xB, xA);
+  double nr[3] = {RA[3 * k], RA[3 * k + 1], RA[3 * k + 2]};
+  if (dot3(DAB, nr) < 0.0) { nr[0] = -nr[0]; nr[1] = -nr[1]; nr[2] = -nr[2]; }
+  double n[3] = {nr[0], nr[1], nr[2]};
+  if (!ref1) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+  int ku = (k + 1) % 3, kv = (k + 2) % 3;
+  const double *u = RA + 3 * ku, *v = RA + 3 * kv;
+  double cA[3];
+  for (int i = 0; i < 3; i++) cA[i] = xA[i] + hA[k] * nr[i];
+  int j = 0;
+  double bj = fabs(dot3(RB, nr));
+  for (int q = 1; q < 3; q++) { double c = fabs(dot3(RB + 3 * q, nr)); if (c > bj) { bj = c; j = q; } }
+  double sB = dot3(RB + 3 * j, nr) > 0.0 ? -hB[j] : hB[j];
+  int jp = (j + 1) % 3, jq = (j + 2) % 3;
+  static const double cs[4][2] = {{1.0, 1.0}, {-1.0, 1.0}, {-1.0, -1.0}, {1.0, -1.0}};
+  P2 poly[16];
+  double deep = INFINITY, deep_c[3] = {0.0, 0.0, 0.0};
+  for (int c = 0; c < 4; c++) {
+    double P[3], rel[3];
+    for (int i = 0; i < 3; i++)
+      P[i] = ((xB[i] + sB * RB[3 * j + i]) + (cs[c][0] * hB[jp]) * RB[3 * jp + i]) + (cs[c][1] * hB[jq]) * RB[3 * jq + i];
+    sub3(rel, P, cA);
+    poly[c].x = dot3(rel, u);
+    poly[c].y = dot3(rel, v);
+    poly[c].h = dot3(rel, nr);
+    if (poly[c].h < deep) { deep = poly[c].h; deep_c[0] = P[0]; deep_c[1] = P[1]; deep_c[2] = P[2]; }
+  }
+  int nq = 4;
+  nq = bb_clip(poly, nq, 0, hA[ku], 1.0);
+  if (nq) nq = bb_clip(poly, nq, 0, hA[ku], -1.0);
+  if (nq) nq = bb_clip(poly, nq, 1, hA[kv], 1.0);
+  if (nq) nq = bb_clip(poly, nq, 1, hA[kv], -1.0);
+  P2 pts[16];
+  double dep[16];
+  int np = 0;
+  /* clipped vertices closer than BB_MERGE x the face size to a kept one are the
+   * same point (equal-size faces: a corner on the rectangle's edge) */
+  double mtol = BB_MERGE * (hA[ku] > hA[kv] ? hA[ku] : hA[kv]);
+  mtol = mtol * mtol;
+  for (int i = 0; i < nq; i++) {
+    if (!(poly[i].h < margin)) continue;
+    int dup = 0;
+    for (int q = 0; q < np; q++) if (dist2d(&pts[q], &poly[i]) < mtol) dup = 1;
+    if (!dup) { pts[np] = poly[i]; dep[np] = -poly[i].h; np++; }
+  }
+  make_frame(n, t1, t2);
+  if (np == 0) {
+    /* no incident-face point over the reference face: the deepest corner */
+    double pos[3];
+    for (int i = 0; i < 3; i++) pos[i] = deep_c[i] - (0.5 * deep) * nr[i];
+    add_contact(md, d, pair, g1, g2, pos, n, t1, t2, deep);
+    return;
+  }
+  int sel[4], ns;
+  select4(pts, dep, np, sel, &ns);
+  for (int q = 0; q < ns; q++) {
+    const P2* p = &pts[sel[q]];
+    double pos[3];
+    for (int i = 0; i < 3; i++) pos[i] = ((cA[i] + p->x * u[i]) + p->y * v[i]) + (0.5 * p->h) * nr[i];
+    add_contact(md, d, pair, g1, g2, pos, n, t1, t2, p->h);
   }
 }
 
@@ -1095,7 +1280,8 @@ static void collision(const Mdl* md, Dat* d) {
       if (p < 256) g_pair_bp[p]++;
       int n0 = d->ncon;
       long s0 = g_sup_calls;
-      collide_pair(md, d, p);
+      if (IA(md, pair_kind)[p] == MGS_PAIR_BOXBOX) collide_boxbox(md, d, p);
+      else collide_pair(md, d, p);
       if (p < 256) g_pair_sup[p] += g_sup_calls - s0;
       if (p < 256 && d->ncon > n0) g_pair_hit[p]++;
     }
