@@ -150,6 +150,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline threads (default: OMP_NUM_THREADS, else the cores this process may run on)")
+    ap.add_argument("--no-shard-check", dest="shard_check", action="store_false",
+                    help="N > 1: skip rank 0's single-GPU re-evaluation of every rank's block")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
@@ -164,10 +166,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # one GPU per rank; a rehearsal with more ranks than GPUs (a 1-GPU box)
+    # shares the devices round-robin over gloo, since RCCL needs distinct GPUs
+    ngpu = torch.cuda.device_count()
+    shared = world > 1 and world > ngpu
+    local = local % max(1, ngpu) if shared else local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
 
@@ -225,7 +235,7 @@ def main():
                            d_active=d_free.data_ptr(), stream=sp)
         n_wide[0] = 0
         if wide is not None:
-            torch.ne(d_stats[:, 2], 0, out=d_ovf.view(torch.bool))
+            torch.ne(d_stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"], 0, out=d_ovf.view(torch.bool))
             if not bool(d_ovf.any()):
                 return
             n_wide[0] = 1
@@ -257,7 +267,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt], dtype=torch.float64, device="cpu" if shared else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
@@ -275,6 +285,25 @@ def main():
                        "(filter_to_stable.py:39-50 call pattern): host SE3 processing, schedule, PCIe "
                        "copies and the host round trip between mask and rollout included; per rank, "
                        "median over batches"}
+    shard_check = None
+    if world > 1 and args.shard_check:
+        # the global candidate set is the concatenation of the
+        # seed-b blocks (rank b evaluates block b); rank 0 re-evaluates every
+        # block on its own GPU and compares the gathered labels bit for bit
+        from mgs.env.sharding import gather_results
+        t0c = time.perf_counter()
+        g = gather_results({"H": np.asarray(H)[None], "J": np.asarray(J)[None], "free": free[None],
+                            "labels": labels[None]})
+        if rank == 0:
+            same = True
+            for b in range(world):
+                pb = SE3Pose.from_mat(g["H"][b])
+                mb, lb, _ = e2e_api(env, pb, g["J"][b], h, 1)
+                same = same and bool(np.array_equal(mb, g["free"][b]) and np.array_equal(lb, g["labels"][b]))
+            shard_check = {"blocks": world, "candidates": world * N, "labels_identical_to_single_rank": same,
+                           "seconds": time.perf_counter() - t0c,
+                           "what": "labels gathered from the N ranks == rank 0 evaluating every block alone"}
+        dist.barrier()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -303,6 +332,7 @@ def main():
                    "parallelism": f"batch split x{world}"},
         "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
                    "rollouts_per_s": float(free.sum()) * world * args.steps / dt,
+                   "shard_check": shard_check,
                    "end_to_end_api": e2e,
                    "issue": issue_summary(),
                    "rollout_kernel_ms": roll_avg, "collision_kernel_ms": float(np.mean(coll_ms)),
@@ -311,7 +341,8 @@ def main():
                    "mean_nefc": float(stats[:, 5].sum() / max(1, steps_exec)),
                    "solver_iters_per_step": float(stats[:, 3].sum() / max(1, steps_exec)),
                    "overflow_candidates": int(d_ovf.sum().item()) if wide is not None
-                   else int((stats[:, 2] != 0).sum()),
+                   else int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum()),
+                   "diverged_candidates": int((stats[:, 2] & abi.MGS["MGS_FLAG_DIVERGED"] != 0).sum()),
                    "escalation_kernel_ms": float(np.mean(wide_ms)) if wide_ms else None,
                    "still_capped_after_escalation": int((stats[:, 2] != 0).sum()) if wide is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -77,6 +77,14 @@ extern "C" {
 #define MGS_EFC_LIMIT 2
 #define MGS_EFC_CONTACT 3
 
+/* stats[:, 2] flags */
+#define MGS_FLAG_CONTACTS 1        /* contacts exceeded ncon_max at some step (re-run wider) */
+#define MGS_FLAG_ROWS 2            /* constraint rows exceeded nefc_max (re-run wider) */
+#define MGS_FLAG_CAPACITY 3        /* either capacity flag */
+#define MGS_FLAG_DIVERGED 4        /* qpos / qvel / qacc NaN or beyond 1e10 (MuJoCo mj_checkPos /
+                                      mj_checkVel / mj_checkAcc, mjMAXVAL): the candidate stops, label 0 */
+#define MGS_MAXVAL 1e10
+
 /* narrowphase of a geom pair (pair_kind) */
 #define MGS_PAIR_CONVEX 0          /* general convex path: MPR + feature clipping (mjc_Convex role) */
 #define MGS_PAIR_BOXBOX 1          /* box-box separating-axis collider (mjc_BoxBox role) */

@@ -1338,9 +1338,9 @@ DEVI int bb_clip(P2* Q, int nq, int axis, double lim, double sgn, P2* buf) {
     double dc = lim - sgn * (axis ? cur->y : cur->x);
     double dp = lim - sgn * (axis ? prv->y : prv->x);
     if (dc >= 0.0) {
-      if (dp < 0.0) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
-      buf[no++] = *cur;
-    } else if (dp >= 0.0) {
+      if (dp < 0.0 && no < 16) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+      if (no < 16) buf[no++] = *cur;
+    } else if (dp >= 0.0 && no < 16) {
       buf[no++] = lerp2(prv, cur, dp / (dp - dc));
     }
   }
@@ -3399,6 +3399,22 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
       if (uni(d.NEFC) > maxefc) maxefc = uni(d.NEFC);
       sumcon += uni(d.NCON);
       sumefc += uni(d.NEFC);
+      // divergence guard (MuJoCo's mj_checkPos / mj_checkVel / mj_checkAcc flag a
+      // NaN or |x| > mjMAXVAL and reset the data): the candidate stops here,
+      // label 0, flagged in stats[2]
+      {
+        int bad = 0;
+        for (int k = lane; k < md.m.nq; k += WAVE) bad |= !(fabs(d.qpos[k]) <= MGS_MAXVAL);
+        for (int k = lane; k < md.m.nv; k += WAVE)
+          bad |= !(fabs(d.qvel[k]) <= MGS_MAXVAL) || !(fabs(d.qacc_ws[k]) <= MGS_MAXVAL);
+        if (__ballot(bad)) {
+          ok = 0;
+          fstep = gstep;
+          if (lane == 0) d.OVERFLOW |= MGS_FLAG_DIVERGED;
+          wsync();
+          break;
+        }
+      }
       int ce = sc.check_every[p];
       if (sc.vclip > 0.0) {
         for (int k = lane; k < md.m.nv; k += WAVE) {

@@ -49,7 +49,9 @@ def gen_stable_scene(cfg, rng=None):
                                     steps_each=int(cfg.get("steps_each", 900)),
                                     steps_final=int(cfg.get("steps_final", 9000)),
                                     ncon_max=cfg.get("settle_ncon"))
+    gen_bad = np.asarray(getattr(env, "last_bad_scenes", np.zeros(len(states), bool)), bool)
     stable, _, _ = env.is_stable_states(states)
+    stable = stable & ~gen_bad      # truncated / diverged while settling: never saved
     if not stable.any():
         raise ValueError("Scene unstable")
     env.set_state(states[int(np.argmax(stable))])

@@ -28,6 +28,10 @@ class EngineError(RuntimeError):
 
 def load_library(wide: bool = False):
     path = LIB_WIDE_PATH if wide else LIB_PATH
+    # build-variant experiments (tools/): MGS_LIB_MAIN names another build of the
+    # same C-ABI under mgs/_lib to load as the main library
+    if not wide and os.environ.get("MGS_LIB_MAIN"):
+        path = os.path.join(LIB_DIR, os.environ["MGS_LIB_MAIN"])
     if path in _libs:
         return _libs[path]
     if not os.path.isfile(path):
@@ -79,6 +83,13 @@ def library_for(nv: int, nefc_max: int):
     if W.mgs_supports_nv(nv) and nefc_max <= W.mgs_max_rows():
         return W
     raise EngineError(f"no kernel instantiated for nv={nv} with {nefc_max} constraint rows (MGS_NV_LIST)")
+
+
+def supported_nvs():
+    """dof counts with a compiled kernel in the main or the wide library
+    (MGS_NV_LIST of each build)"""
+    libs = [load_library()] + ([load_library(wide=True)] if os.path.isfile(LIB_WIDE_PATH) else [])
+    return sorted({nv for L in libs for nv in range(1, 257) if L.mgs_supports_nv(nv)})
 
 
 LDS_PER_CU = 160 * 1024

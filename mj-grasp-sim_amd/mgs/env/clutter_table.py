@@ -31,9 +31,14 @@ from typing import List, Optional
 
 import numpy as np
 
+from mgs.core.abi import MGS
 from mgs.core.mjcf import CompiledModel, compile_xml
 from mgs.env.gravityless_object_grasping import RolloutPlan, apply_enough_stable
 from mgs.util.geo.transforms import SE3Pose
+
+# stats[:, 2] flags that a wider re-run resolves (contacts / rows over capacity);
+# MGS_FLAG_DIVERGED (a diverged state) is final
+FLAG_CAPACITY = MGS["MGS_FLAG_CAPACITY"]
 
 # clutter_table.py:41-79, restated (lights and the camera element are render-only)
 XML = r"""
@@ -112,6 +117,7 @@ class ClutterTableEnv:
             if self.objects else probe.nv
         self.ref_nq = probe.nq + 7
         self.ref_nv = probe.nv + 6
+        self._check_kernel(probe.nv)
         self.nbody = probe.nbody
         self.neq = len(probe.eq_type)
         self.nu = probe.nu
@@ -119,6 +125,19 @@ class ClutterTableEnv:
         self._model_key = None
         self._model = None
         self._engines = {}
+
+    def _check_kernel(self, nv):
+        """kernels are compiled per dof count (csrc/mgs_capi.hip MGS_NV_LIST): fail
+        here, with the supported sizes, rather than at the first simulation"""
+        from mgs.core.engine import supported_nvs
+        ok = supported_nvs()
+        if nv not in ok:
+            g = self._gripper_nv
+            piles = sorted({(v - g) // 6 for v in ok if v > g and (v - g) % 6 == 0})
+            raise ValueError(
+                f"no GPU kernel for this scene: {len(self.objects) - len(self.removed)} free objects with this "
+                f"gripper give nv={nv}; compiled dof counts are {ok}, i.e. piles of {piles} free objects for "
+                f"this gripper (add nv={nv} to MGS_NV_LIST in csrc/mgs_capi.hip and rebuild)")
 
     # -- state vector (mjSTATE_INTEGRATION of the reference model) ------------
     def _sizes(self):
@@ -202,6 +221,7 @@ class ClutterTableEnv:
         key = (tuple(np.round(cam, 15)), tuple((n, tuple(v)) for n, v in sorted(frozen.items())))
         if key != self._model_key:
             self._model = self._compile(cam, frozen)
+            self._check_kernel(self._model.nv)      # remove_obj lowers nv by 6 per object
             self._model_key = key
             self._engines = {}
         cm = self._model
@@ -342,13 +362,13 @@ class ClutterTableEnv:
         GravitylessObjectGrasping.rollout)."""
         res = self.engine_for_state(env_state).rollout(plan)
         cap = self.ncon_max
-        ov = np.nonzero(res["stats"][:, 2])[0]
+        ov = np.nonzero(res["stats"][:, 2] & FLAG_CAPACITY)[0]
         while len(ov) and cap < max_ncon:
             cap = min(2 * cap, max_ncon)
             sub = self.engine_for_state(env_state, ncon_max=cap).rollout(plan.subset(ov))
             for k in ("label", "fail_step", "obj_qpos", "stats"):
                 res[k][ov] = sub[k]
-            ov = ov[np.nonzero(sub["stats"][:, 2])[0]]
+            ov = ov[np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0]]
         res["overflow"] = len(ov)
         return res
 
@@ -431,15 +451,19 @@ class ClutterTableEnv:
         plan, vs = self.free_plan(states, nsteps)
         cap = self.ncon_max if ncon_max is None else int(ncon_max)
         res = self._sim_engine(states[0], cap).simulate(plan, vstate=vs, vclip=vclip)
-        ov = np.nonzero(res["stats"][:, 2])[0]
+        ov = np.nonzero(res["stats"][:, 2] & FLAG_CAPACITY)[0]
         while len(ov) and cap < max_ncon:
             cap = min(2 * cap, max_ncon)
             sub = self.engine_for_state(states[0], ncon_max=cap).simulate(plan.subset(ov), vstate=vs[ov],
                                                                           vclip=vclip)
             for k in res:
                 res[k][ov] = sub[k]
-            ov = ov[np.nonzero(sub["stats"][:, 2])[0]]
+            ov = ov[np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0]]
         self.last_overflow = len(ov)
+        # states whose run is not MuJoCo's: contacts / rows still truncated at
+        # max_ncon, or a diverged state (MGS_FLAG_DIVERGED); callers treat them as
+        # unstable rather than keep a truncated pile
+        self.last_bad = res["stats"][:, 2] != 0
         return self.apply_free(states, res, nsteps)
 
     def _sim_engine(self, state, ncon_max):
@@ -470,11 +494,23 @@ class ClutterTableEnv:
         drop = np.concatenate([np.tile([0.0, 0.0, 0.8], (len(xyzw), 1)), xyzw[:, [3, 0, 1, 2]]], axis=1)
         states = np.tile(self._state, (len(xyzw), 1))
         q0, v0 = 1, 1 + self.ref_nq
+        bad = np.zeros(len(states), bool)
+        self.last_bad = None
         for _, qs, _ in self._obj_slices():
             states[:, q0 + qs.start:q0 + qs.stop] = drop
             states[:, v0:v0 + self.ref_nv] = 0.0
             states = self.simulate_states(states, steps_each, vclip, ncon_max=ncon_max)
-        return self.simulate_states(states, steps_final, vclip, ncon_max=ncon_max)
+            bad |= self._last_bad(len(states))
+        states = self.simulate_states(states, steps_final, vclip, ncon_max=ncon_max)
+        self.last_bad_scenes = bad | self._last_bad(len(states))
+        return states
+
+    def _last_bad(self, n):
+        """the bad-state mask of the last simulate_states call, consumed (zeros
+        if the call left none, e.g. a substituted simulator)"""
+        b = getattr(self, "last_bad", None)
+        self.last_bad = None
+        return np.zeros(n, bool) if b is None or len(b) != n else np.asarray(b, bool)
 
     def gen_clutter(self, rng=None, **kw):
         """clutter_table.py:197-222 on this env's state."""
@@ -490,14 +526,18 @@ class ClutterTableEnv:
         the largest sum is < tol.  Returns (stable, largest sum, advanced states)."""
         states = np.atleast_2d(np.asarray(states, dtype=np.float64))
         delta = np.zeros((len(states), len(self.object_names)))
+        bad = np.zeros(len(states), bool)
+        self.last_bad = None
         for _ in range(rounds):
             new = self.simulate_states(states, steps)
+            bad |= self._last_bad(len(states))
             for k, (_, qs, _) in enumerate(self._obj_slices()):
                 a = 1 + qs.start
                 delta[:, k] += np.sum(np.abs(new[:, a:a + 3] - states[:, a:a + 3]), axis=1)
             states = new
         mx = np.max(delta, axis=1, initial=0.0)
-        return mx < tol, mx, states
+        # a truncated (capacity) or diverged run is not a stable pile
+        return (mx < tol) & ~bad, mx, states
 
     def is_stable(self) -> bool:
         """clutter_table.py:160-195 (advances this env's state like the reference)."""

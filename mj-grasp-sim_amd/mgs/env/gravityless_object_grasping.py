@@ -31,10 +31,15 @@ from typing import List, Optional
 
 import numpy as np
 
+from mgs.core.abi import MGS
 from mgs.core.mjcf import CompiledModel, compile_xml
 from mgs.gripper.base import MjShakableOpenCloseGripper
 from mgs.obj.base import CollisionMeshObject
 from mgs.util.geo.transforms import SE3Pose
+
+# stats[:, 2] flags that a wider re-run resolves (contacts / rows over capacity);
+# MGS_FLAG_DIVERGED (a diverged state) is final
+FLAG_CAPACITY = MGS["MGS_FLAG_CAPACITY"]
 
 # Environment template: options, ground box and geom order restated from the
 # reference (gravityless_object_grasping.py:34-54).  Geom order is
@@ -162,13 +167,13 @@ class GravitylessObjectGrasping:
         capped run's.  res['overflow'] counts candidates still capped."""
         res = self.engine.rollout(plan)
         cap = self.ncon_max
-        ov = np.nonzero(res["stats"][:, 2])[0]
+        ov = np.nonzero(res["stats"][:, 2] & FLAG_CAPACITY)[0]
         while len(ov) and cap < max_ncon:
             cap = min(2 * cap, max_ncon)
             sub = self.engine_for(cap).rollout(plan.subset(ov))
             for k in ("label", "fail_step", "obj_qpos", "stats"):
                 res[k][ov] = sub[k]
-            ov = ov[np.nonzero(sub["stats"][:, 2])[0]]
+            ov = ov[np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0]]
         res["overflow"] = len(ov)
         return res
 

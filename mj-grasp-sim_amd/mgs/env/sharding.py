@@ -25,13 +25,18 @@ def gather_results(local: dict, group=None) -> dict:
     return {k: np.concatenate([p[k] for p in parts]) for k in local}
 
 
-def evaluate_sharded(env, poses, joints, horizon="h200", enough_stable=None, group=None):
+def evaluate_sharded(env, poses, joints, horizon="h200", enough_stable=None, group=None, evaluate=None):
     """filter_to_stable over a batch sharded across the ranks of `group`
-    (each rank drives its own GPU through `env.engine`)."""
+    (each rank drives its own GPU through `env.engine`).  `evaluate(poses,
+    joints) -> (mask, stable)` is the per-rank evaluator, default
+    `env.evaluate(..., horizon=horizon)`; the CPU tests pass the oracle's."""
     import torch.distributed as dist
     from mgs.env.gravityless_object_grasping import apply_enough_stable
+    if evaluate is None:
+        def evaluate(p, j):
+            return env.evaluate(p, j, horizon=horizon)
     lo, hi = shard_bounds(len(poses), dist.get_world_size(group), dist.get_rank(group))
-    mask, stable = env.evaluate(poses[lo:hi], joints[lo:hi], horizon=horizon)
-    out = gather_results({"mask": mask, "stable": stable}, group)
+    mask, stable = evaluate(poses[lo:hi], joints[lo:hi])
+    out = gather_results({"mask": np.asarray(mask, bool), "stable": np.asarray(stable, bool)}, group)
     out["stable"] = apply_enough_stable(out["stable"], enough_stable)
     return out["mask"], out["stable"]

@@ -5,7 +5,8 @@ quaternions are cast to float32 on construction (:34-45), composition goes
 through 4x4 matrices built with scipy's Rotation (:93-97, :109-121) and
 `from_mat` uses `as_quat(canonical=False)` (:79-88).  These casts define the
 input quantisation of the hot path, so they are kept
-bit-for-bit; tests/golden/se3_golden.npz pins them against the reference.
+bit-for-bit; tests/golden/se3_golden.npz (tests/golden/make_se3_golden.py, generated
+from the reference's own SE3Pose) pins them (tests/test_model_and_host.py).
 """
 from __future__ import annotations
 
@@ -13,6 +14,8 @@ from dataclasses import dataclass
 
 import numpy as np
 from scipy.spatial.transform import Rotation
+
+from mgs.util.geo.operations import quaternion_apply, quaternion_invert
 
 
 _PAR_MIN, _PAR_CHUNKS = 2048, 4
@@ -106,14 +109,15 @@ class SE3Pose:
         return out
 
     def inverse(self) -> "SE3Pose":
-        # reference semantics (transforms.py:102-107): mutates self, returns a copy
-        R = Rotation.from_quat(_wxyz_to_xyzw(self.quat) if self.type == "wxyz" else self.quat)
-        inv = R.inv()
-        q = inv.as_quat(canonical=False)
-        q = _xyzw_to_wxyz(q) if self.type == "wxyz" else q
-        p = -inv.apply(self.pos)
-        self.pos, self.quat = p.astype(np.float32), q.astype(np.float32)
-        return SE3Pose(p, q, self.type)
+        """reference transforms.py:102-107: conjugate quaternion and
+        -quaternion_apply(conj, pos) in the reference's numpy arithmetic
+        (operations.py); the receiver is mutated with the un-cast (float64)
+        values and a new, float32 SE3Pose is returned."""
+        inv_quat = quaternion_invert(self.quat, type=self.type)
+        inv_pos = -quaternion_apply(inv_quat, self.pos, type=self.type)
+        self.pos = inv_pos
+        self.quat = inv_quat
+        return SE3Pose(inv_pos, inv_quat, self.type)
 
     @classmethod
     def randn_se3(cls, num, rng=None) -> "SE3Pose":

@@ -1065,9 +1065,9 @@ static int bb_clip(P2* Q, int nq, int axis, double lim, double sgn) {
     double dc = lim - sgn * (axis ? cur->y : cur->x);
     double dp = lim - sgn * (axis ? prv->y : prv->x);
     if (dc >= 0.0) {
-      if (dp < 0.0) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
-      buf[no++] = *cur;
-    } else if (dp >= 0.0) {
+      if (dp < 0.0 && no < 16) buf[no++] = lerp2(prv, cur, dp / (dp - dc));
+      if (no < 16) buf[no++] = *cur;
+    } else if (dp >= 0.0 && no < 16) {
       buf[no++] = lerp2(prv, cur, dp / (dp - dc));
     }
   }
@@ -2426,6 +2426,13 @@ static void rollout_batch(const mgs_model_desc* desc, const int32_t* I, const do
           if (d->nefc > maxefc) maxefc = d->nefc;
           sumcon += d->ncon;
           sumefc += d->nefc;
+          /* divergence guard (mj_checkPos / mj_checkVel / mj_checkAcc): stop, label 0 */
+          {
+            int bad = 0;
+            for (int k = 0; k < nq; k++) bad |= !(fabs(d->qpos[k]) <= MGS_MAXVAL);
+            for (int k = 0; k < nv; k++) bad |= !(fabs(d->qvel[k]) <= MGS_MAXVAL) || !(fabs(d->qacc_ws[k]) <= MGS_MAXVAL);
+            if (bad) { ok = 0; fstep = gstep; d->overflow |= MGS_FLAG_DIVERGED; break; }
+          }
           if (sc->vclip > 0.0)
             for (int k = 0; k < nv; k++) {
               if (d->qvel[k] > sc->vclip) d->qvel[k] = sc->vclip;

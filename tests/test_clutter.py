@@ -160,3 +160,21 @@ def test_eval_grasps_cli(cenv, ccand, tmp_path, monkeypatch):
     idx = np.nonzero(free)[0]
     lab = om.rollout(cenv.stable_plan(P[idx], J[sel][idx], st, nstep_lift=300, close_steps=300), nthreads=8)["label"]
     assert res["success_rate"] == pytest.approx(lab.sum() / len(sel)) and res["num_objects"] == 5
+
+
+def test_unsupported_pile_size_fails_clearly():
+    """kernels exist per dof count (MGS_NV_LIST); a pile whose nv has none is
+    refused when the env is built, with the supported pile sizes in the message
+    (not at the first simulation)"""
+    from mgs.core.engine import supported_nvs
+    from mgs.env.clutter_table import ClutterTableEnv
+    from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+    from mgs.obj.selector import get_object
+    from mgs.util.geo.transforms import SE3Pose
+    grip = GripperRobotiq2f85(SE3Pose(np.array([5.0, 5.0, 1.0]), np.array([1.0, 0, 0, 0]), "wxyz"))
+    objs = [get_object("003_cracker_box") for _ in range(9)]
+    for i, o in enumerate(objs):
+        o.name = f"o{i}"
+    assert 14 + 6 * 9 not in supported_nvs()
+    with pytest.raises(ValueError, match="no GPU kernel for this scene"):
+        ClutterTableEnv(grip, objs)

@@ -240,3 +240,15 @@ def test_contact_capacity_escalation(env):
     assert env.ncon_max == 20
     r20 = env.rollout(plan.subset(ov))
     assert not r20["stats"][:, 2].any()
+
+
+def test_divergence_guard_parity(env, eng, candidates, oracle_model):
+    """injected NaN / beyond-mjMAXVAL states: the GPU stops and flags exactly the
+    candidates the oracle does (obj_qpos compared with NaN == NaN)."""
+    from test_oracle import _guard_plan
+    plan = _guard_plan(env, candidates, oracle_model)
+    rg = eng.rollout(plan)
+    ro = oracle_model.rollout(plan)
+    for k in ("label", "fail_step", "stats"):
+        assert np.array_equal(rg[k], ro[k]), k
+    assert np.array_equal(rg["obj_qpos"], ro["obj_qpos"], equal_nan=True)

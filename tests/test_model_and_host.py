@@ -96,3 +96,24 @@ def test_gso_loader_format():
     assert cm.jnt_names[-1] == "mug:joint" and cm.nv == 14
     g = cm.geom_names.index("geom:ground")
     assert len(cm.geom_names) == g + 2 and cm.pair_condim.max() == 4
+
+
+def test_se3_pose_against_reference_golden():
+    """SE3Pose from_mat / @ / to_mat / inverse bit-exact against the reference's
+    own SE3Pose (tests/golden/se3_golden.npz, tests/golden/make_se3_golden.py;
+    reference transforms.py:79-121, operations.py:20-112), including inverse's
+    mutation of the receiver with float64 values."""
+    import os
+    from mgs.util.geo.transforms import SE3Pose
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "se3_golden.npz"))
+    a = SE3Pose.from_mat(g["H"])
+    assert np.array_equal(a.pos, g["a_pos"]) and np.array_equal(a.quat, g["a_quat"])
+    assert np.array_equal(a.to_mat(), g["a_mat"])
+    b = SE3Pose(g["b_pos"], g["b_quat"], "wxyz")
+    ab = a @ b
+    assert np.array_equal(ab.pos, g["ab_pos"]) and np.array_equal(ab.quat, g["ab_quat"])
+    c = SE3Pose(np.copy(a.pos), np.copy(a.quat), "wxyz")
+    inv = c.inverse()
+    assert np.array_equal(inv.pos, g["inv_pos"]) and np.array_equal(inv.quat, g["inv_quat"])
+    assert c.pos.dtype == g["self_pos"].dtype and np.array_equal(c.pos, g["self_pos"])
+    assert c.quat.dtype == g["self_quat"].dtype and np.array_equal(c.quat, g["self_quat"])

@@ -113,3 +113,33 @@ def test_empty_batch(env, oracle_model):
     poses = SE3Pose(np.zeros((0, 3), np.float32), np.zeros((0, 4), np.float32), "wxyz")
     q, mp, mq, _ = env.initial_state(poses, np.zeros((0, 8)))
     assert oracle_model.collision_free(q, mp, mq).shape == (0,)
+
+
+def _guard_plan(env, candidates, oracle_model, n=4):
+    """n collision-free candidates (the rollouts the pipeline runs), two of them
+    given a bad initial state"""
+    from conftest import plan_for
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(oracle_model.collision_free(q, mp, mq))[0][:n]
+    plan = plan_for(env, poses[idx], J[idx])
+    plan.qpos_init = plan.qpos_init.copy()
+    plan.qpos_init[1, 17] = np.nan        # object x: a NaN state
+    plan.qpos_init[2, 0] = 2e10           # gripper x beyond mjMAXVAL
+    return plan
+
+
+def test_divergence_guard_oracle(env, candidates, oracle_model):
+    """MuJoCo's mj_checkPos / mj_checkVel / mj_checkAcc (NaN or |x| > 1e10) stop a
+    candidate: label 0, fail step = the step that produced the bad state, flag
+    MGS_FLAG_DIVERGED in stats[:, 2]; healthy candidates are untouched."""
+    from mgs.core.abi import MGS
+    plan = _guard_plan(env, candidates, oracle_model)
+    r = oracle_model.rollout(plan)
+    div = MGS["MGS_FLAG_DIVERGED"]
+    assert list(r["stats"][:, 2] & div) == [0, div, div, 0]
+    assert not r["label"][1] and not r["label"][2]
+    assert r["fail_step"][1] == 0 and r["fail_step"][2] == 0
+    clean = oracle_model.rollout(plan.subset([0, 3]))
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(clean[k], r[k][[0, 3]])

@@ -16,6 +16,24 @@ def _free_port():
     return p
 
 
+def _oracle_evaluate(env):
+    """per-rank evaluator for mgs.env.sharding.evaluate_sharded on the CPU: the
+    oracle in place of the GPU engine (same signature as env.evaluate)"""
+    from oracle import oracle as O
+    from conftest import plan_for
+    om = O.OracleModel(env.model)
+
+    def evaluate(poses, joints):
+        q, mp, mq, _ = env.initial_state(poses, joints)
+        mask = om.collision_free(q, mp, mq)
+        stable = np.zeros(len(poses), bool)
+        idx = np.nonzero(mask)[0]
+        if len(idx):
+            stable[idx] = om.rollout(plan_for(env, poses[idx], joints[idx]))["label"]
+        return mask, stable
+    return evaluate
+
+
 def _worker(rank, world, port, outq):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -23,31 +41,22 @@ def _worker(rank, world, port, outq):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
-    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, apply_enough_stable
-    from mgs.env.sharding import gather_results, shard_bounds
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    from mgs.env.sharding import evaluate_sharded
     from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
     from mgs.obj.selector import get_object
     from mgs.sampler.antipodal import robotiq_candidates
     from mgs.util.geo.transforms import SE3Pose
-    from oracle import oracle as O
-    from conftest import plan_for
     dist.init_process_group("gloo", rank=rank, world_size=world)
     env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
                                     get_object("003_cracker_box"))
     H, J, _ = robotiq_candidates(env.obj, 96, seed=3)
     poses = SE3Pose.from_mat(H)
-    lo, hi = shard_bounds(len(poses), world, rank)
-    om = O.OracleModel(env.model)
-    q, mp, mq, _ = env.initial_state(poses[lo:hi], J[lo:hi])
-    mask = om.collision_free(q, mp, mq)
-    stable = np.zeros(hi - lo, bool)
-    idx = np.nonzero(mask)[0]
-    if len(idx):
-        stable[idx] = om.rollout(plan_for(env, poses[lo:hi][idx], J[lo:hi][idx]))["label"]
-    out = gather_results({"mask": mask, "stable": stable})
-    out["stable"] = apply_enough_stable(out["stable"], 3)
+    # the product entry point: shard bounds, per-rank evaluation, gather, the
+    # global enough_stable prefix
+    mask, stable = evaluate_sharded(env, poses, J, enough_stable=3, evaluate=_oracle_evaluate(env))
     if rank == 0:
-        outq.put({k: v.tolist() for k, v in out.items()})
+        outq.put({"mask": mask.tolist(), "stable": stable.tolist()})
     dist.destroy_process_group()
 
 
