@@ -154,6 +154,8 @@ def main():
                     help="N > 1: skip rank 0's single-GPU re-evaluation of every rank's block")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
@@ -211,58 +213,73 @@ def main():
     d_mq = torch.as_tensor(mquat, **f64).contiguous()
     d_ps = torch.as_tensor(plan.phase_start, **f64).contiguous()
     d_pt = torch.as_tensor(plan.phase_target, **f64).contiguous()
-    d_free = torch.zeros(N, dtype=torch.uint8, device=dev)
-    d_label = torch.zeros(N, dtype=torch.uint8, device=dev)
-    d_fail = torch.zeros(N, dtype=torch.int32, device=dev)
-    d_objq = torch.zeros((N, 7), **f64)
-    d_stats = torch.zeros((N, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
-    # contact-capacity escalation (GravitylessObjectGrasping.rollout): candidates
-    # whose contacts exceeded ncon_max at some step are re-run with a wider engine,
-    # selected on the device and merged into the outputs; a one-byte host check
-    # skips the launch when nothing overflowed (the usual case)
-    wide = env.engine_for(2 * env.ncon_max) if args.escalate else None
-    w_label, w_fail, w_objq, w_stats = (torch.zeros_like(t) for t in (d_label, d_fail, d_objq, d_stats))
-    d_ovf = torch.zeros(N, dtype=torch.uint8, device=dev)
-    n_wide = [0]
+    # S pipelines, each with its own engine (device work buffers, HIP events),
+    # output buffers and HIP stream; step k runs on pipeline k % S, so one batch's
+    # rollout tail overlaps the next batch's start (no host synchronisation
+    # inside the timed loop).  Every step does the whole filter_to_stable pass.
+    from mgs.core.engine import Engine
 
-    def step():
-        eng.collision_free_device(N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(), d_free.data_ptr(),
-                                  predicate="any", stream=sp)
-        eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
-                           d_label.data_ptr(), d_fail.data_ptr(), d_objq.data_ptr(), d_stats.data_ptr(),
-                           d_active=d_free.data_ptr(), stream=sp)
-        n_wide[0] = 0
-        if wide is not None:
-            torch.ne(d_stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"], 0, out=d_ovf.view(torch.bool))
-            if not bool(d_ovf.any()):
-                return
-            n_wide[0] = 1
-            wide.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
-                                w_label.data_ptr(), w_fail.data_ptr(), w_objq.data_ptr(), w_stats.data_ptr(),
-                                d_active=d_ovf.data_ptr(), stream=sp)
-            m = d_ovf.bool()
-            d_label.copy_(torch.where(m, w_label, d_label))
-            d_fail.copy_(torch.where(m, w_fail, d_fail))
-            d_objq.copy_(torch.where(m[:, None], w_objq, d_objq))
-            d_stats.copy_(torch.where(m[:, None], w_stats, d_stats))
+    class Pipe:
+        def __init__(self, s):
+            self.eng = env.engine if s == 0 else Engine(env.model, device=local, ncon_max=env.ncon_max,
+                                                          nefc_max=env.nefc_max)
+            # contact-capacity escalation (GravitylessObjectGrasping.rollout):
+            # candidates whose contacts / rows exceeded the capacity are re-run
+            # with a wider engine, selected on the device (d_ovf) and merged into
+            # the outputs; launched every step, it returns at once when no
+            # candidate overflowed (the usual case)
+            self.wide = (env.engine_for(2 * env.ncon_max) if s == 0 else
+                         Engine(env.model, device=local, ncon_max=2 * env.ncon_max)) if args.escalate else None
+            self.stream = torch.cuda.current_stream(dev) if s == 0 else torch.cuda.Stream(dev)
+            self.free = torch.zeros(N, dtype=torch.uint8, device=dev)
+            self.label = torch.zeros(N, dtype=torch.uint8, device=dev)
+            self.fail = torch.zeros(N, dtype=torch.int32, device=dev)
+            self.objq = torch.zeros((N, 7), **f64)
+            self.stats = torch.zeros((N, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
+            self.w = [torch.zeros_like(t) for t in (self.label, self.fail, self.objq, self.stats)]
+            self.ovf = torch.zeros(N, dtype=torch.uint8, device=dev)
+            self.events = []
 
-    for _ in range(args.warmup):
-        step()
+        def step(self, timed):
+            sp = self.stream.cuda_stream
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+            with torch.cuda.stream(self.stream):
+                if ev:
+                    ev[0].record(self.stream)
+                self.eng.collision_free_device(N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(),
+                                               self.free.data_ptr(), predicate="any", stream=sp)
+                if ev:
+                    ev[1].record(self.stream)
+                self.eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
+                                        self.label.data_ptr(), self.fail.data_ptr(), self.objq.data_ptr(),
+                                        self.stats.data_ptr(), d_active=self.free.data_ptr(), stream=sp)
+                if ev:
+                    ev[2].record(self.stream)
+                if self.wide is not None:
+                    torch.ne(self.stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"], 0, out=self.ovf.view(torch.bool))
+                    wl, wf, wo, ws = self.w
+                    self.wide.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(),
+                                             d_pt.data_ptr(), wl.data_ptr(), wf.data_ptr(), wo.data_ptr(),
+                                             ws.data_ptr(), d_active=self.ovf.data_ptr(), stream=sp)
+                    m = self.ovf.bool()
+                    self.label.copy_(torch.where(m, wl, self.label))
+                    self.fail.copy_(torch.where(m, wf, self.fail))
+                    self.objq.copy_(torch.where(m[:, None], wo, self.objq))
+                    self.stats.copy_(torch.where(m[:, None], ws, self.stats))
+                if ev:
+                    ev[3].record(self.stream)
+                    self.events.append(ev)
+
+    pipes = [Pipe(s) for s in range(max(1, args.streams))]
+    for k in range(max(args.warmup, len(pipes))):       # every pipeline warmed up
+        pipes[k % len(pipes)].step(False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    roll_ms, coll_ms, wide_ms = [], [], []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        # per-launch kernel durations (HIP events recorded on this stream by the library)
-        roll_ms.append(eng.last_kernel_ms())
-        coll_ms.append(eng.last_collision_ms())
-        if n_wide[0]:
-            wide_ms.append(wide.last_kernel_ms())
+    for k in range(args.steps):
+        pipes[k % len(pipes)].step(True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -271,6 +288,16 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    # per-launch kernel durations from the HIP events on each pipeline's stream
+    coll_ms = [e[0].elapsed_time(e[1]) for p in pipes for e in p.events]
+    roll_ms = [e[1].elapsed_time(e[2]) for p in pipes for e in p.events]
+    esc_ms = [e[2].elapsed_time(e[3]) for p in pipes for e in p.events]
+    P0 = pipes[0]
+    d_free, d_label, d_fail, d_stats, d_ovf = P0.free, P0.label, P0.fail, P0.stats, P0.ovf
+    same_pipes = all(torch.equal(p.label, P0.label) and torch.equal(p.free, P0.free) and
+                     torch.equal(p.fail, P0.fail) for p in pipes[1:])
+    wide = P0.wide
+    wide_ms = esc_ms if wide is not None else []
 
     free = d_free.cpu().numpy().astype(bool)
     labels = d_label.cpu().numpy().astype(bool)
@@ -329,9 +356,10 @@ def main():
         "config": {"workload": f"Robotiq2F85 x YCB 003_cracker_box, {N} candidates/GPU, collision mask + "
                                f"{args.horizon} close-lift-shake rollout ({horizon} steps, dt 1 ms)",
                    "candidates_per_gpu": N, "horizon_steps": horizon, "solver": env.model.options.get("solver"),
-                   "parallelism": f"batch split x{world}"},
+                   "parallelism": f"batch split x{world}", "streams": len(pipes)},
         "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
                    "rollouts_per_s": float(free.sum()) * world * args.steps / dt,
+                   "pipelines_identical": bool(same_pipes),
                    "shard_check": shard_check,
                    "end_to_end_api": e2e,
                    "issue": issue_summary(),
@@ -343,8 +371,9 @@ def main():
                    "overflow_candidates": int(d_ovf.sum().item()) if wide is not None
                    else int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum()),
                    "diverged_candidates": int((stats[:, 2] & abi.MGS["MGS_FLAG_DIVERGED"] != 0).sum()),
-                   "escalation_kernel_ms": float(np.mean(wide_ms)) if wide_ms else None,
-                   "still_capped_after_escalation": int((stats[:, 2] != 0).sum()) if wide is not None else None},
+                   "escalation_pass_ms": float(np.mean(wide_ms)) if wide_ms else None,
+                   "still_capped_after_escalation": int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum())
+                   if wide is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
