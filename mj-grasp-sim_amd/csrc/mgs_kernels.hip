@@ -2169,6 +2169,27 @@ DEVI void load_frc(Frc& F, const double* f, int ne, int lane) {
   for (int h = 0; h < MGS_RPL; h++) F.v[h] = (lane + h * WAVE < ne) ? f[lane + h * WAVE] : 0.0;
 }
 
+// MuJoCo's costChange (oracle cost_change1 / cost_change): dual-cost change of
+// an update; one that raises the cost by more than 1e-10 is undone
+DEVI double cost_change1(double A, double delta, double res) {
+  return ((0.5 * delta) * delta) * A + delta * res;
+}
+
+template <int N, int LD>
+DEVI double cost_change(const double* A, const double* delta, const double* res) {
+  double vav = 0.0, dr = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    double ad = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j++) ad = ad + A[i * LD + j] * delta[j];
+    vav = vav + delta[i] * ad;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) dr = dr + delta[i] * res[i];
+  return 0.5 * vav + dr;
+}
+
 // one PGS update of the contact block starting at row r with DIM rows
 template <int DIM>
 DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u, Frc& F, int noslip) {
@@ -2196,7 +2217,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
     if (fn < 0.0) fn = 0.0;
     double dn = fn - old[0];
     nw[0] = fn;
-    if (fn == 0.0) {
+    if (fn < 1e-15) {
 #pragma unroll
       for (int j = 1; j < DIM; j++) nw[j] = 0.0;
     } else {
@@ -2223,12 +2244,11 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
     double del[DIM];
 #pragma unroll
     for (int i = 0; i < DIM; i++) del[i] = nw[i] - old[i];
+    dc = cost_change<DIM, DIM>(Ab, del, res);
+    if (dc > 1e-10) {
 #pragma unroll
-    for (int i = 0; i < DIM; i++) {
-      double ad = 0.0;
-#pragma unroll
-      for (int j = 0; j < DIM; j++) ad = ad + Ab[i * DIM + j] * del[j];
-      dc = dc + del[i] * (0.5 * ad + res[i]);
+      for (int i = 0; i < DIM; i++) { nw[i] = old[i]; del[i] = 0.0; }
+      dc = 0.0;
     }
     double s = u;
 #pragma unroll
@@ -2248,7 +2268,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
       bq[i] = s;
     }
     double fnorm = old[0];
-    if (fnorm > 0.0) {
+    if (!(fnorm < 1e-15)) {
       if (DIM == 3) {
         qcqp2(Ab[4], Ab[5], Ab[8], bq[0], bq[1], mu, fnorm, &nw[1], &nw[2]);
       } else {
@@ -2266,12 +2286,11 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
     double del[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) del[i] = nw[1 + i] - old[1 + i];
+    dc = cost_change<NF, DIM>(Ab + DIM + 1, del, res + 1);
+    if (dc > 1e-10) {
 #pragma unroll
-    for (int i = 0; i < NF; i++) {
-      double ad = 0.0;
-#pragma unroll
-      for (int j = 0; j < NF; j++) ad = ad + Ab[(1 + i) * DIM + 1 + j] * del[j];
-      dc = dc + del[i] * (0.5 * ad + res[1 + i]);
+      for (int i = 0; i < NF; i++) { nw[1 + i] = old[1 + i]; del[i] = 0.0; }
+      dc = 0.0;
     }
     double s = u;
 #pragma unroll
@@ -2384,7 +2403,9 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
         double fnew[1] = {fo - res * (1.0 / AR)};
         if (t != MGS_EFC_EQUALITY) project_scalar(t, row_floss(md, d, r), fnew);
         double delta = fnew[0] - fo;
-        improvement = improvement - delta * (0.5 * AR * delta + res);
+        double ch = cost_change1(AR, delta, res);
+        if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
+        improvement = improvement - ch;
         if (delta != 0.0) {
           double s = u + g * delta;
           if (lane < nv) u = s;
@@ -2428,7 +2449,9 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
         double fnew[1] = {fo - res * (1.0 / Arr)};
         project_scalar(t, row_floss(md, d, r), fnew);
         double delta = fnew[0] - fo;
-        improvement = improvement - delta * (0.5 * Arr * delta + res);
+        double ch = cost_change1(Arr, delta, res);
+        if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
+        improvement = improvement - ch;
         if (delta != 0.0) {
           double s = u + g * delta;
           if (lane < nv) u = s;
@@ -2452,8 +2475,10 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
 // qacc = qacc_smooth + L^-T D^-1/2 u ; qfrc_constraint = L D^1/2 u, lane i owns
 // dof i: backward substitution column by column (k descending, as the oracle),
 // the L-multiply row by row (k ascending), broadcasts by v_readlane.
+// u_main: the main solver's u (MuJoCo saves qacc_warmstart before noslip;
+// qacc feeds only the warmstart, implicitfast integrates qfrc_constraint)
 template <int NV>
-DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
+DEVI void finalize_solution(const Mdl& md, Dat& d, double u_main, double u) {
   int lane = lane_id();
   int li = lane < NV ? lane : 0;
 #if MGS_REG_ROWS
@@ -2466,7 +2491,7 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u) {
 #define FS_LR(k) d.M[li * NV + (k)]
 #define FS_LC(k) d.M[(k) * NV + li]
 #endif
-  double z = u * d.isD[li];
+  double z = u_main * d.isD[li];
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
     double zk = readlane_d(z, k);
@@ -3158,9 +3183,10 @@ DEVI void solve(const Mdl& md, Dat& d) {
     if (md.m.noslip_iterations > 0) contact_blocks(md, d);   // overwrites the cone Hessians
   }
   PT(16);
+  double u_main = u;
   noslip(md, d, scale, F, u);
   PT(17);
-  finalize_solution<NV>(md, d, u);
+  finalize_solution<NV>(md, d, u_main, u);
   PT(18);
 }
 

@@ -1694,6 +1694,25 @@ static void qcqp(int n, const double* A, const double* b, const double* mu, doub
   else qcqp3(A, b, mu, r, x);
 }
 
+/* MuJoCo's costChange (engine_solver.c): the change of the dual cost
+ * 0.5 d'Ad + d'res of a block update; an update that raises the cost by more
+ * than 1e-10 is undone (force restored, change 0).  PGS and noslip apply it
+ * to every scalar row and every contact block. */
+static double cost_change1(double A, double delta, double res) {
+  return ((0.5 * delta) * delta) * A + delta * res;
+}
+
+static double cost_change(int n, const double* A, const double* delta, const double* res) {
+  double vav = 0.0, dr = 0.0;
+  for (int i = 0; i < n; i++) {
+    double ad = 0.0;
+    for (int j = 0; j < n; j++) ad = ad + A[i * n + j] * delta[j];
+    vav = vav + delta[i] * ad;
+  }
+  for (int i = 0; i < n; i++) dr = dr + delta[i] * res[i];
+  return 0.5 * vav + dr;
+}
+
 static void project_block(const Dat* d, int r, double* f) {
   int t = d->efc_type[r];
   if (t == MGS_EFC_FRICTION) {
@@ -1775,7 +1794,9 @@ static void solve_pgs_main(const Mdl* md, Dat* d) {
         double fnew[1] = {fo - res * d->efc_ARinv[r]};
         if (t != MGS_EFC_EQUALITY) project_block(d, r, fnew);
         double delta = fnew[0] - fo;
-        improvement = improvement - delta * (0.5 * AR * delta + res);
+        double ch = cost_change1(AR, delta, res);
+        if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
+        improvement = improvement - ch;
         if (delta != 0.0) {
           d->efc_f[r] = fnew[0];
           for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Gr[k] * delta;
@@ -1796,7 +1817,7 @@ static void solve_pgs_main(const Mdl* md, Dat* d) {
         if (fn < 0.0) fn = 0.0;
         double dn = fn - old[0];
         nw[0] = fn;
-        if (fn == 0.0) {
+        if (fn < O_MINVAL) {
           for (int j = 1; j < dim; j++) nw[j] = 0.0;
         } else {
           int nf = dim - 1;
@@ -1814,11 +1835,10 @@ static void solve_pgs_main(const Mdl* md, Dat* d) {
         }
         double del[6];
         for (int i = 0; i < dim; i++) del[i] = nw[i] - old[i];
-        double dc = 0.0;
-        for (int i = 0; i < dim; i++) {
-          double ad = 0.0;
-          for (int j = 0; j < dim; j++) ad = ad + Ab[i * dim + j] * del[j];
-          dc = dc + del[i] * (0.5 * ad + res[i]);
+        double dc = cost_change(dim, Ab, del, res);
+        if (dc > 1e-10) {
+          for (int i = 0; i < dim; i++) { nw[i] = old[i]; del[i] = 0.0; }
+          dc = 0.0;
         }
         improvement = improvement - dc;
         for (int i = 0; i < dim; i++) d->efc_f[r + i] = nw[i];
@@ -1859,7 +1879,9 @@ static void noslip(const Mdl* md, Dat* d) {
         double fnew[1] = {fo - res * d->efc_Ainv[r]};
         project_block(d, r, fnew);
         double delta = fnew[0] - fo;
-        improvement = improvement - delta * (0.5 * d->efc_A[r] * delta + res);
+        double ch = cost_change1(d->efc_A[r], delta, res);
+        if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
+        improvement = improvement - ch;
         if (delta != 0.0) {
           d->efc_f[r] = fnew[0];
           for (int k = 0; k < nv; k++) d->w[k] = d->w[k] + Gr[k] * delta;
@@ -1882,14 +1904,13 @@ static void noslip(const Mdl* md, Dat* d) {
           }
           bq[i] = s;
         }
-        if (d->efc_f[r] > 0.0) qcqp(nf, Ac, bq, d->efc_mu + 5 * r, d->efc_f[r], nw);
-        else for (int i = 0; i < nf; i++) nw[i] = 0.0;
+        if (d->efc_f[r] < O_MINVAL) for (int i = 0; i < nf; i++) nw[i] = 0.0;
+        else qcqp(nf, Ac, bq, d->efc_mu + 5 * r, d->efc_f[r], nw);
         for (int i = 0; i < nf; i++) del[i] = nw[i] - old[i];
-        double dc = 0.0;
-        for (int i = 0; i < nf; i++) {
-          double ad = 0.0;
-          for (int j = 0; j < nf; j++) ad = ad + Ac[i * nf + j] * del[j];
-          dc = dc + del[i] * (0.5 * ad + res[i]);
+        double dc = cost_change(nf, Ac, del, res);
+        if (dc > 1e-10) {
+          for (int i = 0; i < nf; i++) { nw[i] = old[i]; del[i] = 0.0; }
+          dc = 0.0;
         }
         improvement = improvement - dc;
         for (int i = 0; i < nf; i++) d->efc_f[r + 1 + i] = nw[i];
@@ -1907,12 +1928,15 @@ static void noslip(const Mdl* md, Dat* d) {
   }
 }
 
-/* qacc = qacc_smooth + L^-T D^-1/2 u ;  qfrc_constraint = L D^1/2 u */
-static void finalize_solution(const Mdl* md, Dat* d) {
+/* qacc = qacc_smooth + L^-T D^-1/2 u_main ;  qfrc_constraint = L D^1/2 u.
+ * u_main is the main solver's u: MuJoCo's mj_fwdConstraint saves
+ * qacc_warmstart before mj_solNoSlip runs, and qacc feeds nothing but the
+ * warmstart (implicitfast integrates qfrc_smooth + qfrc_constraint). */
+static void finalize_solution(const Mdl* md, Dat* d, const double* u_main) {
   int nv = md->m->nv;
   double z[128];
   for (int i = nv - 1; i >= 0; i--) {
-    double s = d->w[i] * d->isD[i];
+    double s = u_main[i] * d->isD[i];
     for (int k = nv - 1; k > i; k--) s = fma(-d->L[k * nv + i], z[k], s);   /* k descending (kernel order) */
     z[i] = s;
   }
@@ -2247,8 +2271,10 @@ static void solve_newton(const Mdl* md, Dat* d) {
 static void solve(const Mdl* md, Dat* d) {
   if (md->m->solver == 0) solve_pgs_main(md, d);
   else solve_newton(md, d);
+  double u_main[128];
+  memcpy(u_main, d->w, sizeof(double) * md->m->nv);
   noslip(md, d);
-  finalize_solution(md, d);
+  finalize_solution(md, d, u_main);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -59,6 +59,28 @@ def test_allegro_host_bookkeeping(aenv, acand):
     assert np.array_equal(q[:, idx], J[:3])
 
 
+def test_allegro_free_close_known_answer(aenv, aom):
+    """Free-space close (object out of reach) against allegro.yaml:7 qpos_close,
+    which close_gripper_at sends as the servo targets (allegro.py:354-357):
+    the unobstructed first and ring fingers settle on it exactly (position
+    servos, no gravity); the thumb (target 1.4 clamped to its ctrlrange 1.396)
+    meets the middle finger, so those two chains rest short of it on that one
+    contact.  The hand comes to rest."""
+    from mgs.util.geo.transforms import SE3Pose
+    close = np.array([-0.08, 0.95, 1, 0.95, 0, 0.95, 1.2, 0.85, 0.08, 0.95, 1.2, 0.9, 1.4, 0.55, 0.29, 1.45])
+    pose = SE3Pose(np.array([[0.0, 0.0, 0.0]]), np.array([[1.0, 0, 0, 0]]), "wxyz")
+    q, mp, mq, _ = aenv.initial_state(pose, np.zeros((1, 16)))
+    q[0, 23] = 1.0          # object x: far from the hand
+    tr, nc, qv = aom.trace(q[0], mp[0], mq[0], close, 3000)
+    qf = tr[-1, 7:23]
+    assert np.abs(qf[0:4] - close[0:4]).max() < 1e-9          # first finger
+    assert np.abs(qf[8:12] - close[8:12]).max() < 1e-9        # ring finger
+    assert np.abs(qf[4:8] - close[4:8]).max() < 1e-2          # middle finger, held by the thumb
+    assert np.abs(qf[12:16] - close[12:16]).max() < 1.5e-2    # thumb
+    assert nc[-1] == 1
+    assert np.abs(qv).max() < 1e-9
+
+
 def test_allegro_oracle_grasps(aenv, acand, aom):
     from conftest import plan_for
     poses, J = acand
