@@ -113,9 +113,25 @@ def issue_summary():
     sq, cs = j.get("sq", {}), j.get("executed_candidate_steps")
     if not sq or not cs:
         return None
-    out = {k.replace("SQ_", "").lower() + "_per_candidate_step": v / cs for k, v in sq.items()}
+    # SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
+    # (MI355X_MICROARCH.md, per-instruction constants table); instruction
+    # counters count wave-instructions
+    quad = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+    out = {}
+    for k, v in sq.items():
+        name = k.replace("SQ_", "").lower()
+        if k in quad:
+            out[name + "_cycles_per_candidate_step"] = 4.0 * v / cs
+        else:
+            out[name + "_per_candidate_step"] = v / cs
     if "SQ_WAIT_ANY" in sq and "SQ_WAVE_CYCLES" in sq:
-        out["wait_any_frac"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
+        # latency view: the share of a wave's lifetime spent issuing, parked at
+        # s_waitcnt (LDS / memory) and stalled at issue; one wave per SIMD
+        # (register-limited), so parked cycles are idle SIMD cycles
+        w = sq["SQ_WAVE_CYCLES"]
+        out["issue_frac"] = sq.get("SQ_ACTIVE_INST_ANY", 0.0) / w
+        out["wait_any_frac"] = sq["SQ_WAIT_ANY"] / w
+        out["wait_inst_any_frac"] = sq.get("SQ_WAIT_INST_ANY", 0.0) / w
     out["source"] = "profiles/pmc_rollout.json (" + j.get("kernel", "") + ")"
     return out
 
@@ -142,7 +158,7 @@ def e2e_api(env, poses, J, h, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--candidates", type=int, default=8192)
     ap.add_argument("--horizon", default="h200")

@@ -114,10 +114,12 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
 // 28, Shadow + free object = 34.  Wide library (MGS_WIDE: 4 rows per lane, G in
 // HBM) for clutter piles of 5 free objects: Panda 38, Robotiq 44, Allegro 52,
 // Shadow 58.
+#ifndef MGS_NV_LIST            /* a -D override builds one instantiation (tools/isa_stats.sh) */
 #ifdef MGS_WIDE
 #define MGS_NV_LIST(X) X(38) X(44) X(52) X(58)
 #else
 #define MGS_NV_LIST(X) X(14) X(20) X(28) X(34)
+#endif
 #endif
 
 static bool nv_supported(int nv) {

@@ -1,14 +1,18 @@
-"""Summarise a tools/prof_r01.sh output directory into profiles/:
+"""Summarise a tools/prof_r0N.sh output directory into profiles/:
 
-  profiles/r01_rocprof_kernel_stats.csv   kernel-trace --stats of the bench command
-  profiles/r01_pmc_{fetch,write,sq}.csv   the rollout kernel's counter rows
+  profiles/<tag>_rocprof_kernel_stats.csv kernel-trace --stats of the bench command
+  profiles/<tag>_pmc_{fetch,write,sq}.csv the rollout kernel's counter rows
   profiles/pmc_rollout.json               HBM bytes per launch (FETCH_SIZE x 2, the
                                           gfx950 half-count correction of
                                           MI355X_MICROARCH.md, + WRITE_SIZE; KiB) and
                                           per executed candidate-step, SQ totals
   profiles/r01_bench.json                 the bench line of the same run
 
-    python tools/pmc_summary.py gpurun_out/r01d
+    python tools/pmc_summary.py gpurun_out/r02p [tag]
+
+Counters are averaged over the rollout dispatches of the pass (the round-2
+passes run a single-pipeline bench without the escalation pass, so every
+dispatch is one full rollout launch of the headline batch).
 """
 import csv
 import json
@@ -25,22 +29,23 @@ def rows(path, kernel="mgs_rollout_kernel"):
         return [r for r in csv.DictReader(f) if kernel in r["Kernel_Name"]]
 
 
-def main(d):
-    shutil.copy(os.path.join(d, "trace", "bench_kernel_stats.csv"), os.path.join(PROF, "r01_rocprof_kernel_stats.csv"))
-    shutil.copy(os.path.join(d, "bench.json"), os.path.join(PROF, "r01_bench.json"))
-    out = {"source": "rocprofv3 --kernel-trace --pmc <counters> (separate passes) on `python3 bench.py --steps 1 "
-                     "--warmup 0 --cpu-budget 0` (tools/prof_r01.sh)",
+def main(d, tag="r02"):
+    shutil.copy(os.path.join(d, "trace", "bench_kernel_stats.csv"), os.path.join(PROF, f"{tag}_rocprof_kernel_stats.csv"))
+    out = {"source": "rocprofv3 --kernel-trace --pmc <counters> (separate passes) on `python3 bench.py --streams 1 "
+                     "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate` (tools/prof_r02.sh); "
+                     "per rollout dispatch",
            "kernel": "mgs_rollout_kernel<20>"}
     sums = {}
     for name in ("fetch", "write", "sq"):
         p = os.path.join(d, f"pmc_{name}", "pmc_counter_collection.csv")
         rr = rows(p)
-        with open(os.path.join(PROF, f"r01_pmc_{name}.csv"), "w", newline="") as f:
+        with open(os.path.join(PROF, f"{tag}_pmc_{name}.csv"), "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=list(rr[0].keys()))
             w.writeheader()
             w.writerows(rr)
+        ndisp = len({r["Dispatch_Id"] for r in rr}) or 1
         for r in rr:
-            sums[r["Counter_Name"]] = sums.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            sums[r["Counter_Name"]] = sums.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) / ndisp
     with open(os.path.join(d, "pmc_fetch.json")) as f:
         steps = json.loads(f.read().strip().splitlines()[-1])["detail"]["executed_candidate_steps"]
     hbm = (2.0 * sums["FETCH_SIZE"] + sums["WRITE_SIZE"]) * 1024.0
@@ -55,4 +60,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:3])
