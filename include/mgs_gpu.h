@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 8
+#define MGS_ABI_VERSION 9
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -351,6 +351,63 @@ int mgs_simulate(mgs_batch* batch, const mgs_schedule* sched, int n, const doubl
 int mgs_simulate_device(mgs_batch* batch, const mgs_schedule* sched, int n, const double* d_qpos_init,
                         const double* d_vstate_init, const double* d_mocap_quat, const double* d_phase_start,
                         const double* d_phase_target, double* d_state_out, int32_t* d_stats, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Contact-based dexterous-hand sampler (ContactBasedDiff.generate_grasps,
+ * mgs/sampler/contact.py:176-297): farthest-point seeds, local contact-target
+ * selection, and a batched AdamW fit of the hand pose (6-D rotation, position)
+ * and joints so that the fingertip contact points reach the targets
+ * (contact.py:98-158 update/loss_fn; forward kinematics
+ * mgs/sampler/kin/base.py:80-113; assignment mgs/sampler/kin/jax_util.py:205-224).
+ * The kinematic model is data (mgs/sampler/kin/shadow.py:17-223).  Host
+ * pointers, synchronous on `device`; kernel_ms (may be NULL) = kernel time. */
+#define MGS_KIN_MAXDOF 24
+#define MGS_KIN_MAXTIP 5
+#define MGS_KIN_MAXCHAIN 6
+#define MGS_KIN_MAXPERM 120
+typedef struct mgs_kin_desc {
+  int32_t ndof, ntip, nperm, iters;
+  int32_t chain_len[MGS_KIN_MAXTIP];                 /* dofs from the palm to tip a */
+  int32_t chain[MGS_KIN_MAXTIP][MGS_KIN_MAXCHAIN];   /* dof indices, root first */
+  int32_t perm[MGS_KIN_MAXPERM][MGS_KIN_MAXTIP];     /* itertools.permutations order */
+  double kin_tf[MGS_KIN_MAXDOF][7];                  /* parent -> joint frame: wxyz, xyz */
+  double joint_tf[MGS_KIN_MAXDOF][6];                /* prismatic direction, revolute axis */
+  double range[MGS_KIN_MAXDOF][2];
+  double pregrasp[MGS_KIN_MAXDOF];
+  double tip_point[MGS_KIN_MAXTIP][3];               /* chosen contact point, tip frame */
+  double tip_normal[MGS_KIN_MAXTIP][3];              /* contact normal point, tip frame */
+  double lr, b1, b2, eps, eps_root, weight_decay;    /* optax.adamw(lr) */
+  double w_cos;                                      /* weight of the normal-alignment term */
+} mgs_kin_desc;
+
+/* sizeof(mgs_kin_desc) as compiled (the Python mirror checks its layout) */
+int mgs_kin_desc_size(void);
+
+/* farthest_point_sampling (jax_util.py:182-203): k indices into points (n * 3),
+ * out_idx[0] = 0, each next index the first argmax of the running minimum
+ * squared distance to the chosen set. */
+int mgs_contact_fps(int device, const double* points, int n, int k, int32_t* out_idx, double* kernel_ms);
+
+/* Per seed i of k seeds (seeds: k * 3): out_nn[i] = the nearest other seed
+ * (argsort(dists)[:, 1], contact.py:226-228) and out_sel[i * ntip ...] = the
+ * ntip largest random keys among seeds within `radius` (non-admissible keys
+ * -inf), in ascending stable-argsort order (contact.py:201-210).  The keys are
+ * splitmix64(rng_seed, i * k + j) uniforms in [0, 1) (the reference draws them
+ * with jax.random.uniform, which is not restated). */
+int mgs_contact_seeds(int device, const double* seeds, int k, double radius, uint64_t rng_seed, int ntip,
+                      int32_t* out_nn, int32_t* out_sel, double* kernel_ms);
+
+/* The AdamW fit of n candidates: rot_init (n * 9, the initial rotation matrix,
+ * row-major), pos_init (n * 3), targets / normals (n * ntip * 3, the offset
+ * contact targets and their surface normals in selection order).  The initial
+ * fingertip-target assignment uses rot_init (contact.py:254-278); the loop
+ * re-assigns every iteration (loss_fn).  Outputs: out_rot (n * 9, rows of the
+ * Gram-Schmidt matrix of the final 6-D rotation), out_pos (n * 3), out_joints
+ * (n * ndof, clipped to the ranges), out_loss (n, may be NULL: the loss at the
+ * last iteration). */
+int mgs_contact_optimize(int device, const mgs_kin_desc* kin, int n, const double* rot_init, const double* pos_init,
+                         const double* targets, const double* normals, double* out_rot, double* out_pos,
+                         double* out_joints, double* out_loss, double* kernel_ms);
 
 /* Duration (ms) of the last rollout kernel launch, measured with HIP events
  * on the launch stream (waits for it). */

@@ -13,6 +13,7 @@
 #endif
 #include "mgs_kernels.hip"
 #include "mgs_sampler.hip"
+#include "mgs_contact.hip"
 
 namespace {
 thread_local std::string g_err;
@@ -552,6 +553,135 @@ int mgs_antipodal_contacts(int device, const double* tri, int ntri, int n, const
   if (e0) hipEventDestroy(e0);
   if (e1) hipEventDestroy(e1);
   hipFree(dT); hipFree(dO); hipFree(dD); hipFree(dU); hipFree(dS); hipFree(dN);
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// contact-based dexterous-hand sampler (csrc/mgs_contact.hip)
+}  // extern "C"
+namespace {
+struct DevBufs {
+  std::vector<void*> p;
+  bool ok = true;
+  template <class T>
+  T* get(size_t n) {
+    void* q = nullptr;
+    if (hipMalloc(&q, (n > 0 ? n : 1) * sizeof(T)) != hipSuccess) { ok = false; return nullptr; }
+    p.push_back(q);
+    return (T*)q;
+  }
+  ~DevBufs() { for (void* q : p) hipFree(q); }
+};
+struct EvTimer {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  EvTimer() { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, nullptr); }
+  int finish(double* ms) {
+    hipEventRecord(e1, nullptr);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e != hipSuccess) return fail(MGS_EHIP, "HIP error: %s", hipGetErrorString(e));
+    float f = 0.f;
+    hipEventElapsedTime(&f, e0, e1);
+    if (ms) *ms = f;
+    return MGS_OK;
+  }
+  ~EvTimer() { hipEventDestroy(e0); hipEventDestroy(e1); }
+};
+}  // namespace
+extern "C" {
+
+int mgs_kin_desc_size(void) { return (int)sizeof(mgs_kin_desc); }
+
+int mgs_contact_fps(int device, const double* points, int n, int k, int32_t* out_idx, double* kernel_ms) {
+  if (n < 0 || k < 0 || (k > 0 && n == 0) || k > n) return fail(MGS_EINVAL, "mgs_contact_fps: need 0 <= k <= n%s");
+  if (k == 0) return MGS_OK;
+  if (!points || !out_idx) return fail(MGS_EINVAL, "mgs_contact_fps: null argument%s");
+  HIPCHK(hipSetDevice(device));
+  DevBufs b;
+  double* dX = b.get<double>(3 * (size_t)n);
+  double* dD = b.get<double>((size_t)n);
+  int32_t* dO = b.get<int32_t>((size_t)k);
+  if (!b.ok) return fail(MGS_ENOMEM, "device allocation failed%s");
+  HIPCHK(hipMemcpy(dX, points, 3 * (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+  EvTimer t;
+  hipLaunchKernelGGL(mgs_fps_kernel, dim3(1), dim3(MGS_FPS_THREADS), 0, nullptr, dX, n, k, dD, dO);
+  int rc = t.finish(kernel_ms);
+  if (rc == MGS_OK) HIPCHK(hipMemcpy(out_idx, dO, (size_t)k * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return rc;
+}
+
+int mgs_contact_seeds(int device, const double* seeds, int k, double radius, uint64_t rng_seed, int ntip,
+                      int32_t* out_nn, int32_t* out_sel, double* kernel_ms) {
+  if (k < 0 || ntip < 1 || ntip > MGS_KIN_MAXTIP) return fail(MGS_EINVAL, "mgs_contact_seeds: bad size%s");
+  if (k == 0) return MGS_OK;
+  if (!seeds || !out_nn || !out_sel) return fail(MGS_EINVAL, "mgs_contact_seeds: null argument%s");
+  HIPCHK(hipSetDevice(device));
+  DevBufs b;
+  double* dS = b.get<double>(3 * (size_t)k);
+  int32_t* dN = b.get<int32_t>((size_t)k);
+  int32_t* dL = b.get<int32_t>((size_t)k * ntip);
+  if (!b.ok) return fail(MGS_ENOMEM, "device allocation failed%s");
+  HIPCHK(hipMemcpy(dS, seeds, 3 * (size_t)k * sizeof(double), hipMemcpyHostToDevice));
+  EvTimer t;
+  hipLaunchKernelGGL(mgs_seeds_kernel, dim3((k + MGS_SEED_TILE - 1) / MGS_SEED_TILE), dim3(MGS_SEED_TILE), 0,
+                     nullptr, dS, k, radius, rng_seed, ntip, dN, dL);
+  int rc = t.finish(kernel_ms);
+  if (rc == MGS_OK) {
+    HIPCHK(hipMemcpy(out_nn, dN, (size_t)k * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_sel, dL, (size_t)k * ntip * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
+  return rc;
+}
+
+int mgs_contact_optimize(int device, const mgs_kin_desc* kin, int n, const double* rot_init, const double* pos_init,
+                         const double* targets, const double* normals, double* out_rot, double* out_pos,
+                         double* out_joints, double* out_loss, double* kernel_ms) {
+  if (!kin || n < 0) return fail(MGS_EINVAL, "mgs_contact_optimize: bad argument%s");
+  if (kin->ndof < 1 || kin->ndof > MGS_KIN_MAXDOF || kin->ntip < 1 || kin->ntip > MGS_KIN_MAXTIP ||
+      kin->nperm < 1 || kin->nperm > MGS_KIN_MAXPERM || kin->iters < 0)
+    return fail(MGS_EINVAL, "mgs_contact_optimize: kinematic model out of range%s");
+  for (int a = 0; a < kin->ntip; a++) {
+    if (kin->chain_len[a] < 1 || kin->chain_len[a] > MGS_KIN_MAXCHAIN)
+      return fail(MGS_EINVAL, "mgs_contact_optimize: chain length out of range%s");
+    for (int s = 0; s < kin->chain_len[a]; s++)
+      if (kin->chain[a][s] < 0 || kin->chain[a][s] >= kin->ndof)
+        return fail(MGS_EINVAL, "mgs_contact_optimize: chain dof out of range%s");
+  }
+  for (int q = 0; q < kin->nperm; q++)
+    for (int a = 0; a < kin->ntip; a++)
+      if (kin->perm[q][a] < 0 || kin->perm[q][a] >= kin->ntip)
+        return fail(MGS_EINVAL, "mgs_contact_optimize: permutation entry out of range%s");
+  if (n == 0) return MGS_OK;
+  if (!rot_init || !pos_init || !targets || !normals || !out_rot || !out_pos || !out_joints)
+    return fail(MGS_EINVAL, "mgs_contact_optimize: null argument%s");
+  HIPCHK(hipSetDevice(device));
+  const size_t nt = (size_t)kin->ntip, nd = (size_t)kin->ndof, nn = (size_t)n;
+  DevBufs b;
+  mgs_kin_desc* dK = b.get<mgs_kin_desc>(1);
+  double* dR = b.get<double>(9 * nn);
+  double* dP = b.get<double>(3 * nn);
+  double* dT = b.get<double>(3 * nt * nn);
+  double* dN = b.get<double>(3 * nt * nn);
+  double* oR = b.get<double>(9 * nn);
+  double* oP = b.get<double>(3 * nn);
+  double* oJ = b.get<double>(nd * nn);
+  double* oL = b.get<double>(nn);
+  if (!b.ok) return fail(MGS_ENOMEM, "device allocation failed%s");
+  HIPCHK(hipMemcpy(dK, kin, sizeof(mgs_kin_desc), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dR, rot_init, 9 * nn * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dP, pos_init, 3 * nn * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dT, targets, 3 * nt * nn * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dN, normals, 3 * nt * nn * sizeof(double), hipMemcpyHostToDevice));
+  EvTimer t;
+  hipLaunchKernelGGL(mgs_contact_opt_kernel, dim3((n + 63) / 64), dim3(64), 0, nullptr, dK, n, dR, dP, dT, dN,
+                     oR, oP, oJ, oL);
+  int rc = t.finish(kernel_ms);
+  if (rc == MGS_OK) {
+    HIPCHK(hipMemcpy(out_rot, oR, 9 * nn * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_pos, oP, 3 * nn * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_joints, oJ, nd * nn * sizeof(double), hipMemcpyDeviceToHost));
+    if (out_loss) HIPCHK(hipMemcpy(out_loss, oL, nn * sizeof(double), hipMemcpyDeviceToHost));
+  }
   return rc;
 }
 

@@ -65,6 +65,10 @@ def load_library(wide: bool = False):
     L.mgs_simulate.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
                                P(c_i)]
     L.mgs_simulate_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mgs_contact_fps.argtypes = [ctypes.c_int, P(c_d), ctypes.c_int, ctypes.c_int, P(c_i), P(c_d)]
+    L.mgs_contact_seeds.argtypes = [ctypes.c_int, P(c_d), ctypes.c_int, c_d, ctypes.c_uint64, ctypes.c_int, P(c_i),
+                                    P(c_i), P(c_d)]
+    L.mgs_contact_optimize.argtypes = [ctypes.c_int, P(abi.KinDesc), ctypes.c_int] + [P(c_d)] * 9
     L.mgs_supports_nv.argtypes = [ctypes.c_int]
     L.mgs_supports_nv.restype = ctypes.c_int
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
@@ -294,6 +298,59 @@ def antipodal_contacts(tri, origin, direction, u_choice, eps, device=0):
                                     ptr(sec, ctypes.c_double), ptr(cnt, ctypes.c_int32), ctypes.byref(ms)),
            "mgs_antipodal_contacts", L)
     return sec, cnt, ms.value
+
+
+def _device_lib(device):
+    L = load_library()
+    if L.mgs_device_count() <= device:
+        raise EngineError("no HIP device visible for the MI355X engine")
+    return L
+
+
+def contact_fps(points, k, device=0):
+    """farthest-point seeds on the GPU (mgs_contact_fps): (indices (k,), kernel ms)"""
+    L = _device_lib(device)
+    x = np.ascontiguousarray(points, np.float64).reshape(-1, 3)
+    out = np.zeros(k, np.int32)
+    ms = ctypes.c_double(0.0)
+    _check(L.mgs_contact_fps(device, ptr(x, ctypes.c_double), len(x), int(k), ptr(out, ctypes.c_int32),
+                             ctypes.byref(ms)), "mgs_contact_fps", L)
+    return out, ms.value
+
+
+def contact_seeds(seeds, radius, rng_seed, ntip, device=0):
+    """nearest seed and the random admissible picks (mgs_contact_seeds):
+    (nn (k,), sel (k, ntip), kernel ms)"""
+    L = _device_lib(device)
+    s = np.ascontiguousarray(seeds, np.float64).reshape(-1, 3)
+    k = len(s)
+    nn = np.zeros(k, np.int32)
+    sel = np.zeros((k, ntip), np.int32)
+    ms = ctypes.c_double(0.0)
+    _check(L.mgs_contact_seeds(device, ptr(s, ctypes.c_double), k, float(radius), int(rng_seed) & (2**64 - 1),
+                               int(ntip), ptr(nn, ctypes.c_int32), ptr(sel, ctypes.c_int32), ctypes.byref(ms)),
+           "mgs_contact_seeds", L)
+    return nn, sel, ms.value
+
+
+def contact_optimize(kin_desc, rot_init, pos_init, targets, normals, device=0):
+    """the batched AdamW fit (mgs_contact_optimize): dict of rot (n,3,3) rows,
+    pos (n,3), joints (n,ndof), loss (n,), kernel_ms"""
+    L = _device_lib(device)
+    R0 = np.ascontiguousarray(rot_init, np.float64).reshape(-1, 9)
+    n = len(R0)
+    nt = kin_desc.ntip
+    p0 = np.ascontiguousarray(pos_init, np.float64).reshape(n, 3)
+    T = np.ascontiguousarray(targets, np.float64).reshape(n, nt, 3)
+    N = np.ascontiguousarray(normals, np.float64).reshape(n, nt, 3)
+    oR, oP = np.zeros((n, 3, 3)), np.zeros((n, 3))
+    oJ, oL = np.zeros((n, kin_desc.ndof)), np.zeros(n)
+    ms = ctypes.c_double(0.0)
+    d = ctypes.c_double
+    _check(L.mgs_contact_optimize(device, ctypes.byref(kin_desc), n, ptr(R0, d), ptr(p0, d), ptr(T, d), ptr(N, d),
+                                  ptr(oR, d), ptr(oP, d), ptr(oJ, d), ptr(oL, d), ctypes.byref(ms)),
+           "mgs_contact_optimize", L)
+    return dict(rot=oR, pos=oP, joints=oJ, loss=oL, kernel_ms=ms.value)
 
 
 def tree_probe(a, c, n):

@@ -27,8 +27,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        src = os.path.join(_HERE, "mgs_oracle.c")
-        if not os.path.isfile(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+        srcs = [os.path.join(_HERE, f) for f in ("mgs_oracle.c", "mgs_contact_oracle.c")]
+        if not os.path.isfile(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(f) for f in srcs):
             build()
         L = ctypes.CDLL(_LIB)
         c_i, c_d, c_u8 = ctypes.c_int32, ctypes.c_double, ctypes.c_uint8
@@ -170,3 +170,70 @@ def tree_dot(a, b, n):
     a = np.ascontiguousarray(a, np.float64)
     b = np.ascontiguousarray(b, np.float64)
     return lib().oracle_tree_dot(ptr(a, ctypes.c_double), ptr(b, ctypes.c_double), n)
+
+
+# ---------------------------------------------------------------------------
+# contact-based dexterous-hand sampler (oracle/mgs_contact_oracle.c; checker)
+def _contact_lib():
+    L = lib()
+    P, d, i32 = ctypes.POINTER, ctypes.c_double, ctypes.c_int32
+    L.oracle_contact_fps.argtypes = [P(d), ctypes.c_int, ctypes.c_int, P(i32)]
+    L.oracle_contact_seeds.argtypes = [P(d), ctypes.c_int, d, ctypes.c_uint64, ctypes.c_int, P(i32), P(i32),
+                                       ctypes.c_int]
+    L.oracle_contact_optimize.argtypes = [P(abi.KinDesc), ctypes.c_int] + [P(d)] * 8 + [ctypes.c_int]
+    L.oracle_contact_fk.argtypes = [P(abi.KinDesc), P(d), P(d), P(d)]
+    L.oracle_contact_loss_grad.argtypes = [P(abi.KinDesc), P(d), P(d), P(d), P(d)]
+    L.oracle_contact_loss_grad.restype = d
+    return L
+
+
+def contact_fps(points, k):
+    x = np.ascontiguousarray(points, np.float64).reshape(-1, 3)
+    out = np.zeros(k, np.int32)
+    _contact_lib().oracle_contact_fps(ptr(x, ctypes.c_double), len(x), int(k), ptr(out, ctypes.c_int32))
+    return out
+
+
+def contact_seeds(seeds, radius, rng_seed, ntip, nthreads=8):
+    s = np.ascontiguousarray(seeds, np.float64).reshape(-1, 3)
+    k = len(s)
+    nn = np.zeros(k, np.int32)
+    sel = np.zeros((k, ntip), np.int32)
+    _contact_lib().oracle_contact_seeds(ptr(s, ctypes.c_double), k, float(radius), int(rng_seed) & (2**64 - 1),
+                                        int(ntip), ptr(nn, ctypes.c_int32), ptr(sel, ctypes.c_int32), nthreads)
+    return nn, sel
+
+
+def contact_optimize(desc, rot_init, pos_init, targets, normals, nthreads=8):
+    d = ctypes.c_double
+    R0 = np.ascontiguousarray(rot_init, np.float64).reshape(-1, 9)
+    n = len(R0)
+    p0 = np.ascontiguousarray(pos_init, np.float64).reshape(n, 3)
+    T = np.ascontiguousarray(targets, np.float64).reshape(n, desc.ntip, 3)
+    N = np.ascontiguousarray(normals, np.float64).reshape(n, desc.ntip, 3)
+    oR, oP, oJ, oL = np.zeros((n, 3, 3)), np.zeros((n, 3)), np.zeros((n, desc.ndof)), np.zeros(n)
+    _contact_lib().oracle_contact_optimize(ctypes.byref(desc), n, ptr(R0, d), ptr(p0, d), ptr(T, d), ptr(N, d),
+                                           ptr(oR, d), ptr(oP, d), ptr(oJ, d), ptr(oL, d), nthreads)
+    return dict(rot=oR, pos=oP, joints=oJ, loss=oL)
+
+
+def contact_fk(desc, theta):
+    """hand-frame tip points (ntip, 3 points, 3) and their chain derivatives
+    (ntip, MAXCHAIN, 3, 3)"""
+    d = ctypes.c_double
+    th = np.ascontiguousarray(theta, np.float64)
+    mc = abi.MGS["MGS_KIN_MAXCHAIN"]
+    X = np.zeros((desc.ntip, 3, 3))
+    dX = np.zeros((desc.ntip, mc, 3, 3))
+    _contact_lib().oracle_contact_fk(ctypes.byref(desc), ptr(th, d), ptr(X, d), ptr(dX, d))
+    return X, dX
+
+
+def contact_loss_grad(desc, prm, targets, normals):
+    d = ctypes.c_double
+    p = np.ascontiguousarray(prm, np.float64)
+    T = np.ascontiguousarray(targets, np.float64)
+    N = np.ascontiguousarray(normals, np.float64)
+    g = np.zeros(len(p))
+    loss = _contact_lib().oracle_contact_loss_grad(ctypes.byref(desc), ptr(p, d), ptr(T, d), ptr(N, d), ptr(g, d))
+    return loss, g

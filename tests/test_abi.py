@@ -55,6 +55,14 @@ def test_struct_mirror_matches_header():
     assert [f for f, _ in abi.ModelDesc._fields_] == names
 
 
+def test_kin_desc_mirror_matches_library(lib):
+    """the contact sampler's model struct: ctypes layout == the compiled one"""
+    from mgs.core import abi
+    lib.mgs_kin_desc_size.restype = ctypes.c_int
+    assert lib.mgs_kin_desc_size() == ctypes.sizeof(abi.KinDesc)
+    assert abi.KinDesc.perm.size == ctypes.sizeof(ctypes.c_int32) * 120 * 5
+
+
 def test_pack_fills_every_offset(env):
     from mgs.core import abi
     fields, ib, db = env.model.pack(ncon_max=16)

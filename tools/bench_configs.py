@@ -161,6 +161,34 @@ def sampler(n=8192, subdiv=5):
                 bit_exact=bool(np.array_equal(sg, so) and np.array_equal(cg, co)))
 
 
+def contact(n=10000, cpu_n=256):
+    """the contact-based Shadow Hand sampler (mgs.sampler.contact): n grasps on
+    one object; GPU stages timed by HIP events, the wall clock of
+    generate_grasps, and the C oracle's fit on a cpu_n sample (16 threads)"""
+    import copy
+    from mgs.obj.selector import get_object
+    from mgs.sampler import contact as C
+    from mgs.sampler.kin.model import ShadowKinematicsModel
+    from oracle import oracle as O
+    kin = ShadowKinematicsModel()
+    obj = get_object("005_tomato_soup_can")
+    C.ContactBasedDiff(obj, rng=np.random.default_rng(9)).generate_grasps(64, kin)     # warm-up
+    s = C.ContactBasedDiff(obj, rng=np.random.default_rng(0))
+    t0 = time.perf_counter()
+    H, aux = s.generate_grasps(n, kin)
+    dt = time.perf_counter() - t0
+    inp, desc = C.ContactBasedDiff(obj, rng=np.random.default_rng(0)).prepare(n, kin)
+    t1 = time.perf_counter()
+    O.contact_optimize(desc, inp["rot_init"][:cpu_n], inp["pos_init"][:cpu_n], inp["targets"][:cpu_n],
+                       inp["normals"][:cpu_n], nthreads=16)
+    cpu = (time.perf_counter() - t1) / cpu_n
+    km = s.last["kernel_ms"]
+    return dict(value=n / dt, unit="grasps/s", grasps=n, seconds=dt, kernel_ms=km,
+                fit_grasps_per_s_gpu=n / (km["optimize"] * 1e-3),
+                fit_grasps_per_s_cpu_oracle_16t=1.0 / cpu, median_final_loss=float(np.median(s.last["loss"])),
+                iterations=desc.iters)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["c3", "c4", "c5", "sampler"])
@@ -191,6 +219,9 @@ def main():
             out = dict(config="scenes", workload=f"gen_clutter + is_stable, {a.scene_piles} Robotiq piles of 5 "
                                                  "fast-subset objects, 5 x 900 + 9000 + 1000 steps",
                        **scenes(a.scene_piles, ncon=a.scene_ncon))
+        elif c == "contact":
+            out = dict(config="contact", workload="contact-based Shadow Hand sampler (FPS seeds, local targets, "
+                                                  "150 AdamW steps), 10000 grasps on 005_tomato_soup_can", **contact())
         elif c == "sampler":
             out = dict(config="sampler", workload="antipodal ray casting, 8192 points x 20480-face icosphere",
                        **sampler())
