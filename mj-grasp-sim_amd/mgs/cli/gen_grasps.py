@@ -28,7 +28,7 @@ def run(cfg):
     os.makedirs(out, exist_ok=True)
     t0 = time.perf_counter()
     H, J = candidates(gripper, obj, int(cfg.get("num_grasps", 8192)), int(cfg.get("seed", 0)),
-                      cfg.get("sampler", "device"))
+                      cfg.get("sampler", "device"), gripper_name=cfg.gripper.name)
     np.savez(os.path.join(out, "candidates.npz"), pose=H, joints=J)
     t1 = time.perf_counter()
     env = GravitylessObjectGrasping(gripper, obj)
