@@ -6,8 +6,11 @@ One step = the reference's filter_to_stable pipeline (mgs/cli/filter_to_stable.p
 39-50) over one batch: collision mask of every candidate, then the close ->
 lift -> shake rollout of the collision-free ones (h200 horizon).  Inputs are
 host-prepared once (float32 SE3 processing, mocap schedule), uploaded, and
-resident in HBM when the timed region starts; both kernels run back-to-back on
-one stream with no host round trip (the rollout reads the mask on the device).
+resident in HBM when the timed region starts; each step runs the mask, the
+rollout (which reads the mask on the device) and the masked capacity-escalation
+launch on one HIP stream with no host round trip.  Steps rotate over
+`--streams` pipelines (engine + stream each, default 3), so one batch's
+rollout tail overlaps the next batches' work; every step is a whole batch.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--candidates 8192]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -170,7 +173,7 @@ def main():
                     help="N > 1: skip rank 0's single-GPU re-evaluation of every rank's block")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",

@@ -9,7 +9,9 @@
 
 #ifdef MGS_WIDE
 #define MGS_RPL 4
+#ifndef MGS_G_LDS          /* -DMGS_G_LDS: the wide build with G kept in LDS (experiments) */
 #define MGS_G_GLOBAL 1
+#endif
 #endif
 #include "mgs_kernels.hip"
 #include "mgs_sampler.hip"

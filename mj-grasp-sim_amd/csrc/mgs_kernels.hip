@@ -560,6 +560,31 @@ DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
     }
   }
 }
+// The same factor without register rows (wide build, nv 38-58, where NV-long
+// register rows spill): left-looking, lane i keeps row i in LDS; column c of
+// every row takes sum_{k<c} l_ik (l_ck d_k) in ascending k -- the products and
+// order of the right-looking loop above, so the factor is bit-identical.  The
+// l_ck d_k are parked in the (dead) upper triangle, V[c][k] at A[k][c].  The
+// diagonal keeps the original entries (meaninertia reads them).
+template <int NV>
+DEVI void ldl_factor_lds(double* A, double* Dv, double* Dinv) {
+  const int lane = lane_id();
+  const int li = lane < NV ? lane : 0;
+  for (int c = 0; c < NV; c++) {
+    double s = A[li * NV + c];
+    for (int k = 0; k < c; k++) s = __builtin_fma(-A[li * NV + k], A[k * NV + c], s);
+    double dc = readlane_d(s, c);
+    double inv = 1.0 / dc;
+    if (lane == 0) { Dv[c] = dc; Dinv[c] = inv; }
+    if (lane > c && lane < NV) {
+      double l = s * inv;
+      A[li * NV + c] = l;
+      A[c * NV + li] = l * dc;
+    }
+    wsync();
+  }
+}
+
 template <int NV>
 DEVI void store_lower(double* A, const double (&r)[NV]) {
   int lane = lane_id();
@@ -572,6 +597,7 @@ DEVI void store_lower(double* A, const double (&r)[NV]) {
 }
 template <int NV>
 DEVI void ldl_factor(double* A, double* Dv, double* Dinv) {
+#if MGS_REG_ROWS
   int lane = lane_id();
   int li = lane < NV ? lane : 0;
   double r[NV];
@@ -579,6 +605,9 @@ DEVI void ldl_factor(double* A, double* Dv, double* Dinv) {
   for (int k = 0; k < NV; k++) r[k] = A[li * NV + k];
   ldl_factor_regs<NV>(r, Dv, Dinv);
   store_lower<NV>(A, r);
+#else
+  ldl_factor_lds<NV>(A, Dv, Dinv);
+#endif
 }
 
 // x = (L D L^T)^-1 b, all lanes (lane i owns x_i).  Forward substitution
@@ -3078,14 +3107,9 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     hessian_mfma<NV>(md, d, ne);
     PT(23);
     {
-      int li = lane < NV ? lane : 0;
-      double hr[NV];
-#pragma unroll
-      for (int k = 0; k < NV; k++) hr[k] = d.nH[li * NV + k];
       PT(24);
-      ldl_factor_regs<NV>(hr, d.tmp, d.tmp2);
+      ldl_factor<NV>(d.nH, d.tmp, d.tmp2);
       PT(25);
-      store_lower<NV>(d.nH, hr);
     }
     PT(13);
     ldl_solve<NV>(d.nH, d.tmp2, d.ng, d.ndir);

@@ -32,6 +32,8 @@ def load_library(wide: bool = False):
     # same C-ABI under mgs/_lib to load as the main library
     if not wide and os.environ.get("MGS_LIB_MAIN"):
         path = os.path.join(LIB_DIR, os.environ["MGS_LIB_MAIN"])
+    if wide and os.environ.get("MGS_LIB_WIDE"):
+        path = os.path.join(LIB_DIR, os.environ["MGS_LIB_WIDE"])
     if path in _libs:
         return _libs[path]
     if not os.path.isfile(path):

@@ -15,6 +15,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X; runs the HIP engine through the C-ABI")
 
 
+def pytest_runtest_setup(item):
+    """GPU tests start the HIP runtime through torch first (the engine's device
+    count is read after it), whichever GPU test of a selection runs first"""
+    if item.get_closest_marker("gpu") is not None:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+
+
 @pytest.fixture(scope="session")
 def env():
     from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
