@@ -7,8 +7,9 @@ One step = the reference's filter_to_stable pipeline (mgs/cli/filter_to_stable.p
 lift -> shake rollout of the collision-free ones (h200 horizon).  Inputs are
 host-prepared once (float32 SE3 processing, mocap schedule), uploaded, and
 resident in HBM when the timed region starts; each step runs the mask, the
-rollout (which reads the mask on the device) and the masked capacity-escalation
-launch on one HIP stream with no host round trip.  Steps rotate over
+rollout (which reads the mask on the device) and a device-side count of
+capacity overflows on one HIP stream with no host round trip; overflowed
+candidates are re-run wider after the loop, inside the timed region.  Steps rotate over
 `--streams` pipelines (engine + stream each, default 3), so one batch's
 rollout tail overlaps the next batches' work; every step is a whole batch.
 
@@ -65,7 +66,7 @@ def cpu_baseline(env, poses, joints, h, budget_s, threads):
     """The oracle (C restatement, OpenMP over candidates) on the host cores, on a
     bounded leading sample of the same candidate block; returns a dict."""
     from oracle import oracle as O
-    om = O.OracleModel(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+    om = O.OracleModel(env.model, ncon_max=40)         # the escalation ceiling: MuJoCo has no cap
     q, mp, mq, _ = env.initial_state(poses, joints)
     # pilot on 256 candidates to size the sample to the time budget
     n_pilot = min(256, len(poses))
@@ -244,11 +245,11 @@ def main():
                                                           nefc_max=env.nefc_max)
             # contact-capacity escalation (GravitylessObjectGrasping.rollout):
             # candidates whose contacts / rows exceeded the capacity are re-run
-            # with a wider engine, selected on the device (d_ovf) and merged into
-            # the outputs; launched every step, it returns at once when no
-            # candidate overflowed (the usual case)
-            self.wide = (env.engine_for(2 * env.ncon_max) if s == 0 else
-                         Engine(env.model, device=local, ncon_max=2 * env.ncon_max)) if args.escalate else None
+            # with a wider engine.  Each step counts its steps-with-overflow on
+            # the device; after the loop (still inside the timed region) one
+            # launch re-runs every overflowed candidate once per such step, all
+            # replicas concurrently, and the results are merged (escalate_all)
+            self.wide = args.escalate
             self.stream = torch.cuda.current_stream(dev) if s == 0 else torch.cuda.Stream(dev)
             self.free = torch.zeros(N, dtype=torch.uint8, device=dev)
             self.label = torch.zeros(N, dtype=torch.uint8, device=dev)
@@ -256,12 +257,13 @@ def main():
             self.objq = torch.zeros((N, 7), **f64)
             self.stats = torch.zeros((N, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
             self.w = [torch.zeros_like(t) for t in (self.label, self.fail, self.objq, self.stats)]
-            self.ovf = torch.zeros(N, dtype=torch.uint8, device=dev)
+            self.ovf_steps = torch.zeros((), dtype=torch.int64, device=dev)
+            self.nsteps = 0
             self.events = []
 
         def step(self, timed):
             sp = self.stream.cuda_stream
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
             with torch.cuda.stream(self.stream):
                 if ev:
                     ev[0].record(self.stream)
@@ -274,22 +276,50 @@ def main():
                                         self.stats.data_ptr(), d_active=self.free.data_ptr(), stream=sp)
                 if ev:
                     ev[2].record(self.stream)
-                if self.wide is not None:
-                    torch.ne(self.stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"], 0, out=self.ovf.view(torch.bool))
-                    wl, wf, wo, ws = self.w
-                    self.wide.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(),
-                                             d_pt.data_ptr(), wl.data_ptr(), wf.data_ptr(), wo.data_ptr(),
-                                             ws.data_ptr(), d_active=self.ovf.data_ptr(), stream=sp)
-                    m = self.ovf.bool()
-                    self.label.copy_(torch.where(m, wl, self.label))
-                    self.fail.copy_(torch.where(m, wf, self.fail))
-                    self.objq.copy_(torch.where(m[:, None], wo, self.objq))
-                    self.stats.copy_(torch.where(m[:, None], ws, self.stats))
-                if ev:
-                    ev[3].record(self.stream)
                     self.events.append(ev)
+                if self.wide:
+                    self.ovf_steps += ((self.stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"]) != 0).any()
+            self.nsteps += 1
 
     pipes = [Pipe(s) for s in range(max(1, args.streams))]
+    wide_eng = env.engine_for(2 * env.ncon_max) if args.escalate else None    # built before timing
+
+    def escalate_all():
+        """re-run, wider, every overflowed candidate of every step that had one
+        (one launch: replicas run concurrently), merge the results; returns
+        (steps escalated, replicas identical)"""
+        jobs = []
+        for p in pipes:
+            k = int(p.ovf_steps.item()) if args.escalate else 0
+            if k:
+                ov = np.nonzero(p.stats[:, 2].cpu().numpy() & abi.MGS["MGS_FLAG_CAPACITY"])[0]
+                jobs.append((p, ov, k))
+        if not jobs:
+            return 0, True, 0
+        allidx = np.concatenate([np.tile(ov, k) for _, ov, k in jobs])
+        # GravitylessObjectGrasping.rollout's loop: double the capacity up to 40
+        cap = 2 * env.ncon_max
+        sub = env.engine_for(cap).rollout(plan.subset(allidx))
+        pos = np.nonzero(sub["stats"][:, 2] & abi.MGS["MGS_FLAG_CAPACITY"])[0]
+        while len(pos) and cap < 40:
+            cap = min(2 * cap, 40)
+            s2 = env.engine_for(cap).rollout(plan.subset(allidx[pos]))
+            for key in ("label", "fail_step", "obj_qpos", "stats"):
+                sub[key][pos] = s2[key]
+            pos = pos[np.nonzero(s2["stats"][:, 2] & abi.MGS["MGS_FLAG_CAPACITY"])[0]]
+        same, off = True, 0
+        for p, ov, k in jobs:
+            m = len(ov)
+            for key in ("label", "fail_step", "obj_qpos", "stats"):
+                blk = sub[key][off:off + m * k].reshape((k, m) + sub[key].shape[1:])
+                same = same and bool((blk == blk[:1]).all())
+            sel = torch.as_tensor(ov, device=dev)
+            p.label[sel] = torch.as_tensor(sub["label"][off:off + m].astype(np.uint8), device=dev)
+            p.fail[sel] = torch.as_tensor(sub["fail_step"][off:off + m].astype(np.int32), device=dev)
+            p.objq[sel] = torch.as_tensor(sub["obj_qpos"][off:off + m], **f64)
+            p.stats[sel] = torch.as_tensor(sub["stats"][off:off + m].astype(np.int32), device=dev)
+            off += m * k
+        return sum(k for _, _, k in jobs), same, max(len(ov) for _, ov, _ in jobs)
     for k in range(max(args.warmup, len(pipes))):       # every pipeline warmed up
         pipes[k % len(pipes)].step(False)
     torch.cuda.synchronize(dev)
@@ -297,8 +327,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    for p in pipes:
+        p.ovf_steps.zero_()
     for k in range(args.steps):
         pipes[k % len(pipes)].step(True)
+    torch.cuda.synchronize(dev)
+    escalated_steps, esc_same, n_ovf = escalate_all()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -310,13 +344,11 @@ def main():
     # per-launch kernel durations from the HIP events on each pipeline's stream
     coll_ms = [e[0].elapsed_time(e[1]) for p in pipes for e in p.events]
     roll_ms = [e[1].elapsed_time(e[2]) for p in pipes for e in p.events]
-    esc_ms = [e[2].elapsed_time(e[3]) for p in pipes for e in p.events]
     P0 = pipes[0]
-    d_free, d_label, d_fail, d_stats, d_ovf = P0.free, P0.label, P0.fail, P0.stats, P0.ovf
+    d_free, d_label, d_fail, d_stats = P0.free, P0.label, P0.fail, P0.stats
     same_pipes = all(torch.equal(p.label, P0.label) and torch.equal(p.free, P0.free) and
                      torch.equal(p.fail, P0.fail) for p in pipes[1:])
-    wide = P0.wide
-    wide_ms = esc_ms if wide is not None else []
+    wide = wide_eng
 
     free = d_free.cpu().numpy().astype(bool)
     labels = d_label.cpu().numpy().astype(bool)
@@ -387,10 +419,10 @@ def main():
                    "mean_ncon": float(stats[:, 4].sum() / max(1, steps_exec)),
                    "mean_nefc": float(stats[:, 5].sum() / max(1, steps_exec)),
                    "solver_iters_per_step": float(stats[:, 3].sum() / max(1, steps_exec)),
-                   "overflow_candidates": int(d_ovf.sum().item()) if wide is not None
+                   "overflow_candidates": n_ovf if escalated_steps
                    else int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum()),
                    "diverged_candidates": int((stats[:, 2] & abi.MGS["MGS_FLAG_DIVERGED"] != 0).sum()),
-                   "escalation_pass_ms": float(np.mean(wide_ms)) if wide_ms else None,
+                   "escalated_steps": escalated_steps, "escalation_replicas_identical": esc_same,
                    "still_capped_after_escalation": int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum())
                    if wide is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

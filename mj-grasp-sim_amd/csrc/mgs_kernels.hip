@@ -2122,6 +2122,7 @@ DEVI void qcqp2(double A0, double A1, double A3, double bb0, double bb1, const d
     double delta = -val / deriv;
     if (delta < 1e-10) break;
     la = la + delta;
+    PCNT(45, 1);
   }
   double o0 = v1 * mu[0], o1 = v2 * mu[1];
   // active constraint: put the result on the ellipsoid (MuJoCo PGS / noslip)
@@ -2233,6 +2234,8 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
     old[i] = getf(F, r + i);
     res[i] = noslip ? (jw + d.efc_b[r + i]) : ((jw + d.efc_R[r + i] * old[i]) + d.efc_b[r + i]);
   }
+  PT(42);
+  PCNT(46, 1);
   double Ab[DIM * DIM];
 #pragma unroll
   for (int i = 0; i < DIM; i++) {
@@ -2312,6 +2315,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
 #pragma unroll
       for (int i = 1; i < DIM; i++) nw[i] = 0.0;
     }
+    PT(43);
     double del[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) del[i] = nw[1 + i] - old[1 + i];
@@ -2328,6 +2332,7 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
 #pragma unroll
     for (int i = 0; i < NF; i++) setf(F, r + 1 + i, nw[1 + i], lane);
   }
+  PT(44);
   return dc;
 }
 

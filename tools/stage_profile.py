@@ -10,12 +10,13 @@ NAMES = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll:
          'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
          'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
          'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne',
-         'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)']
+         'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)',
+         'noslip/pgs block: residual', 'noslip/pgs block: qcqp', 'noslip/pgs block: update']
 
 
 def report(buf, r, ncand, horizon):
     v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64),
-                        np.array(buf[39:42], dtype=np.float64)])
+                        np.array(buf[39:45], dtype=np.float64)])
     cnt = np.array(buf[26:31], dtype=np.float64)
     tot = v.sum()
     print('N=%d candidates, kernel %.1f ms, labels %d, overflow %d' % (
@@ -26,6 +27,10 @@ def report(buf, r, ncand, horizon):
     print('ticks per candidate-step: %.0f' % (tot / steps))
     print('per candidate-step: narrowphase pairs %.2f, hits %.2f, support calls %.2f, big-hull scans %.2f, '
           'big-hull pairs %.2f' % tuple(cnt / steps))
+    c2 = np.array(buf[36:39], dtype=np.float64) / steps
+    c3 = np.array(buf[45:47], dtype=np.float64) / steps
+    print('per candidate-step: ls_eval calls %.2f, newton_eval calls %.2f, noslip sweeps %.2f, '
+          'qcqp iterations %.2f, block updates %.2f' % (*c2, *c3))
 
 
 def main():
@@ -53,27 +58,7 @@ def main():
     L.mgs_prof_read(buf)
     r = env.engine.rollout(plan)
     L.mgs_prof_read(buf)
-    v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64), np.array(buf[39:42], dtype=np.float64)])
-    cnt = np.array(buf[26:31], dtype=np.float64)
-    names = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll: MPR', 'coll: feature+clip',
-             'crb', 'ldl(M)', 'act+passive+rne+smooth', 'con: J rows', 'con: G transform', 'con: params+blocks',
-             'newton: setup', 'newton: hessian', 'newton: ldl+solve+jv', 'newton: linesearch', 'newton: eval+grad',
-             'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
-             'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
-             'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne', 'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)']
-    tot = v.sum()
-    print('N=%d collision-free candidates, kernel %.1f ms, labels %d, mean iters/step %.1f, overflow %d' % (
-        len(idx), r['kernel_ms'], r['label'].sum(), r['stats'][:, 3].sum() / max(1, r['stats'][:, 3].size) / 200, (r['stats'][:, 2] != 0).sum()))
-    for n_, x in zip(names, v):
-        print('%-28s %6.1f%%  %.3g ticks' % (n_, 100 * x / tot, x))
-    steps = len(idx) * 200
-    print('ticks per candidate-step: %.0f' % (tot / steps))
-
-    steps_exec = r['stats'][:, 3].size and None
-    print('per candidate-step (all %d steps counted): narrowphase pairs %.2f, hits %.2f, support calls %.2f, big-hull support scans %.2f, big-hull pairs %.2f' % (
-        steps, cnt[0] / steps, cnt[1] / steps, cnt[2] / steps, cnt[3] / steps, cnt[4] / steps))
-    cnt2 = np.array(buf[36:39], dtype=np.float64)
-    print('per candidate-step: ls_eval calls %.2f, newton_eval calls %.2f, noslip sweeps %.2f' % tuple(cnt2 / steps))
+    report(buf, r, len(idx), 200)
 
 
 if __name__ == "__main__":
