@@ -120,7 +120,7 @@ def issue_summary():
     # SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
     # (MI355X_MICROARCH.md, per-instruction constants table); instruction
     # counters count wave-instructions
-    quad = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+    quad = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")
     out = {}
     for k, v in sq.items():
         name = k.replace("SQ_", "").lower()
@@ -136,6 +136,10 @@ def issue_summary():
         out["issue_frac"] = sq.get("SQ_ACTIVE_INST_ANY", 0.0) / w
         out["wait_any_frac"] = sq["SQ_WAIT_ANY"] / w
         out["wait_inst_any_frac"] = sq.get("SQ_WAIT_INST_ANY", 0.0) / w
+    f64 = sum(sq.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                        "SQ_INSTS_VALU_TRANS_F64"))
+    if f64 and sq.get("SQ_INSTS_VALU"):
+        out["f64_arith_share_of_valu"] = f64 / sq["SQ_INSTS_VALU"]
     out["source"] = "profiles/pmc_rollout.json (" + j.get("kernel", "") + ")"
     return out
 

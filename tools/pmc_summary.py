@@ -36,8 +36,10 @@ def main(d, tag="r02"):
                      "per rollout dispatch",
            "kernel": "mgs_rollout_kernel<20>"}
     sums = {}
-    for name in ("fetch", "write", "sq"):
+    for name in ("fetch", "write", "sq", "valu"):
         p = os.path.join(d, f"pmc_{name}", "pmc_counter_collection.csv")
+        if not os.path.isfile(p):
+            continue
         rr = rows(p)
         with open(os.path.join(PROF, f"{tag}_pmc_{name}.csv"), "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=list(rr[0].keys()))

@@ -13,6 +13,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench -f csv
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc_fetch -o pmc -f csv -- python3 $P > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err && \
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc_write -o pmc -f csv -- python3 $P > $OUT/pmc_write.json 2> $OUT/pmc_write.err && \
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM -d $OUT/pmc_sq -o pmc -f csv -- python3 $P > $OUT/pmc_sq.json 2> $OUT/pmc_sq.err && \
-timeout -k 10 60 rocprofv3 --list-avail > $OUT/list_avail.txt 2>&1 ; \
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_VALU SQ_INSTS_SALU -d $OUT/pmc_valu -o pmc -f csv -- python3 $P > $OUT/pmc_valu.json 2> $OUT/pmc_valu.err && \
 timeout -k 10 200 python3 tools/stage_profile.py 160 > $OUT/stages.txt 2>&1 && \
 timeout -k 10 300 python3 tools/stage_profile_clutter.py 300 > $OUT/stages_clutter.txt 2>&1
