@@ -7,10 +7,10 @@ One step = the reference's filter_to_stable pipeline (mgs/cli/filter_to_stable.p
 lift -> shake rollout of the collision-free ones (h200 horizon).  Inputs are
 host-prepared once (float32 SE3 processing, mocap schedule), uploaded, and
 resident in HBM when the timed region starts; each step runs the mask, the
-rollout (which reads the mask on the device) and a device-side count of
-capacity overflows on one HIP stream with no host round trip; overflowed
-candidates are re-run wider after the loop, inside the timed region.  Steps rotate over
-`--streams` pipelines (engine + stream each, default 3), so one batch's
+rollout (which reads the mask on the device) and the device-built list of
+capacity overflows on one HIP stream with no host round trip; the listed
+candidates are re-run wider on a side stream (the env's escalation).  Steps rotate over
+`--streams` pipelines (engine + stream each, default 4), so one batch's
 rollout tail overlaps the next batches' work; every step is a whole batch.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--candidates 8192]
@@ -31,6 +31,11 @@ sys.path.insert(0, os.path.join(ROOT, "mj-grasp-sim_amd"))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
+
+# one hardware queue per HIP stream: S pipeline streams + S escalation streams
+# (HIP's default of 4 queues would serialise an escalation re-run with the next
+# step of the pipeline sharing its queue); set before the runtime starts
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
@@ -178,9 +183,11 @@ def main():
                     help="N > 1: skip rank 0's single-GPU re-evaluation of every rank's block")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
+    ap.add_argument("--esc-grid", type=int, default=1, help="workgroups of the escalation list re-run")
+    ap.add_argument("--esc-side", type=int, default=1, help="1: escalation re-runs on a side stream per pipeline")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
     args = ap.parse_args()
@@ -242,30 +249,42 @@ def main():
     # rollout tail overlaps the next batch's start (no host synchronisation
     # inside the timed loop).  Every step does the whole filter_to_stable pass.
     from mgs.core.engine import Engine
+    NS = abi.MGS["MGS_NSTATS"]
+    ESC_GRID = args.esc_grid
 
     class Pipe:
         def __init__(self, s):
             self.eng = env.engine if s == 0 else Engine(env.model, device=local, ncon_max=env.ncon_max,
                                                           nefc_max=env.nefc_max)
-            # contact-capacity escalation (GravitylessObjectGrasping.rollout):
-            # candidates whose contacts / rows exceeded the capacity are re-run
-            # with a wider engine.  Each step counts its steps-with-overflow on
-            # the device; after the loop (still inside the timed region) one
-            # launch re-runs every overflowed candidate once per such step, all
-            # replicas concurrently, and the results are merged (escalate_all)
-            self.wide = args.escalate
             self.stream = torch.cuda.current_stream(dev) if s == 0 else torch.cuda.Stream(dev)
             self.free = torch.zeros(N, dtype=torch.uint8, device=dev)
             self.label = torch.zeros(N, dtype=torch.uint8, device=dev)
             self.fail = torch.zeros(N, dtype=torch.int32, device=dev)
             self.objq = torch.zeros((N, 7), **f64)
-            self.stats = torch.zeros((N, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
-            self.w = [torch.zeros_like(t) for t in (self.label, self.fail, self.objq, self.stats)]
-            self.ovf_steps = torch.zeros((), dtype=torch.int64, device=dev)
-            self.nsteps = 0
+            self.stats = torch.zeros((N, NS), dtype=torch.int32, device=dev)
+            # contact-capacity escalation (GravitylessObjectGrasping.rollout: the
+            # candidates whose contacts / rows exceeded the capacity are re-run
+            # with twice the capacity): after each step's rollout the overflowed
+            # candidates are listed on the device (mgs_overflow_list_device) and
+            # re-run from that list on this pipeline's escalation stream
+            # (mgs_rollout_list_device, ESC_GRID workgroups looping over it) into
+            # the step's own escalation outputs, so the next step never waits
+            self.wide = Engine(env.model, device=local, ncon_max=2 * env.ncon_max) if args.escalate else None
+            self.esc_stream = torch.cuda.Stream(dev)
+            self.esc = []          # per step: count, list, label, fail, objq, stats
             self.events = []
+            self.last = -1
 
-        def step(self, timed):
+        def esc_buffers(self, k):
+            while len(self.esc) <= k:
+                self.esc.append((torch.zeros(1, dtype=torch.int32, device=dev),
+                                 torch.zeros(N, dtype=torch.int32, device=dev),
+                                 torch.zeros(N, dtype=torch.uint8, device=dev),
+                                 torch.zeros(N, dtype=torch.int32, device=dev), torch.zeros((N, 7), **f64),
+                                 torch.zeros((N, NS), dtype=torch.int32, device=dev)))
+            return self.esc[k]
+
+        def step(self, k, timed):
             sp = self.stream.cuda_stream
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
             with torch.cuda.stream(self.stream):
@@ -281,62 +300,47 @@ def main():
                 if ev:
                     ev[2].record(self.stream)
                     self.events.append(ev)
-                if self.wide:
-                    self.ovf_steps += ((self.stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"]) != 0).any()
-            self.nsteps += 1
+                if self.wide is not None:
+                    cnt, lst, el, ef, eo, es = self.esc_buffers(k)
+                    self.eng.overflow_list_device(N, self.stats.data_ptr(), cnt.data_ptr(), lst.data_ptr(), stream=sp)
+                    done = torch.cuda.Event()
+                    done.record(self.stream)
+                    es_ = self.esc_stream if args.esc_side else self.stream
+                    es_.wait_event(done)
+                    self.wide.rollout_list_device(sched, N, cnt.data_ptr(), lst.data_ptr(), ESC_GRID, d_q.data_ptr(),
+                                                  d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(), el.data_ptr(),
+                                                  ef.data_ptr(), eo.data_ptr(), es.data_ptr(),
+                                                  stream=es_.cuda_stream)
+            self.last = k
+
+        def merge_last(self):
+            """this pipeline's last step with its escalated candidates merged;
+            returns (escalated count, still capped after escalation)"""
+            if self.wide is None or self.last < 0:
+                return 0, 0
+            cnt, lst, el, ef, eo, es = self.esc[self.last]
+            m = int(cnt.item())
+            if m == 0:
+                return 0, 0
+            idx = lst[:m].long()
+            self.label[idx] = el[idx]
+            self.fail[idx] = ef[idx]
+            self.objq[idx] = eo[idx]
+            self.stats[idx] = es[idx]
+            return m, int(((es[idx, 2] & abi.MGS["MGS_FLAG_CAPACITY"]) != 0).sum().item())
 
     pipes = [Pipe(s) for s in range(max(1, args.streams))]
-    wide_eng = env.engine_for(2 * env.ncon_max) if args.escalate else None    # built before timing
-
-    def escalate_all():
-        """re-run, wider, every overflowed candidate of every step that had one
-        (one launch: replicas run concurrently), merge the results; returns
-        (steps escalated, replicas identical)"""
-        jobs = []
-        for p in pipes:
-            k = int(p.ovf_steps.item()) if args.escalate else 0
-            if k:
-                ov = np.nonzero(p.stats[:, 2].cpu().numpy() & abi.MGS["MGS_FLAG_CAPACITY"])[0]
-                jobs.append((p, ov, k))
-        if not jobs:
-            return 0, True, 0
-        allidx = np.concatenate([np.tile(ov, k) for _, ov, k in jobs])
-        # GravitylessObjectGrasping.rollout's loop: double the capacity up to 40
-        cap = 2 * env.ncon_max
-        sub = env.engine_for(cap).rollout(plan.subset(allidx))
-        pos = np.nonzero(sub["stats"][:, 2] & abi.MGS["MGS_FLAG_CAPACITY"])[0]
-        while len(pos) and cap < 40:
-            cap = min(2 * cap, 40)
-            s2 = env.engine_for(cap).rollout(plan.subset(allidx[pos]))
-            for key in ("label", "fail_step", "obj_qpos", "stats"):
-                sub[key][pos] = s2[key]
-            pos = pos[np.nonzero(s2["stats"][:, 2] & abi.MGS["MGS_FLAG_CAPACITY"])[0]]
-        same, off = True, 0
-        for p, ov, k in jobs:
-            m = len(ov)
-            for key in ("label", "fail_step", "obj_qpos", "stats"):
-                blk = sub[key][off:off + m * k].reshape((k, m) + sub[key].shape[1:])
-                same = same and bool((blk == blk[:1]).all())
-            sel = torch.as_tensor(ov, device=dev)
-            p.label[sel] = torch.as_tensor(sub["label"][off:off + m].astype(np.uint8), device=dev)
-            p.fail[sel] = torch.as_tensor(sub["fail_step"][off:off + m].astype(np.int32), device=dev)
-            p.objq[sel] = torch.as_tensor(sub["obj_qpos"][off:off + m], **f64)
-            p.stats[sel] = torch.as_tensor(sub["stats"][off:off + m].astype(np.int32), device=dev)
-            off += m * k
-        return sum(k for _, _, k in jobs), same, max(len(ov) for _, ov, _ in jobs)
-    for k in range(max(args.warmup, len(pipes))):       # every pipeline warmed up
-        pipes[k % len(pipes)].step(False)
+    for k in range(max(args.warmup, len(pipes))):       # every pipeline (and its escalation) warmed up
+        pipes[k % len(pipes)].step(k // len(pipes), False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for p in pipes:
-        p.ovf_steps.zero_()
     for k in range(args.steps):
-        pipes[k % len(pipes)].step(True)
+        pipes[k % len(pipes)].step(k // len(pipes), True)
     torch.cuda.synchronize(dev)
-    escalated_steps, esc_same, n_ovf = escalate_all()
+    merged = [p.merge_last() for p in pipes]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -352,7 +356,7 @@ def main():
     d_free, d_label, d_fail, d_stats = P0.free, P0.label, P0.fail, P0.stats
     same_pipes = all(torch.equal(p.label, P0.label) and torch.equal(p.free, P0.free) and
                      torch.equal(p.fail, P0.fail) for p in pipes[1:])
-    wide = wide_eng
+    wide = P0.wide
 
     free = d_free.cpu().numpy().astype(bool)
     labels = d_label.cpu().numpy().astype(bool)
@@ -423,12 +427,12 @@ def main():
                    "mean_ncon": float(stats[:, 4].sum() / max(1, steps_exec)),
                    "mean_nefc": float(stats[:, 5].sum() / max(1, steps_exec)),
                    "solver_iters_per_step": float(stats[:, 3].sum() / max(1, steps_exec)),
-                   "overflow_candidates": n_ovf if escalated_steps
+                   "overflow_candidates": merged[0][0] if wide is not None
                    else int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum()),
                    "diverged_candidates": int((stats[:, 2] & abi.MGS["MGS_FLAG_DIVERGED"] != 0).sum()),
-                   "escalated_steps": escalated_steps, "escalation_replicas_identical": esc_same,
-                   "still_capped_after_escalation": int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum())
-                   if wide is not None else None},
+                   "escalation": "per step on the device: overflow list + list re-run (grid %d) on a side stream"
+                   % ESC_GRID if wide is not None else None,
+                   "still_capped_after_escalation": merged[0][1] if wide is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,

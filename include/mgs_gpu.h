@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 9
+#define MGS_ABI_VERSION 10
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -321,6 +321,23 @@ int mgs_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n,
                        const double* d_phase_start, const double* d_phase_target,
                        const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step,
                        double* d_obj_qpos, int32_t* d_stats, void* stream);
+
+/* Capacity escalation on the device (GravitylessObjectGrasping.rollout's
+ * re-run of the candidates that overflowed the contact / constraint-row
+ * capacity, with no host round trip): mgs_overflow_list_device zeroes *d_count
+ * and writes the indices i < n with stats[i * MGS_NSTATS + 2] & flag_mask into
+ * d_list (n ints; arrival order), asynchronously on `stream`;
+ * mgs_rollout_list_device re-runs exactly those candidates (as
+ * mgs_rollout_device would, outputs written at their indices, other entries
+ * untouched) with `grid` workgroups that loop over the list, so an empty or
+ * short list costs a handful of workgroups instead of one per batch entry.
+ * grid <= the batch capacity. */
+int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32_t* d_count, int32_t* d_list,
+                             void* stream);
+int mgs_rollout_list_device(mgs_batch* batch, const mgs_schedule* sched, int n, const int32_t* d_count,
+                            const int32_t* d_list, int grid, const double* d_qpos_init, const double* d_mocap_quat,
+                            const double* d_phase_start, const double* d_phase_target, uint8_t* d_label,
+                            int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, void* stream);
 
 /* Antipodal candidate ray casting (AntipodalGraspGenerator.generate_grasps,
  * mgs/sampler/antipodal.py:96-172, trimesh intersects_location): for each of

@@ -347,7 +347,8 @@ int mgs_collision_free(mgs_batch* b, int n, const double* qpos_init, const doubl
 static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
                           const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
                           const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
-                          int32_t* d_stats, const double* d_vstate, double* d_state_out, void* stream) {
+                          int32_t* d_stats, const double* d_vstate, double* d_state_out, void* stream,
+                          const int32_t* d_list = nullptr, const int32_t* d_count = nullptr, int grid = 0) {
   if (!b || !sched || n < 0) return fail(MGS_EINVAL, "mgs_rollout_device: bad argument%s");
   if (sched->nphase < 1 || sched->nphase > MGS_MAX_PHASES) return fail(MGS_EINVAL, "bad phase count%s");
   if (n == 0) return MGS_OK;
@@ -355,12 +356,13 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
   Lay lay;
-  int lrc = launch_layout(b, n, &lay);
+  const int nwg = d_list ? grid : n;
+  int lrc = launch_layout(b, nwg, &lay);
   if (lrc) return lrc;
   HIPCHK(hipEventRecord(b->e0, st));
-#define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
+#define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(nwg), dim3(64), b->m->lds_bytes, st, md, \
       md.I, md.D, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
-      d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out)
+      d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count)
   switch (md.m.nv) {
 #define MGS_CASE(NV_) case NV_: MGS_LAUNCH_ROLL(NV_); break;
     MGS_NV_LIST(MGS_CASE)
@@ -378,6 +380,28 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
                        int32_t* d_stats, void* stream) {
   return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
                         d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream);
+}
+
+int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32_t* d_count, int32_t* d_list,
+                             void* stream) {
+  if (n < 0 || !d_stats || !d_count || !d_list) return fail(MGS_EINVAL, "mgs_overflow_list_device: bad argument%s");
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(d_count, 0, sizeof(int32_t), st));
+  if (n == 0) return MGS_OK;
+  hipLaunchKernelGGL(mgs_overflow_list_kernel, dim3((n + 255) / 256), dim3(256), 0, st, d_stats, n, flag_mask, d_count,
+                     d_list);
+  HIPCHK(hipGetLastError());
+  return MGS_OK;
+}
+
+int mgs_rollout_list_device(mgs_batch* b, const mgs_schedule* sched, int n, const int32_t* d_count,
+                            const int32_t* d_list, int grid, const double* d_qpos_init, const double* d_mocap_quat,
+                            const double* d_phase_start, const double* d_phase_target, uint8_t* d_label,
+                            int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, void* stream) {
+  if (!b || !d_count || !d_list || grid < 1 || grid > b->cap)
+    return fail(MGS_EINVAL, "mgs_rollout_list_device: bad argument (1 <= grid <= batch capacity)%s");
+  return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, nullptr, d_label,
+                        d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, d_list, d_count, grid);
 }
 
 int mgs_simulate_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,

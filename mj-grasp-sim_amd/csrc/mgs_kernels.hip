@@ -3375,21 +3375,14 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   }
 }
 
+// one candidate's rollout (the body of mgs_rollout_kernel)
 template <int NV>
-__global__ void __launch_bounds__(64)
-mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
-                   mgs_schedule sc, int n, const double* __restrict__ qpos_init,
-                   const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
-                   const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
-                   uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
-                   int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
-                   double* __restrict__ state_out) {
-  extern __shared__ double smem[];
-  Mdl md = mdarg;
-  md.I = mI;
-  md.D = mD;
-  int i = blockIdx.x;
-  if (i >= n) return;
+DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_schedule& sc, int i,
+                      const double* __restrict__ qpos_init, const double* __restrict__ mocap_quat,
+                      const double* __restrict__ phase_start, const double* __restrict__ phase_target,
+                      const uint8_t* __restrict__ active, uint8_t* __restrict__ label,
+                      int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
+                      const double* __restrict__ vstate_init, double* __restrict__ state_out) {
   int lane = lane_id();
   if (active && !active[i]) {
     // collision-mask reject: not simulated (filter_to_stable.py:39-44)
@@ -3502,6 +3495,43 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
     for (int k = lane; k < nv; k += WAVE) { so[nq + k] = d.qvel[k]; so[nq + nv + k] = d.qacc_ws[k]; }
   }
   PROF_FLUSH
+}
+
+// One workgroup (one wave) per candidate: candidate blockIdx.x, or -- list mode
+// (list != nullptr) -- candidates list[s] for s = blockIdx.x, blockIdx.x +
+// gridDim.x, ... < *list_count: a small grid re-runs a device-built subset
+// (capacity escalation) without launching a workgroup per batch entry.
+template <int NV>
+__global__ void __launch_bounds__(64)
+mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
+                   mgs_schedule sc, int n, const double* __restrict__ qpos_init,
+                   const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
+                   const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
+                   uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
+                   int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
+                   double* __restrict__ state_out, const int32_t* __restrict__ list,
+                   const int32_t* __restrict__ list_count) {
+  extern __shared__ double smem[];
+  Mdl md = mdarg;
+  md.I = mI;
+  md.D = mD;
+  const int end = list ? *list_count : (blockIdx.x < (unsigned)n ? (int)blockIdx.x + 1 : 0);
+  const int stride = list ? (int)gridDim.x : 1;
+  for (int s = blockIdx.x; s < end; s += stride) {
+    int i = list ? list[s] : s;
+    if (i < 0 || i >= n) continue;
+    rollout_one<NV>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target, active, label,
+                    fail_step, obj_qpos, stats, vstate_init, state_out);
+  }
+}
+
+// capacity-escalation list: indices of the candidates whose stats flags meet
+// mask (order of arrival; each re-run is independent of the order)
+__global__ void __launch_bounds__(256)
+mgs_overflow_list_kernel(const int32_t* __restrict__ stats, int n, int mask, int32_t* __restrict__ count,
+                         int32_t* __restrict__ list) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && (stats[MGS_NSTATS * i + 2] & mask)) list[atomicAdd(count, 1)] = i;
 }
 
 // device-side arithmetic probe (tests): sqrt, division, sincos against the oracle

@@ -52,6 +52,9 @@ def load_library(wide: bool = False):
     L.mgs_rollout.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d),
                               P(abi.RolloutOut)]
     L.mgs_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mgs_overflow_list_device.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp, vp]
+    L.mgs_rollout_list_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, ctypes.c_int, vp, vp, vp, vp,
+                                          vp, vp, vp, vp, vp]
     L.mgs_last_kernel_ms.argtypes = [vp]
     L.mgs_last_kernel_ms.restype = ctypes.c_double
     L.mgs_last_collision_ms.argtypes = [vp]
@@ -270,6 +273,19 @@ class Engine:
         self._ck(self.lib.mgs_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps, d_pt,
                                            d_active, d_label, d_fail, d_objq, d_stats, stream),
                "mgs_rollout_device")
+
+    def overflow_list_device(self, n, d_stats, d_count, d_list, stream=None, mask=None):
+        """device list of the candidates whose stats flag a capacity overflow"""
+        m = abi.MGS["MGS_FLAG_CAPACITY"] if mask is None else int(mask)
+        self._ck(self.lib.mgs_overflow_list_device(n, d_stats, m, d_count, d_list, stream), "mgs_overflow_list_device")
+
+    def rollout_list_device(self, sched, n, d_count, d_list, grid, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail,
+                            d_objq, d_stats, stream=None):
+        """re-run the candidates of a device list with `grid` workgroups looping
+        over it (outputs at their batch indices)"""
+        self._ck(self.lib.mgs_rollout_list_device(self.batch(grid), ctypes.byref(sched), n, d_count, d_list, grid,
+                                                d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats,
+                                                stream), "mgs_rollout_list_device")
 
     def last_collision_ms(self):
         return self.lib.mgs_last_collision_ms(self._batch)

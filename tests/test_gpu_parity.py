@@ -183,6 +183,56 @@ def test_device_entry_with_active_mask(env, eng, candidates, oracle_model):
     assert np.array_equal(objq.cpu().numpy()[rej], q[rej][:, plan.obj_qposadr:plan.obj_qposadr + 7])
 
 
+def test_device_overflow_list_and_list_rollout(env, eng, candidates):
+    """mgs_overflow_list_device picks the flagged candidates; mgs_rollout_list_device
+    with a grid smaller than the list (workgroups loop over it) reproduces
+    mgs_rollout_device's outputs at the listed indices and touches nothing else."""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    plan = plan_for(env, poses, J)
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                              check_offset=getattr(plan, "check_offset", None))
+    n = len(q)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+    dq, dmq, dps, dpt = t(q), t(mq), t(plan.phase_start), t(plan.phase_target)
+
+    def outs(fill):
+        return (torch.full((n,), fill, dtype=torch.uint8, device=dev), torch.full((n,), -7, dtype=torch.int32, device=dev),
+                torch.full((n, 7), 9.0, dtype=torch.float64, device=dev),
+                torch.full((n, abi.MGS["MGS_NSTATS"]), -1, dtype=torch.int32, device=dev))
+    full = outs(0)
+    eng.rollout_device(sched, n, dq.data_ptr(), dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
+                       *[x.data_ptr() for x in full])
+    # synthetic flags: every 7th candidate overflowed
+    flags = torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
+    pick = np.arange(3, n, 7)
+    flags[torch.as_tensor(pick, device=dev), 2] = abi.MGS["MGS_FLAG_CONTACTS"]
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    lst = torch.zeros(n, dtype=torch.int32, device=dev)
+    eng.overflow_list_device(n, flags.data_ptr(), cnt.data_ptr(), lst.data_ptr())
+    sub = outs(5)
+    eng.rollout_list_device(sched, n, cnt.data_ptr(), lst.data_ptr(), 3, dq.data_ptr(), dmq.data_ptr(),
+                            dps.data_ptr(), dpt.data_ptr(), *[x.data_ptr() for x in sub])
+    torch.cuda.synchronize()
+    k = int(cnt.item())
+    assert k == len(pick) and sorted(lst.cpu().numpy()[:k]) == list(pick)
+    for a, b in zip(full, sub):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.array_equal(a[pick], b[pick])
+    rest = np.setdiff1d(np.arange(n), pick)
+    assert np.all(sub[0].cpu().numpy()[rest] == 5) and np.all(sub[1].cpu().numpy()[rest] == -7)
+    # an empty list launches and changes nothing
+    cnt.zero_()
+    eng.rollout_list_device(sched, n, cnt.data_ptr(), lst.data_ptr(), 3, dq.data_ptr(), dmq.data_ptr(),
+                            dps.data_ptr(), dpt.data_ptr(), *[x.data_ptr() for x in sub])
+    torch.cuda.synchronize()
+    assert np.all(sub[0].cpu().numpy()[rest] == 5)
+
+
 def test_full_size_properties(env, eng, oracle_model):
     """8192 candidates (the benchmark size): determinism, permutation
     invariance and sub-batch consistency, tied to the oracle on a slice."""
