@@ -10,7 +10,7 @@ resident in HBM when the timed region starts; each step runs the mask, the
 rollout (which reads the mask on the device) and the device-built list of
 capacity overflows on one HIP stream with no host round trip; the listed
 candidates are re-run wider on a side stream (the env's escalation).  Steps rotate over
-`--streams` pipelines (engine + stream each, default 4), so one batch's
+`--streams` pipelines (engine + stream each, default 3), so one batch's
 rollout tail overlaps the next batches' work; every step is a whole batch.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--candidates 8192]
@@ -33,9 +33,9 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 # one hardware queue per HIP stream: S pipeline streams + S escalation streams
-# (HIP's default of 4 queues would serialise an escalation re-run with the next
+# (the default of 4 queues would serialise an escalation re-run with the next
 # step of the pipeline sharing its queue); set before the runtime starts
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
@@ -183,7 +183,7 @@ def main():
                     help="N > 1: skip rank 0's single-GPU re-evaluation of every rank's block")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
     ap.add_argument("--esc-grid", type=int, default=1, help="workgroups of the escalation list re-run")

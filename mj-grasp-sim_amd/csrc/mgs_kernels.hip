@@ -289,30 +289,54 @@ DEVI int next_pow2(int n) {
 // body b; bodies of one tree depth are independent given their parents, so the
 // levels run in order and the bodies of a level in parallel.  Per-body
 // arithmetic is the oracle's.
-DEVI void body_kin(const Mdl& md, Dat& d, int b) {
-  const int32_t *parent = IA(md, body_parentid), *mocapid = IA(md, body_mocapid);
-  const int32_t *jntnum = IA(md, body_jntnum), *jntadr = IA(md, body_jntadr);
+// a body's static model data (and its first joint's), loaded into registers
+// once per kinematics pass before the level loop: the global loads of every
+// level are then in flight together instead of one dependent round trip per
+// tree level
+struct BodyStatic {
+  int parent, mocap, jn, j0, jt, qa;
+  double bpos[3], bquat[4], ipos[3], jpos[3], jaxis[3], q0;
+};
+DEVI void body_static(const Mdl& md, int b, BodyStatic& s) {
+  s.parent = IA(md, body_parentid)[b];
+  s.mocap = IA(md, body_mocapid)[b];
+  s.jn = IA(md, body_jntnum)[b];
+  s.j0 = IA(md, body_jntadr)[b];
+  int j = s.jn > 0 ? s.j0 : 0;
+  s.jt = IA(md, jnt_type)[j];
+  s.qa = IA(md, jnt_qposadr)[j];
+  const double *bpos = DA(md, body_pos) + 3 * b, *bquat = DA(md, body_quat) + 4 * b, *ipos = DA(md, body_ipos) + 3 * b;
+  const double *jpos = DA(md, jnt_pos) + 3 * j, *jaxis = DA(md, jnt_axis) + 3 * j;
+  for (int k = 0; k < 3; k++) { s.bpos[k] = bpos[k]; s.ipos[k] = ipos[k]; s.jpos[k] = jpos[k]; s.jaxis[k] = jaxis[k]; }
+  for (int k = 0; k < 4; k++) s.bquat[k] = bquat[k];
+  s.q0 = DA(md, qpos0)[s.qa];
+}
+
+DEVI void body_kin(const Mdl& md, Dat& d, int b, const BodyStatic& bs) {
   const int32_t *jtype = IA(md, jnt_type), *qadr = IA(md, jnt_qposadr);
-  const double *bpos = DA(md, body_pos), *bquat = DA(md, body_quat);
-  const double *ipos = DA(md, body_ipos);
-  const double *jpos = DA(md, jnt_pos), *jaxis = DA(md, jnt_axis), *qpos0 = DA(md, qpos0);
+  const double *jposA = DA(md, jnt_pos), *jaxisA = DA(md, jnt_axis), *qpos0 = DA(md, qpos0);
   double pos[3], quat[4], mat[9];
-  if (mocapid[b] >= 0) {
-    const double* mp = d.mocap_pos + 3 * mocapid[b];
-    const double* mq = d.mocap_quat + 4 * mocapid[b];
+  if (bs.mocap >= 0) {
+    const double* mp = d.mocap_pos + 3 * bs.mocap;
+    const double* mq = d.mocap_quat + 4 * bs.mocap;
     pos[0] = mp[0]; pos[1] = mp[1]; pos[2] = mp[2];
     quat[0] = mq[0]; quat[1] = mq[1]; quat[2] = mq[2]; quat[3] = mq[3];
     normalize4(quat);
   } else {
-    int p = parent[b];
+    int p = bs.parent;
     double t[3];
-    mulmv3(t, d.xmat + 9 * p, bpos + 3 * b);
+    mulmv3(t, d.xmat + 9 * p, bs.bpos);
     add3(pos, d.xpos + 3 * p, t);
-    quatmul(quat, d.xquat + 4 * p, bquat + 4 * b);
-    for (int k = 0; k < jntnum[b]; k++) {
-      int j = jntadr[b] + k;
-      int a = qadr[j];
-      if (jtype[j] == MGS_JNT_FREE) {
+    quatmul(quat, d.xquat + 4 * p, bs.bquat);
+    for (int k = 0; k < bs.jn; k++) {
+      int j = bs.j0 + k;
+      // the first joint's data are preloaded; further joints of the body load here
+      int jt = k == 0 ? bs.jt : jtype[j];
+      int a = k == 0 ? bs.qa : qadr[j];
+      const double* jpos = k == 0 ? bs.jpos : jposA + 3 * j;
+      const double* jaxis = k == 0 ? bs.jaxis : jaxisA + 3 * j;
+      double q0 = k == 0 ? bs.q0 : qpos0[a];
+      if (jt == MGS_JNT_FREE) {
         pos[0] = d.qpos[a]; pos[1] = d.qpos[a + 1]; pos[2] = d.qpos[a + 2];
         quat[0] = d.qpos[a + 3]; quat[1] = d.qpos[a + 4]; quat[2] = d.qpos[a + 5]; quat[3] = d.qpos[a + 6];
         normalize4(quat);
@@ -321,21 +345,21 @@ DEVI void body_kin(const Mdl& md, Dat& d, int b) {
       } else {
         double anc[3], axw[3];
         quat2mat(mat, quat);
-        mulmv3(axw, mat, jaxis + 3 * j);
-        mulmv3(t, mat, jpos + 3 * j);
+        mulmv3(axw, mat, jaxis);
+        mulmv3(t, mat, jpos);
         add3(anc, t, pos);
         d.xaxis[3 * j] = axw[0]; d.xaxis[3 * j + 1] = axw[1]; d.xaxis[3 * j + 2] = axw[2];
         d.xanchor[3 * j] = anc[0]; d.xanchor[3 * j + 1] = anc[1]; d.xanchor[3 * j + 2] = anc[2];
-        if (jtype[j] == MGS_JNT_HINGE) {
+        if (jt == MGS_JNT_HINGE) {
           double ql[4], qn[4];
-          axisangle2quat(ql, jaxis + 3 * j, d.qpos[a] - qpos0[a]);
+          axisangle2quat(ql, jaxis, d.qpos[a] - q0);
           quatmul(qn, quat, ql);
           quat[0] = qn[0]; quat[1] = qn[1]; quat[2] = qn[2]; quat[3] = qn[3];
           quat2mat(mat, quat);
-          mulmv3(t, mat, jpos + 3 * j);
+          mulmv3(t, mat, jpos);
           sub3(pos, anc, t);
         } else {
-          double dq = d.qpos[a] - qpos0[a];
+          double dq = d.qpos[a] - q0;
           pos[0] = pos[0] + axw[0] * dq;
           pos[1] = pos[1] + axw[1] * dq;
           pos[2] = pos[2] + axw[2] * dq;
@@ -349,7 +373,7 @@ DEVI void body_kin(const Mdl& md, Dat& d, int b) {
   quat2mat(mat, quat);
   for (int k = 0; k < 9; k++) d.xmat[9 * b + k] = mat[k];
   double t[3];
-  mulmv3(t, mat, ipos + 3 * b);
+  mulmv3(t, mat, bs.ipos);
   add3(d.xipos + 3 * b, pos, t);
 }
 
@@ -366,8 +390,10 @@ DEVI void kinematics(const Mdl& md, Dat& d) {
   wsync();
   int maxd = max_depth(md);
   int myd = (lane < nb) ? depth[lane] : -1;
+  BodyStatic bs;
+  body_static(md, (lane < nb && lane > 0) ? lane : (nb > 1 ? 1 : 0), bs);
   for (int L = 1; L <= maxd; L++) {
-    if (myd == L) body_kin(md, d, lane);
+    if (myd == L) body_kin(md, d, lane, bs);
     wsync();
   }
   const int32_t* gbody = IA(md, geom_bodyid);
@@ -386,21 +412,36 @@ DEVI void kinematics(const Mdl& md, Dat& d) {
 // arr[p] += arr[c] over the tree from the leaves up, children of each parent in
 // decreasing body index (the oracle's `for b = nb-1..1: arr[parent] += arr[b]`
 // order per parent); W doubles per body; world included iff with_world.
+// The child list (first ACC_KIDS entries) is loaded into registers before the
+// level loop, so the levels do not each wait on a dependent global load.
+#define ACC_KIDS 4
 template <int W>
 DEVI void accumulate_up(const Mdl& md, double* arr, int with_world) {
   int lane = lane_id(), nb = md.m.nbody;
   const int32_t* depth = IA(md, body_depth);
   int maxd = max_depth(md);
+  int lb = lane < nb ? lane : 0;
   int myd = (lane < nb) ? depth[lane] : -1;
+  const int32_t* kids = IA(md, body_child) + IA(md, body_childadr)[lb];
+  int nk = IA(md, body_childnum)[lb];
+  int kr[ACC_KIDS];
+#pragma unroll
+  for (int q = 0; q < ACC_KIDS; q++) kr[q] = kids[q < nk ? q : 0];
   for (int L = maxd; L >= 1; L--) {
     if (myd == L - 1 && (with_world || lane > 0)) {
       double acc[W];
 #pragma unroll
       for (int k = 0; k < W; k++) acc[k] = arr[W * lane + k];
-      const int32_t* kids = IA(md, body_child) + IA(md, body_childadr)[lane];
-      int nk = IA(md, body_childnum)[lane];
       for (int q = 0; q < nk; q++) {   // children in decreasing body index
-        int c = kids[q];
+        int c;
+        if (q < ACC_KIDS) {
+          c = kr[0];
+#pragma unroll
+          for (int r = 1; r < ACC_KIDS; r++)
+            if (q == r) c = kr[r];
+        } else {
+          c = kids[q];
+        }
 #pragma unroll
         for (int k = 0; k < W; k++) acc[k] = acc[k] + arr[W * c + k];
       }
@@ -513,16 +554,37 @@ DEVI void crb(const Mdl& md, Dat& d) {
   accumulate_up<10>(md, d.crb, 0);
   for (int k = lane; k < nv * nv; k += WAVE) d.M[k] = 0.0;
   wsync();
-  for (int i = lane; i < nv; i += WAVE) {
+  if (nv <= WAVE) {
+    // lane i walks dof i's ancestors; the walk reads a lane-resident copy of
+    // dof_parentid through cross-lane permutes (in wave-uniform control flow,
+    // every lane participating) instead of one dependent global load per step
+    int dp_lane = lane < nv ? dpar[lane] : -1;
+    int i = lane < nv ? lane : 0;
     double buf[6];
     mul_inert_vec(buf, d.crb + 10 * dbody[i], d.cdof + 6 * i);
-    d.M[i * nv + i] = dot6(d.cdof + 6 * i, buf) + arm[i];
-    int j = dpar[i];
-    while (j >= 0) {
-      double v = dot6(d.cdof + 6 * j, buf);
-      d.M[i * nv + j] = v;
-      d.M[j * nv + i] = v;
-      j = dpar[j];
+    if (lane < nv) d.M[i * nv + i] = dot6(d.cdof + 6 * i, buf) + arm[i];
+    int j = dp_lane;
+    while (__ballot(j >= 0)) {
+      if (j >= 0) {
+        double v = dot6(d.cdof + 6 * j, buf);
+        d.M[i * nv + j] = v;
+        d.M[j * nv + i] = v;
+      }
+      int jn = __shfl(dp_lane, j >= 0 ? j : 0);
+      j = j >= 0 ? jn : -1;
+    }
+  } else {
+    for (int i = lane; i < nv; i += WAVE) {
+      double buf[6];
+      mul_inert_vec(buf, d.crb + 10 * dbody[i], d.cdof + 6 * i);
+      d.M[i * nv + i] = dot6(d.cdof + 6 * i, buf) + arm[i];
+      int j = dpar[i];
+      while (j >= 0) {
+        double v = dot6(d.cdof + 6 * j, buf);
+        d.M[i * nv + j] = v;
+        d.M[j * nv + i] = v;
+        j = dpar[j];
+      }
     }
   }
   wsync();
@@ -719,18 +781,17 @@ DEVI void passive(const Mdl& md, Dat& d) {
 // recursive Newton-Euler bias forces (oracle rne()): forward velocity /
 // acceleration pass by tree level (lane per body), cfrc accumulated up the tree
 // in the oracle's child order, then one dof per lane.
-DEVI void rne_body(const Mdl& md, Dat& d, int b) {
-  const int32_t *parent = IA(md, body_parentid), *dnum = IA(md, body_dofnum), *dadr = IA(md, body_dofadr);
-  int p = parent[b];
+// p, nd, da: the body's parent, dof count and first dof (preloaded by rne)
+DEVI void rne_body(Dat& d, int b, int p, int nd, int da) {
   double cv[6], ca[6];
   for (int k = 0; k < 6; k++) { cv[k] = d.cvel[6 * p + k]; ca[k] = d.cacc[6 * p + k]; }
-  for (int i = 0; i < dnum[b]; i++) {
-    int dd = dadr[b] + i;
+  for (int i = 0; i < nd; i++) {
+    int dd = da + i;
     cross_motion(d.cdof_dot + 6 * dd, cv, d.cdof + 6 * dd);
     for (int k = 0; k < 6; k++) cv[k] = cv[k] + d.cdof[6 * dd + k] * d.qvel[dd];
   }
-  for (int i = 0; i < dnum[b]; i++) {
-    int dd = dadr[b] + i;
+  for (int i = 0; i < nd; i++) {
+    int dd = da + i;
     for (int k = 0; k < 6; k++) ca[k] = ca[k] + d.cdof_dot[6 * dd + k] * d.qvel[dd];
   }
   for (int k = 0; k < 6; k++) { d.cvel[6 * b + k] = cv[k]; d.cacc[6 * b + k] = ca[k]; }
@@ -750,9 +811,11 @@ DEVI void rne(const Mdl& md, Dat& d) {
   }
   wsync();
   int maxd = max_depth(md);
+  int lb = lane < nb ? lane : 0;
   int myd = (lane < nb) ? depth[lane] : -1;
+  int bp = IA(md, body_parentid)[lb], bnd = IA(md, body_dofnum)[lb], bda = IA(md, body_dofadr)[lb];
   for (int L = 1; L <= maxd; L++) {
-    if (myd == L) rne_body(md, d, lane);
+    if (myd == L) rne_body(d, lane, bp, bnd, bda);
     wsync();
   }
   accumulate_up<6>(md, d.cfrc, 0);
