@@ -171,7 +171,7 @@ def e2e_api(env, poses, J, h, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--candidates", type=int, default=8192)
     ap.add_argument("--horizon", default="h200")
@@ -188,6 +188,9 @@ def main():
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
     ap.add_argument("--esc-grid", type=int, default=1, help="workgroups of the escalation list re-run")
     ap.add_argument("--esc-side", type=int, default=1, help="1: escalation re-runs on a side stream per pipeline")
+    ap.add_argument("--esc-resume", type=int, default=1,
+                    help="1: overflowing candidates stop at the overflowing step and the escalation continues "
+                         "them from there (0: re-run from the start)")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
     args = ap.parse_args()
@@ -251,6 +254,8 @@ def main():
     from mgs.core.engine import Engine
     NS = abi.MGS["MGS_NSTATS"]
     ESC_GRID = args.esc_grid
+    RESUME = bool(args.escalate and args.esc_resume)
+    RW = env.engine.resume_width()
 
     class Pipe:
         def __init__(self, s):
@@ -268,10 +273,13 @@ def main():
             # candidates are listed on the device (mgs_overflow_list_device) and
             # re-run from that list on this pipeline's escalation stream
             # (mgs_rollout_list_device, ESC_GRID workgroups looping over it) into
-            # the step's own escalation outputs, so the next step never waits
+            # the step's own escalation outputs, so the next step never waits;
+            # with --esc-resume the capped rollout stops an overflowing candidate
+            # at that step and leaves its state in the step's resume records
+            # (mgs_rollout_resumable_device), which the list re-run continues
             self.wide = Engine(env.model, device=local, ncon_max=2 * env.ncon_max) if args.escalate else None
             self.esc_stream = torch.cuda.Stream(dev)
-            self.esc = []          # per step: count, list, label, fail, objq, stats
+            self.esc = []          # per step: count, list, label, fail, objq, stats, resume records
             self.events = []
             self.last = -1
 
@@ -281,7 +289,8 @@ def main():
                                  torch.zeros(N, dtype=torch.int32, device=dev),
                                  torch.zeros(N, dtype=torch.uint8, device=dev),
                                  torch.zeros(N, dtype=torch.int32, device=dev), torch.zeros((N, 7), **f64),
-                                 torch.zeros((N, NS), dtype=torch.int32, device=dev)))
+                                 torch.zeros((N, NS), dtype=torch.int32, device=dev),
+                                 torch.zeros((N, RW) if RESUME else 1, **f64)))
             return self.esc[k]
 
         def step(self, k, timed):
@@ -294,14 +303,22 @@ def main():
                                                self.free.data_ptr(), predicate="any", stream=sp)
                 if ev:
                     ev[1].record(self.stream)
-                self.eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(),
-                                        self.label.data_ptr(), self.fail.data_ptr(), self.objq.data_ptr(),
-                                        self.stats.data_ptr(), d_active=self.free.data_ptr(), stream=sp)
+                if RESUME:
+                    rec = self.esc_buffers(k)[6]
+                    self.eng.rollout_resumable_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(),
+                                                      d_pt.data_ptr(), self.label.data_ptr(), self.fail.data_ptr(),
+                                                      self.objq.data_ptr(), self.stats.data_ptr(), rec.data_ptr(),
+                                                      d_active=self.free.data_ptr(), stream=sp)
+                else:
+                    self.eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(),
+                                            d_pt.data_ptr(), self.label.data_ptr(), self.fail.data_ptr(),
+                                            self.objq.data_ptr(), self.stats.data_ptr(),
+                                            d_active=self.free.data_ptr(), stream=sp)
                 if ev:
                     ev[2].record(self.stream)
                     self.events.append(ev)
                 if self.wide is not None:
-                    cnt, lst, el, ef, eo, es = self.esc_buffers(k)
+                    cnt, lst, el, ef, eo, es, rec = self.esc_buffers(k)
                     self.eng.overflow_list_device(N, self.stats.data_ptr(), cnt.data_ptr(), lst.data_ptr(), stream=sp)
                     done = torch.cuda.Event()
                     done.record(self.stream)
@@ -310,7 +327,8 @@ def main():
                     self.wide.rollout_list_device(sched, N, cnt.data_ptr(), lst.data_ptr(), ESC_GRID, d_q.data_ptr(),
                                                   d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(), el.data_ptr(),
                                                   ef.data_ptr(), eo.data_ptr(), es.data_ptr(),
-                                                  stream=es_.cuda_stream)
+                                                  stream=es_.cuda_stream,
+                                                  d_resume_in=rec.data_ptr() if RESUME else None)
             self.last = k
 
         def merge_last(self):
@@ -318,7 +336,7 @@ def main():
             returns (escalated count, still capped after escalation)"""
             if self.wide is None or self.last < 0:
                 return 0, 0
-            cnt, lst, el, ef, eo, es = self.esc[self.last]
+            cnt, lst, el, ef, eo, es, _ = self.esc[self.last]
             m = int(cnt.item())
             if m == 0:
                 return 0, 0
@@ -430,8 +448,9 @@ def main():
                    "overflow_candidates": merged[0][0] if wide is not None
                    else int((stats[:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum()),
                    "diverged_candidates": int((stats[:, 2] & abi.MGS["MGS_FLAG_DIVERGED"] != 0).sum()),
-                   "escalation": "per step on the device: overflow list + list re-run (grid %d) on a side stream"
-                   % ESC_GRID if wide is not None else None,
+                   "escalation": "per step on the device: overflow list + list re-run (grid %d) on a side stream, %s"
+                   % (ESC_GRID, "resumed from the overflowing step" if RESUME else "from the start")
+                   if wide is not None else None,
                    "still_capped_after_escalation": merged[0][1] if wide is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,

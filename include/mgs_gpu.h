@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 10
+#define MGS_ABI_VERSION 11
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -261,7 +261,14 @@ typedef struct mgs_rollout_out {
   double* obj_qpos;        /* n * 7: object free-joint qpos when the candidate stopped (may be NULL) */
   int32_t* stats;          /* n * MGS_NSTATS: max ncon, max nefc, overflow flags, total solver
                               iterations, sum of ncon and sum of nefc over executed steps (may be NULL) */
+  double* resume;          /* n * (nq + 2 nv + MGS_RESUME_EXTRA), may be NULL.  When set, a candidate
+                              that exceeds the contact / row capacity stops at that step (fail_step
+                              -3) and its record holds the state entering it (qpos, qvel,
+                              qacc_warmstart, time) and the schedule position / partial stats, from
+                              which mgs_rollout_resume continues it with more capacity */
 } mgs_rollout_out;
+#define MGS_RESUME_EXTRA 9         /* time, phase, step in phase, global step, max ncon, max nefc,
+                                      sum ncon, sum nefc, solver iterations */
 
 typedef struct mgs_model mgs_model;
 typedef struct mgs_batch mgs_batch;
@@ -310,6 +317,13 @@ int mgs_rollout(mgs_batch* batch, const mgs_schedule* sched, int n,
                 const double* phase_start, const double* phase_target,
                 mgs_rollout_out* out);
 
+/* mgs_rollout continuing each candidate from its resume record (n records as
+ * returned in mgs_rollout_out.resume by a capped run of the same candidates,
+ * same schedule): GravitylessObjectGrasping.rollout's capacity escalation. */
+int mgs_rollout_resume(mgs_batch* batch, const mgs_schedule* sched, int n, const double* qpos_init,
+                       const double* mocap_quat, const double* phase_start, const double* phase_target,
+                       const double* resume, mgs_rollout_out* out);
+
 /* Same as mgs_rollout but with inputs already resident on the device (device
  * pointers, same layouts); outputs stay on the device.  Used to time the
  * kernel with inputs in HBM.  stream may be NULL (default stream).
@@ -336,8 +350,20 @@ int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32
                              void* stream);
 int mgs_rollout_list_device(mgs_batch* batch, const mgs_schedule* sched, int n, const int32_t* d_count,
                             const int32_t* d_list, int grid, const double* d_qpos_init, const double* d_mocap_quat,
-                            const double* d_phase_start, const double* d_phase_target, uint8_t* d_label,
-                            int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, void* stream);
+                            const double* d_phase_start, const double* d_phase_target, const double* d_resume_in,
+                            uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats,
+                            void* stream);
+/* mgs_rollout_device that stops each overflowing candidate at the overflowing
+ * step and writes its resume record to d_resume_out (n records, see
+ * mgs_rollout_out.resume); mgs_rollout_list_device with d_resume_in != NULL
+ * continues the listed candidates from those records (the capped run and the
+ * wider one are identical up to that step), so the escalation costs only the
+ * remaining steps. */
+int mgs_rollout_resumable_device(mgs_batch* batch, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                                 const double* d_mocap_quat, const double* d_phase_start,
+                                 const double* d_phase_target, const uint8_t* d_active, uint8_t* d_label,
+                                 int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
+                                 void* stream);
 
 /* Antipodal candidate ray casting (AntipodalGraspGenerator.generate_grasps,
  * mgs/sampler/antipodal.py:96-172, trimesh intersects_location): for each of

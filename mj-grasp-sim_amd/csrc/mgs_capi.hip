@@ -174,6 +174,7 @@ struct mgs_batch {
   int32_t *d_fail, *d_stats;
   double* d_G;      // MGS_G_GLOBAL: per-candidate constraint rows (HBM)
   size_t g_elems;
+  double* d_resume; // resume records (n * (nq + 2 nv + MGS_RESUME_EXTRA)), allocated on first use
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
@@ -267,6 +268,7 @@ void mgs_batch_close(mgs_batch* b) {
   hipFree(b->d_qpos); hipFree(b->d_mpos); hipFree(b->d_mquat); hipFree(b->d_ps); hipFree(b->d_pt);
   hipFree(b->d_objq); hipFree(b->d_label); hipFree(b->d_free); hipFree(b->d_fail); hipFree(b->d_stats);
   if (b->d_G) hipFree(b->d_G);
+  if (b->d_resume) hipFree(b->d_resume);
   if (b->e0) hipEventDestroy(b->e0);
   if (b->e1) hipEventDestroy(b->e1);
   if (b->e2) hipEventDestroy(b->e2);
@@ -348,7 +350,8 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
                           const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
                           const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
                           int32_t* d_stats, const double* d_vstate, double* d_state_out, void* stream,
-                          const int32_t* d_list = nullptr, const int32_t* d_count = nullptr, int grid = 0) {
+                          const int32_t* d_list = nullptr, const int32_t* d_count = nullptr, int grid = 0,
+                          double* d_resume_out = nullptr, const double* d_resume_in = nullptr) {
   if (!b || !sched || n < 0) return fail(MGS_EINVAL, "mgs_rollout_device: bad argument%s");
   if (sched->nphase < 1 || sched->nphase > MGS_MAX_PHASES) return fail(MGS_EINVAL, "bad phase count%s");
   if (n == 0) return MGS_OK;
@@ -362,7 +365,7 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   HIPCHK(hipEventRecord(b->e0, st));
 #define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(nwg), dim3(64), b->m->lds_bytes, st, md, \
       md.I, md.D, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
-      d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count)
+      d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in)
   switch (md.m.nv) {
 #define MGS_CASE(NV_) case NV_: MGS_LAUNCH_ROLL(NV_); break;
     MGS_NV_LIST(MGS_CASE)
@@ -396,12 +399,25 @@ int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32
 
 int mgs_rollout_list_device(mgs_batch* b, const mgs_schedule* sched, int n, const int32_t* d_count,
                             const int32_t* d_list, int grid, const double* d_qpos_init, const double* d_mocap_quat,
-                            const double* d_phase_start, const double* d_phase_target, uint8_t* d_label,
-                            int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, void* stream) {
+                            const double* d_phase_start, const double* d_phase_target, const double* d_resume_in,
+                            uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats,
+                            void* stream) {
   if (!b || !d_count || !d_list || grid < 1 || grid > b->cap)
     return fail(MGS_EINVAL, "mgs_rollout_list_device: bad argument (1 <= grid <= batch capacity)%s");
   return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, nullptr, d_label,
-                        d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, d_list, d_count, grid);
+                        d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, d_list, d_count, grid, nullptr,
+                        d_resume_in);
+}
+
+int mgs_rollout_resumable_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                                 const double* d_mocap_quat, const double* d_phase_start,
+                                 const double* d_phase_target, const uint8_t* d_active, uint8_t* d_label,
+                                 int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
+                                 void* stream) {
+  if (!d_resume_out) return fail(MGS_EINVAL, "mgs_rollout_resumable_device: null resume buffer%s");
+  return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
+                        d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, nullptr, nullptr, 0,
+                        d_resume_out, nullptr);
 }
 
 int mgs_simulate_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
@@ -466,9 +482,9 @@ double mgs_last_kernel_ms(mgs_batch* b) {
   return ms;
 }
 
-int mgs_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* qpos_init,
-                const double* mocap_quat, const double* phase_start, const double* phase_target,
-                mgs_rollout_out* out) {
+static int rollout_host(mgs_batch* b, const mgs_schedule* sched, int n, const double* qpos_init,
+                        const double* mocap_quat, const double* phase_start, const double* phase_target,
+                        const double* resume_in, mgs_rollout_out* out) {
   if (!b || !sched || !out || n < 0 || n > b->cap) return fail(MGS_EINVAL, "mgs_rollout: bad argument%s");
   if (n == 0) return MGS_OK;
   if (!qpos_init || !mocap_quat || !phase_start || !phase_target || !out->label)
@@ -476,18 +492,40 @@ int mgs_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* qp
   const mgs_model_desc& d = b->m->desc;
   int np = sched->nphase;
   HIPCHK(hipSetDevice(b->m->device));
+  const size_t rs = (size_t)d.nq + 2 * (size_t)d.nv + MGS_RESUME_EXTRA;
+  // resume records: one buffer serves as the output of a resumable run or the
+  // input of a resumed one
+  if ((out->resume || resume_in) && !b->d_resume &&
+      hipMalloc(&b->d_resume, sizeof(double) * rs * (size_t)b->cap) != hipSuccess)
+    return fail(MGS_ENOMEM, "resume buffer allocation failed%s");
   HIPCHK(hipMemcpy(b->d_qpos, qpos_init, sizeof(double) * n * d.nq, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_mquat, mocap_quat, sizeof(double) * n * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_ps, phase_start, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_pt, phase_target, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
-  int rc = mgs_rollout_device(b, sched, n, b->d_qpos, b->d_mquat, b->d_ps, b->d_pt, nullptr, b->d_label,
-                              b->d_fail, b->d_objq, b->d_stats, nullptr);
+  if (resume_in) HIPCHK(hipMemcpy(b->d_resume, resume_in, sizeof(double) * rs * n, hipMemcpyHostToDevice));
+  int rc = launch_rollout(b, sched, n, b->d_qpos, b->d_mquat, b->d_ps, b->d_pt, nullptr, b->d_label, b->d_fail,
+                          b->d_objq, b->d_stats, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                          out->resume ? b->d_resume : nullptr, resume_in ? b->d_resume : nullptr);
   if (rc) return rc;
   HIPCHK(hipMemcpy(out->label, b->d_label, n, hipMemcpyDeviceToHost));
   if (out->fail_step) HIPCHK(hipMemcpy(out->fail_step, b->d_fail, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   if (out->obj_qpos) HIPCHK(hipMemcpy(out->obj_qpos, b->d_objq, sizeof(double) * n * 7, hipMemcpyDeviceToHost));
   if (out->stats) HIPCHK(hipMemcpy(out->stats, b->d_stats, sizeof(int32_t) * n * MGS_NSTATS, hipMemcpyDeviceToHost));
+  if (out->resume) HIPCHK(hipMemcpy(out->resume, b->d_resume, sizeof(double) * rs * n, hipMemcpyDeviceToHost));
   return MGS_OK;
+}
+
+int mgs_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* qpos_init,
+                const double* mocap_quat, const double* phase_start, const double* phase_target,
+                mgs_rollout_out* out) {
+  return rollout_host(b, sched, n, qpos_init, mocap_quat, phase_start, phase_target, nullptr, out);
+}
+
+int mgs_rollout_resume(mgs_batch* b, const mgs_schedule* sched, int n, const double* qpos_init,
+                       const double* mocap_quat, const double* phase_start, const double* phase_target,
+                       const double* resume, mgs_rollout_out* out) {
+  if (!resume) return fail(MGS_EINVAL, "mgs_rollout_resume: null resume records%s");
+  return rollout_host(b, sched, n, qpos_init, mocap_quat, phase_start, phase_target, resume, out);
 }
 
 // test hook: device arithmetic on n inputs (out: n*4 = sqrt|x|, x/y, sin, cos)

@@ -3445,7 +3445,8 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
                       const double* __restrict__ phase_start, const double* __restrict__ phase_target,
                       const uint8_t* __restrict__ active, uint8_t* __restrict__ label,
                       int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
-                      const double* __restrict__ vstate_init, double* __restrict__ state_out) {
+                      const double* __restrict__ vstate_init, double* __restrict__ state_out,
+                      double* __restrict__ resume_out, const double* __restrict__ resume_in) {
   int lane = lane_id();
   if (active && !active[i]) {
     // collision-mask reject: not simulated (filter_to_stable.py:39-44)
@@ -3468,12 +3469,35 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
   reset(md, d, qpos_init + (size_t)i * md.m.nq, ps, mocap_quat + 4 * i,
         vstate_init ? vstate_init + (size_t)i * 2 * md.m.nv : nullptr);
   int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
+  const int nq = md.m.nq, nvr = md.m.nv, RS = nq + 2 * nvr + MGS_RESUME_EXTRA;
+  int p0 = 0, t0 = 0;
+  if (resume_in) {
+    // continue a capacity-capped run from its last step before the overflow
+    // (the capped run and a wider one are identical up to that step)
+    const double* rec = resume_in + (size_t)i * RS;
+    for (int k = lane; k < nq; k += WAVE) d.qpos[k] = rec[k];
+    for (int k = lane; k < nvr; k += WAVE) { d.qvel[k] = rec[nq + k]; d.qacc_ws[k] = rec[nq + nvr + k]; }
+    const double* tail = rec + nq + 2 * nvr;
+    if (lane == 0) { d.time[0] = tail[0]; d.ITERS = (int)tail[8]; }
+    p0 = (int)tail[1]; t0 = (int)tail[2]; gstep = (int)tail[3];
+    maxcon = (int)tail[4]; maxefc = (int)tail[5]; sumcon = (int)tail[6]; sumefc = (int)tail[7];
+    wsync();
+  }
   PROF_DECL
-  for (int p = 0; p < np && ok; p++) {
+  for (int p = p0; p < np && ok; p++) {
     if (lane == 0)
       for (int u = 0; u < md.m.nu; u++) d.ctrl[u] = sc.ctrl[p * 32 + u];
     int ns = sc.nsteps[p];
-    for (int t = 0; t < ns && ok; t++) {
+    for (int t = (p == p0 ? t0 : 0); t < ns && ok; t++) {
+      // resume snapshot: the state entering this step goes to the candidate's
+      // record (write-only, L2-resident: one record per candidate rewritten
+      // each step); if the step overflows, the schedule position completes it
+      if (resume_out) {
+        double* rec = resume_out + (size_t)i * RS;
+        for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
+        for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
+        if (lane == 0) { rec[nq + 2 * nvr] = d.time[0]; rec[nq + 2 * nvr + 8] = d.ITERS; }
+      }
       double frac = (double)t / (double)ns;
       if (lane == 0)
         for (int k = 0; k < 3; k++) d.mocap_pos[k] = ps[3 * p + k] + (pt[3 * p + k] - ps[3 * p + k]) * frac;
@@ -3506,6 +3530,18 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       forward<NV>(md, d, 1);
       integrate<NV>(md, d);
 #endif
+      if (resume_out && (uni(d.OVERFLOW) & MGS_FLAG_CAPACITY)) {
+        // capacity exceeded in this step: record where to resume and stop (the
+        // escalation re-runs from here with more capacity)
+        if (lane == 0) {
+          double* tail = resume_out + (size_t)i * RS + nq + 2 * nvr;
+          tail[1] = p; tail[2] = t; tail[3] = gstep;
+          tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
+        }
+        ok = 0;
+        fstep = -3;
+        break;
+      }
       if (uni(d.NCON) > maxcon) maxcon = uni(d.NCON);
       if (uni(d.NEFC) > maxefc) maxefc = uni(d.NEFC);
       sumcon += uni(d.NCON);
@@ -3541,6 +3577,7 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       gstep++;
     }
     if (ok && sc.check_at_end[p] && !obj_contact(md, d)) { ok = 0; fstep = gstep - 1; }
+    if (fstep == -3) break;
   }
   if (lane == 0) {
     label[i] = (uint8_t)ok;
@@ -3573,7 +3610,8 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
                    uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
                    int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
                    double* __restrict__ state_out, const int32_t* __restrict__ list,
-                   const int32_t* __restrict__ list_count) {
+                   const int32_t* __restrict__ list_count, double* __restrict__ resume_out,
+                   const double* __restrict__ resume_in) {
   extern __shared__ double smem[];
   Mdl md = mdarg;
   md.I = mI;
@@ -3584,7 +3622,7 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
     int i = list ? list[s] : s;
     if (i < 0 || i >= n) continue;
     rollout_one<NV>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target, active, label,
-                    fail_step, obj_qpos, stats, vstate_init, state_out);
+                    fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in);
   }
 }
 

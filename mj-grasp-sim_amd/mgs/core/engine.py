@@ -54,7 +54,10 @@ def load_library(wide: bool = False):
     L.mgs_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mgs_overflow_list_device.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp, vp]
     L.mgs_rollout_list_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, ctypes.c_int, vp, vp, vp, vp,
-                                          vp, vp, vp, vp, vp]
+                                          vp, vp, vp, vp, vp, vp]
+    L.mgs_rollout_resumable_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 11
+    L.mgs_rollout_resume.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
+                                     P(abi.RolloutOut)]
     L.mgs_last_kernel_ms.argtypes = [vp]
     L.mgs_last_kernel_ms.restype = ctypes.c_double
     L.mgs_last_collision_ms.argtypes = [vp]
@@ -212,7 +215,15 @@ class Engine:
                "mgs_collision_free")
         return out.astype(bool)
 
-    def rollout(self, plan):
+    def resume_width(self):
+        """doubles per resume record (mgs_rollout_out.resume)"""
+        return self.cm.nq + 2 * self.cm.nv + abi.MGS["MGS_RESUME_EXTRA"]
+
+    def rollout(self, plan, resumable=False, resume_from=None):
+        """mgs_rollout.  resumable: candidates overflowing the capacity stop at
+        that step (fail_step -3) and result["resume"] holds their records;
+        resume_from: records of such a capped run, continued here
+        (mgs_rollout_resume) instead of restarting from the plan."""
         n = len(plan.qpos_init)
         sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
                                   check_offset=getattr(plan, "check_offset", None))
@@ -222,17 +233,31 @@ class Engine:
         stats = np.zeros((n, abi.MGS["MGS_NSTATS"]), np.int32)
         if n == 0:
             return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats)
+        rec = np.zeros((n, self.resume_width()), np.float64) if resumable else None
         out = abi.RolloutOut(ptr(label, ctypes.c_uint8), ptr(fail, ctypes.c_int32),
-                             ptr(objq, ctypes.c_double), ptr(stats, ctypes.c_int32))
+                             ptr(objq, ctypes.c_double), ptr(stats, ctypes.c_int32),
+                             None if rec is None else ptr(rec, ctypes.c_double))
         q = np.ascontiguousarray(plan.qpos_init, np.float64)
         mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
         ps = np.ascontiguousarray(plan.phase_start, np.float64)
         pt = np.ascontiguousarray(plan.phase_target, np.float64)
-        self._ck(self.lib.mgs_rollout(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
-                                    ptr(mq, ctypes.c_double), ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double),
-                                    ctypes.byref(out)), "mgs_rollout")
-        return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats,
-                    kernel_ms=self.lib.mgs_last_kernel_ms(self._batch))
+        if resume_from is None:
+            self._ck(self.lib.mgs_rollout(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
+                                        ptr(mq, ctypes.c_double), ptr(ps, ctypes.c_double),
+                                        ptr(pt, ctypes.c_double), ctypes.byref(out)), "mgs_rollout")
+        else:
+            rs = np.ascontiguousarray(resume_from, np.float64)
+            if rs.shape != (n, self.resume_width()):
+                raise ValueError(f"resume records have shape {rs.shape}, expected {(n, self.resume_width())}")
+            self._ck(self.lib.mgs_rollout_resume(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
+                                               ptr(mq, ctypes.c_double), ptr(ps, ctypes.c_double),
+                                               ptr(pt, ctypes.c_double), ptr(rs, ctypes.c_double),
+                                               ctypes.byref(out)), "mgs_rollout_resume")
+        res = dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats,
+                   kernel_ms=self.lib.mgs_last_kernel_ms(self._batch))
+        if rec is not None:
+            res["resume"] = rec
+        return res
 
     def simulate(self, plan, vstate=None, vclip=0.0):
         """Free simulation (mgs_simulate): final qpos, qvel, qacc_warmstart and stats
@@ -279,13 +304,22 @@ class Engine:
         m = abi.MGS["MGS_FLAG_CAPACITY"] if mask is None else int(mask)
         self._ck(self.lib.mgs_overflow_list_device(n, d_stats, m, d_count, d_list, stream), "mgs_overflow_list_device")
 
+    def rollout_resumable_device(self, sched, n, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats,
+                                 d_resume_out, d_active=None, stream=None):
+        """rollout_device whose overflowing candidates stop at the overflowing
+        step and leave a resume record (n x resume_width() doubles)"""
+        self._ck(self.lib.mgs_rollout_resumable_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps,
+                                                     d_pt, d_active, d_label, d_fail, d_objq, d_stats,
+                                                     d_resume_out, stream), "mgs_rollout_resumable_device")
+
     def rollout_list_device(self, sched, n, d_count, d_list, grid, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail,
-                            d_objq, d_stats, stream=None):
+                            d_objq, d_stats, stream=None, d_resume_in=None):
         """re-run the candidates of a device list with `grid` workgroups looping
-        over it (outputs at their batch indices)"""
+        over it (outputs at their batch indices); d_resume_in: continue each
+        from its resume record instead of from the start"""
         self._ck(self.lib.mgs_rollout_list_device(self.batch(grid), ctypes.byref(sched), n, d_count, d_list, grid,
-                                                d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats,
-                                                stream), "mgs_rollout_list_device")
+                                                d_qpos, d_mquat, d_ps, d_pt, d_resume_in, d_label, d_fail, d_objq,
+                                                d_stats, stream), "mgs_rollout_list_device")
 
     def last_collision_ms(self):
         return self.lib.mgs_last_collision_ms(self._batch)

@@ -161,19 +161,25 @@ class GravitylessObjectGrasping:
     def rollout(self, plan: "RolloutPlan", max_ncon: int = 40):
         """engine.rollout with capacity escalation: MuJoCo has no contact cap, the
         kernel's per-candidate contact arrays do (ncon_max, LDS-resident).  A
-        candidate that exceeded it at any step (stats[:, 2] != 0) is re-run from
-        its initial state with twice the capacity (constraint rows capped at 128),
-        until none overflows or max_ncon is reached; its results replace the
-        capped run's.  res['overflow'] counts candidates still capped."""
-        res = self.engine.rollout(plan)
+        candidate that exceeds it (stats[:, 2] & FLAG_CAPACITY) stops at that step
+        and is continued from the state entering it with twice the capacity
+        (constraint rows capped at 128) -- the capped and the wider run are
+        identical up to there -- until none overflows or max_ncon is reached (the
+        last stage runs on capped, flagged); its results replace the capped
+        run's.  res['overflow'] counts candidates still capped."""
         cap = self.ncon_max
+        res = self.engine.rollout(plan, resumable=cap < max_ncon)
+        rec = res.pop("resume", None)
         ov = np.nonzero(res["stats"][:, 2] & FLAG_CAPACITY)[0]
         while len(ov) and cap < max_ncon:
             cap = min(2 * cap, max_ncon)
-            sub = self.engine_for(cap).rollout(plan.subset(ov))
+            sub = self.engine_for(cap).rollout(plan.subset(ov), resumable=cap < max_ncon, resume_from=rec[ov])
             for k in ("label", "fail_step", "obj_qpos", "stats"):
                 res[k][ov] = sub[k]
-            ov = ov[np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0]]
+            keep = np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0]
+            ov = ov[keep]
+            if "resume" in sub:
+                rec[ov] = sub["resume"][keep]
         res["overflow"] = len(ov)
         return res
 

@@ -292,6 +292,62 @@ def test_contact_capacity_escalation(env):
     assert not r20["stats"][:, 2].any()
 
 
+def test_resumed_escalation_equals_wide_run(env, candidates):
+    """Capacity 4 overflows most candidates: each stops at its overflowing step
+    and is continued from the state entering it at 8, 16, 32 and 40 contacts
+    (mgs_rollout_resume, chained).  Every output equals one run at 40 from the
+    start, bit for bit; so does the device path (resumable rollout -> overflow
+    list -> list rollout continuing from the records)."""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    e4 = GravitylessObjectGrasping(env.gripper, env.obj, ncon_max=4)
+    poses, J = candidates
+    q, mp, mq, _ = e4.initial_state(poses, J)
+    idx = np.nonzero(e4.engine.collision_free(q, mp, mq))[0][:96]
+    plan = plan_for(e4, poses[idx], J[idx])
+    n = len(idx)
+    ref = e4.engine_for(40).rollout(plan)
+    capped = e4.engine.rollout(plan, resumable=True)
+    stopped = np.nonzero(capped["stats"][:, 2] & abi.MGS["MGS_FLAG_CAPACITY"])[0]
+    assert len(stopped) > n // 4
+    assert np.all(capped["fail_step"][stopped] == -3) and not capped["label"][stopped].any()
+    res = e4.rollout(plan, max_ncon=40)
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(res[k], ref[k]), k
+    assert res["overflow"] == int((ref["stats"][:, 2] & abi.MGS["MGS_FLAG_CAPACITY"] != 0).sum())
+    # device path, one stage 4 -> 40
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                              check_offset=getattr(plan, "check_offset", None))
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+    dq, dmq, dps, dpt = t(plan.qpos_init), t(plan.mocap_quat), t(plan.phase_start), t(plan.phase_target)
+    NS = abi.MGS["MGS_NSTATS"]
+    outs = lambda: (torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.int32, device=dev),  # noqa
+                    torch.zeros((n, 7), dtype=torch.float64, device=dev),
+                    torch.zeros((n, NS), dtype=torch.int32, device=dev))
+    main, esc = outs(), outs()
+    rec = torch.zeros((n, e4.engine.resume_width()), dtype=torch.float64, device=dev)
+    e4.engine.rollout_resumable_device(sched, n, dq.data_ptr(), dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
+                                       *[x.data_ptr() for x in main], rec.data_ptr())
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    lst = torch.zeros(n, dtype=torch.int32, device=dev)
+    e4.engine.overflow_list_device(n, main[3].data_ptr(), cnt.data_ptr(), lst.data_ptr())
+    e4.engine_for(40).rollout_list_device(sched, n, cnt.data_ptr(), lst.data_ptr(), 5, dq.data_ptr(),
+                                          dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
+                                          *[x.data_ptr() for x in esc], d_resume_in=rec.data_ptr())
+    torch.cuda.synchronize()
+    k = int(cnt.item())
+    lo = np.sort(lst.cpu().numpy()[:k])
+    assert np.array_equal(lo, stopped)
+    got = [x.cpu().numpy() for x in main]
+    for a, e in zip(got, [x.cpu().numpy() for x in esc]):
+        a[lo] = e[lo]
+    for key, a in zip(("label", "fail_step", "obj_qpos", "stats"), got):
+        assert np.array_equal(a.astype(ref[key].dtype), ref[key]), key
+
+
 def test_divergence_guard_parity(env, eng, candidates, oracle_model):
     """injected NaN / beyond-mjMAXVAL states: the GPU stops and flags exactly the
     candidates the oracle does (obj_qpos compared with NaN == NaN)."""
