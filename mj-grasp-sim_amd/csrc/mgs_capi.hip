@@ -65,7 +65,7 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
 #ifdef MGS_G_GLOBAL
   us[U_G] = 0;               // G in HBM (batch buffer), see bind()
 #else
-  us[U_G] = ne * (nv + 0);   // row stride: GS in the kernel
+  us[U_G] = ne * (nv + MGS_GPAD);   // row stride: GS in the kernel
 #endif
   us[U_aref] = ne;
   us[U_scratch] = (2 * ne > nv ? 2 * ne : nv);

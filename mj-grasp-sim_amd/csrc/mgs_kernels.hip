@@ -34,7 +34,19 @@
 #define WAVE 64
 // row stride of the constraint matrix G (doubles).  An odd stride (NV + 1) makes
 // row walks bank-conflict free but measured no faster and costs 680 B of LDS
-#define GS (NV + 0)
+// G row stride (doubles): NV + MGS_GPAD.  With lanes over rows reading G[r * GS + k],
+// an odd stride spreads the 32 lanes of a ds_read_b64 group over distinct banks
+#ifndef MGS_GPAD
+#ifdef MGS_G_GLOBAL
+#define MGS_GPAD 0
+#else
+#define MGS_GPAD 1
+#endif
+#endif
+#define GS (NV + MGS_GPAD)
+#if defined(MGS_G_GLOBAL) && MGS_GPAD != 0
+#error "G rows in HBM are unpadded (launch_layout sizes them nefc_max * nv)"
+#endif
 #define DEVI __device__ __attribute__((always_inline)) inline
 
 struct P2 { double x, y, h; };
@@ -115,7 +127,11 @@ __shared__ unsigned long long s_prof[65];
 #define PCNT(k, v)
 #define PROF_FLUSH
 #endif
+#ifdef MGS_WSYNC_FENCE
+DEVI void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+#else
 DEVI void wsync() { __syncthreads(); }
+#endif
 
 // ---------------------------------------------------------------------------
 // math primitives: identical expressions to the oracle
@@ -1733,7 +1749,7 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   BU(qDeriv, U_qDeriv);
 #undef BU
   d.con_hb = d.con_blk;   // Newton cone Hessians reuse the contact-block slots
-  d.gs = l.nv + 0;
+  d.gs = l.nv + MGS_GPAD;
   int* ib = (int*)(s + l.o[L_ints]);
   d.ints = ib;
   int ncmax = l.ncon_max, nemax = l.nefc_max;
@@ -3349,10 +3365,13 @@ DEVI void integrate(const Mdl& md, Dat& d) {
   for (int k = lane; k < nv; k += WAVE) qa[k] = d.qfrc_smooth[k] + d.qfrc_constraint[k];
   wsync();
   ldl_solve<NV>(d.M, d.Dinv, qa, qa);
-  if (lane == 0) {
-    for (int k = 0; k < nv; k++) d.qvel[k] = d.qvel[k] + dt * qa[k];
+  // qvel per dof, then qpos per joint (lanes over joints: their qpos ranges
+  // are disjoint, each lane runs the oracle's per-joint expressions)
+  for (int k = lane; k < nv; k += WAVE) d.qvel[k] = d.qvel[k] + dt * qa[k];
+  wsync();
+  {
     const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
-    for (int j = 0; j < md.m.njnt; j++) {
+    for (int j = lane; j < md.m.njnt; j += WAVE) {
       int a = jq[j], v = jd[j];
       if (jtype[j] == MGS_JNT_FREE) {
         d.qpos[a] = d.qpos[a] + dt * d.qvel[v];
@@ -3369,7 +3388,7 @@ DEVI void integrate(const Mdl& md, Dat& d) {
         d.qpos[a] = d.qpos[a] + dt * d.qvel[v];
       }
     }
-    d.time[0] = d.time[0] + dt;
+    if (lane == 0) d.time[0] = d.time[0] + dt;
   }
   wsync();
 }
@@ -3601,8 +3620,13 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
 // (list != nullptr) -- candidates list[s] for s = blockIdx.x, blockIdx.x +
 // gridDim.x, ... < *list_count: a small grid re-runs a device-built subset
 // (capacity escalation) without launching a workgroup per batch entry.
+#ifdef MGS_WAVES_PER_EU
+#define MGS_ROLL_ATTR __attribute__((amdgpu_waves_per_eu(MGS_WAVES_PER_EU)))
+#else
+#define MGS_ROLL_ATTR
+#endif
 template <int NV>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) MGS_ROLL_ATTR
 mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
                    mgs_schedule sc, int n, const double* __restrict__ qpos_init,
                    const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
