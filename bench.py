@@ -171,8 +171,8 @@ def e2e_api(env, poses, J, h, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--candidates", type=int, default=8192)
     ap.add_argument("--horizon", default="h200")
     ap.add_argument("--solver", default=None, help="override the model's solver (Newton | PGS)")
@@ -437,6 +437,7 @@ def main():
         "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
                    "rollouts_per_s": float(free.sum()) * world * args.steps / dt,
                    "pipelines_identical": bool(same_pipes),
+                   "static_layout_kernel": env.engine.static_layout(),
                    "shard_check": shard_check,
                    "end_to_end_api": e2e,
                    "issue": issue_summary(),

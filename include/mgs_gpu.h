@@ -286,6 +286,15 @@ void mgs_model_free(mgs_model* model);
  * needed).  The host picks the contact/row capacity with it: a CU holds
  * floor(160 KiB / bytes) candidates in flight. */
 int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes);
+/* The LDS carve-up itself (offsets in doubles: the persistent arrays, the
+ * time-multiplexed U views, then ncon_max, nefc_max, nv, total), host-only.
+ * Writes at most cap words and their count to *nwords.  The build bakes the
+ * headline model's layout into a constant-offset kernel instantiation
+ * (tools/gen_static_layout.py); launches whose layout matches it use that one. */
+int mgs_model_layout(const mgs_model_desc* desc, int32_t* out, int cap, int32_t* nwords);
+/* 1 if this model's rollouts run the static-layout instantiation (its layout
+ * equals the one baked in at build time), 0 if the runtime-offset one. */
+int mgs_model_static_layout(const mgs_model* model);
 
 /* Capacity limits of this library build: constraint rows per candidate
  * (libmgs_gpu.so 128, libmgs_gpu_wide.so 256) and whether a kernel is

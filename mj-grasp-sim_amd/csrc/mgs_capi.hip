@@ -141,7 +141,28 @@ static bool nv_supported(int nv) {
 #define MGS_STATIC_LDS 0
 #endif
 
+// the launch's layout is the one baked into the static-layout instantiation
+static bool static_layout_match(const Lay& l) {
+#if MGS_SL_NV > 0
+  if (l.nv != MGS_SL_NV) return false;
+  for (int i = 0; i < L_COUNT; i++) if (l.o[i] != mgs_sl_words[i]) return false;
+  for (int i = 0; i < U_COUNT; i++) if (l.u[i] != mgs_sl_words[L_COUNT + i]) return false;
+  const int* t = mgs_sl_words + L_COUNT + U_COUNT;
+  return l.ncon_max == t[0] && l.nefc_max == t[1] && l.nv == t[2] && l.total_doubles == t[3];
+#else
+  (void)l;
+  return false;
+#endif
+}
+
 static hipError_t set_lds_limit(int nv, int bytes) {
+#if MGS_SL_NV > 0
+  if (nv == MGS_SL_NV) {
+    hipError_t e = hipFuncSetAttribute((const void*)mgs_rollout_kernel<MGS_SL_NV, 1>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
+  }
+#endif
   switch (nv) {
 #define MGS_CASE(NV_)                                                                                      \
   case NV_: {                                                                                              \
@@ -366,6 +387,14 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
 #define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(nwg), dim3(64), b->m->lds_bytes, st, md, \
       md.I, md.D, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
       d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in)
+#if MGS_SL_NV > 0
+  if (static_layout_match(lay)) {
+    hipLaunchKernelGGL((mgs_rollout_kernel<MGS_SL_NV, 1>), dim3(nwg), dim3(64), b->m->lds_bytes, st, md, md.I, md.D,
+                       lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
+                       d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out,
+                       d_resume_in);
+  } else
+#endif
   switch (md.m.nv) {
 #define MGS_CASE(NV_) case NV_: MGS_LAUNCH_ROLL(NV_); break;
     MGS_NV_LIST(MGS_CASE)
@@ -760,6 +789,23 @@ int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes) {
   *out_bytes = (int64_t)b;
   return MGS_OK;
 }
+
+int mgs_model_layout(const mgs_model_desc* desc, int32_t* out, int cap, int32_t* nwords) {
+  if (!desc || !out || !nwords) return fail(MGS_EINVAL, "mgs_model_layout: null argument%s");
+  size_t b = 0;
+  Lay l = make_layout(*desc, &b);
+  int32_t w[L_COUNT + U_COUNT + 4];
+  int k = 0;
+  for (int i = 0; i < L_COUNT; i++) w[k++] = l.o[i];
+  for (int i = 0; i < U_COUNT; i++) w[k++] = l.u[i];
+  w[k++] = l.ncon_max; w[k++] = l.nefc_max; w[k++] = l.nv; w[k++] = l.total_doubles;
+  if (cap < k) return fail(MGS_EINVAL, "mgs_model_layout: output too small%s");
+  for (int i = 0; i < k; i++) out[i] = w[i];
+  *nwords = k;
+  return MGS_OK;
+}
+
+int mgs_model_static_layout(const mgs_model* m) { return m && static_layout_match(m->lay) ? 1 : 0; }
 
 int mgs_device_count(void) {
   int n = 0;

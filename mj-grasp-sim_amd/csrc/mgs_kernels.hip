@@ -1719,8 +1719,25 @@ struct Lay {
   double* gmem;     // MGS_G_GLOBAL: per-candidate G rows in HBM (nefc_max * nv doubles each)
 };
 
+// Static layout: the headline model's carve-up (tools/gen_static_layout.py ->
+// mgs_static_layout.h) as compile-time offsets.  A kernel instantiated with
+// SL = 1 binds every view at a constant LDS address, so the ~80 views need no
+// SGPRs (their spills to VGPR lanes and reloads disappear) and LDS accesses
+// carry their offsets as instruction immediates.  The host launches it only
+// for a launch whose runtime layout equals this one.
+#if defined(MGS_STATIC_LAYOUT) && !defined(MGS_WIDE)
+#include "mgs_static_layout.h"
+#else
+#define MGS_SL_NV 0
+constexpr int mgs_sl_words[L_COUNT + U_COUNT + 4] = {0};
+#endif
+static_assert(sizeof(mgs_sl_words) == sizeof(int) * (L_COUNT + U_COUNT + 4), "static layout size");
+
+template <int SL>
 DEVI void bind(Dat& d, double* s, const Lay& l) {
-#define B(f) d.f = s + l.o[L_##f]
+#define LO(k) (SL ? mgs_sl_words[k] : l.o[k])
+#define LU(k) (SL ? mgs_sl_words[L_COUNT + (k)] : l.u[k])
+#define B(f) d.f = s + LO(L_##f)
   B(qpos); B(qvel); B(qacc_ws); B(ctrl); B(mocap_pos); B(mocap_quat); B(time);
   B(xpos); B(xquat); B(xmat); B(subtree_com); B(cinert); B(cdof);
   B(M); B(Dv); B(Dinv); B(sD); B(isD); B(tmp); B(tmp2);
@@ -1729,9 +1746,9 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   B(con_pos); B(con_frame); B(con_dist); B(con_mu); B(con_blk);
   B(efc_R); B(efc_b);
 #undef B
-  double* U = s + l.o[L_U];
-#define BU(f, k) d.f = U + l.u[k]
-  d.poly = (P2*)(U + l.u[U_poly]);
+  double* U = s + LO(L_U);
+#define BU(f, k) d.f = U + LU(k)
+  d.poly = (P2*)(U + LU(U_poly));
   BU(pdep, U_pdep); BU(geom_xpos, U_geom_xpos); BU(geom_xmat, U_geom_xmat); BU(xipos, U_xipos);
   BU(xanchor, U_xanchor); BU(xaxis, U_xaxis); BU(subtree_mass, U_subtree_mass); BU(comacc, U_comacc);
   BU(crb, U_crb); BU(cvel, U_cvel); BU(cacc, U_cacc); BU(cfrc, U_cfrc); BU(cdof_dot, U_cdof_dot);
@@ -1749,10 +1766,11 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   BU(qDeriv, U_qDeriv);
 #undef BU
   d.con_hb = d.con_blk;   // Newton cone Hessians reuse the contact-block slots
-  d.gs = l.nv + MGS_GPAD;
-  int* ib = (int*)(s + l.o[L_ints]);
+  d.gs = (SL ? mgs_sl_words[L_COUNT + U_COUNT + 2] : l.nv) + MGS_GPAD;
+  int* ib = (int*)(s + LO(L_ints));
   d.ints = ib;
-  int ncmax = l.ncon_max, nemax = l.nefc_max;
+  int ncmax = SL ? mgs_sl_words[L_COUNT + U_COUNT] : l.ncon_max;
+  int nemax = SL ? mgs_sl_words[L_COUNT + U_COUNT + 1] : l.nefc_max;
   d.con_pair = ib + 16;
   d.con_g1 = d.con_pair + ncmax;
   d.con_g2 = d.con_g1 + ncmax;
@@ -1760,6 +1778,8 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   d.efc_dim = d.efc_type + nemax;
   d.efc_con = d.efc_dim + nemax;
   d.efc_state = d.efc_con + nemax;
+#undef LO
+#undef LU
 }
 
 // A_rr = G_r . G_r in the oracle's order (its efc_A)
@@ -3447,7 +3467,7 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   int i = blockIdx.x;
   if (i >= n) return;
   Dat d;
-  bind(d, smem, lay);
+  bind<0>(d, smem, lay);
   reset(md, d, qpos_init + (size_t)i * md.m.nq, mocap_pos + 3 * i, mocap_quat + 4 * i);
   forward<NV>(md, d, 0);
   if (lane_id() == 0) {
@@ -3458,7 +3478,7 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
 }
 
 // one candidate's rollout (the body of mgs_rollout_kernel)
-template <int NV>
+template <int NV, int SL>
 DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_schedule& sc, int i,
                       const double* __restrict__ qpos_init, const double* __restrict__ mocap_quat,
                       const double* __restrict__ phase_start, const double* __restrict__ phase_target,
@@ -3481,7 +3501,7 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
     return;
   }
   Dat d;
-  bind(d, smem, lay);
+  bind<SL>(d, smem, lay);
   int np = sc.nphase;
   const double* ps = phase_start + (size_t)i * np * 3;
   const double* pt = phase_target + (size_t)i * np * 3;
@@ -3625,7 +3645,7 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
 #else
 #define MGS_ROLL_ATTR
 #endif
-template <int NV>
+template <int NV, int SL = 0>
 __global__ void __launch_bounds__(64) MGS_ROLL_ATTR
 mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
                    mgs_schedule sc, int n, const double* __restrict__ qpos_init,
@@ -3645,7 +3665,7 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
   for (int s = blockIdx.x; s < end; s += stride) {
     int i = list ? list[s] : s;
     if (i < 0 || i >= n) continue;
-    rollout_one<NV>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target, active, label,
+    rollout_one<NV, SL>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target, active, label,
                     fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in);
   }
 }

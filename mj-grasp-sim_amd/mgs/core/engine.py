@@ -67,6 +67,8 @@ def load_library(wide: bool = False):
     L.mgs_lds_bytes.argtypes = [vp]
     L.mgs_device_count.restype = ctypes.c_int
     L.mgs_model_lds_bytes.argtypes = [P(abi.ModelDesc), P(ctypes.c_int64)]
+    L.mgs_model_layout.argtypes = [P(abi.ModelDesc), P(ctypes.c_int32), ctypes.c_int, P(ctypes.c_int32)]
+    L.mgs_model_static_layout.argtypes = [vp]
     L.mgs_max_rows.restype = ctypes.c_int
     L.mgs_antipodal_contacts.argtypes = [ctypes.c_int, P(c_d), ctypes.c_int, ctypes.c_int, P(c_d), P(c_d), P(c_d),
                                          c_d, P(c_d), P(c_i), P(c_d)]
@@ -115,6 +117,18 @@ def lds_bytes_for(cm, ncon_max, nefc_max=None):
     out = ctypes.c_int64()
     _check(L.mgs_model_lds_bytes(ctypes.byref(desc), ctypes.byref(out)), "mgs_model_lds_bytes")
     return int(out.value)
+
+
+def layout_for(cm, ncon_max, nefc_max=None):
+    """The kernels' LDS carve-up for this model and capacity (mgs_model_layout:
+    offsets in doubles, then ncon_max, nefc_max, nv, total), host only."""
+    fields, _, _ = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
+    L = library_for(cm.nv, int(fields["nefc_max"]))
+    desc = abi.make_desc(fields)
+    buf = (ctypes.c_int32 * 256)()
+    n = ctypes.c_int32()
+    _check(L.mgs_model_layout(ctypes.byref(desc), buf, 256, ctypes.byref(n)), "mgs_model_layout")
+    return [int(x) for x in buf[:n.value]]
 
 
 def default_rows(cm, worst: int) -> int:
@@ -323,6 +337,10 @@ class Engine:
 
     def last_collision_ms(self):
         return self.lib.mgs_last_collision_ms(self._batch)
+
+    def static_layout(self):
+        """True if this engine's rollouts run the constant-offset (baked layout) kernel"""
+        return bool(self.lib.mgs_model_static_layout(self._model))
 
     def lds_bytes(self):
         return self.lib.mgs_lds_bytes(self._model)

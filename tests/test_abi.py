@@ -83,3 +83,26 @@ def test_engine_fails_loudly_without_gpu(env, lib):
         pytest.skip("a GPU is visible")
     with pytest.raises(engine.EngineError):
         engine.Engine(env.model)
+
+
+def test_layout_export_is_consistent(env):
+    """mgs_model_layout: offsets ascend, the total matches mgs_model_lds_bytes"""
+    from mgs.core.engine import layout_for, lds_bytes_for
+    w = layout_for(env.model, env.ncon_max, env.nefc_max)
+    nc, ne, nv, total = w[-4:]
+    assert (nc, ne, nv) == (env.ncon_max, env.nefc_max, env.model.nv)
+    assert total * 8 == lds_bytes_for(env.model, env.ncon_max, env.nefc_max)
+
+
+def test_static_layout_header_is_current(env):
+    """the baked headline layout (mgs_static_layout.h) equals the layout the
+    headline engine launches with, so bench.py runs the constant-offset kernel
+    (a stale header would silently fall back to the runtime-offset one)"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_static_layout as G
+    path = G.OUT
+    if not os.path.isfile(path):
+        pytest.skip("no static layout baked into this build")
+    nv, words = G.headline_layout()
+    assert open(path).read() == G.render(nv, words)

@@ -358,3 +358,23 @@ def test_divergence_guard_parity(env, eng, candidates, oracle_model):
     for k in ("label", "fail_step", "stats"):
         assert np.array_equal(rg[k], ro[k]), k
     assert np.array_equal(rg["obj_qpos"], ro["obj_qpos"], equal_nan=True)
+
+
+def test_static_layout_kernel_matches_runtime_layout(env, eng, candidates):
+    """The headline engine runs the constant-offset instantiation (its layout is
+    the baked one); an engine one row smaller runs the runtime-offset one.  On
+    candidates that fit both capacities every output is identical."""
+    from conftest import plan_for
+    from mgs.core.engine import Engine
+    assert eng.static_layout()
+    other = Engine(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max - 1)
+    assert not other.static_layout()
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(eng.collision_free(q, mp, mq))[0][:64]
+    plan = plan_for(env, poses[idx], J[idx])
+    a, b = eng.rollout(plan), other.rollout(plan)
+    ok = (a["stats"][:, 2] == 0) & (b["stats"][:, 2] == 0)
+    assert ok.sum() > 0.9 * len(idx)
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(a[k][ok], b[k][ok]), k
