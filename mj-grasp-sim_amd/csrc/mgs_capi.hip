@@ -161,6 +161,9 @@ static hipError_t set_lds_limit(int nv, int bytes) {
     hipError_t e = hipFuncSetAttribute((const void*)mgs_rollout_kernel<MGS_SL_NV, 1>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)mgs_collision_kernel<MGS_SL_NV, 1>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
   }
 #endif
   switch (nv) {
@@ -340,6 +343,12 @@ int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, co
   HIPCHK(hipEventRecord(b->e2, st));
 #define MGS_LAUNCH_COLL(NV_) hipLaunchKernelGGL(mgs_collision_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
       md.I, md.D, lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free)
+#if MGS_SL_NV > 0
+  if (static_layout_match(lay)) {
+    hipLaunchKernelGGL((mgs_collision_kernel<MGS_SL_NV, 1>), dim3(n), dim3(64), b->m->lds_bytes, st, md, md.I, md.D,
+                       lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free);
+  } else
+#endif
   switch (md.m.nv) {
 #define MGS_CASE(NV_) case NV_: MGS_LAUNCH_COLL(NV_); break;
     MGS_NV_LIST(MGS_CASE)

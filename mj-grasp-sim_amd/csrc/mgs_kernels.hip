@@ -3454,7 +3454,7 @@ DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mp
 
 // ---------------------------------------------------------------------------
 // kernels: one 64-lane workgroup per candidate
-template <int NV>
+template <int NV, int SL = 0>
 __global__ void __launch_bounds__(64)
 mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
                      const double* __restrict__ qpos_init,
@@ -3467,7 +3467,7 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   int i = blockIdx.x;
   if (i >= n) return;
   Dat d;
-  bind<0>(d, smem, lay);
+  bind<SL>(d, smem, lay);
   reset(md, d, qpos_init + (size_t)i * md.m.nq, mocap_pos + 3 * i, mocap_quat + 4 * i);
   forward<NV>(md, d, 0);
   if (lane_id() == 0) {
