@@ -141,15 +141,17 @@ static bool nv_supported(int nv) {
 #define MGS_STATIC_LDS 0
 #endif
 
-// the launch's layout is the one baked into the static-layout instantiation
-static bool static_layout_match(const Lay& l) {
+// the launch's model description and layout are the ones baked into the
+// static-layout instantiations
+static bool static_layout_match(const mgs_model_desc& desc, const Lay& l) {
 #if MGS_SL_NV > 0
-  if (l.nv != MGS_SL_NV) return false;
+  if (l.nv != MGS_SL_NV || !mgs_sl_desc_equal(desc)) return false;
   for (int i = 0; i < L_COUNT; i++) if (l.o[i] != mgs_sl_words[i]) return false;
   for (int i = 0; i < U_COUNT; i++) if (l.u[i] != mgs_sl_words[L_COUNT + i]) return false;
   const int* t = mgs_sl_words + L_COUNT + U_COUNT;
   return l.ncon_max == t[0] && l.nefc_max == t[1] && l.nv == t[2] && l.total_doubles == t[3];
 #else
+  (void)desc;
   (void)l;
   return false;
 #endif
@@ -344,7 +346,7 @@ int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, co
 #define MGS_LAUNCH_COLL(NV_) hipLaunchKernelGGL(mgs_collision_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
       md.I, md.D, lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free)
 #if MGS_SL_NV > 0
-  if (static_layout_match(lay)) {
+  if (static_layout_match(b->m->desc, lay)) {
     hipLaunchKernelGGL((mgs_collision_kernel<MGS_SL_NV, 1>), dim3(n), dim3(64), b->m->lds_bytes, st, md, md.I, md.D,
                        lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free);
   } else
@@ -397,7 +399,7 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
       md.I, md.D, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
       d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in)
 #if MGS_SL_NV > 0
-  if (static_layout_match(lay)) {
+  if (static_layout_match(b->m->desc, lay)) {
     hipLaunchKernelGGL((mgs_rollout_kernel<MGS_SL_NV, 1>), dim3(nwg), dim3(64), b->m->lds_bytes, st, md, md.I, md.D,
                        lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
                        d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out,
@@ -814,7 +816,7 @@ int mgs_model_layout(const mgs_model_desc* desc, int32_t* out, int cap, int32_t*
   return MGS_OK;
 }
 
-int mgs_model_static_layout(const mgs_model* m) { return m && static_layout_match(m->lay) ? 1 : 0; }
+int mgs_model_static_layout(const mgs_model* m) { return m && static_layout_match(m->desc, m->lay) ? 1 : 0; }
 
 int mgs_device_count(void) {
   int n = 0;

@@ -1730,6 +1730,7 @@ struct Lay {
 #else
 #define MGS_SL_NV 0
 constexpr int mgs_sl_words[L_COUNT + U_COUNT + 4] = {0};
+constexpr mgs_model_desc mgs_sl_desc = {};
 #endif
 static_assert(sizeof(mgs_sl_words) == sizeof(int) * (L_COUNT + U_COUNT + 4), "static layout size");
 
@@ -3462,6 +3463,7 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
                      uint8_t* __restrict__ out) {
   extern __shared__ double smem[];
   Mdl md = mdarg;
+  if constexpr (SL != 0) md.m = mgs_sl_desc;
   md.I = mI;
   md.D = mD;
   int i = blockIdx.x;
@@ -3658,6 +3660,9 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
                    const double* __restrict__ resume_in) {
   extern __shared__ double smem[];
   Mdl md = mdarg;
+  // SL: the model description is the baked one too, so sizes, table offsets and
+  // options are compile-time constants (trip counts, immediate offsets)
+  if constexpr (SL != 0) md.m = mgs_sl_desc;
   md.I = mI;
   md.D = mD;
   const int end = list ? *list_count : (blockIdx.x < (unsigned)n ? (int)blockIdx.x + 1 : 0);

@@ -105,4 +105,4 @@ def test_static_layout_header_is_current(env):
     if not os.path.isfile(path):
         pytest.skip("no static layout baked into this build")
     nv, words = G.headline_layout()
-    assert open(path).read() == G.render(nv, words)
+    assert open(path).read() == G.render(nv, words, G.headline_desc())
