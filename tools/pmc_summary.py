@@ -34,7 +34,7 @@ def main(d, tag="r02"):
     out = {"source": "rocprofv3 --kernel-trace --pmc <counters> (separate passes) on `python3 bench.py --streams 1 "
                      "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate` (tools/prof_r02.sh); "
                      "per rollout dispatch",
-           "kernel": "mgs_rollout_kernel<20>"}
+           "kernel": "mgs_rollout_kernel<20, 1> (static-layout instantiation)"}
     sums = {}
     for name in ("fetch", "write", "sq", "valu"):
         p = os.path.join(d, f"pmc_{name}", "pmc_counter_collection.csv")
