@@ -3320,13 +3320,15 @@ DEVI void solve(const Mdl& md, Dat& d) {
 }
 
 // ---------------------------------------------------------------------------
+// mj_forward up to the constraint rows (everything before the solver): a
+// candidate whose contacts / rows overflow here still holds the state entering
+// the step (qpos, qvel, qacc_warmstart, time change only in solve / integrate)
 template <int NV>
-DEVI void forward(const Mdl& md, Dat& d, int full) {
+DEVI void forward_rows(const Mdl& md, Dat& d) {
   int nv = md.m.nv, lane = lane_id();
   kinematics(md, d);
   com_pos(md, d);
   collision(md, d);
-  if (!full) return;
   crb(md, d);
   ldl_factor<NV>(d.M, d.Dv, d.Dinv);
   for (int k = lane; k < nv; k += WAVE) {
@@ -3341,6 +3343,17 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
   wsync();
   ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
   make_constraints<NV>(md, d);
+}
+
+template <int NV>
+DEVI void forward(const Mdl& md, Dat& d, int full) {
+  if (!full) {
+    kinematics(md, d);
+    com_pos(md, d);
+    collision(md, d);
+    return;
+  }
+  forward_rows<NV>(md, d);
   solve<NV>(md, d);
 }
 
@@ -3530,15 +3543,6 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       for (int u = 0; u < md.m.nu; u++) d.ctrl[u] = sc.ctrl[p * 32 + u];
     int ns = sc.nsteps[p];
     for (int t = (p == p0 ? t0 : 0); t < ns && ok; t++) {
-      // resume snapshot: the state entering this step goes to the candidate's
-      // record (write-only, L2-resident: one record per candidate rewritten
-      // each step); if the step overflows, the schedule position completes it
-      if (resume_out) {
-        double* rec = resume_out + (size_t)i * RS;
-        for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
-        for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
-        if (lane == 0) { rec[nq + 2 * nvr] = d.time[0]; rec[nq + 2 * nvr + 8] = d.ITERS; }
-      }
       double frac = (double)t / (double)ns;
       if (lane == 0)
         for (int k = 0; k < 3; k++) d.mocap_pos[k] = ps[3 * p + k] + (pt[3 * p + k] - ps[3 * p + k]) * frac;
@@ -3565,24 +3569,34 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
       PT(8);
       make_constraints<NV>(md, d);
-      solve<NV>(md, d);
-      integrate<NV>(md, d); PT(21);
 #else
-      forward<NV>(md, d, 1);
-      integrate<NV>(md, d);
+      forward_rows<NV>(md, d);
 #endif
       if (resume_out && (uni(d.OVERFLOW) & MGS_FLAG_CAPACITY)) {
-        // capacity exceeded in this step: record where to resume and stop (the
-        // escalation re-runs from here with more capacity)
+        // capacity exceeded in this step (contacts in collision, rows in
+        // make_constraints, both before anything of the state moved): the
+        // state entering the step, the schedule position and the partial stats
+        // go to the candidate's resume record and the candidate stops (the
+        // escalation continues it from here with more capacity)
+        double* rec = resume_out + (size_t)i * RS;
+        for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
+        for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
         if (lane == 0) {
-          double* tail = resume_out + (size_t)i * RS + nq + 2 * nvr;
+          double* tail = rec + nq + 2 * nvr;
+          tail[0] = d.time[0];
           tail[1] = p; tail[2] = t; tail[3] = gstep;
           tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
+          tail[8] = d.ITERS;
         }
         ok = 0;
         fstep = -3;
         break;
       }
+      solve<NV>(md, d);
+      integrate<NV>(md, d);
+#ifdef MGS_PROFILE
+      PT(21);
+#endif
       if (uni(d.NCON) > maxcon) maxcon = uni(d.NCON);
       if (uni(d.NEFC) > maxefc) maxefc = uni(d.NEFC);
       sumcon += uni(d.NCON);
