@@ -348,6 +348,13 @@ def main():
             return m, int(((es[idx, 2] & abi.MGS["MGS_FLAG_CAPACITY"]) != 0).sum().item())
 
     pipes = [Pipe(s) for s in range(max(1, args.streams))]
+    # every step's escalation buffers allocated up front: first-touch device
+    # allocations inside the timed loop cost several % on a fresh box
+    per_pipe = -(-max(args.warmup, len(pipes), args.steps) // len(pipes))
+    for p in pipes:
+        if p.wide is not None:
+            p.esc_buffers(per_pipe)
+    torch.cuda.synchronize(dev)
     for k in range(max(args.warmup, len(pipes))):       # every pipeline (and its escalation) warmed up
         pipes[k % len(pipes)].step(k // len(pipes), False)
     torch.cuda.synchronize(dev)
