@@ -1229,20 +1229,8 @@ DEVI double cross2(const P2* o, const P2* a, const P2* b) {
   return (a->x - o->x) * (b->y - o->y) - (a->y - o->y) * (b->x - o->x);
 }
 
-DEVI int hull2d(P2* pts, int n, P2* out) {
-  for (int i = 1; i < n; i++) {
-    P2 key = pts[i];
-    int j = i - 1;
-    while (j >= 0 && (pts[j].x > key.x || (pts[j].x == key.x && pts[j].y > key.y))) {
-      pts[j + 1] = pts[j];
-      j--;
-    }
-    pts[j + 1] = key;
-  }
-  int m = 0;
-  for (int i = 0; i < n; i++)
-    if (m == 0 || pts[i].x != pts[m - 1].x || pts[i].y != pts[m - 1].y) pts[m++] = pts[i];
-  n = m;
+// monotone-chain half of hull2d on points already sorted and deduplicated
+DEVI int hull_chain(const P2* pts, int n, P2* out) {
   if (n <= 2) {
     for (int i = 0; i < n; i++) out[i] = pts[i];
     return n;
@@ -1258,6 +1246,57 @@ DEVI int hull2d(P2* pts, int n, P2* out) {
     out[k++] = pts[i];
   }
   return k - 1;
+}
+
+// hull2d's stable (x, y) insertion sort and duplicate removal, across lanes:
+// lane i ranks point i against all n (ties by index: the stable order),
+// scatters it, then keeps the first of each run of equal (x, y) with a ballot
+// compaction -- the same array the sequential code leaves.  Returns the count
+// (uniform), or -1 when a coordinate is NaN (the caller then runs hull2d).
+DEVI int sort_dedup_wave(P2* pts, int n) {
+  int lane = lane_id();
+  P2 me;
+  me.x = me.y = me.h = 0.0;
+  if (lane < n) me = pts[lane];
+  if (__ballot(lane < n && (me.x != me.x || me.y != me.y))) return -1;
+  int rank = 0;
+  for (int j = 0; j < n; j++) {
+    double xj = readlane_d(me.x, j), yj = readlane_d(me.y, j);
+    int before = (xj < me.x) || (xj == me.x && (yj < me.y || (yj == me.y && j < lane)));
+    rank += before;
+  }
+  wsync();
+  if (lane < n) pts[rank] = me;
+  wsync();
+  P2 cur, prv;
+  cur.x = cur.y = cur.h = 0.0;
+  prv = cur;
+  if (lane < n) cur = pts[lane];
+  if (lane > 0 && lane < n) prv = pts[lane - 1];
+  int keep = lane < n && (lane == 0 || cur.x != prv.x || cur.y != prv.y);
+  unsigned long long mk = __ballot(keep);
+  unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
+  int pos = __popcll(mk & lt);
+  wsync();
+  if (keep) pts[pos] = cur;
+  wsync();
+  return __popcll(mk);
+}
+
+DEVI int hull2d(P2* pts, int n, P2* out) {
+  for (int i = 1; i < n; i++) {
+    P2 key = pts[i];
+    int j = i - 1;
+    while (j >= 0 && (pts[j].x > key.x || (pts[j].x == key.x && pts[j].y > key.y))) {
+      pts[j + 1] = pts[j];
+      j--;
+    }
+    pts[j + 1] = key;
+  }
+  int m = 0;
+  for (int i = 0; i < n; i++)
+    if (m == 0 || pts[i].x != pts[m - 1].x || pts[i].y != pts[m - 1].y) pts[m++] = pts[i];
+  return hull_chain(pts, m, out);
 }
 
 DEVI P2 lerp2(const P2* a, const P2* b, double t) {
@@ -1312,6 +1351,47 @@ DEVI int clip_poly(const P2* P, int np, P2* Q, int nq, P2* buf) {
     }
     for (int i = 0; i < no; i++) Q[i] = buf[i];
     nq = no;
+  }
+  return nq;
+}
+
+// clip_poly across lanes (lanes over the clipped polygon's vertices, np
+// reference edges in order): per edge each vertex emits the entry intersection
+// and / or itself exactly as the sequential pass does, a ballot prefix places
+// them, points past K_MAXPOLY are dropped as there.  Degenerate subjects (1 or
+// 2 points) run the sequential code on lane 0.  Returns the count (uniform).
+DEVI int clip_poly_wave(const P2* P, int np, P2* Q, int nq, P2* buf) {
+  int lane = lane_id();
+  if (nq <= 2) {
+    int r = 0;
+    if (lane == 0) r = clip_poly(P, np, Q, nq, buf);
+    r = __shfl(r, 0);
+    wsync();
+    return r;
+  }
+  unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
+  for (int e = 0; e < np && nq > 0; e++) {
+    P2 a = P[e], b = P[(e + 1) % np];
+    P2 cur, prv;
+    cur.x = cur.y = cur.h = 0.0;
+    prv = cur;
+    if (lane < nq) {
+      cur = Q[lane];
+      prv = Q[(lane + nq - 1) % nq];
+    }
+    double dc = cross2(&a, &b, &cur);
+    double dp = cross2(&a, &b, &prv);
+    int e1 = lane < nq && ((dc >= 0.0 && dp < 0.0) || (dc < 0.0 && dp >= 0.0));
+    int e2 = lane < nq && dc >= 0.0;
+    unsigned long long m1 = __ballot(e1), m2 = __ballot(e2);
+    int pos = __popcll(m1 & lt) + __popcll(m2 & lt);
+    int total = __popcll(m1) + __popcll(m2);
+    if (e1 && pos < K_MAXPOLY) buf[pos] = lerp2(&prv, &cur, dp / (dp - dc));
+    if (e2 && pos + e1 < K_MAXPOLY) buf[pos + e1] = cur;
+    nq = total < K_MAXPOLY ? total : K_MAXPOLY;
+    wsync();
+    if (lane < nq) Q[lane] = buf[lane];
+    wsync();
   }
   return nq;
 }
@@ -1400,18 +1480,39 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   int na = feature(pc, 1, n, t1, t2, +1, tol, 1, fa, &s1);
   int nb = feature(pc, 2, n, t1, t2, -1, tol, 1, fb, &s2);
   PT(40);
+  const int refB = (nb >= na);
+  // sort + dedup of both feature sets across lanes (uniform counts), the
+  // monotone chains on lane 0, clipping and the depth filter across lanes
+  // (lanes over polygon vertices), selection on lane 0
+  int mr = sort_dedup_wave(refB ? fb : fa, refB ? nb : na);
+  int mi = sort_dedup_wave(refB ? fa : fb, refB ? na : nb);
+  int nr = 0, ni = 0;
   if (lane == 0) {
-    int refB = (nb >= na);
-    int nr = refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly);
-    int ni = refB ? hull2d(fa, na, inc) : hull2d(fb, nb, inc);
-    int np = 0;
-    if (nr >= 3) {
-      int nc = clip_poly(refpoly, nr, inc, ni, buf);
-      for (int i = 0; i < nc; i++) {
-        double dd = refB ? (inc[i].h - s2) : (s1 - inc[i].h);
-        if (dd > 0.0) { pts[np] = inc[i]; dep[np] = dd; np++; }
-      }
+    nr = mr >= 0 ? hull_chain(refB ? fb : fa, mr, refpoly) : (refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly));
+    ni = mi >= 0 ? hull_chain(refB ? fa : fb, mi, inc) : (refB ? hull2d(fa, na, inc) : hull2d(fb, nb, inc));
+  }
+  nr = __shfl(nr, 0);
+  ni = __shfl(ni, 0);
+  wsync();
+  int np = 0;
+  if (nr >= 3) {
+    int nc = clip_poly_wave(refpoly, nr, inc, ni, buf);
+    P2 q;
+    q.x = q.y = q.h = 0.0;
+    double dd = 0.0;
+    if (lane < nc) {
+      q = inc[lane];
+      dd = refB ? (q.h - s2) : (s1 - q.h);
     }
+    int keep = lane < nc && dd > 0.0;
+    unsigned long long mk = __ballot(keep);
+    unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
+    int pos = __popcll(mk & lt);
+    if (keep) { pts[pos] = q; dep[pos] = dd; }
+    np = __popcll(mk);
+    wsync();
+  }
+  if (lane == 0) {
     int ncmax = md.m.ncon_max;
     if (np == 0) {
       add_contact(d, ncmax, pair, g1, g2, mpos, n, t1, t2, -dn);
