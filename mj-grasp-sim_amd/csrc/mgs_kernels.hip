@@ -2191,25 +2191,31 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   PT(32);
   const int32_t *gbody = IA(md, geom_bodyid), *pcd = IA(md, pair_condim);
   const double *pfr = DA(md, pair_friction), *pmar = DA(md, pair_margin);
+  // contact rows, every contact at once: lane c places contact c's dim rows
+  // after the rows of contacts 0..c-1 (the sequential order); contacts from
+  // the first one that does not fit on are dropped with the overflow flag (the
+  // sequential loop stops there).  Then lanes over (contact, dof) pairs fill
+  // the J columns.
   int ncon = uni(d.NCON);
-  for (int c = 0; c < ncon; c++) {
-    int p = uni(d.con_pair[c]);
-    int dim = pcd[p];
-    if (d.NEFC + dim > md.m.nefc_max) {
-      if (lane == 0) d.OVERFLOW |= 2;
-      break;
-    }
-    int b1 = gbody[d.con_g1[c]], b2 = gbody[d.con_g2[c]];
-    const double* pt = d.con_pos + 3 * c;
-    const double* fr = d.con_frame + 9 * c;
-    int r = d.NEFC;
-    wsync();
-    if (lane == 0) {
-      for (int j = 0; j < dim; j++) add_row(md, d, MGS_EFC_CONTACT, j == 0 ? d.con_dist[c] : 0.0, pmar[p], dim, c);
-      for (int j = 0; j < dim; j++) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
-    }
-    wsync();
-    {
+  if (ncon > WAVE) {
+    // more contacts than lanes (wide capacities): one contact at a time
+    for (int c = 0; c < ncon; c++) {
+      int p = uni(d.con_pair[c]);
+      int dim = pcd[p];
+      if (d.NEFC + dim > md.m.nefc_max) {
+        if (lane == 0) d.OVERFLOW |= 2;
+        break;
+      }
+      int b1 = gbody[d.con_g1[c]], b2 = gbody[d.con_g2[c]];
+      const double* pt = d.con_pos + 3 * c;
+      const double* fr = d.con_frame + 9 * c;
+      int r = d.NEFC;
+      wsync();
+      if (lane == 0) {
+        for (int j = 0; j < dim; j++) add_row(md, d, MGS_EFC_CONTACT, j == 0 ? d.con_dist[c] : 0.0, pmar[p], dim, c);
+        for (int j = 0; j < dim; j++) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
+      }
+      wsync();
       int col = lane < nv ? lane : 0;
       double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
       jac_col(md, d, b1, pt, col, cjp1, cjr1);
@@ -2222,6 +2228,56 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
           J[(r + 3) * d.gs + col] = dot3(fr, dr);
         }
       }
+    }
+  } else {
+    const int ne0 = uni(d.NEFC);
+    int cp = 0, cdim = 0;
+    if (lane < ncon) {
+      cp = d.con_pair[lane];
+      cdim = pcd[cp];
+    }
+    int rc = ne0;
+    for (int j = 0; j < ncon; j++) {
+      int dj = __builtin_amdgcn_readlane(cdim, j);
+      if (j < lane) rc += dj;
+    }
+    int bad = lane < ncon && rc + cdim > md.m.nefc_max;
+    unsigned long long mb = __ballot(bad);
+    int nkeep = mb ? (__ffsll((long long)mb) - 1) : ncon;
+    if (lane < nkeep) {
+      for (int j = 0; j < cdim; j++) {
+        int r = rc + j;
+        d.efc_type[r] = MGS_EFC_CONTACT; d.efc_pos[r] = j == 0 ? d.con_dist[lane] : 0.0;
+        d.efc_margin[r] = pmar[cp]; d.efc_dim[r] = cdim; d.efc_con[r] = lane;
+        d.con_mu[5 * lane + j] = (j < cdim - 1) ? pfr[5 * cp + j] : 0.0;
+      }
+    }
+    int last = nkeep > 0 ? nkeep - 1 : 0;
+    int ne_end = nkeep > 0 ? __builtin_amdgcn_readlane(rc + cdim, last) : ne0;
+    for (int q0 = 0; q0 < nkeep * nv; q0 += WAVE) {
+      int q = q0 + lane;
+      int c = q / nv, col = q - c * nv;
+      int cs = c < nkeep ? c : nkeep - 1;
+      int r = __shfl(rc, cs), dim = __shfl(cdim, cs);
+      if (q < nkeep * nv) {
+        int b1 = gbody[d.con_g1[c]], b2 = gbody[d.con_g2[c]];
+        const double* pt = d.con_pos + 3 * c;
+        const double* fr = d.con_frame + 9 * c;
+        double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
+        jac_col(md, d, b1, pt, col, cjp1, cjr1);
+        jac_col(md, d, b2, pt, col, cjp2, cjr2);
+        double dp[3] = {cjp2[0] - cjp1[0], cjp2[1] - cjp1[1], cjp2[2] - cjp1[2]};
+        for (int j = 0; j < dim && j < 3; j++) J[(r + j) * d.gs + col] = dot3(fr + 3 * j, dp);
+        if (dim >= 4) {
+          double dr[3] = {cjr2[0] - cjr1[0], cjr2[1] - cjr1[1], cjr2[2] - cjr1[2]};
+          J[(r + 3) * d.gs + col] = dot3(fr, dr);
+        }
+      }
+    }
+    wsync();
+    if (lane == 0) {
+      d.NEFC = ne_end;
+      if (nkeep < ncon) d.OVERFLOW |= 2;
     }
   }
   wsync();
