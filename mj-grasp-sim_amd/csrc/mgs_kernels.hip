@@ -3477,6 +3477,30 @@ DEVI void solve(const Mdl& md, Dat& d) {
 }
 
 // ---------------------------------------------------------------------------
+// M survives the step in the unused tail of the G rows (rows >= nefc are never
+// read), so integrate need not recompute it: the copy sits in the last nv*nv
+// doubles of the G slot, clear of the dynamics-stage views that share U with G,
+// and is valid while the step's rows stay below it.  The wide build (G in HBM)
+// recomputes.
+template <int NV>
+DEVI double* m_copy_slot(const Mdl& md, const Dat& d) {
+#ifdef MGS_G_GLOBAL
+  return nullptr;
+#else
+  const int nv = md.m.nv;
+  const int tail0 = md.m.nefc_max * GS - nv * NV;
+  const int dyn_end = 6 * (3 * md.m.nbody + nv) + 3 * nv;
+  return tail0 >= dyn_end ? d.G + tail0 : nullptr;
+#endif
+}
+template <int NV>
+DEVI void save_M(const Mdl& md, Dat& d) {
+  double* mc = m_copy_slot<NV>(md, d);
+  if (!mc) return;
+  for (int k = lane_id(); k < md.m.nv * NV; k += WAVE) mc[k] = d.M[k];
+  wsync();
+}
+
 // mj_forward up to the constraint rows (everything before the solver): a
 // candidate whose contacts / rows overflow here still holds the state entering
 // the step (qpos, qvel, qacc_warmstart, time change only in solve / integrate)
@@ -3487,6 +3511,7 @@ DEVI void forward_rows(const Mdl& md, Dat& d) {
   com_pos(md, d);
   collision(md, d);
   crb(md, d);
+  save_M<NV>(md, d);
   ldl_factor<NV>(d.M, d.Dv, d.Dinv);
   for (int k = lane; k < nv; k += WAVE) {
     double sd = sqrt(d.Dv[k]);
@@ -3518,8 +3543,17 @@ template <int NV>
 DEVI void integrate(const Mdl& md, Dat& d) {
   int nv = md.m.nv, lane = lane_id();
   double dt = md.m.timestep;
-  // recompute M (it was factored in place), then MI = M - dt*qDeriv
-  crb(md, d);
+  // M (factored in place by forward): from its copy in the G tail when the
+  // step's rows left it intact, else recomputed; then MI = M - dt*qDeriv
+  {
+    const double* mc = m_copy_slot<NV>(md, d);
+    if (mc && uni(d.NEFC) * GS <= (int)(mc - d.G)) {
+      for (int k = lane; k < nv * NV; k += WAVE) d.M[k] = mc[k];
+      wsync();
+    } else {
+      crb(md, d);
+    }
+  }
   PT(19);
   // M - dt * qDeriv, lane i forms row i of qDeriv (-damping on the diagonal,
   // then each active affine actuator's mom_i (mom_j dv) in actuator order) and
@@ -3712,6 +3746,7 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       wsync(); PT(2);
       collision(md, d); PT(5);
       crb(md, d); PT(6);
+      save_M<NV>(md, d);
       ldl_factor<NV>(d.M, d.Dv, d.Dinv);
       for (int k = lane; k < md.m.nv; k += WAVE) { double sd = sqrt(d.Dv[k]); d.sD[k] = sd; d.isD[k] = 1.0 / sd; }
       wsync(); PT(7);
