@@ -2054,6 +2054,132 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   wsync();
   const int32_t *et = IA(md, eq_type), *eo1 = IA(md, eq_obj1id), *eo2 = IA(md, eq_obj2id);
   const double* ed = DA(md, eq_data);
+  if (md.m.neq <= WAVE) {
+    // every equality at once.  Lane e: its rows' place (connect 3, weld 6,
+    // joint 1, in equality order) and values; the kept set is what the
+    // sequential loop below keeps: it stops at the first equality whose rows
+    // do not fit (flagging the overflow), and after the first row-producing
+    // one when the row-overflow flag is already up.  Then lanes over
+    // (equality, dof) fill the J columns with the sequential expressions.
+    const int neq = md.m.neq;
+    const int32_t *jqa = IA(md, jnt_qposadr), *jda = IA(md, jnt_dofadr);
+    int typ = -1, need = 0;
+    if (lane < neq) {
+      typ = et[lane];
+      need = typ == MGS_EQ_CONNECT ? 3 : typ == MGS_EQ_WELD ? 6 : typ == MGS_EQ_JOINT ? 1 : 0;
+    }
+    int re = 0;
+    for (int j = 0; j < neq; j++) {
+      int nj = __builtin_amdgcn_readlane(need, j);
+      if (j < lane) re += nj;
+    }
+    unsigned long long mprod = __ballot(need > 0);
+    unsigned long long mbad = __ballot(need > 0 && re + need > md.m.nefc_max);
+    int ebad = mbad ? __ffsll((long long)mbad) - 1 : neq;
+    int nkeep = ebad;
+    if ((uni(d.OVERFLOW) & 2) && mprod) {
+      int efirst = __ffsll((long long)mprod) - 1;
+      if (efirst + 1 < nkeep) nkeep = efirst + 1;
+    }
+    if (lane < nkeep && need > 0) {
+      const double* data = ed + 11 * lane;
+      if (typ == MGS_EQ_JOINT) {
+        int j1 = eo1[lane], j2 = eo2[lane];
+        double q1 = d.qpos[jqa[j1]] - data[5];
+        double pos;
+        if (j2 >= 0) {
+          double x = d.qpos[jqa[j2]] - data[6];
+          double poly = data[0] + x * (data[1] + x * (data[2] + x * (data[3] + x * data[4])));
+          pos = q1 - poly;
+        } else {
+          pos = q1 - data[0];
+        }
+        d.efc_type[re] = MGS_EFC_EQUALITY; d.efc_pos[re] = pos; d.efc_margin[re] = 0.0;
+        d.efc_dim[re] = 1; d.efc_con[re] = lane;
+      } else {
+        int b1 = eo1[lane], b2 = eo2[lane];
+        double p1[3], p2[3], t[3];
+        mulmv3(t, d.xmat + 9 * b1, data);
+        add3(p1, d.xpos + 3 * b1, t);
+        if (typ == MGS_EQ_CONNECT) {
+          mulmv3(t, d.xmat + 9 * b2, data + 3);
+          add3(p2, d.xpos + 3 * b2, t);
+        } else {
+          p2[0] = d.xpos[3 * b2]; p2[1] = d.xpos[3 * b2 + 1]; p2[2] = d.xpos[3 * b2 + 2];
+        }
+        for (int k = 0; k < 3; k++) {
+          d.efc_type[re + k] = MGS_EFC_EQUALITY; d.efc_pos[re + k] = p1[k] - p2[k]; d.efc_margin[re + k] = 0.0;
+          d.efc_dim[re + k] = 1; d.efc_con[re + k] = lane;
+        }
+        if (typ == MGS_EQ_WELD) {
+          double q1r[4], q2c[4], qe[4];
+          quatmul(q1r, d.xquat + 4 * b1, data + 3);
+          q2c[0] = d.xquat[4 * b2]; q2c[1] = -d.xquat[4 * b2 + 1];
+          q2c[2] = -d.xquat[4 * b2 + 2]; q2c[3] = -d.xquat[4 * b2 + 3];
+          quatmul(qe, q2c, q1r);
+          double ts = data[7];
+          for (int k = 0; k < 3; k++) {
+            d.efc_type[re + 3 + k] = MGS_EFC_EQUALITY; d.efc_pos[re + 3 + k] = qe[1 + k] * ts;
+            d.efc_margin[re + 3 + k] = 0.0; d.efc_dim[re + 3 + k] = 1; d.efc_con[re + 3 + k] = lane;
+          }
+        }
+      }
+    }
+    int last = nkeep > 0 ? nkeep - 1 : 0;
+    int ne_eq = nkeep > 0 ? __builtin_amdgcn_readlane(re + need, last) : 0;
+    for (int q0 = 0; q0 < nkeep * nv; q0 += WAVE) {
+      int q = q0 + lane;
+      int e = q / nv, col = q - e * nv;
+      int es = e < nkeep ? e : nkeep - 1;
+      int r = __shfl(re, es), ty = __shfl(typ, es);
+      if (q < nkeep * nv && ty >= 0) {
+        const double* data = ed + 11 * e;
+        if (ty == MGS_EQ_JOINT) {
+          int j1 = eo1[e], j2 = eo2[e];
+          double v = (col == jda[j1]) ? 1.0 : 0.0;
+          if (j2 >= 0 && col == jda[j2]) {
+            double x = d.qpos[jqa[j2]] - data[6];
+            double deriv = data[1] + x * (2.0 * data[2] + x * (3.0 * data[3] + x * (4.0 * data[4])));
+            v = v - deriv;
+          }
+          J[r * d.gs + col] = v;
+        } else if (ty == MGS_EQ_CONNECT || ty == MGS_EQ_WELD) {
+          int b1 = eo1[e], b2 = eo2[e];
+          double p1[3], p2[3], t[3];
+          mulmv3(t, d.xmat + 9 * b1, data);
+          add3(p1, d.xpos + 3 * b1, t);
+          if (ty == MGS_EQ_CONNECT) {
+            mulmv3(t, d.xmat + 9 * b2, data + 3);
+            add3(p2, d.xpos + 3 * b2, t);
+          } else {
+            p2[0] = d.xpos[3 * b2]; p2[1] = d.xpos[3 * b2 + 1]; p2[2] = d.xpos[3 * b2 + 2];
+          }
+          double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
+          jac_col(md, d, b1, p1, col, cjp1, cjr1);
+          jac_col(md, d, b2, p2, col, cjp2, cjr2);
+          for (int k = 0; k < 3; k++) J[(r + k) * d.gs + col] = cjp1[k] - cjp2[k];
+          if (ty == MGS_EQ_WELD) {
+            double q1r[4], q2c[4];
+            quatmul(q1r, d.xquat + 4 * b1, data + 3);
+            q2c[0] = d.xquat[4 * b2]; q2c[1] = -d.xquat[4 * b2 + 1];
+            q2c[2] = -d.xquat[4 * b2 + 2]; q2c[3] = -d.xquat[4 * b2 + 3];
+            double ts = data[7];
+            double ax[4] = {0.0, cjr1[0] - cjr2[0], cjr1[1] - cjr2[1], cjr1[2] - cjr2[2]};
+            double t1q[4], t2q[4];
+            quatmul(t1q, q2c, ax);
+            quatmul(t2q, t1q, q1r);
+            for (int k = 0; k < 3; k++) J[(r + 3 + k) * d.gs + col] = (0.5 * t2q[1 + k]) * ts;
+          }
+        }
+      }
+    }
+    wsync();
+    if (lane == 0) {
+      d.NEFC = ne_eq;
+      if (ebad < neq) d.OVERFLOW |= 2;
+    }
+    wsync();
+  } else
   for (int e = 0; e < md.m.neq; e++) {
     const double* data = ed + 11 * e;
     if (et[e] == MGS_EQ_CONNECT || et[e] == MGS_EQ_WELD) {
