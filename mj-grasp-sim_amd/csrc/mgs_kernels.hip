@@ -2056,11 +2056,10 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   const double* ed = DA(md, eq_data);
   if (md.m.neq <= WAVE) {
     // every equality at once.  Lane e: its rows' place (connect 3, weld 6,
-    // joint 1, in equality order) and values; the kept set is what the
-    // sequential loop below keeps: it stops at the first equality whose rows
-    // do not fit (flagging the overflow), and after the first row-producing
-    // one when the row-overflow flag is already up.  Then lanes over
-    // (equality, dof) fill the J columns with the sequential expressions.
+    // joint 1, in equality order) and values; the kept set is the oracle's
+    // (make_constraints): equalities before the first one whose rows do not
+    // fit, which flags the overflow.  Then lanes over (equality, dof) fill the
+    // J columns with the sequential expressions.
     const int neq = md.m.neq;
     const int32_t *jqa = IA(md, jnt_qposadr), *jda = IA(md, jnt_dofadr);
     int typ = -1, need = 0;
@@ -2073,14 +2072,9 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       int nj = __builtin_amdgcn_readlane(need, j);
       if (j < lane) re += nj;
     }
-    unsigned long long mprod = __ballot(need > 0);
     unsigned long long mbad = __ballot(need > 0 && re + need > md.m.nefc_max);
     int ebad = mbad ? __ffsll((long long)mbad) - 1 : neq;
     int nkeep = ebad;
-    if ((uni(d.OVERFLOW) & 2) && mprod) {
-      int efirst = __ffsll((long long)mprod) - 1;
-      if (efirst + 1 < nkeep) nkeep = efirst + 1;
-    }
     if (lane < nkeep && need > 0) {
       const double* data = ed + 11 * lane;
       if (typ == MGS_EQ_JOINT) {
@@ -2195,12 +2189,15 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         add3(p1, d.xpos + 3 * b1, t);
         p2[0] = d.xpos[3 * b2]; p2[1] = d.xpos[3 * b2 + 1]; p2[2] = d.xpos[3 * b2 + 2];
       }
-      if (lane == 0) {
-        if (d.NEFC + (et[e] == MGS_EQ_WELD ? 6 : 3) > md.m.nefc_max) d.OVERFLOW |= 2;
-        else for (int k = 0; k < 3; k++) add_row(md, d, MGS_EFC_EQUALITY, p1[k] - p2[k], 0.0, 1, e);
+      // this equality's rows do not fit: flag and stop (the oracle's rule; a
+      // flag left from an earlier step does not stop the loop)
+      if (uni(d.NEFC) + (et[e] == MGS_EQ_WELD ? 6 : 3) > md.m.nefc_max) {
+        if (lane == 0) d.OVERFLOW |= 2;
+        break;
       }
+      if (lane == 0)
+        for (int k = 0; k < 3; k++) add_row(md, d, MGS_EFC_EQUALITY, p1[k] - p2[k], 0.0, 1, e);
       wsync();
-      if (d.OVERFLOW & 2) break;
       int r0 = d.NEFC - 3;
       double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
       int col = lane < nv ? lane : 0;
@@ -2242,12 +2239,12 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       } else {
         pos = q1 - data[0];
       }
-      if (lane == 0) {
-        if (d.NEFC + 1 > md.m.nefc_max) d.OVERFLOW |= 2;
-        else add_row(md, d, MGS_EFC_EQUALITY, pos, 0.0, 1, e);
+      if (uni(d.NEFC) + 1 > md.m.nefc_max) {
+        if (lane == 0) d.OVERFLOW |= 2;
+        break;
       }
+      if (lane == 0) add_row(md, d, MGS_EFC_EQUALITY, pos, 0.0, 1, e);
       wsync();
-      if (d.OVERFLOW & 2) break;
       int r = d.NEFC - 1;
       for (int c = lane; c < nv; c += WAVE) J[r * d.gs + c] = 0.0;
       wsync();

@@ -378,3 +378,22 @@ def test_static_layout_kernel_matches_runtime_layout(env, eng, candidates):
     assert ok.sum() > 0.9 * len(idx)
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(a[k][ok], b[k][ok]), k
+
+
+@pytest.mark.parametrize("nefc_max", [10, 16, 40])
+def test_row_capacity_overflow_parity(env, candidates, nefc_max):
+    """Constraint-row capacities below the equality rows (10 < 13), just above
+    them (16) and mid-range (40): which equality / friction / limit / contact
+    rows are kept, the overflow flags, and everything downstream match the
+    oracle at the same capacity (the kernel places equality and contact rows for
+    all of them at once; the oracle appends them one by one)."""
+    from conftest import plan_for
+    from mgs.core.engine import Engine
+    from oracle import oracle as O
+    poses, J = candidates
+    plan = plan_for(env, poses[:40], J[:40])
+    e = Engine(env.model, ncon_max=8, nefc_max=nefc_max)
+    om = O.OracleModel(env.model, ncon_max=8, nefc_max=nefc_max)
+    rg, ro = e.rollout(plan), om.rollout(plan, nthreads=8)
+    _assert_same(rg, ro, f"nefc_max={nefc_max}")
+    assert (rg["stats"][:, 2] & 2).any()
