@@ -3102,6 +3102,76 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const dou
   return tot;
 }
 
+// newton_eval at two points in one pass over the rows: c0 at wa (cost only:
+// its violations go to the idle scratch slot, nothing else is stored), c1 at
+// wb with every side effect of newton_eval(wb).  Same arithmetic per cost as
+// two newton_eval calls; the row loads and the latency chains are shared.
+template <int NV>
+DEVI void newton_eval_pair(const Mdl& md, Dat& d, const double* wa, const double* wb, int P, const double* mupR,
+                           const double* k1R, double& c0, double& c1) {
+  int ne = uni(d.NEFC), lane = lane_id();
+  PCNT(37, 2);
+  double qa = (lane < NV) ? wa[lane] - d.nw0[lane] : 0.0;
+  double qb = (lane < NV) ? wb[lane] - d.nw0[lane] : 0.0;
+  double gauss0 = 0.5 * tree_sum(qa * qa, P);
+  double gauss1 = 0.5 * tree_sum(qb * qb, P);
+  double* jar0 = d.scratch;   // idle until the first Newton Hessian
+#if MGS_REG_ROWS
+  double ra[NV], rb[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) { ra[k] = wa[k]; rb[k] = wb[k]; }
+#else
+  const double *ra = wa, *rb = wb;
+#endif
+  for (int r = lane; r < ne; r += WAVE) {
+    const double* Gr = d.G + r * GS;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+      double g = Gr[k];
+      s0 = __builtin_fma(g, ra[k], s0);
+      s1 = __builtin_fma(g, rb[k], s1);
+    }
+    jar0[r] = s0 - d.efc_aref[r];
+    d.efc_jar[r] = s1 - d.efc_aref[r];
+  }
+  wsync();
+  double cr0[MGS_RPL], cr1[MGS_RPL];
+#pragma unroll
+  for (int h = 0; h < MGS_RPL; h++) {
+    cr0[h] = 0.0;
+    cr1[h] = 0.0;
+    int r = lane + h * WAVE;
+    if (r < ne && efc_lead(d, r)) {
+      int t = d.efc_type[r];
+      int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
+      double jr[4], f[4], hb[16];
+      int st = ST_OFF;
+#pragma unroll
+      for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? jar0[r + a] : 0.0;
+      cr0[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true, mupR[h], k1R[h]);
+      st = ST_OFF;
+#pragma unroll
+      for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
+      cr1[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true, mupR[h], k1R[h]);
+#pragma unroll
+      for (int a = 0; a < 4; a++)
+        if (a < dim) { d.efc_f[r + a] = f[a]; d.efc_state[r + a] = st; }
+      if (st == ST_CONE) {
+        double* o = d.con_hb + 16 * d.efc_con[r];
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (a < dim && b < dim) o[a * dim + b] = hb[a * 4 + b];
+      }
+    }
+  }
+  c0 = gauss0 + tree_rows(cr0, ne);
+  c1 = gauss1 + tree_rows(cr1, ne);
+  wsync();
+}
+
 // g = (w - w0) - G^T f   (lanes over dofs, rows summed in order)
 template <int NV>
 DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
@@ -3465,8 +3535,8 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   if (ne > 0) {
     // (oracle: evaluate warmstart, smooth, keep the cheaper; evaluating the
     // smooth point first leaves the warmstart's rows current in the common case)
-    double c0 = newton_eval<NV>(md, d, d.nw0, P, mupR, k1R);
-    double cws = newton_eval<NV>(md, d, d.nw, P, mupR, k1R);
+    double c0, cws;
+    newton_eval_pair<NV>(md, d, d.nw0, d.nw, P, mupR, k1R, c0, cws);
     if (cws < c0) {
       C = cws;
     } else {
