@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 11
+#define MGS_ABI_VERSION 12
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -189,7 +189,7 @@ typedef struct mgs_model_desc {
   /* convex hulls */
   int32_t i_hull_vertadr;
   int32_t i_hull_vertnum;
-  int32_t d_hull_vert;      /* 3 * nhullvert, in geom frame */
+  int32_t d_hull_vert;      /* 3 * nhullvert, in geom frame; per hull x[n], y[n], z[n] */
   int32_t d_hull_center;    /* 3 * nhull, interior point (vertex centroid) */
   /* admissible pairs with mixed contact parameters */
   int32_t i_pair_geom1;

@@ -916,7 +916,7 @@ DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   for (int k = 0; k < 9; k++) { c.R1[k] = d.geom_xmat[9 * g1 + k]; c.R2[k] = d.geom_xmat[9 * g2 + k]; }
   for (int k = 0; k < 3; k++) { c.x1[k] = d.geom_xpos[3 * g1 + k]; c.x2[k] = d.geom_xpos[3 * g2 + k]; }
   int i1 = (lane < c.n1) ? lane : 0, i2 = (lane < c.n2) ? lane : 0;
-  for (int k = 0; k < 3; k++) { c.c1[k] = c.V1[3 * i1 + k]; c.c2[k] = c.V2[3 * i2 + k]; }
+  for (int k = 0; k < 3; k++) { c.c1[k] = c.V1[k * c.n1 + i1]; c.c2[k] = c.V2[k * c.n2 + i2]; }
   c.r1 = DA(md, geom_radius)[g1];
   c.r2 = DA(md, geom_radius)[g2];
 }
@@ -940,7 +940,7 @@ DEVI void sup_load(SupChunk& c, const double* V, int n, int base) {
   for (int u = 0; u < SUP_CH; u++) {
     int i = base + u * WAVE + lane;
     int ii = i < n ? i : 0;
-    c.x[u] = V[3 * ii]; c.y[u] = V[3 * ii + 1]; c.z[u] = V[3 * ii + 2];
+    c.x[u] = V[ii]; c.y[u] = V[n + ii]; c.z[u] = V[2 * n + ii];
   }
 }
 DEVI void sup_take_chunk(SupAcc& a, const SupChunk& c, int n, int base, const double* dl) {
@@ -1204,7 +1204,7 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
     int pred = 0;
     if (i < num) {
       if (num <= WAVE) { vx = cv[0]; vy = cv[1]; vz = cv[2]; }
-      else { vx = V[3 * i]; vy = V[3 * i + 1]; vz = V[3 * i + 2]; }
+      else { vx = V[i]; vy = V[num + i]; vz = V[2 * num + i]; }
       s = base + ((vx * nl[0] + vy * nl[1]) + vz * nl[2]);
       pred = sign > 0 ? (s >= lim) : (s <= lim);
     }
@@ -1245,6 +1245,54 @@ DEVI int hull_chain(const P2* pts, int n, P2* out) {
     while (k >= lo && cross2(&out[k - 2], &out[k - 1], &pts[i]) <= 0.0) k--;
     out[k++] = pts[i];
   }
+  return k - 1;
+}
+
+// hull_chain with the stack held across lanes (lane k keeps out[k] in
+// registers) and the points broadcast from their lanes: the same pushes, pops
+// and cross2 tests as the sequential loop, in the same order, but every access
+// is a readlane instead of a dependent LDS round trip.  All lanes run it
+// (uniform k); n <= K_MAXF, so the stack (< 2n entries) fits one wave.
+DEVI int hull_chain_wave(const P2* pts, int n, P2* out) {
+  int lane = lane_id();
+  P2 me;
+  me.x = me.y = me.h = 0.0;
+  if (lane < n) me = pts[lane];
+  if (n <= 2) {
+    if (lane < n) out[lane] = me;
+    return n;
+  }
+  P2 st;
+  st.x = st.y = st.h = 0.0;
+  int k = 0;
+  for (int i = 0; i < n; i++) {
+    P2 b;
+    b.x = readlane_d(me.x, i); b.y = readlane_d(me.y, i); b.h = readlane_d(me.h, i);
+    while (k >= 2) {
+      P2 o, a;
+      o.x = readlane_d(st.x, k - 2); o.y = readlane_d(st.y, k - 2);
+      a.x = readlane_d(st.x, k - 1); a.y = readlane_d(st.y, k - 1);
+      if (cross2(&o, &a, &b) <= 0.0) k--;
+      else break;
+    }
+    if (lane == k) st = b;
+    k++;
+  }
+  int lo = k + 1;
+  for (int i = n - 2; i >= 0; i--) {
+    P2 b;
+    b.x = readlane_d(me.x, i); b.y = readlane_d(me.y, i); b.h = readlane_d(me.h, i);
+    while (k >= lo) {
+      P2 o, a;
+      o.x = readlane_d(st.x, k - 2); o.y = readlane_d(st.y, k - 2);
+      a.x = readlane_d(st.x, k - 1); a.y = readlane_d(st.y, k - 1);
+      if (cross2(&o, &a, &b) <= 0.0) k--;
+      else break;
+    }
+    if (lane == k) st = b;
+    k++;
+  }
+  if (lane < k) out[lane] = st;
   return k - 1;
 }
 
@@ -1482,17 +1530,21 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   PT(40);
   const int refB = (nb >= na);
   // sort + dedup of both feature sets across lanes (uniform counts), the
-  // monotone chains on lane 0, clipping and the depth filter across lanes
-  // (lanes over polygon vertices), selection on lane 0
+  // monotone chains with a lane-held stack, clipping and the depth filter
+  // across lanes (lanes over polygon vertices), selection on lane 0
   int mr = sort_dedup_wave(refB ? fb : fa, refB ? nb : na);
   int mi = sort_dedup_wave(refB ? fa : fb, refB ? na : nb);
-  int nr = 0, ni = 0;
-  if (lane == 0) {
-    nr = mr >= 0 ? hull_chain(refB ? fb : fa, mr, refpoly) : (refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly));
-    ni = mi >= 0 ? hull_chain(refB ? fa : fb, mi, inc) : (refB ? hull2d(fa, na, inc) : hull2d(fb, nb, inc));
+  int nr = mr >= 0 ? hull_chain_wave(refB ? fb : fa, mr, refpoly) : -1;
+  int ni = mi >= 0 ? hull_chain_wave(refB ? fa : fb, mi, inc) : -1;
+  if (nr < 0 || ni < 0) {   // a NaN coordinate: the sequential hull2d on lane 0
+    wsync();
+    if (lane == 0) {
+      if (nr < 0) nr = refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly);
+      if (ni < 0) ni = refB ? hull2d(fa, na, inc) : hull2d(fb, nb, inc);
+    }
+    nr = __shfl(nr, 0);
+    ni = __shfl(ni, 0);
   }
-  nr = __shfl(nr, 0);
-  ni = __shfl(ni, 0);
   wsync();
   int np = 0;
   if (nr >= 3) {

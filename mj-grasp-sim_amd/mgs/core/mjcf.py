@@ -1094,7 +1094,11 @@ class CompiledModel:
             put_d(n, getattr(self, n))
         put_i("hull_vertadr", self.hull_vertadr)
         put_i("hull_vertnum", self.hull_vertnum)
-        put_d("hull_vert", self.hull_vert)
+        # per hull x[n], y[n], z[n] (SoA): the kernels' support scans then read
+        # 64 consecutive doubles per load instead of a 24-byte stride
+        put_d("hull_vert", np.concatenate([self.hull_vert[a:a + n].T.ravel()
+                                           for a, n in zip(self.hull_vertadr, self.hull_vertnum)])
+              if len(self.hull_vertnum) else self.hull_vert)
         put_d("hull_center", self.hull_center)
         for n in ["pair_geom1", "pair_geom2", "pair_condim", "pair_kind"]:
             put_i(n, getattr(self, n))

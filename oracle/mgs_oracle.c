@@ -642,11 +642,11 @@ static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, d
   double best = -INFINITY;
   int bi = 0;
   for (int i = 0; i < num; i++) {
-    double s = (V[3 * i] * dl[0] + V[3 * i + 1] * dl[1]) + V[3 * i + 2] * dl[2];
+    double s = (V[i] * dl[0] + V[num + i] * dl[1]) + V[2 * num + i] * dl[2];
     if (s > best) { best = s; bi = i; }
   }
-  double t[3];
-  mulmv3(t, R, V + 3 * bi);
+  double t[3], vb[3] = {V[bi], V[num + bi], V[2 * num + bi]};
+  mulmv3(t, R, vb);
   add3(out, d->geom_xpos + 3 * g, t);
   /* rounded geoms (sphere, capsule): hull (+) ball; dir is a unit vector */
   double r = DA(md, geom_radius)[g];
@@ -824,17 +824,17 @@ static int feature(const Mdl* md, const Dat* d, int g, const double* n, const do
   if (r > 0.0) base = (sign > 0) ? base + r : base - r;   /* rounded: surface = hull (+) ball */
   double best = (sign > 0) ? -INFINITY : INFINITY;
   for (int i = 0; i < num; i++) {
-    double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
+    double s = base + ((V[i] * nl[0] + V[num + i] * nl[1]) + V[2 * num + i] * nl[2]);
     if (sign > 0 ? (s > best) : (s < best)) best = s;
   }
   *ext = best;
   int cnt = 0;
   double lim = (sign > 0) ? best - tol : best + tol;
   for (int i = 0; i < num && cnt < O_MAXF; i++) {
-    double s = base + ((V[3 * i] * nl[0] + V[3 * i + 1] * nl[1]) + V[3 * i + 2] * nl[2]);
+    double s = base + ((V[i] * nl[0] + V[num + i] * nl[1]) + V[2 * num + i] * nl[2]);
     if (sign > 0 ? (s >= lim) : (s <= lim)) {
-      double t[3], P[3];
-      mulmv3(t, R, V + 3 * i);
+      double t[3], P[3], vi[3] = {V[i], V[num + i], V[2 * num + i]};
+      mulmv3(t, R, vi);
       add3(P, x, t);
       out[cnt].x = dot3(P, t1);
       out[cnt].y = dot3(P, t2);
