@@ -1418,15 +1418,26 @@ DEVI int clip_poly_wave(const P2* P, int np, P2* Q, int nq, P2* buf) {
     return r;
   }
   unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
+  // the reference polygon across lanes (np <= K_MAXPOLY < WAVE): its edges are
+  // readlane broadcasts; the clipped polygon stays in registers (cur, prv)
+  // between edges and only the compaction goes through LDS, ping-ponging
+  // between buf and Q
+  P2 pe;
+  pe.x = pe.y = pe.h = 0.0;
+  if (lane < np) pe = P[lane];
+  P2 cur, prv;
+  cur.x = cur.y = cur.h = 0.0;
+  prv = cur;
+  if (lane < nq) {
+    cur = Q[lane];
+    prv = Q[(lane + nq - 1) % nq];
+  }
+  P2* out = buf;
   for (int e = 0; e < np && nq > 0; e++) {
-    P2 a = P[e], b = P[(e + 1) % np];
-    P2 cur, prv;
-    cur.x = cur.y = cur.h = 0.0;
-    prv = cur;
-    if (lane < nq) {
-      cur = Q[lane];
-      prv = Q[(lane + nq - 1) % nq];
-    }
+    int en = (e + 1) % np;
+    P2 a, b;
+    a.x = readlane_d(pe.x, e); a.y = readlane_d(pe.y, e); a.h = 0.0;
+    b.x = readlane_d(pe.x, en); b.y = readlane_d(pe.y, en); b.h = 0.0;
     double dc = cross2(&a, &b, &cur);
     double dp = cross2(&a, &b, &prv);
     int e1 = lane < nq && ((dc >= 0.0 && dp < 0.0) || (dc < 0.0 && dp >= 0.0));
@@ -1434,13 +1445,22 @@ DEVI int clip_poly_wave(const P2* P, int np, P2* Q, int nq, P2* buf) {
     unsigned long long m1 = __ballot(e1), m2 = __ballot(e2);
     int pos = __popcll(m1 & lt) + __popcll(m2 & lt);
     int total = __popcll(m1) + __popcll(m2);
-    if (e1 && pos < K_MAXPOLY) buf[pos] = lerp2(&prv, &cur, dp / (dp - dc));
-    if (e2 && pos + e1 < K_MAXPOLY) buf[pos + e1] = cur;
+    // out was last read two edges ago, before the previous edge's barrier
+    if (e1 && pos < K_MAXPOLY) out[pos] = lerp2(&prv, &cur, dp / (dp - dc));
+    if (e2 && pos + e1 < K_MAXPOLY) out[pos + e1] = cur;
     nq = total < K_MAXPOLY ? total : K_MAXPOLY;
     wsync();
-    if (lane < nq) Q[lane] = buf[lane];
-    wsync();
+    if (lane < nq) {
+      cur = out[lane];
+      prv = out[(lane + nq - 1) % nq];
+    }
+    out = (out == buf) ? Q : buf;
   }
+  if (out == Q) {   // the last compaction went to buf: the caller reads Q
+    wsync();
+    if (lane < nq) Q[lane] = cur;
+  }
+  wsync();
   return nq;
 }
 
