@@ -1554,6 +1554,7 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   // across lanes (lanes over polygon vertices), selection on lane 0
   int mr = sort_dedup_wave(refB ? fb : fa, refB ? nb : na);
   int mi = sort_dedup_wave(refB ? fa : fb, refB ? na : nb);
+  PT(47);
   int nr = mr >= 0 ? hull_chain_wave(refB ? fb : fa, mr, refpoly) : -1;
   int ni = mi >= 0 ? hull_chain_wave(refB ? fa : fb, mi, inc) : -1;
   if (nr < 0 || ni < 0) {   // a NaN coordinate: the sequential hull2d on lane 0
@@ -1566,6 +1567,7 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
     ni = __shfl(ni, 0);
   }
   wsync();
+  PT(48);
   int np = 0;
   if (nr >= 3) {
     int nc = clip_poly_wave(refpoly, nr, inc, ni, buf);
@@ -1584,6 +1586,7 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
     np = __popcll(mk);
     wsync();
   }
+  PT(49);
   if (lane == 0) {
     int ncmax = md.m.ncon_max;
     if (np == 0) {

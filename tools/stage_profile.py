@@ -10,13 +10,15 @@ NAMES = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll:
          'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
          'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
          'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne',
-         'coll: big-hull support calls', 'coll: feature passes', 'coll: clip+select (lane 0)',
-         'noslip/pgs block: residual', 'noslip/pgs block: qcqp', 'noslip/pgs block: update']
+         'coll: big-hull support calls', 'coll: feature passes', 'coll: select4+add (lane 0)',
+         'noslip/pgs block: residual', 'noslip/pgs block: qcqp', 'noslip/pgs block: update',
+         'coll: sort+dedup', 'coll: hull chains', 'coll: clip+depth filter']
 
 
 def report(buf, r, ncand, horizon):
     v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64),
-                        np.array(buf[39:45], dtype=np.float64)])
+                        np.array(buf[39:45], dtype=np.float64),
+                        np.array(buf[47:50], dtype=np.float64)])
     cnt = np.array(buf[26:31], dtype=np.float64)
     tot = v.sum()
     print('N=%d candidates, kernel %.1f ms, labels %d, overflow %d' % (
