@@ -854,40 +854,45 @@ struct SupAcc {
   int bi;
 };
 DEVI void sup_init(SupAcc& a) { a.best = -INFINITY; a.bi = 0x7fffffff; a.vx = a.vy = a.vz = 0.0; }
-DEVI void sup_take(SupAcc& a, double ob, int oi) {
-  if (ob > a.best || (ob == a.best && oi < a.bi)) { a.best = ob; a.bi = oi; }
-}
-DEVI void sup_dpp_level(SupAcc& a, int sel) {
-  double ob = dpp_d(a.best, sel);
-  int oi;
-  switch (sel) {
-    case 0: oi = __builtin_amdgcn_mov_dpp(a.bi, 0xB1, 0xF, 0xF, false); break;
-    case 1: oi = __builtin_amdgcn_mov_dpp(a.bi, 0x4E, 0xF, 0xF, false); break;
-    case 2: oi = __builtin_amdgcn_mov_dpp(a.bi, 0x141, 0xF, 0xF, false); break;
-    default: oi = __builtin_amdgcn_mov_dpp(a.bi, 0x140, 0xF, 0xF, false); break;
-  }
-  sup_take(a, ob, oi);
-}
 // reduce and return the winning local-frame vertex (uniform).  Only lanes
 // < min(n, 64) hold candidates, so the reduction stops at the smallest power of
-// two covering them (8-vertex boxes: three DPP levels and one readlane).
+// two covering them (8-vertex boxes: three DPP levels).  The value alone is
+// reduced (one v_max_f64 per DPP level; lane values are never NaN: they only
+// change on a strict '>'), then the lanes holding it are found with a ballot
+// and the smallest vertex index among them wins -- the (value, index) order of
+// the oracle's ascending scan.  Lane l holds vertices l, l+64, ..., so for a
+// hull of <= 64 vertices the lowest tied lane is the answer; larger hulls
+// compare the tied lanes' indices (exact ties only).
 DEVI void sup_finish(SupAcc& a, double* v, int n) {
   int P = n < WAVE ? next_pow2(n) : WAVE;
-  if (P > 1) sup_dpp_level(a, 0);
-  if (P > 2) sup_dpp_level(a, 1);
-  if (P > 4) sup_dpp_level(a, 2);
-  if (P > 8) sup_dpp_level(a, 3);
-  SupAcc u;
-  u.best = readlane_d(a.best, 0);
-  u.bi = __builtin_amdgcn_readlane(a.bi, 0);
+  double m = a.best;
+  if (P > 1) m = __builtin_fmax(m, dpp_d(m, 0));
+  if (P > 2) m = __builtin_fmax(m, dpp_d(m, 1));
+  if (P > 4) m = __builtin_fmax(m, dpp_d(m, 2));
+  if (P > 8) m = __builtin_fmax(m, dpp_d(m, 3));
+  double M = readlane_d(m, 0);
   if (P > 16) {
-    sup_take(u, readlane_d(a.best, 16), __builtin_amdgcn_readlane(a.bi, 16));
+    M = __builtin_fmax(M, readlane_d(m, 16));
     if (P > 32) {
-      sup_take(u, readlane_d(a.best, 32), __builtin_amdgcn_readlane(a.bi, 32));
-      sup_take(u, readlane_d(a.best, 48), __builtin_amdgcn_readlane(a.bi, 48));
+      M = __builtin_fmax(M, readlane_d(m, 32));
+      M = __builtin_fmax(M, readlane_d(m, 48));
     }
   }
-  int bi = (u.bi == 0x7fffffff) ? 0 : u.bi;
+  unsigned long long tied = __ballot(a.bi != 0x7fffffff && a.best == M);
+  int bi = 0;
+  if (tied) {
+    int l = __ffsll((long long)tied) - 1;
+    bi = __builtin_amdgcn_readlane(a.bi, l);
+    if (n > WAVE) {
+      tied &= tied - 1ull;
+      while (tied) {
+        int l2 = __ffsll((long long)tied) - 1;
+        tied &= tied - 1ull;
+        int b2 = __builtin_amdgcn_readlane(a.bi, l2);
+        if (b2 < bi) bi = b2;
+      }
+    }
+  }
   int wl = bi & (WAVE - 1);
   v[0] = readlane_d(a.vx, wl);
   v[1] = readlane_d(a.vy, wl);
