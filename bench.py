@@ -18,7 +18,9 @@ rollout tail overlaps the next batches' work; every step is a whole batch.
 
 Multi-GPU: weak scaling, one process per GPU, each rank evaluates its own
 8192-candidate block (seed = rank); no data-path collective -- only the
-timing barrier and the max-over-ranks reduction.
+timing barrier and the max-over-ranks reduction.  Run directly with --gpus N
+(no WORLD_SIZE in the environment), the script starts the N ranks itself as
+child processes before any GPU call; under a launcher, WORLD_SIZE must equal N.
 """
 import argparse
 import json
@@ -73,8 +75,8 @@ def cpu_baseline(env, poses, joints, h, budget_s, threads):
     from oracle import oracle as O
     om = O.OracleModel(env.model, ncon_max=40)         # the escalation ceiling: MuJoCo has no cap
     q, mp, mq, _ = env.initial_state(poses, joints)
-    # pilot on 256 candidates to size the sample to the time budget
-    n_pilot = min(256, len(poses))
+    # pilot (two candidates per thread, at least 16) to size the sample to the time budget
+    n_pilot = min(max(16, 2 * threads), len(poses))
     t0 = time.perf_counter()
     free = om.collision_free(q[:n_pilot], mp[:n_pilot], mq[:n_pilot], nthreads=threads)
     idx = np.nonzero(free)[0]
@@ -107,7 +109,17 @@ def host_info():
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "cpus_visible": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count()}
+    quota = None
+    try:
+        # cgroup v2 CPU bandwidth limit ("max 100000" = none): the share of the
+        # visible CPUs this process can actually use
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            quota = None if q == "max" else float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "cpus_visible": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count(),
+            "cgroup_cpu_quota": quota}
 
 
 def issue_summary():
@@ -168,6 +180,32 @@ def e2e_api(env, poses, J, h, steps):
     return mask, labels, float(np.median(ts))
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE from a launcher): start N
+    fresh child processes of this script, one rank per GPU (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set), before anything in this parent touches the GPU,
+    and exit with the worst child status.  Rank 0 prints the JSON line."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,11 +233,24 @@ def main():
                          "them from there (0: re-run from the start)")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
+    ap.add_argument("--dry-run", action="store_true", help="print each rank's layout and exit (no GPU work)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     if args.cpu_threads is None:
-        args.cpu_threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+        # every CPU this process may run on (all cores), whatever
+        # OMP_NUM_THREADS the box exports
+        args.cpu_threads = len(os.sched_getaffinity(0))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        # launcher check (tests/test_bench_launch.py): the rank layout, no GPU work
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "world": world, "master": os.environ.get("MASTER_ADDR")}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -485,12 +536,19 @@ def main():
         cb = cpu_baseline(env, poses, J, h, args.cpu_budget, args.cpu_threads)
         n = cb["n"]
         agree = bool(np.array_equal(cb["free"], free[:n]) and np.array_equal(cb["labels"], labels[:n]))
+        # one thread (the reference is single-threaded MuJoCo): a smaller bounded sample
+        c1 = cpu_baseline(env, poses, J, h, max(2.0, args.cpu_budget / 3), 1)
+        agree1 = bool(np.array_equal(c1["free"], free[:c1["n"]]) and np.array_equal(c1["labels"], labels[:c1["n"]]))
         out["cpu_baseline"] = {"value": cb["value"], "unit": "candidates/s", "cores": args.cpu_threads,
                                "kind": "port", "host": host_info(),
                                "sample": f"first {n} of the {N} candidates (mask + h200 rollouts of the "
                                          f"collision-free ones), oracle/ C restatement, OpenMP "
-                                         f"{args.cpu_threads} threads, {cb['seconds']:.1f} s",
-                               "labels_identical_to_gpu": agree}
+                                         f"{args.cpu_threads} threads (every CPU in the affinity mask), "
+                                         f"{cb['seconds']:.1f} s",
+                               "labels_identical_to_gpu": agree,
+                               "one_thread": {"value": c1["value"], "unit": "candidates/s", "cores": 1,
+                                              "sample": f"first {c1['n']} candidates, {c1['seconds']:.1f} s",
+                                              "labels_identical_to_gpu": agree1}}
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

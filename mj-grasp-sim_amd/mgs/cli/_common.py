@@ -30,6 +30,14 @@ def save_grasps(path, poses, joints):
     np.savez(path, **{"pose": poses.to_mat(), "joints": joints})
 
 
+def evaluators(env, cfg):
+    """(collision_mask, stable_mask) callables on (poses, joints) of a
+    GravitylessObjectGrasping env for this configuration's horizon -- the two
+    stages the CLIs shard over ranks (mgs.env.sharding)."""
+    kw = horizon_kwargs(cfg)
+    return env.grasp_collision_mask, lambda p, j: env.grasp_stability_evaluation_from_joints(p, j, **kw)
+
+
 def horizon_kwargs(cfg):
     """stability keyword arguments of a named horizon (ref8000 = the reference's)."""
     from mgs.env.gravityless_object_grasping import HORIZONS

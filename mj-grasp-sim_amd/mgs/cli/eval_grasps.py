@@ -14,24 +14,29 @@ import numpy as np
 
 from mgs.cli._hydra import main
 from mgs.env.selector import get_env_from_dict, load_scene
+from mgs.env.sharding import cli_device, filter_sharded, init_cli_group
 from mgs.util.geo.transforms import SE3Pose
 
 
 def eval_grasps(cfg, scene_def, grasps, **stable_kw):
-    env = get_env_from_dict(cfg.env, scene_def)
+    """collision mask, then the stable mask of the collision-free grasps
+    (reference :20-36), split over the launch's ranks when WORLD_SIZE > 1"""
+    env = get_env_from_dict(cfg.env, scene_def, device=cli_device())
     b2c = env.gripper.base_to_contact_transform().inverse().to_mat()
     pose, joints = grasps
     pose = np.einsum("nij,jk->nik", pose, b2c)
-    mask = env.grasp_collision_mask(SE3Pose.from_mat(pose, type="wxyz"), joints)
+    state = scene_def["env_state"]["state"]
+    mask, stable = filter_sharded(env.grasp_collision_mask,
+                                  lambda p, j: env.grasp_stable_mask(p, j, state, **stable_kw),
+                                  SE3Pose.from_mat(pose, type="wxyz"), joints)
     if mask.sum() == 0:
         return 0.0, {"num_objects": len(env.object_names)}
-    stable = env.grasp_stable_mask(SE3Pose.from_mat(pose[mask], type="wxyz"), joints[mask],
-                                   scene_def["env_state"]["state"], **stable_kw)
     return float(stable.sum()) / float(len(pose)), {"num_objects": len(env.object_names)}
 
 
 @main("eval_grasps")
 def run(cfg):
+    rank, _ = init_cli_group()
     input_dir = os.getenv("MGS_INPUT_DIR")
     assert input_dir is not None, "No input_dir defined!"
     root = os.path.join(input_dir, cfg.gripper.name)
@@ -44,6 +49,8 @@ def run(cfg):
     if cfg.get("lift_steps") is not None:
         kw = dict(nstep_lift=int(cfg.lift_steps), close_steps=int(cfg.lift_steps))
     rate, aux = eval_grasps(cfg, scene_def, (g["pose"], g["joints"]), **kw)
+    if rank != 0:
+        return
     res = {"success_rate": float(rate), "num_objects": aux["num_objects"], "scene_id": scene}
     with open(os.path.join(d, "grasp_evaluation.json"), "w") as f:
         json.dump(res, f, indent=2)

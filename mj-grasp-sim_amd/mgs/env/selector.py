@@ -23,9 +23,9 @@ def get_env(cfg, gripper, obj_list):
     raise ValueError(f"Unknown environment {_name(cfg)}")
 
 
-def get_env_from_dict(cfg, scene_dict):
+def get_env_from_dict(cfg, scene_dict, **kw):
     if _name(cfg) == "ClutterTable":
-        return ClutterTableEnv.from_dict(scene_dict)
+        return ClutterTableEnv.from_dict(scene_dict, **kw)
     raise ValueError(f"Unknown environment {_name(cfg)}")
 
 

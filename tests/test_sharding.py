@@ -60,6 +60,70 @@ def _worker(rank, world, port, outq):
     dist.destroy_process_group()
 
 
+def _oracle_evaluators(env, cfg):
+    """mgs.cli._common.evaluators with the oracle in place of the GPU engine"""
+    from oracle import oracle as O
+    from mgs.cli._common import horizon_kwargs
+    om = O.OracleModel(env.model, ncon_max=env.ncon_max)
+    kw = horizon_kwargs(cfg)
+
+    def mask(p, j):
+        q, mp, mq, _ = env.initial_state(p, j)
+        return om.collision_free(q, mp, mq)
+
+    def stable(p, j):
+        return om.rollout(env.rollout_plan(p, j, **kw))["label"]
+    return mask, stable
+
+
+def _cli_worker(rank, world, port, indir, argv):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "mj-grasp-sim_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world), MGS_INPUT_DIR=indir)
+    from mgs.cli import _common, filter_to_stable
+    _common.evaluators = _oracle_evaluators
+    filter_to_stable.run(argv)
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def test_filter_to_stable_cli_two_ranks_writes_single_rank_files(tmp_path):
+    """`torchrun --nproc-per-node 2 -m mgs.cli.filter_to_stable` (WORLD_SIZE 2,
+    gloo gather) writes the files of the one-process run"""
+    import shutil
+    import torch.multiprocessing as mp
+    from mgs.cli import gen_grasp_candidates
+    src = tmp_path / "cand"
+    os.environ["MGS_OUTPUT_DIR"] = str(src)
+    try:
+        gen_grasp_candidates.run(["id=0", "num_grasps=40", "sampler=host", "seed=5"])
+    finally:
+        del os.environ["MGS_OUTPUT_DIR"]
+    sub = os.path.join("Robotiq2f85Gripper", "003_cracker_box")
+    argv = ["id=0", "horizon=h200"]
+    ctx = mp.get_context("spawn")
+    outs = {}
+    for world in (1, 2):
+        d = tmp_path / f"w{world}"
+        shutil.copytree(src, d)
+        port = _free_port()
+        procs = [ctx.Process(target=_cli_worker, args=(r, world, port, str(d), argv)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0
+        outs[world] = {f: np.load(d / sub / f) for f in ("candidates_collision_free.npz", "stable_grasps.npz")}
+    for f in outs[1]:
+        for k in ("pose", "joints"):
+            assert np.array_equal(outs[1][f][k], outs[2][f][k]), (f, k)
+    assert len(outs[1]["candidates_collision_free.npz"]["pose"]) > 0
+
+
 def test_shard_bounds_cover():
     from mgs.env.sharding import shard_bounds
     for n in [0, 1, 7, 8192, 8193]:
