@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 12
+#define MGS_ABI_VERSION 13
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -127,6 +127,8 @@ typedef struct mgs_model_desc {
   double tolerance;
   double noslip_tolerance;
   double mpr_tolerance;
+  double meaninertia; /* MuJoCo stat.meaninertia: mean diagonal of M at qpos0 (mj_setConst);
+                         the solvers' tolerance scale is 1 / (meaninertia * max(1, nv)) */
   double gravity[3];
   /* body arrays: int */
   int32_t i_body_parentid;
@@ -190,7 +192,8 @@ typedef struct mgs_model_desc {
   int32_t i_hull_vertadr;
   int32_t i_hull_vertnum;
   int32_t d_hull_vert;      /* 3 * nhullvert, in geom frame; per hull x[n], y[n], z[n] */
-  int32_t d_hull_center;    /* 3 * nhull, interior point (vertex centroid) */
+  int32_t d_hull_center;    /* 3 * nhull, MPR interior point in geom frame (the geom origin, as
+                               MuJoCo's ccd centre geom_xpos; meshes are recentred on their COM) */
   /* admissible pairs with mixed contact parameters */
   int32_t i_pair_geom1;
   int32_t i_pair_geom2;
@@ -288,19 +291,30 @@ void mgs_model_free(mgs_model* model);
 int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes);
 /* The LDS carve-up itself (offsets in doubles: the persistent arrays, the
  * time-multiplexed U views, then ncon_max, nefc_max, nv, total), host-only.
- * Writes at most cap words and their count to *nwords.  The build bakes the
- * headline model's layout into a constant-offset kernel instantiation
- * (tools/gen_static_layout.py); launches whose layout matches it use that one. */
+ * Writes at most cap words and their count to *nwords.  A model-specialised
+ * code object bakes exactly these words (mgs/core/special.py). */
 int mgs_model_layout(const mgs_model_desc* desc, int32_t* out, int cap, int32_t* nwords);
-/* 1 if this model's rollouts run the static-layout instantiation (its layout
- * equals the one baked in at build time), 0 if the runtime-offset one. */
-int mgs_model_static_layout(const mgs_model* model);
+/* Attach a model-specialised code object: mgs_special.hip compiled for this
+ * model (hipcc --genco with the header mgs/core/special.py generates from the
+ * model description and mgs_model_layout), in which every LDS view, size,
+ * table offset and option is a compile-time constant.  The object's baked ABI
+ * version, library flavour (rows per lane), description and layout are read
+ * back and must equal this model's, else MGS_EINVAL and nothing changes.  From
+ * then on the model's collision and rollout launches use its kernels; a dof
+ * count without a library instantiation (mgs_supports_nv == 0) runs only
+ * this way.  Stage timers of an MGS_PROFILE object: mgs_model_prof_read. */
+int mgs_model_attach_special(mgs_model* model, const char* code_object_path);
+/* 1 if a specialised code object is attached, 0 if the runtime-offset kernels run. */
+int mgs_model_special(const mgs_model* model);
 
 /* Capacity limits of this library build: constraint rows per candidate
  * (libmgs_gpu.so 128, libmgs_gpu_wide.so 256) and whether a kernel is
  * instantiated for a dof count (1/0). */
 int mgs_max_rows(void);
 int mgs_supports_nv(int nv);
+/* constraint rows per lane of this build's kernels (2 main, 4 wide): the
+ * flavour a specialised code object must be compiled for (-DMGS_WIDE if 4) */
+int mgs_rows_per_lane(void);
 
 /* Device buffers for up to `capacity` candidates. */
 int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out);

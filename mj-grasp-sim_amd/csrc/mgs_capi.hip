@@ -14,6 +14,7 @@
 #endif
 #endif
 #include "mgs_kernels.hip"
+#include "mgs_launch.h"
 #include "mgs_sampler.hip"
 #include "mgs_contact.hip"
 
@@ -112,12 +113,15 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
 }
 }  // namespace
 
-// dof counts with a compiled kernel instantiation.  Main library: Panda +
-// free object = 14, Robotiq 2F-85 + free object = 20, Allegro + free object =
-// 28, Shadow + free object = 34.  Wide library (MGS_WIDE: 4 rows per lane, G in
-// HBM) for clutter piles of 5 free objects: Panda 38, Robotiq 44, Allegro 52,
-// Shadow 58.
-#ifndef MGS_NV_LIST            /* a -D override builds one instantiation (tools/isa_stats.sh) */
+// dof counts with a compiled kernel instantiation (mgs_inst.hip, one translation
+// unit each).  Main library: Panda + free object = 14, Robotiq 2F-85 + free
+// object = 20, Allegro + free object = 28, Shadow + free object = 34.  Wide
+// library (MGS_WIDE: 4 rows per lane, G in HBM) for clutter piles of 5 free
+// objects: Panda 38, Robotiq 44, Allegro 52, Shadow 58.  Any other dof count
+// (up to 64) runs through a model-specialised code object
+// (mgs_model_attach_special).  The list is MGS_NV_LIST from the build
+// (__graft_entry__.py), here the default.
+#ifndef MGS_NV_LIST
 #ifdef MGS_WIDE
 #define MGS_NV_LIST(X) X(38) X(44) X(52) X(58)
 #else
@@ -125,14 +129,20 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
 #endif
 #endif
 
-static bool nv_supported(int nv) {
+#define MGS_DECL(NV_) template <> const KernelSet* mgs_kernels_nv<NV_>();
+MGS_NV_LIST(MGS_DECL)
+#undef MGS_DECL
+
+static const KernelSet* kernels_for(int nv) {
   switch (nv) {
-#define MGS_CASE(NV_) case NV_: return true;
+#define MGS_CASE(NV_) case NV_: return mgs_kernels_nv<NV_>();
     MGS_NV_LIST(MGS_CASE)
 #undef MGS_CASE
-    default: return false;
+    default: return nullptr;
   }
 }
+
+static bool nv_supported(int nv) { return kernels_for(nv) != nullptr; }
 
 // static LDS of the kernels (the diagnostic stage timers of the MGS_PROFILE build)
 #ifdef MGS_PROFILE
@@ -141,46 +151,12 @@ static bool nv_supported(int nv) {
 #define MGS_STATIC_LDS 0
 #endif
 
-// the launch's model description and layout are the ones baked into the
-// static-layout instantiations
-static bool static_layout_match(const mgs_model_desc& desc, const Lay& l) {
-#if MGS_SL_NV > 0
-  if (l.nv != MGS_SL_NV || !mgs_sl_desc_equal(desc)) return false;
-  for (int i = 0; i < L_COUNT; i++) if (l.o[i] != mgs_sl_words[i]) return false;
-  for (int i = 0; i < U_COUNT; i++) if (l.u[i] != mgs_sl_words[L_COUNT + i]) return false;
-  const int* t = mgs_sl_words + L_COUNT + U_COUNT;
-  return l.ncon_max == t[0] && l.nefc_max == t[1] && l.nv == t[2] && l.total_doubles == t[3];
-#else
-  (void)desc;
-  (void)l;
-  return false;
-#endif
-}
-
 static hipError_t set_lds_limit(int nv, int bytes) {
-#if MGS_SL_NV > 0
-  if (nv == MGS_SL_NV) {
-    hipError_t e = hipFuncSetAttribute((const void*)mgs_rollout_kernel<MGS_SL_NV, 1>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)mgs_collision_kernel<MGS_SL_NV, 1>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (e != hipSuccess) return e;
-  }
-#endif
-  switch (nv) {
-#define MGS_CASE(NV_)                                                                                      \
-  case NV_: {                                                                                              \
-    hipError_t e = hipFuncSetAttribute((const void*)mgs_rollout_kernel<NV_>,                               \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);                 \
-    if (e != hipSuccess) return e;                                                                         \
-    return hipFuncSetAttribute((const void*)mgs_collision_kernel<NV_>,                                     \
-                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);                         \
-  }
-    MGS_NV_LIST(MGS_CASE)
-#undef MGS_CASE
-    default: return hipErrorInvalidValue;
-  }
+  const KernelSet* k = kernels_for(nv);
+  if (!k) return hipSuccess;     // specialised-only dof count: nothing to set here
+  hipError_t e = hipFuncSetAttribute(k->rollout_fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute(k->collision_fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 struct mgs_model {
@@ -190,6 +166,9 @@ struct mgs_model {
   double* dD;
   Lay lay;
   size_t lds_bytes;
+  // model-specialised code object (mgs_special.hip), if attached
+  hipModule_t special_mod;
+  hipFunction_t special_collision, special_rollout;
 };
 
 struct mgs_batch {
@@ -213,7 +192,7 @@ const char* mgs_last_error(void) { return g_err.c_str(); }
 int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const double* dbuf, int device,
                      mgs_model** out) {
   if (!desc || !ibuf || !dbuf || !out) return fail(MGS_EINVAL, "mgs_model_create: null argument%s");
-  if (!nv_supported(desc->nv)) return fail(MGS_EINVAL, "no kernel instantiated for this nv (MGS_NV_LIST)%s");
+  if (desc->nv < 1) return fail(MGS_EINVAL, "nv must be >= 1%s");
   if (desc->cone != 1 || desc->integrator != 2)
     return fail(MGS_EINVAL, "only elliptic cones and implicitfast are supported%s");
   if (desc->nu > 32) return fail(MGS_EINVAL, "at most 32 actuators%s");
@@ -254,6 +233,7 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
 
 void mgs_model_free(mgs_model* m) {
   if (!m) return;
+  if (m->special_mod) hipModuleUnload(m->special_mod);
   hipFree(m->dI);
   hipFree(m->dD);
   delete m;
@@ -343,19 +323,16 @@ int mgs_collision_free_device(mgs_batch* b, int n, const double* d_qpos_init, co
   int lrc = launch_layout(b, n, &lay);
   if (lrc) return lrc;
   HIPCHK(hipEventRecord(b->e2, st));
-#define MGS_LAUNCH_COLL(NV_) hipLaunchKernelGGL(mgs_collision_kernel<NV_>, dim3(n), dim3(64), b->m->lds_bytes, st, md, \
-      md.I, md.D, lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free)
-#if MGS_SL_NV > 0
-  if (static_layout_match(b->m->desc, lay)) {
-    hipLaunchKernelGGL((mgs_collision_kernel<MGS_SL_NV, 1>), dim3(n), dim3(64), b->m->lds_bytes, st, md, md.I, md.D,
-                       lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free);
-  } else
-#endif
-  switch (md.m.nv) {
-#define MGS_CASE(NV_) case NV_: MGS_LAUNCH_COLL(NV_); break;
-    MGS_NV_LIST(MGS_CASE)
-#undef MGS_CASE
-    default: return fail(MGS_EINVAL, "no kernel for this nv%s");
+  CollisionArgs a{md, lay, n, d_qpos_init, d_mocap_pos, d_mocap_quat, predicate, d_out_free};
+  if (b->m->special_collision) {
+    const int32_t* I = md.I;
+    const double* D = md.D;
+    void* p[] = {&a.md, &I, &D, &a.lay, &a.n, &a.qpos_init, &a.mocap_pos, &a.mocap_quat, &a.predicate, &a.out};
+    HIPCHK(hipModuleLaunchKernel(b->m->special_collision, n, 1, 1, 64, 1, 1, b->m->lds_bytes, st, p, nullptr));
+  } else {
+    const KernelSet* k = kernels_for(md.m.nv);
+    if (!k) return fail(MGS_EINVAL, "no kernel for this nv in this library and no specialised code object attached%s");
+    k->collision(dim3(n), b->m->lds_bytes, st, a);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->e3, st));
@@ -395,22 +372,19 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   int lrc = launch_layout(b, nwg, &lay);
   if (lrc) return lrc;
   HIPCHK(hipEventRecord(b->e0, st));
-#define MGS_LAUNCH_ROLL(NV_) hipLaunchKernelGGL(mgs_rollout_kernel<NV_>, dim3(nwg), dim3(64), b->m->lds_bytes, st, md, \
-      md.I, md.D, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label, \
-      d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in)
-#if MGS_SL_NV > 0
-  if (static_layout_match(b->m->desc, lay)) {
-    hipLaunchKernelGGL((mgs_rollout_kernel<MGS_SL_NV, 1>), dim3(nwg), dim3(64), b->m->lds_bytes, st, md, md.I, md.D,
-                       lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
-                       d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out,
-                       d_resume_in);
-  } else
-#endif
-  switch (md.m.nv) {
-#define MGS_CASE(NV_) case NV_: MGS_LAUNCH_ROLL(NV_); break;
-    MGS_NV_LIST(MGS_CASE)
-#undef MGS_CASE
-    default: return fail(MGS_EINVAL, "no kernel for this nv%s");
+  RolloutArgs a{md, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
+                d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in};
+  if (b->m->special_rollout) {
+    const int32_t* I = md.I;
+    const double* D = md.D;
+    void* p[] = {&a.md, &I, &D, &a.lay, &a.sc, &a.n, &a.qpos_init, &a.mocap_quat, &a.phase_start, &a.phase_target,
+                 &a.active, &a.label, &a.fail_step, &a.obj_qpos, &a.stats, &a.vstate_init, &a.state_out, &a.list,
+                 &a.list_count, &a.resume_out, &a.resume_in};
+    HIPCHK(hipModuleLaunchKernel(b->m->special_rollout, nwg, 1, 1, 64, 1, 1, b->m->lds_bytes, st, p, nullptr));
+  } else {
+    const KernelSet* k = kernels_for(md.m.nv);
+    if (!k) return fail(MGS_EINVAL, "no kernel for this nv in this library and no specialised code object attached%s");
+    k->rollout(dim3(nwg), b->m->lds_bytes, st, a);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(b->e1, st));
@@ -598,17 +572,32 @@ int mgs_tree_probe(const double* a, const double* c, int n, int nb, double* out)
   return MGS_OK;
 }
 
-// diagnostic build only: read and clear the stage timers (s_memtime ticks)
+// diagnostic build only: read and clear the stage timers (s_memtime ticks) of
+// every dof count's kernels of this library
 int mgs_prof_read(unsigned long long* out) {
 #ifdef MGS_PROFILE
-  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 64));
-  unsigned long long z[64] = {0};
-  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+  for (int k = 0; k < 64; k++) out[k] = 0;
+#define MGS_CASE(NV_) if (mgs_kernels_nv<NV_>()->prof_read(out)) return fail(MGS_EHIP, "stage timer read failed%s");
+  MGS_NV_LIST(MGS_CASE)
+#undef MGS_CASE
   return MGS_OK;
 #else
   (void)out;
   return MGS_EINVAL;
 #endif
+}
+
+// the same for a model's specialised code object (built with -DMGS_PROFILE)
+int mgs_model_prof_read(mgs_model* m, unsigned long long* out) {
+  if (!m || !m->special_mod || !out) return fail(MGS_EINVAL, "mgs_model_prof_read: no specialised code object%s");
+  hipDeviceptr_t p;
+  size_t sz = 0;
+  unsigned long long z[64] = {0};
+  if (hipModuleGetGlobal(&p, &sz, m->special_mod, "g_prof") != hipSuccess || sz != sizeof(z))
+    return fail(MGS_EINVAL, "the specialised code object has no stage timers (not an MGS_PROFILE build)%s");
+  HIPCHK(hipMemcpyDtoH(out, p, sizeof(z)));
+  HIPCHK(hipMemcpyHtoD(p, z, sizeof(z)));
+  return MGS_OK;
 }
 
 int mgs_lds_bytes(mgs_model* m) { return m ? (int)m->lds_bytes : -1; }
@@ -793,6 +782,8 @@ int mgs_max_rows(void) { return 64 * MGS_RPL; }
 
 int mgs_supports_nv(int nv) { return nv_supported(nv) ? 1 : 0; }
 
+int mgs_rows_per_lane(void) { return MGS_RPL; }
+
 int mgs_model_lds_bytes(const mgs_model_desc* desc, int64_t* out_bytes) {
   if (!desc || !out_bytes) return fail(MGS_EINVAL, "mgs_model_lds_bytes: null argument%s");
   size_t b = 0;
@@ -816,7 +807,55 @@ int mgs_model_layout(const mgs_model_desc* desc, int32_t* out, int cap, int32_t*
   return MGS_OK;
 }
 
-int mgs_model_static_layout(const mgs_model* m) { return m && static_layout_match(m->desc, m->lay) ? 1 : 0; }
+int mgs_model_special(const mgs_model* m) { return m && m->special_rollout ? 1 : 0; }
+
+int mgs_model_attach_special(mgs_model* m, const char* path) {
+  if (!m || !path) return fail(MGS_EINVAL, "mgs_model_attach_special: null argument%s");
+  HIPCHK(hipSetDevice(m->device));
+  hipModule_t mod = nullptr;
+  if (hipModuleLoad(&mod, path) != hipSuccess) return fail(MGS_EINVAL, "cannot load code object %s", path);
+  // the object's baked ABI version, description and layout must be this model's
+  auto check = [&]() -> int {
+    hipDeviceptr_t p;
+    size_t sz = 0;
+    int abi = 0, rpl = 0;
+    mgs_model_desc dsc;
+    int32_t w[L_COUNT + U_COUNT + 4];
+    if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_abi") != hipSuccess || sz != sizeof(int) ||
+        hipMemcpyDtoH(&abi, p, sizeof(int)) != hipSuccess || abi != MGS_ABI_VERSION)
+      return fail(MGS_EINVAL, "code object %s is of another ABI version", path);
+    if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_rows_per_lane") != hipSuccess || sz != sizeof(int) ||
+        hipMemcpyDtoH(&rpl, p, sizeof(int)) != hipSuccess || rpl != MGS_RPL)
+      return fail(MGS_EINVAL, "code object %s is of the other library flavour (rows per lane)", path);
+    if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_desc") != hipSuccess || sz != sizeof(dsc) ||
+        hipMemcpyDtoH(&dsc, p, sizeof(dsc)) != hipSuccess || memcmp(&dsc, &m->desc, sizeof(dsc)) != 0)
+      return fail(MGS_EINVAL, "code object %s was specialised for another model description", path);
+    const Lay& l = m->lay;
+    int k = 0;
+    int32_t mine[L_COUNT + U_COUNT + 4];
+    for (int i = 0; i < L_COUNT; i++) mine[k++] = l.o[i];
+    for (int i = 0; i < U_COUNT; i++) mine[k++] = l.u[i];
+    mine[k++] = l.ncon_max; mine[k++] = l.nefc_max; mine[k++] = l.nv; mine[k++] = l.total_doubles;
+    if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_words") != hipSuccess || sz != sizeof(w) ||
+        hipMemcpyDtoH(w, p, sizeof(w)) != hipSuccess || memcmp(w, mine, sizeof(w)) != 0)
+      return fail(MGS_EINVAL, "code object %s was specialised for another LDS layout", path);
+    return MGS_OK;
+  };
+  int rc = check();
+  hipFunction_t fc = nullptr, fr = nullptr;
+  if (rc == MGS_OK && (hipModuleGetFunction(&fc, mod, "mgs_special_collision") != hipSuccess ||
+                       hipModuleGetFunction(&fr, mod, "mgs_special_rollout") != hipSuccess))
+    rc = fail(MGS_EINVAL, "code object %s lacks the specialised kernels", path);
+  if (rc != MGS_OK) {
+    hipModuleUnload(mod);
+    return rc;
+  }
+  if (m->special_mod) hipModuleUnload(m->special_mod);
+  m->special_mod = mod;
+  m->special_collision = fc;
+  m->special_rollout = fr;
+  return MGS_OK;
+}
 
 int mgs_device_count(void) {
   int n = 0;

@@ -110,7 +110,15 @@ DEVI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // Diagnostic stage timers (built only with -DMGS_PROFILE; never in the product build)
 #ifdef MGS_PROFILE
+#ifdef MGS_SPECIAL
+// a specialised code object's timers, read by the host with hipModuleGetGlobal
+extern "C" {
 __device__ unsigned long long g_prof[64];
+}
+#else
+// one copy per translation unit (each dof count's kernels, mgs_inst.hip)
+static __device__ unsigned long long g_prof[64];
+#endif
 // per-workgroup accumulators in static LDS; PT(k) at wave-uniform points only
 __shared__ unsigned long long s_prof[65];
 #define PT(k) do { unsigned long long _n = __builtin_amdgcn_s_memtime(); \
@@ -1900,20 +1908,26 @@ struct Lay {
   double* gmem;     // MGS_G_GLOBAL: per-candidate G rows in HBM (nefc_max * nv doubles each)
 };
 
-// Static layout: the headline model's carve-up (tools/gen_static_layout.py ->
-// mgs_static_layout.h) as compile-time offsets.  A kernel instantiated with
-// SL = 1 binds every view at a constant LDS address, so the ~80 views need no
-// SGPRs (their spills to VGPR lanes and reloads disappear) and LDS accesses
-// carry their offsets as instruction immediates.  The host launches it only
-// for a launch whose runtime layout equals this one.
-#if defined(MGS_STATIC_LAYOUT) && !defined(MGS_WIDE)
-#include "mgs_static_layout.h"
+// Model specialisation: a code object compiled for one model (mgs_special.hip
+// with the header mgs.core.special generates for it, -DMGS_SPECIAL=<header>)
+// carries that model's LDS carve-up and description as compile-time constants.
+// A kernel instantiated with SL = 1 binds every view at a constant LDS address,
+// so the ~80 views need no SGPRs (their spills to VGPR lanes and reloads
+// disappear), LDS accesses carry their offsets as instruction immediates, and
+// sizes / table offsets / options are constants (trip counts, immediates).
+// The host attaches such an object to a model only after comparing the
+// object's baked description and layout with the model's
+// (mgs_model_attach_special).
+#ifdef MGS_SPECIAL
+#include MGS_SPECIAL
+static_assert(MGS_SL_ABI == MGS_ABI_VERSION, "specialisation header of another ABI version: regenerate it");
+static_assert(MGS_SL_DESC_BYTES == sizeof(mgs_model_desc), "specialisation header of another mgs_model_desc");
 #else
 #define MGS_SL_NV 0
 constexpr int mgs_sl_words[L_COUNT + U_COUNT + 4] = {0};
 constexpr mgs_model_desc mgs_sl_desc = {};
 #endif
-static_assert(sizeof(mgs_sl_words) == sizeof(int) * (L_COUNT + U_COUNT + 4), "static layout size");
+static_assert(sizeof(mgs_sl_words) == sizeof(int) * (L_COUNT + U_COUNT + 4), "specialised layout size");
 
 template <int SL>
 DEVI void bind(Dat& d, double* s, const Lay& l) {
@@ -3728,10 +3742,9 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
 template <int NV>
 DEVI void solve(const Mdl& md, Dat& d) {
   int nv = md.m.nv;
-  double meaninertia = 0.0;
-  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d.M[k * nv + k];
-  meaninertia = meaninertia / (double)nv;
-  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
+  // MuJoCo: scale = 1 / (m->stat.meaninertia * max(1, nv)), meaninertia being the
+  // mean diagonal of M at qpos0 (mj_setConst), a model constant
+  double scale = 1.0 / (md.m.meaninertia * (double)(nv > 1 ? nv : 1));
   Frc F;
   double u;
   if (md.m.solver == 0) {
@@ -3932,13 +3945,13 @@ DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mp
 
 // ---------------------------------------------------------------------------
 // kernels: one 64-lane workgroup per candidate
-template <int NV, int SL = 0>
-__global__ void __launch_bounds__(64)
-mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
-                     const double* __restrict__ qpos_init,
-                     const double* __restrict__ mocap_pos, const double* __restrict__ mocap_quat, int predicate,
-                     uint8_t* __restrict__ out) {
-  extern __shared__ double smem[];
+// kernel bodies (mgs_collision_kernel / mgs_rollout_kernel below and the
+// specialised entry points of mgs_special.hip)
+template <int NV, int SL>
+DEVI void collision_entry(double* smem, const Mdl& mdarg, const int32_t* __restrict__ mI,
+                          const double* __restrict__ mD, const Lay& lay, int n, const double* __restrict__ qpos_init,
+                          const double* __restrict__ mocap_pos, const double* __restrict__ mocap_quat,
+                          int predicate, uint8_t* __restrict__ out) {
   Mdl md = mdarg;
   if constexpr (SL != 0) md.m = mgs_sl_desc;
   md.I = mI;
@@ -3956,6 +3969,16 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   }
 }
 
+template <int NV, int SL = 0>
+__global__ void __launch_bounds__(64)
+mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
+                     const double* __restrict__ qpos_init,
+                     const double* __restrict__ mocap_pos, const double* __restrict__ mocap_quat, int predicate,
+                     uint8_t* __restrict__ out) {
+  extern __shared__ double smem[];
+  collision_entry<NV, SL>(smem, mdarg, mI, mD, lay, n, qpos_init, mocap_pos, mocap_quat, predicate, out);
+}
+
 // one candidate's rollout (the body of mgs_rollout_kernel)
 template <int NV, int SL>
 DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_schedule& sc, int i,
@@ -3964,7 +3987,7 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
                       const uint8_t* __restrict__ active, uint8_t* __restrict__ label,
                       int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
                       const double* __restrict__ vstate_init, double* __restrict__ state_out,
-                      double* __restrict__ resume_out, const double* __restrict__ resume_in) {
+                      double* resume_out, const double* resume_in) {
   int lane = lane_id();
   if (active && !active[i]) {
     // collision-mask reject: not simulated (filter_to_stable.py:39-44)
@@ -4126,18 +4149,16 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
 #else
 #define MGS_ROLL_ATTR
 #endif
-template <int NV, int SL = 0>
-__global__ void __launch_bounds__(64) MGS_ROLL_ATTR
-mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
-                   mgs_schedule sc, int n, const double* __restrict__ qpos_init,
-                   const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
-                   const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
-                   uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
-                   int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
-                   double* __restrict__ state_out, const int32_t* __restrict__ list,
-                   const int32_t* __restrict__ list_count, double* __restrict__ resume_out,
-                   const double* __restrict__ resume_in) {
-  extern __shared__ double smem[];
+template <int NV, int SL>
+DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restrict__ mI,
+                        const double* __restrict__ mD, const Lay& lay, const mgs_schedule& sc, int n,
+                        const double* __restrict__ qpos_init, const double* __restrict__ mocap_quat,
+                        const double* __restrict__ phase_start, const double* __restrict__ phase_target,
+                        const uint8_t* __restrict__ active, uint8_t* __restrict__ label,
+                        int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
+                        const double* __restrict__ vstate_init, double* __restrict__ state_out,
+                        const int32_t* __restrict__ list, const int32_t* __restrict__ list_count,
+                        double* resume_out, const double* resume_in) {
   Mdl md = mdarg;
   // SL: the model description is the baked one too, so sizes, table offsets and
   // options are compile-time constants (trip counts, immediate offsets)
@@ -4154,6 +4175,28 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
   }
 }
 
+// resume_out / resume_in may be the same buffer (mgs_rollout_resume continues a
+// capped run's records in place): not __restrict__; each candidate's record is
+// read into LDS before its own record is rewritten
+template <int NV, int SL = 0>
+__global__ void __launch_bounds__(64) MGS_ROLL_ATTR
+mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
+                   mgs_schedule sc, int n, const double* __restrict__ qpos_init,
+                   const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
+                   const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
+                   uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
+                   int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
+                   double* __restrict__ state_out, const int32_t* __restrict__ list,
+                   const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in) {
+  extern __shared__ double smem[];
+  rollout_entry<NV, SL>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target, active,
+                        label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count, resume_out,
+                        resume_in);
+}
+
+// the library's non-template kernels live in the C-ABI translation unit only
+// (the per-dof-count units and specialised code objects define MGS_TEMPLATES_ONLY)
+#ifndef MGS_TEMPLATES_ONLY
 // capacity-escalation list: indices of the candidates whose stats flags meet
 // mask (order of arrival; each re-run is independent of the order)
 __global__ void __launch_bounds__(256)
@@ -4184,3 +4227,4 @@ extern "C" __global__ void __launch_bounds__(64) mgs_tree_probe_kernel(const dou
   double s = tree_sum(leaf, next_pow2(n));
   if (l == 0) out[b] = s;
 }
+#endif  // MGS_TEMPLATES_ONLY

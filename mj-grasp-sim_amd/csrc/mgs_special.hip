@@ -1,0 +1,58 @@
+// mgs_special.hip -- a model-specialised code object.
+//
+// Compiled per model (mgs/core/special.py: hipcc --genco --offload-arch=gfx950
+// -DMGS_SPECIAL="<header>" [-DMGS_WIDE]) with the header that carries the
+// model's description and LDS layout as constants; loaded at run time with
+// hipModuleLoad by mgs_model_attach_special (mgs_capi.hip), which first reads
+// the baked description and layout back from the object (mgs_special_desc,
+// mgs_special_words, mgs_special_abi) and compares them with the model's.
+//
+// The kernels are the rollout / collision kernels of mgs_kernels.hip
+// instantiated at the model's dof count with SL = 1 (every LDS view and every
+// model size / table offset a compile-time constant).  Any dof count up to 64
+// can be specialised, so models the library has no instantiation for (clutter
+// piles of any size, other grippers) run through these objects.
+#include <hip/hip_runtime.h>
+
+#ifdef MGS_WIDE
+#define MGS_RPL 4
+#define MGS_G_GLOBAL 1
+#endif
+#define MGS_TEMPLATES_ONLY
+#include "mgs_kernels.hip"
+
+#ifndef MGS_SPECIAL
+#error "mgs_special.hip is compiled with -DMGS_SPECIAL=<generated header>"
+#endif
+
+extern "C" {
+
+__device__ const int mgs_special_abi = MGS_ABI_VERSION;
+__device__ const int mgs_special_rows_per_lane = MGS_RPL;
+__device__ const mgs_model_desc mgs_special_desc = mgs_sl_desc;
+__device__ const int mgs_special_words[L_COUNT + U_COUNT + 4] = MGS_SL_WORDS_INIT;
+
+__global__ void __launch_bounds__(64)
+mgs_special_collision(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
+                      const double* __restrict__ qpos_init, const double* __restrict__ mocap_pos,
+                      const double* __restrict__ mocap_quat, int predicate, uint8_t* __restrict__ out) {
+  extern __shared__ double smem[];
+  collision_entry<MGS_SL_NV, 1>(smem, mdarg, mI, mD, lay, n, qpos_init, mocap_pos, mocap_quat, predicate, out);
+}
+
+__global__ void __launch_bounds__(64) MGS_ROLL_ATTR
+mgs_special_rollout(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
+                    mgs_schedule sc, int n, const double* __restrict__ qpos_init,
+                    const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
+                    const double* __restrict__ phase_target, const uint8_t* __restrict__ active,
+                    uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
+                    int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
+                    double* __restrict__ state_out, const int32_t* __restrict__ list,
+                    const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in) {
+  extern __shared__ double smem[];
+  rollout_entry<MGS_SL_NV, 1>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target,
+                              active, label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count,
+                              resume_out, resume_in);
+}
+
+}  // extern "C"

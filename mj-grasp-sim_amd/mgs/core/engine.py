@@ -68,7 +68,9 @@ def load_library(wide: bool = False):
     L.mgs_device_count.restype = ctypes.c_int
     L.mgs_model_lds_bytes.argtypes = [P(abi.ModelDesc), P(ctypes.c_int64)]
     L.mgs_model_layout.argtypes = [P(abi.ModelDesc), P(ctypes.c_int32), ctypes.c_int, P(ctypes.c_int32)]
-    L.mgs_model_static_layout.argtypes = [vp]
+    L.mgs_model_attach_special.argtypes = [vp, ctypes.c_char_p]
+    L.mgs_model_special.argtypes = [vp]
+    L.mgs_rows_per_lane.restype = ctypes.c_int
     L.mgs_max_rows.restype = ctypes.c_int
     L.mgs_antipodal_contacts.argtypes = [ctypes.c_int, P(c_d), ctypes.c_int, ctypes.c_int, P(c_d), P(c_d), P(c_d),
                                          c_d, P(c_d), P(c_i), P(c_d)]
@@ -87,16 +89,26 @@ def load_library(wide: bool = False):
     return L
 
 
+# the main library's flavour (2 rows per lane, G and NV-long operand rows on
+# chip) serves dof counts up to this; larger ones use the wide flavour (4 rows
+# per lane, G in HBM), instantiated or specialised (mgs.core.special)
+MAIN_NV_MAX = 34
+
+
 def library_for(nv: int, nefc_max: int):
-    """the library build whose kernels hold this model: the main one when it has
-    a kernel for nv and enough constraint rows, else the wide one."""
+    """the library build (flavour) whose kernels hold this model: the main one
+    when it has a kernel for nv, or nv is small enough for its flavour, and the
+    rows fit; else the wide one.  A dof count without an instantiation in the
+    chosen library runs through a specialised code object."""
+    if nv < 1 or nv > 64:
+        raise EngineError(f"nv={nv}: the kernels hold 1 to 64 dofs (lanes over dofs)")
     L = load_library()
-    if L.mgs_supports_nv(nv) and nefc_max <= L.mgs_max_rows():
+    if nefc_max <= L.mgs_max_rows() and (L.mgs_supports_nv(nv) or nv <= MAIN_NV_MAX):
         return L
     W = load_library(wide=True)
-    if W.mgs_supports_nv(nv) and nefc_max <= W.mgs_max_rows():
+    if nefc_max <= W.mgs_max_rows():
         return W
-    raise EngineError(f"no kernel instantiated for nv={nv} with {nefc_max} constraint rows (MGS_NV_LIST)")
+    raise EngineError(f"nv={nv} with {nefc_max} constraint rows exceeds every library build (mgs_max_rows)")
 
 
 def supported_nvs():
@@ -132,12 +144,12 @@ def layout_for(cm, ncon_max, nefc_max=None):
 
 
 def default_rows(cm, worst: int) -> int:
-    """worst-case constraint rows, capped at what the library that will hold
-    this model provides (the main one when it has a kernel for nv and the rows
-    fit, else the wide one)."""
+    """worst-case constraint rows, capped at what the library flavour that will
+    hold this model provides (the main one for nv <= MAIN_NV_MAX or an
+    instantiated nv, else the wide one)."""
     main = load_library()
     wide = load_library(wide=True) if os.path.isfile(LIB_WIDE_PATH) else None
-    if main.mgs_supports_nv(cm.nv) and (worst <= main.mgs_max_rows() or not (wide and wide.mgs_supports_nv(cm.nv))):
+    if (main.mgs_supports_nv(cm.nv) or cm.nv <= MAIN_NV_MAX) and (worst <= main.mgs_max_rows() or wide is None):
         return min(worst, main.mgs_max_rows())
     return min(worst, wide.mgs_max_rows()) if wide else worst
 
@@ -171,7 +183,12 @@ def _check(rc, what, lib=None):
 class Engine:
     """One compiled model resident on one GPU plus a reusable batch."""
 
-    def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None):
+    def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None, specialize=None):
+        """specialize: True = attach the model-specialised code object, compiling
+        it if it is not cached; "cached" = attach it only if cached; False = the
+        library's runtime-layout kernels.  Default (None): MGS_SPECIALIZE from the
+        environment ("1" / "cached" / "0"), else "cached".  A dof count the
+        library has no kernel for always specialises (compiling if needed)."""
         if nefc_max is None:
             nefc_max = default_rows(cm, int(cm.pack(ncon_max=ncon_max)[0]["nefc_max"]))
         fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
@@ -187,6 +204,15 @@ class Engine:
                "mgs_model_create")
         self._batch = ctypes.c_void_p()
         self._cap = 0
+        if specialize is None:
+            specialize = {"1": True, "0": False}.get(os.environ.get("MGS_SPECIALIZE", "cached"), "cached")
+        if not self.lib.mgs_supports_nv(cm.nv):
+            specialize = True
+        if specialize:
+            from mgs.core import special
+            path = special.code_object(self.lib, self.desc, compile=specialize is True)
+            if path is not None:
+                self._ck(self.lib.mgs_model_attach_special(self._model, path.encode()), "mgs_model_attach_special")
 
     def _ck(self, rc, what):
         _check(rc, what, self.lib)
@@ -338,9 +364,13 @@ class Engine:
     def last_collision_ms(self):
         return self.lib.mgs_last_collision_ms(self._batch)
 
-    def static_layout(self):
-        """True if this engine's rollouts run the constant-offset (baked layout) kernel"""
-        return bool(self.lib.mgs_model_static_layout(self._model))
+    def specialized(self):
+        """True if this engine's launches run a model-specialised code object
+        (constant LDS layout and model description), False if the runtime-offset
+        kernels"""
+        return bool(self.lib.mgs_model_special(self._model))
+
+    static_layout = specialized
 
     def lds_bytes(self):
         return self.lib.mgs_lds_bytes(self._model)

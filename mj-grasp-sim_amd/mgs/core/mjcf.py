@@ -425,6 +425,29 @@ class Compiler:
             m["hull"] = convex_hull_vertices(m["verts"])
         return m["hull"]
 
+    def _mesh_frame(self, name):
+        """MuJoCo's mesh compilation (user_mesh.cc): the mesh is moved to its
+        inertial frame -- centre of mass at the origin, principal axes along x,
+        y, z (mesh_pos, mesh_quat) -- and its vertices are stored as float32
+        (mesh_vert).  Returns (mesh_pos, mesh_quat, float32-rounded hull
+        vertices in that frame as float64).  The principal axes come from
+        numpy's symmetric eigensolver (MuJoCo: mju_eig3), so roundings agree
+        with MuJoCo's only as far as the two frames do."""
+        m = self.meshes[name]
+        if m.get("frame") is None:
+            vol, com, I = self._mesh_massprops(name)
+            if vol > 0 and np.any(I):
+                _, V = np.linalg.eigh(I)
+                V = V[:, ::-1].copy()          # decreasing principal moments
+                if np.linalg.det(V) < 0:
+                    V[:, 2] = -V[:, 2]
+            else:
+                V = np.eye(3)
+            hull = self._mesh_hull(name)
+            local = ((hull - com) @ V).astype(np.float32).astype(np.float64)
+            m["frame"] = (np.asarray(com, np.float64), _normq(mat2quat(V)), local)
+        return m["frame"]
+
     def _mesh_massprops(self, name):
         m = self.meshes[name]
         if m["mass"] is None:
@@ -671,10 +694,15 @@ class Compiler:
                 hulls.append(verts)
             elif t == "mesh":
                 mname = g["mesh"]
+                mpos, mquat, mverts = self._mesh_frame(mname)
                 if mname not in hull_of_mesh:
                     hull_of_mesh[mname] = len(hulls)
-                    hulls.append(self._mesh_hull(mname))
+                    hulls.append(mverts)
                 hid = hull_of_mesh[mname]
+                # MuJoCo offsets a mesh geom's frame by the mesh frame (mesh_pos /
+                # mesh_quat), so the geom origin is the mesh's centre of mass
+                gpos = gpos + quat2mat(gquat) @ mpos
+                gquat = _normq(quat_mul(gquat, mquat))
             elif t in ("sphere", "capsule"):
                 # rounded geoms: a point / a z-segment swept by a ball of radius size[0]
                 s = _f(g["size"], 3)
@@ -896,7 +924,9 @@ class Compiler:
         cm.hull_vertnum = np.array([len(h) for h in hulls], np.int32)
         cm.hull_vertadr = np.concatenate([[0], np.cumsum(cm.hull_vertnum)[:-1]]).astype(np.int32) if hulls else np.zeros(0, np.int32)
         cm.hull_vert = np.concatenate(hulls).reshape(-1, 3) if hulls else np.zeros((0, 3))
-        cm.hull_center = np.array([h.mean(0) for h in hulls]).reshape(-1, 3)
+        # interior point of each hull for MPR: the geom frame origin, as MuJoCo's
+        # ccd centre (geom_xpos); for meshes that is the mesh's centre of mass
+        cm.hull_center = np.zeros((len(hulls), 3))
         cm.pair_geom1 = np.array([p["g1"] for p in pairs], np.int32)
         cm.pair_geom2 = np.array([p["g2"] for p in pairs], np.int32)
         cm.pair_condim = np.array([p["condim"] for p in pairs], np.int32)
@@ -929,7 +959,7 @@ class Compiler:
         cm.actuator_gear = np.array([a["gear"] for a in acts], np.float64)
         cm.body_xpos0 = xpos
         cm.body_xquat0 = xquat
-        cm.body_invweight0, cm.dof_invweight0 = _invweight0(cm)
+        cm.body_invweight0, cm.dof_invweight0, cm.meaninertia = _invweight0(cm)
         return cm
 
 
@@ -1004,7 +1034,9 @@ def _invweight0(cm):
             diw[da + 3:da + 6] = diw[da + 3:da + 6].mean()
         elif t == 1:
             diw[da:da + 3] = diw[da:da + 3].mean()
-    return biw, diw
+    # stat.meaninertia: mean diagonal of M (armature included) at qpos0
+    meaninertia = float(np.trace(M) / nv) if nv else 1.0
+    return biw, diw, meaninertia
 
 
 class CompiledModel:
@@ -1140,7 +1172,7 @@ class CompiledModel:
             ls_iterations=int(o.get("ls_iterations", 50)), ls_tolerance=float(o.get("ls_tolerance", 0.01)),
             timestep=float(o["timestep"]), impratio=float(o["impratio"]),
             tolerance=float(o["tolerance"]), noslip_tolerance=float(o["noslip_tolerance"]),
-            mpr_tolerance=float(o.get("mpr_tolerance", 1e-6)),
+            mpr_tolerance=float(o.get("mpr_tolerance", 1e-6)), meaninertia=float(self.meaninertia),
             gravity=[float(x) for x in o["gravity"]], isize=len(ib), dsize=len(db))
         return fields, ib, db
 

@@ -1741,10 +1741,9 @@ static void project_block(const Dat* d, int r, double* f) {
 static void solve_pgs_main(const Mdl* md, Dat* d) {
   const mgs_model_desc* m = md->m;
   int nv = m->nv, ne = d->nefc;
-  double meaninertia = 0.0;
-  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d->M[k * nv + k];
-  meaninertia = meaninertia / (double)nv;
-  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
+  /* MuJoCo engine_solver.c: scale = 1 / (m->stat.meaninertia * mjMAX(1, nv)) with
+   * stat.meaninertia the mean diagonal of M at qpos0 (mj_setConst) */
+  double scale = 1.0 / (m->meaninertia * (double)(nv > 1 ? nv : 1));
   /* warmstart: f from qacc_warmstart through the primal map, projected;
    * J_r . qacc_ws = G_r . (D^1/2 L^T qacc_ws) */
   double hws[128];
@@ -1860,10 +1859,9 @@ static void solve_pgs_main(const Mdl* md, Dat* d) {
 static void noslip(const Mdl* md, Dat* d) {
   const mgs_model_desc* m = md->m;
   int nv = m->nv, ne = d->nefc;
-  double meaninertia = 0.0;
-  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d->M[k * nv + k];
-  meaninertia = meaninertia / (double)nv;
-  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
+  /* MuJoCo engine_solver.c: scale = 1 / (m->stat.meaninertia * mjMAX(1, nv)) with
+   * stat.meaninertia the mean diagonal of M at qpos0 (mj_setConst) */
+  double scale = 1.0 / (m->meaninertia * (double)(nv > 1 ? nv : 1));
   /* noslip: friction dims only, unregularized, normal forces fixed */
   for (int ns = 0; ns < m->noslip_iterations && ne > 0; ns++) {
     double improvement = 0.0;
@@ -2142,10 +2140,9 @@ static void ls_eval(const Dat* d, double alpha, double A1, double A2, double* d1
 static void solve_newton(const Mdl* md, Dat* d) {
   const mgs_model_desc* m = md->m;
   int nv = m->nv, ne = d->nefc;
-  double meaninertia = 0.0;
-  for (int k = 0; k < nv; k++) meaninertia = meaninertia + d->M[k * nv + k];
-  meaninertia = meaninertia / (double)nv;
-  double scale = 1.0 / (meaninertia * (double)(nv > 1 ? nv : 1));
+  /* MuJoCo engine_solver.c: scale = 1 / (m->stat.meaninertia * mjMAX(1, nv)) with
+   * stat.meaninertia the mean diagonal of M at qpos0 (mj_setConst) */
+  double scale = 1.0 / (m->meaninertia * (double)(nv > 1 ? nv : 1));
   /* per-row constants */
   for (int r = 0; r < ne; r++) {
     double sq = sqrt(d->efc_R[r]);

@@ -94,15 +94,37 @@ def test_layout_export_is_consistent(env):
     assert total * 8 == lds_bytes_for(env.model, env.ncon_max, env.nefc_max)
 
 
-def test_static_layout_header_is_current(env):
-    """the baked headline layout (mgs_static_layout.h) equals the layout the
-    headline engine launches with, so bench.py runs the constant-offset kernel
-    (a stale header would silently fall back to the runtime-offset one)"""
-    import sys
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    import gen_static_layout as G
-    path = G.OUT
-    if not os.path.isfile(path):
-        pytest.skip("no static layout baked into this build")
-    nv, words = G.headline_layout()
-    assert open(path).read() == G.render(nv, words, G.headline_desc())
+def test_specialisation_header(env):
+    """mgs.core.special: the generated header names every mgs_model_desc field
+    (designated initialisers in declaration order) with the ABI version and
+    struct size the kernels static_assert, and the cache key follows the
+    description"""
+    import ctypes
+    from mgs.core import abi, special
+    from mgs.core.engine import library_for
+    fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+    lib = library_for(env.model.nv, int(fields["nefc_max"]))
+    desc = abi.make_desc(fields)
+    header, flags, path = special.plan(lib, desc)
+    names = [n for n, _ in abi.ModelDesc._fields_]
+    pos = [header.index(f".{n} = ") for n in names]
+    assert pos == sorted(pos)
+    assert f"#define MGS_SL_ABI {abi.MGS['MGS_ABI_VERSION']}" in header
+    assert f"#define MGS_SL_DESC_BYTES {ctypes.sizeof(abi.ModelDesc)}" in header
+    assert f"#define MGS_SL_NV {env.model.nv}" in header
+    desc.nefc_max -= 1
+    assert special.plan(lib, desc)[2] != path
+
+
+def test_headline_specialised_object_is_built(env):
+    """build() compiles the headline engine's specialised code object into the
+    in-tree cache (it travels to the GPU box with the tree), so bench.py's
+    headline launches the constant-layout kernels"""
+    from mgs.core import abi, special
+    from mgs.core.engine import library_for
+    fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+    lib = library_for(env.model.nv, int(fields["nefc_max"]))
+    path = special.plan(lib, abi.make_desc(fields))[2]
+    if not os.path.isdir(special.CACHE):
+        pytest.skip("build() ran without the specialised objects")
+    assert os.path.isfile(path), "headline specialised object missing: run __graft_entry__.build()"

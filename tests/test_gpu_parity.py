@@ -360,24 +360,37 @@ def test_divergence_guard_parity(env, eng, candidates, oracle_model):
     assert np.array_equal(rg["obj_qpos"], ro["obj_qpos"], equal_nan=True)
 
 
-def test_static_layout_kernel_matches_runtime_layout(env, eng, candidates):
-    """The headline engine runs the constant-offset instantiation (its layout is
-    the baked one); an engine one row smaller runs the runtime-offset one.  On
-    candidates that fit both capacities every output is identical."""
+def test_specialised_kernels_match_runtime_layout(env, eng, candidates):
+    """The headline engine runs its model-specialised code object (constant
+    layout and description); an engine of the same model and capacity without
+    it runs the library's runtime-offset kernels: every output is identical."""
     from conftest import plan_for
     from mgs.core.engine import Engine
-    assert eng.static_layout()
-    other = Engine(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max - 1)
-    assert not other.static_layout()
+    assert eng.specialized()
+    other = Engine(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max, specialize=False)
+    assert not other.specialized()
     poses, J = candidates
     q, mp, mq, _ = env.initial_state(poses, J)
+    assert np.array_equal(eng.collision_free(q, mp, mq), other.collision_free(q, mp, mq))
     idx = np.nonzero(eng.collision_free(q, mp, mq))[0][:64]
     plan = plan_for(env, poses[idx], J[idx])
     a, b = eng.rollout(plan), other.rollout(plan)
-    ok = (a["stats"][:, 2] == 0) & (b["stats"][:, 2] == 0)
-    assert ok.sum() > 0.9 * len(idx)
     for k in ("label", "fail_step", "obj_qpos", "stats"):
-        assert np.array_equal(a[k][ok], b[k][ok]), k
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_specialised_object_of_another_model_is_refused(env, eng):
+    """mgs_model_attach_special reads the object's baked description and layout
+    back and refuses an object made for another capacity"""
+    import ctypes
+    from mgs.core import abi, special
+    from mgs.core.engine import Engine, EngineError
+    path = special.code_object(eng.lib, eng.desc, compile=False)
+    assert path is not None
+    other = Engine(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max - 1, specialize=False)
+    with pytest.raises(EngineError):
+        other._ck(other.lib.mgs_model_attach_special(other._model, path.encode()), "mgs_model_attach_special")
+    assert not other.specialized()
 
 
 @pytest.mark.parametrize("nefc_max", [10, 16, 40])
