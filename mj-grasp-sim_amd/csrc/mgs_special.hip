@@ -27,10 +27,13 @@
 
 extern "C" {
 
-__device__ const int mgs_special_abi = MGS_ABI_VERSION;
-__device__ const int mgs_special_rows_per_lane = MGS_RPL;
-__device__ const mgs_model_desc mgs_special_desc = mgs_sl_desc;
-__device__ const int mgs_special_words[L_COUNT + U_COUNT + 4] = MGS_SL_WORDS_INIT;
+// what the object was compiled for, read back by mgs_model_attach_special
+// (not const: const namespace-scope variables have internal linkage and would
+// not be visible to hipModuleGetGlobal)
+__device__ int mgs_special_abi = MGS_ABI_VERSION;
+__device__ int mgs_special_rows_per_lane = MGS_RPL;
+__device__ mgs_model_desc mgs_special_desc = mgs_sl_desc;
+__device__ int mgs_special_words[L_COUNT + U_COUNT + 4] = MGS_SL_WORDS_INIT;
 
 __global__ void __launch_bounds__(64)
 mgs_special_collision(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,

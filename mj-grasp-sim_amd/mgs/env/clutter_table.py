@@ -127,17 +127,16 @@ class ClutterTableEnv:
         self._engines = {}
 
     def _check_kernel(self, nv):
-        """kernels are compiled per dof count (csrc/mgs_capi.hip MGS_NV_LIST): fail
-        here, with the supported sizes, rather than at the first simulation"""
-        from mgs.core.engine import supported_nvs
-        ok = supported_nvs()
-        if nv not in ok:
+        """the kernels hold up to 64 dofs (lanes over dofs): dof counts the
+        libraries instantiate run directly, any other through a model-specialised
+        code object (mgs.core.special, compiled on first use); fail here, with
+        the largest pile, rather than at the first simulation"""
+        if nv > 64:
             g = self._gripper_nv
-            piles = sorted({(v - g) // 6 for v in ok if v > g and (v - g) % 6 == 0})
             raise ValueError(
                 f"no GPU kernel for this scene: {len(self.objects) - len(self.removed)} free objects with this "
-                f"gripper give nv={nv}; compiled dof counts are {ok}, i.e. piles of {piles} free objects for "
-                f"this gripper (add nv={nv} to MGS_NV_LIST in csrc/mgs_capi.hip and rebuild)")
+                f"gripper give nv={nv}; the kernels hold at most 64 dofs, i.e. piles of at most {(64 - g) // 6} "
+                f"free objects for this gripper")
 
     # -- state vector (mjSTATE_INTEGRATION of the reference model) ------------
     def _sizes(self):
