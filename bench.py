@@ -98,6 +98,14 @@ def cpu_baseline(env, poses, joints, h, budget_s, threads):
     return dict(value=n / dt, n=n, seconds=dt, free=free, labels=labels)
 
 
+def cpu_share():
+    """CPUs this process can actually run on: the affinity mask, capped by the
+    cgroup v2 CPU quota (rounded up)"""
+    n = len(os.sched_getaffinity(0))
+    q = host_info()["cgroup_cpu_quota"]
+    return max(1, min(n, int(-(-q // 1)))) if q else n
+
+
 def host_info():
     """the CPU the baseline ran on: model name and the cores visible to this process"""
     model = None
@@ -216,7 +224,7 @@ def main():
     ap.add_argument("--solver", default=None, help="override the model's solver (Newton | PGS)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=None,
-                    help="CPU baseline threads (default: OMP_NUM_THREADS, else the cores this process may run on)")
+                    help="CPU baseline threads (default: the CPUs this process may use, cgroup quota included)")
     ap.add_argument("--no-shard-check", dest="shard_check", action="store_false",
                     help="N > 1: skip rank 0's single-GPU re-evaluation of every rank's block")
     ap.add_argument("--e2e-large", type=int, default=8,
@@ -239,9 +247,11 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
     if args.cpu_threads is None:
-        # every CPU this process may run on (all cores), whatever
-        # OMP_NUM_THREADS the box exports
-        args.cpu_threads = len(os.sched_getaffinity(0))
+        # every CPU this process may use (all cores), whatever
+        # OMP_NUM_THREADS the box exports: the affinity mask, capped by the
+        # cgroup CPU bandwidth quota (a 16-CPU quota over 256 visible CPUs on the
+        # GPU box: 256 threads there run 3.5x slower than 16, time-sliced)
+        args.cpu_threads = cpu_share()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -543,7 +553,8 @@ def main():
                                "kind": "port", "host": host_info(),
                                "sample": f"first {n} of the {N} candidates (mask + h200 rollouts of the "
                                          f"collision-free ones), oracle/ C restatement, OpenMP "
-                                         f"{args.cpu_threads} threads (every CPU in the affinity mask), "
+                                         f"{args.cpu_threads} threads (every CPU of the affinity mask within "
+                                         f"the cgroup CPU quota), "
                                          f"{cb['seconds']:.1f} s",
                                "labels_identical_to_gpu": agree,
                                "one_thread": {"value": c1["value"], "unit": "candidates/s", "cores": 1,
