@@ -1645,6 +1645,15 @@ DEVI int bb_clip(P2* Q, int nq, int axis, double lim, double sgn, P2* buf) {
   return no;
 }
 
+// column k (a box axis) of a geom rotation matrix held in LDS, for a k that
+// differs between lanes or is only known in lane 0: a per-lane LDS read, where
+// indexing a register copy with it would go through scratch memory
+DEVI void lds_col(const double* R, int k, double* r) {
+  r[0] = R[k];
+  r[1] = R[3 + k];
+  r[2] = R[6 + k];
+}
+
 DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
   int lane = lane_id();
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
@@ -1660,19 +1669,24 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
   double s = -INFINITY, L[3] = {0.0, 0.0, 0.0};
   int valid = 0;
   if (lane < 3) {
-    const double* Lf = A1 + 3 * lane;
+    double Lf[3];
+    lds_col(R1, lane, Lf);
     double r2 = (h2[0] * fabs(dot3(A2, Lf)) + h2[1] * fabs(dot3(A2 + 3, Lf))) + h2[2] * fabs(dot3(A2 + 6, Lf));
     s = fabs(dot3(D, Lf)) - (h1[lane] + r2);
     valid = 1;
   } else if (lane < 6) {
     int k = lane - 3;
-    const double* Lf = A2 + 3 * k;
+    double Lf[3];
+    lds_col(R2, k, Lf);
     double r1 = (h1[0] * fabs(dot3(A1, Lf)) + h1[1] * fabs(dot3(A1 + 3, Lf))) + h1[2] * fabs(dot3(A1 + 6, Lf));
     s = fabs(dot3(D, Lf)) - (h2[k] + r1);
     valid = 1;
   } else if (lane < 15) {
     int a = (lane - 6) / 3, b = (lane - 6) % 3;
-    cross3(L, A1 + 3 * a, A2 + 3 * b);
+    double Ra[3], Rb[3];
+    lds_col(R1, a, Ra);
+    lds_col(R2, b, Rb);
+    cross3(L, Ra, Rb);
     double ll = sqrt(dot3(L, L));
     if (!(ll < 1e-6)) {
       L[0] = L[0] / ll; L[1] = L[1] / ll; L[2] = L[2] / ll;
@@ -1709,6 +1723,7 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
       double n[3] = {eL[0], eL[1], eL[2]};
       if (dot3(n, D) < 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
       double e1[3] = {x1[0], x1[1], x1[2]}, e2[3] = {x2[0], x2[1], x2[2]};
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         if (k != a) {
           double sg = dot3(A1 + 3 * k, n) >= 0.0 ? h1[k] : -h1[k];
@@ -1719,7 +1734,9 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
           for (int i = 0; i < 3; i++) e2[i] = e2[i] + sg * A2[3 * k + i];
         }
       }
-      const double *U = A1 + 3 * a, *V = A2 + 3 * b;
+      double U[3], V[3];
+      lds_col(R1, a, U);
+      lds_col(R2, b, V);
       double w[3];
       sub3(w, e1, e2);
       double bu = dot3(U, V), du = dot3(U, w), ev = dot3(V, w);
@@ -1735,23 +1752,38 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
       add_contact(d, ncmax, pair, g1, g2, pos, n, t1, t2, ebest);
     } else {
       int ref1 = code < 3, k = code % 3;
-      const double *RA = ref1 ? A1 : A2, *RB = ref1 ? A2 : A1, *hA = ref1 ? h1 : h2, *hB = ref1 ? h2 : h1;
+      // reference / incident box rotations (LDS) and their axes by column reads
+      const double *RA = ref1 ? R1 : R2, *RB = ref1 ? R2 : R1;
+      const double *hA = ref1 ? h1 : h2, *hB = ref1 ? h2 : h1;
       const double *xA = ref1 ? x1 : x2, *xB = ref1 ? x2 : x1;
       double DAB[3];
       sub3(DAB, xB, xA);
-      double nr[3] = {RA[3 * k], RA[3 * k + 1], RA[3 * k + 2]};
+      double nr[3];
+      lds_col(RA, k, nr);
       if (dot3(DAB, nr) < 0.0) { nr[0] = -nr[0]; nr[1] = -nr[1]; nr[2] = -nr[2]; }
       double n[3] = {nr[0], nr[1], nr[2]};
       if (!ref1) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
       int ku = (k + 1) % 3, kv = (k + 2) % 3;
-      const double *u = RA + 3 * ku, *v = RA + 3 * kv;
+      double u[3], v[3];
+      lds_col(RA, ku, u);
+      lds_col(RA, kv, v);
       double cA[3];
       for (int i = 0; i < 3; i++) cA[i] = xA[i] + hA[k] * nr[i];
       int j = 0;
-      double bj = fabs(dot3(RB, nr));
-      for (int q = 1; q < 3; q++) { double c = fabs(dot3(RB + 3 * q, nr)); if (c > bj) { bj = c; j = q; } }
-      double sB = dot3(RB + 3 * j, nr) > 0.0 ? -hB[j] : hB[j];
+      double Bc[3];
+      lds_col(RB, 0, Bc);
+      double bj = fabs(dot3(Bc, nr));
+      for (int q = 1; q < 3; q++) {
+        lds_col(RB, q, Bc);
+        double c = fabs(dot3(Bc, nr));
+        if (c > bj) { bj = c; j = q; }
+      }
+      double Bj[3], Bp[3], Bq[3];
       int jp = (j + 1) % 3, jq = (j + 2) % 3;
+      lds_col(RB, j, Bj);
+      lds_col(RB, jp, Bp);
+      lds_col(RB, jq, Bq);
+      double sB = dot3(Bj, nr) > 0.0 ? -hB[j] : hB[j];
       P2* poly = d.poly;
       P2* buf = d.poly + 16;
       P2* pts = d.poly + 32;
@@ -1761,7 +1793,7 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
         double cp = (c == 0 || c == 3) ? 1.0 : -1.0, cq = (c < 2) ? 1.0 : -1.0;
         double P[3], rel[3];
         for (int i = 0; i < 3; i++)
-          P[i] = ((xB[i] + sB * RB[3 * j + i]) + (cp * hB[jp]) * RB[3 * jp + i]) + (cq * hB[jq]) * RB[3 * jq + i];
+          P[i] = ((xB[i] + sB * Bj[i]) + (cp * hB[jp]) * Bp[i]) + (cq * hB[jq]) * Bq[i];
         sub3(rel, P, cA);
         poly[c].x = dot3(rel, u);
         poly[c].y = dot3(rel, v);
@@ -1821,10 +1853,18 @@ OBB_FN int obb_separated(const double* R1, const double* x1, const double* b1, c
   for (int k = 0; k < 3; k++)
     for (int i = 0; i < 3; i++) { A1[3 * k + i] = R1[3 * i + k]; A2[3 * k + i] = R2[3 * i + k]; }
   for (int q = 0; q < 15; q++) {
+    // the axis by cases on q, each with constant indices, so A1 / A2 stay in
+    // registers (a computed index would address them through scratch)
     double L[3];
-    if (q < 3) { L[0] = A1[3 * q]; L[1] = A1[3 * q + 1]; L[2] = A1[3 * q + 2]; }
-    else if (q < 6) { L[0] = A2[3 * (q - 3)]; L[1] = A2[3 * (q - 3) + 1]; L[2] = A2[3 * (q - 3) + 2]; }
-    else { int a = (q - 6) / 3, b = (q - 6) % 3; cross3(L, A1 + 3 * a, A2 + 3 * b); }
+    switch (q) {
+#define OBB_F(Q, A, K) case Q: L[0] = A[3 * K]; L[1] = A[3 * K + 1]; L[2] = A[3 * K + 2]; break;
+#define OBB_E(Q, a, b) case Q: cross3(L, A1 + 3 * a, A2 + 3 * b); break;
+      OBB_F(0, A1, 0) OBB_F(1, A1, 1) OBB_F(2, A1, 2) OBB_F(3, A2, 0) OBB_F(4, A2, 1) OBB_F(5, A2, 2)
+      OBB_E(6, 0, 0) OBB_E(7, 0, 1) OBB_E(8, 0, 2) OBB_E(9, 1, 0) OBB_E(10, 1, 1) OBB_E(11, 1, 2)
+      OBB_E(12, 2, 0) OBB_E(13, 2, 1) default: cross3(L, A1 + 6, A2 + 6); break;
+#undef OBB_F
+#undef OBB_E
+    }
     double ll = dot3(L, L);
     if (ll < 1e-20) continue;
     double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));

@@ -208,6 +208,11 @@ class Engine:
             specialize = {"1": True, "0": False}.get(os.environ.get("MGS_SPECIALIZE", "cached"), "cached")
         if not self.lib.mgs_supports_nv(cm.nv):
             specialize = True
+        if specialize and os.environ.get("MGS_SPECIAL_OBJECT"):
+            # A/B experiments (tools/ab_special.sh): an explicit object, used by
+            # the engines whose model it was made for (the attach checks that)
+            if self.lib.mgs_model_attach_special(self._model, os.environ["MGS_SPECIAL_OBJECT"].encode()) == 0:
+                specialize = False
         if specialize:
             from mgs.core import special
             path = special.code_object(self.lib, self.desc, compile=specialize is True)

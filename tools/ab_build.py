@@ -1,0 +1,32 @@
+"""Build the headline engine's specialised code object from the working tree's
+kernel sources into mj-grasp-sim_amd/mgs/_lib/ab/<name>.hsaco (A/B experiments,
+tools/ab_special.sh).  Usage: python tools/ab_build.py name [-DFLAG ...]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mj-grasp-sim_amd")]
+
+
+def main():
+    import numpy as np
+    from mgs.core import abi, special
+    from mgs.core.engine import library_for
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
+    from mgs.obj.selector import get_object
+    from mgs.util.geo.transforms import SE3Pose
+    env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
+                                    get_object("003_cracker_box"))
+    fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+    lib = library_for(env.model.nv, int(fields["nefc_max"]))
+    header, flags, _ = special.plan(lib, abi.make_desc(fields))
+    out = os.path.join(special.CACHE, "..", "ab")
+    os.makedirs(out, exist_ok=True)
+    path = os.path.abspath(os.path.join(out, sys.argv[1] + ".hsaco"))
+    special.compile_object(header, flags + sys.argv[2:], path)
+    print(path)
+
+
+if __name__ == "__main__":
+    main()
