@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 13
+#define MGS_ABI_VERSION 14
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -188,6 +188,8 @@ typedef struct mgs_model_desc {
   int32_t d_geom_aabb;      /* 6: local box center (3), half sizes (3) */
   int32_t d_geom_radius;    /* 1: rounding radius; the geom is its hull (+) a ball of this
                                radius (sphere: 1 vertex, capsule: 2 vertices on z; 0 otherwise) */
+  int32_t d_geom_rbound;    /* 1: largest vertex norm of the geom's hull (geom frame): bounds how
+                               far a rotation moves its supports (separation certificates) */
   /* convex hulls */
   int32_t i_hull_vertadr;
   int32_t i_hull_vertnum;

@@ -54,7 +54,7 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   sizes[L_act_force] = nu; sizes[L_act_moment] = nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
   sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = 5 * nc;
   sizes[L_con_blk] = BLKSTRIDE * nc;
-  sizes[L_efc_R] = ne; sizes[L_efc_b] = ne;
+  sizes[L_efc_R] = ne; sizes[L_efc_b] = ne; sizes[L_cert] = K_CERT * CERT_W;
   // U: per-stage sub-layouts, each packed from offset 0 (see the kernel's Lay comment)
   int us[U_COUNT];
   for (int k = 0; k < U_COUNT; k++) us[k] = 0;

@@ -31,6 +31,12 @@
 #define K_MPR_MAXIT 64
 #define K_FEAT_EPS 1e-5
 #define K_BB_MERGE 1e-6     // box-box: merge distance of manifold points, x face half size (oracle BB_MERGE)
+// separation certificates (cert_check): slots per candidate, doubles per slot,
+// the least margin worth keeping and the safety margin of the validity test
+#define K_CERT 8
+#define CERT_W 17
+#define CERT_STORE 1e-6
+#define CERT_EPS 1e-10
 #define WAVE 64
 // row stride of the constraint matrix G (doubles).  An odd stride (NV + 1) makes
 // row walks bank-conflict free but measured no faster and costs 680 B of LDS
@@ -73,6 +79,7 @@ struct Dat {
   double *act_force, *act_moment, *act_length, *act_vel;
   double *con_pos, *con_frame, *con_dist;
   double *efc_R, *efc_b, *con_mu, *con_blk;
+  double* cert;     // separation certificates (K_CERT slots of CERT_W doubles, see cert_check)
   // U region views
   double *crb, *cvel, *cacc, *cfrc, *cdof_dot;          // dynamics stage
   P2* poly;                                           // collision stage
@@ -97,10 +104,12 @@ struct Dat {
 // NV-long operand rows of the triangular solves / G products held in registers
 // (main build) or read from LDS at each use (wide build: nv up to 58 would
 // spill them to scratch).  Same values either way.
+#ifndef MGS_REG_ROWS
 #ifdef MGS_WIDE
 #define MGS_REG_ROWS 0
 #else
 #define MGS_REG_ROWS 1
+#endif
 #endif
 
 DEVI int lane_id() { return (int)__lane_id(); }
@@ -1044,8 +1053,13 @@ DEVI int portal_choose(const SupPt& p0, const SupPt& p1, const SupPt& p2, const 
     else p3 = p4;                                     \
   } while (0)
 
+// On a miss that is certified by a separating direction (the support of the
+// Minkowski difference along dir is <= 0), *cm = -h(dir) >= 0 and cd = dir
+// (unit, world); else *cm = -1.
+#define MPR_CERT(P) do { *cm = -dot3((P).v, dir); cd[0] = dir[0]; cd[1] = dir[1]; cd[2] = dir[2]; } while (0)
 DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1, int g2, double* n, double* depth,
-                         double* pos) {
+                         double* pos, double* cd, double* cm) {
+  *cm = -1.0;
   const double tol = md.m.mpr_tolerance;
   const int32_t* ghull = IA(md, geom_hullid);
   const double* HC = DA(md, hull_center);
@@ -1060,7 +1074,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1,
   dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
   normalize3(dir);
   mink_support(pc, dir, &p1);
-  if (dot3(p1.v, dir) <= 0.0) return 0;
+  if (dot3(p1.v, dir) <= 0.0) { MPR_CERT(p1); return 0; }
   cross3(dir, p0.v, p1.v);
   if (dot3(dir, dir) < 1e-30) {
     double nn = sqrt(dot3(p1.v, p1.v));
@@ -1072,7 +1086,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1,
   }
   normalize3(dir);
   mink_support(pc, dir, &p2);
-  if (dot3(p2.v, dir) <= 0.0) return 0;
+  if (dot3(p2.v, dir) <= 0.0) { MPR_CERT(p2); return 0; }
   {
     double e1[3], e2[3];
     sub3(e1, p1.v, p0.v);
@@ -1087,7 +1101,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1,
   int it;
   for (it = 0; it < K_MPR_MAXIT; it++) {
     mink_support(pc, dir, &p3);
-    if (dot3(p3.v, dir) <= 0.0) return 0;
+    if (dot3(p3.v, dir) <= 0.0) { MPR_CERT(p3); return 0; }
     double c[3];
     int cont = 0;
     cross3(c, p1.v, p3.v);
@@ -1108,7 +1122,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1,
     portal_normal(dir, &p1, &p2, &p3);
     if (dot3(dir, p1.v) >= 0.0) break;
     mink_support(pc, dir, &p4);
-    if (dot3(p4.v, dir) < 0.0) return 0;
+    if (dot3(p4.v, dir) < 0.0) { MPR_CERT(p4); return 0; }
     if (portal_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) return 0;
     PORTAL_EXPAND(p0, p1, p2, p3, p4);
   }
@@ -1140,6 +1154,8 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1,
     PORTAL_EXPAND(p0, p1, p2, p3, p4);
   }
 }
+
+#undef MPR_CERT
 
 DEVI void make_frame(const double* n, double* t1, double* t2) {
   double a[3];
@@ -1528,18 +1544,128 @@ DEVI void add_contact(Dat& d, int ncon_max, int pair, int g1, int g2, const doub
   d.con_g2[c] = g2;
 }
 
+// ---------------------------------------------------------------------------
+// Separation certificates (oracle cert_*).  A convex pair whose MPR missed
+// with a separating direction d (world, unit) -- the Minkowski difference
+// g1 - g2 has support -m < 0 along d -- stays separated while the motion of g1
+// relative to g2 cannot close the margin: in g2's frame the supports of g2 do
+// not change and those of g1 along d_B (d in g2's frame) grow by at most
+// d_B . dp + ||dR||_F rho_1 (dp, dR: change of g1's origin and rotation in
+// g2's frame since the certifying step, rho_1 the largest vertex norm of g1's
+// hull; a rounding ball adds the same term before and after).  A certified pair
+// is skipped by the narrowphase: MPR would miss it again, so the contacts are
+// the ones MuJoCo finds.  Slot (CERT_W doubles): pair, m, d_B (3), g1's origin
+// (3) and rotation (9) in g2's frame at the certifying step; pair -1 = free.
+DEVI void rel_pose(const Dat& d, int g1, int g2, double* p, double* R) {
+  const double *R1 = d.geom_xmat + 9 * g1, *R2 = d.geom_xmat + 9 * g2;
+  double dx[3];
+  sub3(dx, d.geom_xpos + 3 * g1, d.geom_xpos + 3 * g2);
+  mulmtv3(p, R2, dx);
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) R[3 * i + j] = (R2[i] * R1[j] + R2[3 + i] * R1[3 + j]) + R2[6 + i] * R1[6 + j];
+}
+
+DEVI int cert_ok(const Mdl& md, const Dat& d, const double* c) {
+  int pair = (int)c[0];
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  double p[3], R[9], dp[3];
+  rel_pose(d, g1, g2, p, R);
+  sub3(dp, p, c + 5);
+  double f = 0.0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    double e = R[k] - c[8 + k];
+    f = f + e * e;
+  }
+  double grow = dot3(c + 2, dp) + sqrt(f) * DA(md, geom_rbound)[g1];
+  return c[1] - grow > CERT_EPS;
+}
+
+// before a pair chunk's narrowphase (lanes < K_CERT over the slots): slots of
+// the chunk's pairs that left the broadphase set are freed, the others tested;
+// returns the chunk bits of the certified pairs
+DEVI unsigned long long cert_check(const Mdl& md, Dat& d, int c0, unsigned long long ov) {
+  int lane = lane_id();
+  int ok = 0, bit = 0;
+  if (lane < K_CERT) {
+    double* c = d.cert + CERT_W * lane;
+    int pr = (int)c[0];
+    if (pr >= c0 && pr < c0 + WAVE) {
+      bit = pr - c0;
+      if (!((ov >> bit) & 1ull)) c[0] = -1.0;
+      else ok = cert_ok(md, d, c);
+    }
+  }
+  unsigned long long okm = __ballot(ok), skip = 0ull;
+  while (okm) {
+    int l = __ffsll((long long)okm) - 1;
+    okm &= okm - 1ull;
+    skip |= 1ull << __builtin_amdgcn_readlane(bit, l);
+  }
+  wsync();
+  PCNT(58, __popcll(skip));
+#ifdef MGS_NO_CERT
+  skip = 0ull;      // A/B experiments: certificates kept but not used
+#endif
+  return skip;
+}
+
+// after a convex pair's MPR: a certified miss (margin > CERT_STORE) goes to
+// the pair's slot or the first free one; a hit or an uncertified miss frees the
+// pair's slot
+DEVI void cert_update(const Mdl& md, Dat& d, int pair, int g1, int g2, int hit, const double* cd, double cm) {
+  int lane = lane_id();
+  int pr = lane < K_CERT ? (int)d.cert[CERT_W * lane] : 0;
+  unsigned long long mine = __ballot(lane < K_CERT && pr == pair);
+  unsigned long long freem = __ballot(lane < K_CERT && pr < 0);
+  int keep = !hit && cm > CERT_STORE;
+  int sl = mine ? __ffsll((long long)mine) - 1 : ((keep && freem) ? __ffsll((long long)freem) - 1 : -1);
+  if (sl < 0) return;
+  wsync();
+  if (lane == 0) {
+    double* c = d.cert + CERT_W * sl;
+    if (!keep) {
+      c[0] = -1.0;
+    } else {
+      double p[3], R[9], db[3];
+      rel_pose(d, g1, g2, p, R);
+      mulmtv3(db, d.geom_xmat + 9 * g2, cd);
+      c[0] = (double)pair;
+      c[1] = cm;
+      c[2] = db[0]; c[3] = db[1]; c[4] = db[2];
+      c[5] = p[0]; c[6] = p[1]; c[7] = p[2];
+      for (int k = 0; k < 9; k++) c[8 + k] = R[k];
+    }
+  }
+  wsync();
+}
+
 // narrowphase of one admissible pair, all lanes participate
 DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   int lane = lane_id();
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
   double n[3], depth, mpos[3];
   PairCtx pc;
+#ifdef MGS_PROFILE
+  // diagnostic split of the narrowphase between missed and hit pairs: ticks
+  // from here to the MPR verdict (54 miss / 55 hit) and support calls (56 / 57)
+  unsigned long long t_pair = __builtin_amdgcn_s_memtime();
+  unsigned long long sc0 = s_prof[28];
+#endif
   pair_ctx(md, d, g1, g2, pc);
-  int hit = mpr_penetration(md, d, pc, g1, g2, n, &depth, mpos);
+  double cd[3] = {0.0, 0.0, 0.0}, cm;
+  int hit = mpr_penetration(md, d, pc, g1, g2, n, &depth, mpos, cd, &cm);
+  cert_update(md, d, pair, g1, g2, hit, cd, cm);
   PT(4);
   PCNT(26, 1);
   PCNT(27, hit);
   PCNT(30, (pc.n1 > WAVE) + (pc.n2 > WAVE));
+#ifdef MGS_PROFILE
+  PCNT(hit ? 55 : 54, __builtin_amdgcn_s_memtime() - t_pair);
+  PCNT(hit ? 57 : 56, s_prof[28] - sc0);
+#endif
   if (!hit) return;
   double t1[3], t2[3];
   make_frame(n, t1, t2);
@@ -1906,6 +2032,7 @@ DEVI void collision(const Mdl& md, Dat& d) {
         ov = 0;
     }
     unsigned long long mask = __ballot(ov);
+    mask &= ~cert_check(md, d, c0, mask);
     PT(3);
     while (mask) {
       int b = __ffsll((long long)mask) - 1;
@@ -1931,7 +2058,7 @@ enum {
   L_qfrc_smooth, L_qacc_smooth, L_qfrc_constraint,
   L_act_force, L_act_moment, L_act_length, L_act_vel,
   L_con_pos, L_con_frame, L_con_dist, L_con_mu, L_con_blk,
-  L_efc_R, L_efc_b,
+  L_efc_R, L_efc_b, L_cert,
   L_U, L_ints, L_COUNT
 };
 enum {
@@ -1980,7 +2107,7 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   B(qfrc_smooth); B(qacc_smooth); B(qfrc_constraint);
   B(act_force); B(act_moment); B(act_length); B(act_vel);
   B(con_pos); B(con_frame); B(con_dist); B(con_mu); B(con_blk);
-  B(efc_R); B(efc_b);
+  B(efc_R); B(efc_b); B(cert);
 #undef B
   double* U = s + LO(L_U);
 #define BU(f, k) d.f = U + LU(k)
@@ -3686,19 +3813,49 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   PT(12);
   int npair = (nv * (nv + 1)) / 2;
   int it;
+  // row states of the last Hessian build (rows lane, lane + 64, ...)
+  int st_built[MGS_RPL];
+  bool built = false;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
-    // Hessian I + G' W G on the matrix cores.  W is block diagonal (Dr on quad
-    // rows, the cone Hessian on cone blocks, 0 on inactive rows); X = W G row
-    // by row (x = 0.0 + sum_a G_{lead+a,i} w_a), then H_ij = (i == j) +
-    // sum_r G_rj X_ri as v_mfma_f64_16x16x4 k-steps over 4 rows at a time: an
-    // fma chain over the rows in ascending order, which the oracle restates.
-    // Lane l takes row 4s + (l >> 4) of k-step s and column (l & 15) + 16 t.
-    hessian_mfma<NV>(md, d, ne);
-    PT(23);
-    {
+    // H depends on the iteration only through the row states and, on cone
+    // blocks, the forces: when no row changed state since the last build and
+    // none is on a cone, the rebuilt H and its factor would be the same
+    // numbers, so the factor in nH / tmp / tmp2 is kept (the oracle rebuilds;
+    // the results are identical)
+    bool rebuild = true;
+    if (built) {
+      int diff = 0;
+#pragma unroll
+      for (int h = 0; h < MGS_RPL; h++) {
+        int r = lane + h * WAVE;
+        if (r < ne) {
+          int st = d.efc_state[r];
+          if (st != st_built[h] || st == ST_CONE) diff = 1;
+        }
+      }
+      rebuild = __ballot(diff) != 0ull;
+    }
+    if (rebuild) {
+#pragma unroll
+      for (int h = 0; h < MGS_RPL; h++) {
+        int r = lane + h * WAVE;
+        st_built[h] = r < ne ? d.efc_state[r] : ST_OFF;
+      }
+      built = true;
+      // Hessian I + G' W G on the matrix cores.  W is block diagonal (Dr on quad
+      // rows, the cone Hessian on cone blocks, 0 on inactive rows); X = W G row
+      // by row (x = 0.0 + sum_a G_{lead+a,i} w_a), then H_ij = (i == j) +
+      // sum_r G_rj X_ri as v_mfma_f64_16x16x4 k-steps over 4 rows at a time: an
+      // fma chain over the rows in ascending order, which the oracle restates.
+      // Lane l takes row 4s + (l >> 4) of k-step s and column (l & 15) + 16 t.
+      hessian_mfma<NV>(md, d, ne);
+      PT(23);
       PT(24);
       ldl_factor<NV>(d.nH, d.tmp, d.tmp2);
       PT(25);
+      PCNT(51, 1);
+    } else {
+      PCNT(52, 1);
     }
     PT(13);
     ldl_solve<NV>(d.nH, d.tmp2, d.ng, d.ndir);
@@ -3980,6 +4137,7 @@ DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mp
     d.time[0] = 0.0;
     for (int k = 0; k < 16; k++) d.ints[k] = 0;
   }
+  if (lane < K_CERT) d.cert[CERT_W * lane] = -1.0;
   wsync();
 }
 

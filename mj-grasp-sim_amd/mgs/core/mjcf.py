@@ -921,6 +921,8 @@ class Compiler:
             aabb.append(np.concatenate([(lo + hi) / 2, (hi - lo) / 2]))
         cm.geom_aabb = np.array(aabb).reshape(-1, 6)
         cm.geom_radius = np.array([g["radius"] for g in cgeoms], np.float64)
+        cm.geom_rbound = np.array([float(np.max(np.linalg.norm(hulls[g["hull"]], axis=1)))
+                                   for g in cgeoms], np.float64)
         cm.hull_vertnum = np.array([len(h) for h in hulls], np.int32)
         cm.hull_vertadr = np.concatenate([[0], np.cumsum(cm.hull_vertnum)[:-1]]).astype(np.int32) if hulls else np.zeros(0, np.int32)
         cm.hull_vert = np.concatenate(hulls).reshape(-1, 3) if hulls else np.zeros((0, 3))
@@ -1122,7 +1124,7 @@ class CompiledModel:
               else np.zeros(self.nv))
         for n in ["geom_bodyid", "geom_hullid", "geom_side"]:
             put_i(n, getattr(self, n))
-        for n in ["geom_pos", "geom_quat", "geom_aabb", "geom_radius"]:
+        for n in ["geom_pos", "geom_quat", "geom_aabb", "geom_radius", "geom_rbound"]:
             put_d(n, getattr(self, n))
         put_i("hull_vertadr", self.hull_vertadr)
         put_i("hull_vertnum", self.hull_vertnum)

@@ -45,6 +45,12 @@
 #ifndef BB_MERGE
 #define BB_MERGE 1e-6       /* box-box: merge distance of manifold points, x face half size */
 #endif
+/* separation certificates (kernel cert_*): slots, doubles per slot, least
+ * margin kept, validity safety margin */
+#define O_CERT 8
+#define O_CERT_W 17
+#define O_CERT_STORE 1e-6
+#define O_CERT_EPS 1e-10
 
 /* ------------------------------------------------------------------------ */
 typedef struct {
@@ -82,6 +88,7 @@ typedef struct {
   double *Dv, *sD, *isD;
   int *efc_type, *efc_dim, *efc_con;
   double *w;
+  double* cert;      /* O_CERT separation certificate slots */
   int overflow;
   int iters;
 } Dat;
@@ -265,6 +272,7 @@ static Dat* dat_alloc(const Mdl* md) {
   TAKE(efc_mu, 5 * ne); TAKE(efc_blk, 36 * ne); TAKE(efc_hb, 36 * ne); TAKE(efc_dA, ne); TAKE(efc_floss, ne); TAKE(w, nv);
   TAKE(efc_AR, ne); TAKE(efc_ARinv, ne); TAKE(efc_Ainv, ne); TAKE(Dv, nv); TAKE(sD, nv); TAKE(isD, nv);
   TAKE(efc_Dr, ne); TAKE(efc_sqR, ne); TAKE(efc_isR, ne); TAKE(efc_mup, ne); TAKE(efc_k1, ne); TAKE(efc_jar, ne); TAKE(efc_jv, ne); TAKE(hX, ne * nv);
+  TAKE(cert, O_CERT * O_CERT_W);
 #undef TAKE
   if (pass == 0) base = (double*)calloc(tot, sizeof(double));
   }
@@ -694,8 +702,12 @@ static void portal_expand(SupPt* p0, SupPt* p1, SupPt* p2, SupPt* p3, const SupP
 /* Minkowski Portal Refinement (penetration variant, as in libccd, which
  * MuJoCo 3.2.x uses for convex mesh collisions).  Returns 1 on penetration
  * with unit normal n (from geom g1 towards g2), depth > 0 and point pos. */
+/* On a miss certified by a separating direction (support of the Minkowski
+ * difference along dir <= 0): *cm = -h(dir) >= 0, cd = dir; else *cm = -1. */
+#define MPR_CERT(P) do { *cm = -dot3((P).v, dir); cd[0] = dir[0]; cd[1] = dir[1]; cd[2] = dir[2]; } while (0)
 static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* n, double* depth,
-                           double* pos) {
+                           double* pos, double* cd, double* cm) {
+  *cm = -1.0;
   const double tol = md->m->mpr_tolerance;
   const int32_t* ghull = IA(md, geom_hullid);
   const double* HC = DA(md, hull_center);
@@ -711,7 +723,7 @@ static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* 
   normalize3(dir);
   mink_support(md, d, g1, g2, dir, &p1);
   if (g_sep_log && g_sep_n < 200000) { g_sep_val[g_sep_n] = dot3(p1.v, dir); g_sep_pair[g_sep_n] = g1 * 64 + g2; g_sep_n++; }
-  if (dot3(p1.v, dir) <= 0.0) return 0;
+  if (dot3(p1.v, dir) <= 0.0) { MPR_CERT(p1); return 0; }
   cross3(dir, p0.v, p1.v);
   if (dot3(dir, dir) < 1e-30) {
     /* origin on segment v0-v1 */
@@ -724,7 +736,7 @@ static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* 
   }
   normalize3(dir);
   mink_support(md, d, g1, g2, dir, &p2);
-  if (dot3(p2.v, dir) <= 0.0) return 0;
+  if (dot3(p2.v, dir) <= 0.0) { MPR_CERT(p2); return 0; }
   {
     double e1[3], e2[3];
     sub3(e1, p1.v, p0.v);
@@ -739,7 +751,7 @@ static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* 
   int it;
   for (it = 0; it < O_MPR_MAXIT; it++) {
     mink_support(md, d, g1, g2, dir, &p3);
-    if (dot3(p3.v, dir) <= 0.0) return 0;
+    if (dot3(p3.v, dir) <= 0.0) { MPR_CERT(p3); return 0; }
     double c[3];
     int cont = 0;
     cross3(c, p1.v, p3.v);
@@ -761,7 +773,7 @@ static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* 
     portal_normal(dir, &p1, &p2, &p3);
     if (dot3(dir, p1.v) >= 0.0) break;
     mink_support(md, d, g1, g2, dir, &p4);
-    if (dot3(p4.v, dir) < 0.0) return 0;
+    if (dot3(p4.v, dir) < 0.0) { MPR_CERT(p4); return 0; }
     if (portal_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) return 0;
     portal_expand(&p0, &p1, &p2, &p3, &p4);
   }
@@ -794,6 +806,8 @@ static int mpr_penetration(const Mdl* md, const Dat* d, int g1, int g2, double* 
     portal_expand(&p0, &p1, &p2, &p3, &p4);
   }
 }
+
+#undef MPR_CERT
 
 static void make_frame(const double* n, double* t1, double* t2) {
   double a[3];
@@ -992,11 +1006,86 @@ static void add_contact(const Mdl* md, Dat* d, int pair, int g1, int g2, const d
   d->con_g2[c] = g2;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Separation certificates (kernel cert_check / cert_update).  A convex pair
+ * whose MPR missed with separating direction d (the Minkowski difference
+ * g1 - g2 has support -m < 0 along d) stays separated while the motion of g1
+ * relative to g2 cannot close the margin: in g2's frame the supports of g2 are
+ * fixed and those of g1 along d_B grow by at most d_B . dp + ||dR||_F rho_1.
+ * Certified pairs skip the narrowphase (MPR would miss them again).  Slot:
+ * pair, m, d_B (3), g1's origin (3) and rotation (9) in g2's frame at the
+ * certifying step; pair -1 = free.  oracle_set_cull(0) turns the skipping off
+ * (tests: the contacts are the same either way). */
+static int g_nocull = 0;
+void oracle_set_cull(int on) { g_nocull = on ? 0 : 1; }
+static void rel_pose(const Dat* d, int g1, int g2, double* p, double* R) {
+  const double *R1 = d->geom_xmat + 9 * g1, *R2 = d->geom_xmat + 9 * g2;
+  double dx[3];
+  sub3(dx, d->geom_xpos + 3 * g1, d->geom_xpos + 3 * g2);
+  mulmtv3(p, R2, dx);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) R[3 * i + j] = (R2[i] * R1[j] + R2[3 + i] * R1[3 + j]) + R2[6 + i] * R1[6 + j];
+}
+
+static int cert_ok(const Mdl* md, const Dat* d, const double* c) {
+  int pair = (int)c[0];
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  double p[3], R[9], dp[3];
+  rel_pose(d, g1, g2, p, R);
+  sub3(dp, p, c + 5);
+  double f = 0.0;
+  for (int k = 0; k < 9; k++) {
+    double e = R[k] - c[8 + k];
+    f = f + e * e;
+  }
+  double grow = dot3(c + 2, dp) + sqrt(f) * DA(md, geom_rbound)[g1];
+  return c[1] - grow > O_CERT_EPS;
+}
+
+/* slots of the pairs [c0, c0 + 64): freed if the pair left the broadphase set
+ * (ov bits), else tested; returns the bits of the certified pairs */
+static unsigned long long cert_check(const Mdl* md, Dat* d, int c0, unsigned long long ov) {
+  unsigned long long skip = 0ull;
+  for (int k = 0; k < O_CERT; k++) {
+    double* c = d->cert + O_CERT_W * k;
+    int pr = (int)c[0];
+    if (pr < c0 || pr >= c0 + 64) continue;
+    int bit = pr - c0;
+    if (!((ov >> bit) & 1ull)) c[0] = -1.0;
+    else if (cert_ok(md, d, c)) skip |= 1ull << bit;
+  }
+  return g_nocull ? 0ull : skip;
+}
+
+static void cert_update(const Mdl* md, Dat* d, int pair, int g1, int g2, int hit, const double* cd, double cm) {
+  int mine = -1, fr = -1;
+  for (int k = 0; k < O_CERT; k++) {
+    int pr = (int)d->cert[O_CERT_W * k];
+    if (pr == pair && mine < 0) mine = k;
+    if (pr < 0 && fr < 0) fr = k;
+  }
+  int keep = !hit && cm > O_CERT_STORE;
+  int sl = mine >= 0 ? mine : ((keep && fr >= 0) ? fr : -1);
+  if (sl < 0) return;
+  double* c = d->cert + O_CERT_W * sl;
+  if (!keep) { c[0] = -1.0; return; }
+  double p[3], R[9], db[3];
+  rel_pose(d, g1, g2, p, R);
+  mulmtv3(db, d->geom_xmat + 9 * g2, cd);
+  c[0] = (double)pair;
+  c[1] = cm;
+  c[2] = db[0]; c[3] = db[1]; c[4] = db[2];
+  c[5] = p[0]; c[6] = p[1]; c[7] = p[2];
+  for (int k = 0; k < 9; k++) c[8 + k] = R[k];
+}
+
 /* convex-convex narrowphase with multi-contact manifold (<= 4 points) */
 static void collide_pair(const Mdl* md, Dat* d, int pair) {
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
-  double n[3], depth, mpos[3];
-  if (!mpr_penetration(md, d, g1, g2, n, &depth, mpos)) return;
+  double n[3], depth, mpos[3], cd[3] = {0.0, 0.0, 0.0}, cm;
+  int hit = mpr_penetration(md, d, g1, g2, n, &depth, mpos, cd, &cm);
+  cert_update(md, d, pair, g1, g2, hit, cd, cm);
+  if (!hit) return;
   double t1[3], t2[3];
   make_frame(n, t1, t2);
   P2 fa[O_MAXF], fb[O_MAXF];
@@ -1257,7 +1346,12 @@ static void collision(const Mdl* md, Dat* d) {
   const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
   const double *aabb = DA(md, geom_aabb), *pm = DA(md, pair_margin);
   d->ncon = 0;
-  for (int p = 0; p < m->npair; p++) {
+  /* pairs in chunks of 64, as the kernel's lanes: broadphase of the chunk, the
+   * certificates of its pairs, then the narrowphase in pair order */
+  for (int c0 = 0; c0 < m->npair; c0 += 64) {
+  int cend = c0 + 64 < m->npair ? c0 + 64 : m->npair;
+  unsigned long long ovm = 0ull;
+  for (int p = c0; p < cend; p++) {
     int g[2] = {p1[p], p2[p]};
     double c[2][3], hw[2][3];
     for (int s = 0; s < 2; s++) {
@@ -1276,7 +1370,11 @@ static void collision(const Mdl* md, Dat* d) {
     if (ov && obb_separated(d->geom_xmat + 9 * g[0], d->geom_xpos + 3 * g[0], aabb + 6 * g[0],
                             d->geom_xmat + 9 * g[1], d->geom_xpos + 3 * g[1], aabb + 6 * g[1], pm[p]))
       ov = 0;
-    if (ov) {
+    if (ov) ovm |= 1ull << (p - c0);
+  }
+  unsigned long long skip = cert_check(md, d, c0, ovm);
+  for (int p = c0; p < cend; p++) {
+    if (((ovm & ~skip) >> (p - c0)) & 1ull) {
       if (p < 256) g_pair_bp[p]++;
       int n0 = d->ncon;
       long s0 = g_sup_calls;
@@ -1285,6 +1383,7 @@ static void collision(const Mdl* md, Dat* d) {
       if (p < 256) g_pair_sup[p] += g_sup_calls - s0;
       if (p < 256 && d->ncon > n0) g_pair_hit[p]++;
     }
+  }
   }
 }
 
@@ -2389,6 +2488,7 @@ static void reset(const Mdl* md, Dat* d, const double* qpos_init, const double* 
   d->time = 0.0;
   d->overflow = 0;
   d->iters = 0;
+  for (int k = 0; k < O_CERT; k++) d->cert[O_CERT_W * k] = -1.0;
 }
 
 /* ------------------------------------------------------------------------ */

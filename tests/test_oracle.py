@@ -157,3 +157,28 @@ def test_divergence_guard_oracle(env, candidates, oracle_model):
     clean = oracle_model.rollout(plan.subset([0, 3]))
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(clean[k], r[k][[0, 3]])
+
+
+@pytest.mark.parametrize("horizon,n", [("h200", 160), ("ref8000", 3)])
+def test_separation_certificates_are_exact(env, candidates, oracle_model, horizon, n):
+    """Pairs skipped by a separation certificate (kernel / oracle cert_check)
+    are pairs MPR would miss: rollouts with the skipping turned off give the
+    same labels, fail steps, object poses and contact / row statistics, bit
+    for bit, and the skipping removes narrowphase support calls"""
+    import ctypes
+    from conftest import plan_for
+    from oracle import oracle as O
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(oracle_model.collision_free(q, mp, mq, nthreads=8))[0][:n]
+    plan = plan_for(env, poses[idx], J[idx], horizon)
+    L = O.lib()
+    L.oracle_set_cull.argtypes = [ctypes.c_int]
+    try:
+        L.oracle_set_cull(0)
+        off = oracle_model.rollout(plan, nthreads=8)
+    finally:
+        L.oracle_set_cull(1)
+    on = oracle_model.rollout(plan, nthreads=8)
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(on[k], off[k]), k

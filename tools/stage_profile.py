@@ -33,10 +33,19 @@ def report(buf, r, ncand, horizon):
     c3 = np.array(buf[45:47], dtype=np.float64) / steps
     print('per candidate-step: ls_eval calls %.2f, newton_eval calls %.2f, noslip sweeps %.2f, '
           'qcqp iterations %.2f, block updates %.2f' % (*c2, *c3))
+    c4 = np.array(buf[51:58], dtype=np.float64)
+    print('per candidate-step: Newton Hessian builds %.2f, reused %.2f' % tuple(c4[:2] / steps))
+    if c4[3] + c4[4] > 0:
+        print('narrowphase MPR (incl. supports): missed pairs %.1f%% of ticks (%.2f support calls per step), '
+              'hit pairs %.1f%% (%.2f support calls per step)' % (100 * c4[3] / tot, c4[5] / steps,
+                                                                  100 * c4[4] / tot, c4[6] / steps))
 
 
 def main():
-    E.LIB_PATH = E.LIB_PATH.replace('libmgs_gpu.so', 'libmgs_gpu_prof.so')
+    """stage timers of the headline engine's specialised kernels: the profile
+    build of its code object (-DMGS_PROFILE, compiled if not cached) attached
+    in place of the product one"""
+    from mgs.core import special
     from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
     from mgs.obj.selector import get_object
     from mgs.util.geo.transforms import SE3Pose
@@ -49,17 +58,20 @@ def main():
     H, J, W = robotiq_candidates(obj, 4 * N, seed=2)
     poses = SE3Pose.from_mat(H)
     q, mp, mq, _ = env.initial_state(poses, J)
-    free = env.engine.collision_free(q, mp, mq)
+    eng = env.engine
+    free = eng.collision_free(q, mp, mq)
     idx = np.nonzero(free)[0][:N]
     h = HORIZONS['h200']
     plan = env.rollout_plan(poses[idx], J[idx], nstep_lift=h['nstep_lift'], shake_steps=h['shake_steps'],
                             close_steps=h['close_steps'], lift_check_every=h['lift_check_every'])
-    L = E.load_library()
-    L.mgs_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    path = special.code_object(eng.lib, eng.desc, profile=True)
+    eng._ck(eng.lib.mgs_model_attach_special(eng._model, path.encode()), 'mgs_model_attach_special')
+    L = eng.lib
+    L.mgs_model_prof_read.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
     buf = (ctypes.c_ulonglong * 64)()
-    L.mgs_prof_read(buf)
-    r = env.engine.rollout(plan)
-    L.mgs_prof_read(buf)
+    L.mgs_model_prof_read(eng._model, buf)
+    r = eng.rollout(plan)
+    eng._ck(L.mgs_model_prof_read(eng._model, buf), 'mgs_model_prof_read')
     report(buf, r, len(idx), 200)
 
 
