@@ -157,7 +157,7 @@ def default_rows(cm, worst: int) -> int:
 def auto_capacity(cm, ncon_max=20):
     """Constraint-row capacity for `ncon_max` contacts that keeps the most
     candidates in flight per CU: rows are shrunk from the worst case (every
-    contact at the largest condim) down to 3 rows per contact as long as that
+    contact at the largest condim) down to 2 rows per contact as long as that
     raises the per-CU occupancy.  Candidates that exceed a capacity are
     flagged by the kernel and re-run wider (GravitylessObjectGrasping.rollout)."""
     fields, _, _ = cm.pack(ncon_max=ncon_max)
@@ -165,7 +165,10 @@ def auto_capacity(cm, ncon_max=20):
     fixed = worst - ncon_max * (int(cm.pair_condim.max()) if len(cm.pair_condim) else 1)
     full = default_rows(cm, worst)
     best, best_occ = full, LDS_PER_CU // lds_bytes_for(cm, ncon_max, full)
-    floor = min(full, fixed + 3 * ncon_max)
+    # down to 2 rows per contact (a step with more rows than that is rare: the
+    # headline averages 26 rows at 4 contacts, and an overflowing candidate is
+    # continued wider from that step, GravitylessObjectGrasping.rollout)
+    floor = min(full, fixed + 2 * ncon_max)
     for ne in range(full - 1, floor - 1, -1):
         occ = LDS_PER_CU // lds_bytes_for(cm, ncon_max, ne)
         if occ > best_occ:
