@@ -880,19 +880,29 @@ DEVI void sup_init(SupAcc& a) { a.best = -INFINITY; a.bi = 0x7fffffff; a.vx = a.
 // the oracle's ascending scan.  Lane l holds vertices l, l+64, ..., so for a
 // hull of <= 64 vertices the lowest tied lane is the answer; larger hulls
 // compare the tied lanes' indices (exact ties only).
+// v_max_f64 without the operand canonicalisation __builtin_fmax adds (two
+// extra v_max per use): the support values are never signalling NaNs (they
+// come from arithmetic), for which both give the same result.  The s_nop
+// covers the VALU-write -> DPP-read wait states of the next reduction level
+// (the hazard recognizer does not look into inline asm).
+DEVI double max_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2\n\ts_nop 1" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 DEVI void sup_finish(SupAcc& a, double* v, int n) {
   int P = n < WAVE ? next_pow2(n) : WAVE;
   double m = a.best;
-  if (P > 1) m = __builtin_fmax(m, dpp_d(m, 0));
-  if (P > 2) m = __builtin_fmax(m, dpp_d(m, 1));
-  if (P > 4) m = __builtin_fmax(m, dpp_d(m, 2));
-  if (P > 8) m = __builtin_fmax(m, dpp_d(m, 3));
+  if (P > 1) m = max_f64(m, dpp_d(m, 0));
+  if (P > 2) m = max_f64(m, dpp_d(m, 1));
+  if (P > 4) m = max_f64(m, dpp_d(m, 2));
+  if (P > 8) m = max_f64(m, dpp_d(m, 3));
   double M = readlane_d(m, 0);
   if (P > 16) {
-    M = __builtin_fmax(M, readlane_d(m, 16));
+    M = max_f64(M, readlane_d(m, 16));
     if (P > 32) {
-      M = __builtin_fmax(M, readlane_d(m, 32));
-      M = __builtin_fmax(M, readlane_d(m, 48));
+      M = max_f64(M, readlane_d(m, 32));
+      M = max_f64(M, readlane_d(m, 48));
     }
   }
   unsigned long long tied = __ballot(a.bi != 0x7fffffff && a.best == M);
@@ -2871,8 +2881,10 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
 #pragma unroll
   for (int i = 0; i < DIM; i++) {
     g[i] = (lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
-    double jw = tree_sum(g[i] * u, P);
     old[i] = getf(F, r + i);
+    // noslip never reads the normal row's residual: its reduction is skipped
+    if (noslip && i == 0) { res[i] = 0.0; continue; }
+    double jw = tree_sum(g[i] * u, P);
     res[i] = noslip ? (jw + d.efc_b[r + i]) : ((jw + d.efc_R[r + i] * old[i]) + d.efc_b[r + i]);
   }
   PT(42);
@@ -3813,35 +3825,8 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   PT(12);
   int npair = (nv * (nv + 1)) / 2;
   int it;
-  // row states of the last Hessian build (rows lane, lane + 64, ...)
-  int st_built[MGS_RPL];
-  bool built = false;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
-    // H depends on the iteration only through the row states and, on cone
-    // blocks, the forces: when no row changed state since the last build and
-    // none is on a cone, the rebuilt H and its factor would be the same
-    // numbers, so the factor in nH / tmp / tmp2 is kept (the oracle rebuilds;
-    // the results are identical)
-    bool rebuild = true;
-    if (built) {
-      int diff = 0;
-#pragma unroll
-      for (int h = 0; h < MGS_RPL; h++) {
-        int r = lane + h * WAVE;
-        if (r < ne) {
-          int st = d.efc_state[r];
-          if (st != st_built[h] || st == ST_CONE) diff = 1;
-        }
-      }
-      rebuild = __ballot(diff) != 0ull;
-    }
-    if (rebuild) {
-#pragma unroll
-      for (int h = 0; h < MGS_RPL; h++) {
-        int r = lane + h * WAVE;
-        st_built[h] = r < ne ? d.efc_state[r] : ST_OFF;
-      }
-      built = true;
+    {
       // Hessian I + G' W G on the matrix cores.  W is block diagonal (Dr on quad
       // rows, the cone Hessian on cone blocks, 0 on inactive rows); X = W G row
       // by row (x = 0.0 + sum_a G_{lead+a,i} w_a), then H_ij = (i == j) +
@@ -3853,9 +3838,6 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
       PT(24);
       ldl_factor<NV>(d.nH, d.tmp, d.tmp2);
       PT(25);
-      PCNT(51, 1);
-    } else {
-      PCNT(52, 1);
     }
     PT(13);
     ldl_solve<NV>(d.nH, d.tmp2, d.ng, d.ndir);

@@ -332,15 +332,20 @@ class ClutterTableEnv:
         n = len(poses)
         if n == 0:
             return np.zeros(0, dtype=bool)
-        p = poses.pos
-        inb = (p[..., 0] < 0.25) & (p[..., 0] > -0.25) & (p[..., 1] < 0.25) & (p[..., 1] > -0.25) & \
-              (p[..., 2] < 1.0) & (p[..., 2] > 0.0)
+        inb = self.in_bounds(poses)
         out = np.zeros(n, dtype=bool)
         idx = np.nonzero(inb)[0]
         if len(idx):
             q, mp, mq = self._initial_qpos(poses[idx], joints[idx], self._state)
             out[idx] = self.engine_for_state(self._state).collision_free(q, mp, mq, predicate="partition_incl")
         return out
+
+    @staticmethod
+    def in_bounds(poses: SE3Pose) -> np.ndarray:
+        """the reference's workspace box of the collision mask (:344-354)"""
+        p = poses.pos
+        return (p[..., 0] < 0.25) & (p[..., 0] > -0.25) & (p[..., 1] < 0.25) & (p[..., 1] > -0.25) & \
+            (p[..., 2] < 1.0) & (p[..., 2] > 0.0)
 
     def stable_plan(self, poses: SE3Pose, joints: np.ndarray, env_state, nstep_lift=3000, lift_dist=0.3,
                     close_steps=None) -> RolloutPlan:

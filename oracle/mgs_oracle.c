@@ -2477,6 +2477,25 @@ static int obj_contact_incl(const Mdl* md, const Dat* d) {
   return 0;
 }
 
+/* the contact predicates on a given contact list (tests: pinned against the
+ * reference's check_* functions on scripted contacts, tests/golden/
+ * make_golden_more.py): pairs = n (geom1, geom2) collision-geom indices;
+ * predicate MGS_PRED_ANY_CONTACT / PARTITION / PARTITION_INCL */
+int oracle_contact_predicate(const mgs_model_desc* desc, const int32_t* I, const double* D, const int32_t* pairs,
+                             int n, int predicate) {
+  Mdl md = {desc, I, D};
+  Dat d;
+  memset(&d, 0, sizeof(d));
+  int g1[64], g2[64];
+  if (n > 64) n = 64;
+  for (int c = 0; c < n; c++) { g1[c] = pairs[2 * c]; g2[c] = pairs[2 * c + 1]; }
+  d.ncon = n;
+  d.con_g1 = g1;
+  d.con_g2 = g2;
+  if (predicate == MGS_PRED_ANY_CONTACT) return n != 0;
+  return predicate == MGS_PRED_PARTITION_INCL ? obj_contact_incl(&md, &d) : obj_contact(&md, &d);
+}
+
 static void reset(const Mdl* md, Dat* d, const double* qpos_init, const double* mpos, const double* mquat) {
   const mgs_model_desc* m = md->m;
   memcpy(d->qpos, qpos_init, sizeof(double) * m->nq);

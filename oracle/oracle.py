@@ -158,6 +158,18 @@ def antipodal_contacts(tri, origin, direction, u_choice, eps, nthreads=8):
     return sec, cnt
 
 
+def contact_predicate(om, pairs, predicate):
+    """oracle_contact_predicate: the kernels' contact predicate on a given list
+    of (geom1, geom2) collision-geom index pairs"""
+    L = lib()
+    L.oracle_contact_predicate.argtypes = [ctypes.POINTER(abi.ModelDesc), ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.c_int, ctypes.c_int]
+    pr = np.ascontiguousarray(np.asarray(pairs, np.int32).reshape(-1, 2))
+    return bool(L.oracle_contact_predicate(*om._args(), ptr(pr, ctypes.c_int32), len(pr),
+                                           abi.predicate_code(predicate)))
+
+
 def sincos(x):
     x = np.ascontiguousarray(x, np.float64)
     s = np.zeros_like(x)

@@ -33,8 +33,8 @@ def report(buf, r, ncand, horizon):
     c3 = np.array(buf[45:47], dtype=np.float64) / steps
     print('per candidate-step: ls_eval calls %.2f, newton_eval calls %.2f, noslip sweeps %.2f, '
           'qcqp iterations %.2f, block updates %.2f' % (*c2, *c3))
-    c4 = np.array(buf[51:58], dtype=np.float64)
-    print('per candidate-step: Newton Hessian builds %.2f, reused %.2f' % tuple(c4[:2] / steps))
+    c4 = np.array(buf[51:59], dtype=np.float64)
+    print('per candidate-step: pairs skipped by a separation certificate %.2f' % (c4[7] / steps))
     if c4[3] + c4[4] > 0:
         print('narrowphase MPR (incl. supports): missed pairs %.1f%% of ticks (%.2f support calls per step), '
               'hit pairs %.1f%% (%.2f support calls per step)' % (100 * c4[3] / tot, c4[5] / steps,
