@@ -177,3 +177,66 @@ def test_oversized_pile_fails_clearly():
         o.name = f"o{i}"
     with pytest.raises(ValueError, match="piles of at most 8 free objects"):
         ClutterTableEnv(grip, objs)
+
+
+def spread_pile(gripper_name, object_ids):
+    """a pile scene of any size with its objects set apart on the table (the
+    parity of the kernels does not need a settled pile)"""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_clutter_scene import make_env
+    env = make_env(gripper_name, object_ids)
+    parts = env.split_state(env.get_state())
+    q = parts["qpos"].copy()
+    for i, (n, qs, vs) in enumerate(env._obj_slices()):
+        q[qs] = [0.12 * (i - 1.5), 0.06 * (i % 2), 0.06, 1.0, 0.0, 0.0, 0.0]
+    env.set_state(env.join_state(dict(parts, qpos=q)))
+    return env
+
+
+SPREAD_PILES = [("Robotiq2f85Gripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can"]),
+                ("PandaGripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange"])]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gripper,objects", SPREAD_PILES)
+def test_any_pile_size_gpu_parity(gripper, objects):
+    """piles of 3 (Robotiq) and 4 (Panda) objects: nv 32, a dof count no
+    library instantiates, runs through a model-specialised code object, bit-exact
+    against the oracle (mask and a close + lift rollout)"""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+    from mgs.core.engine import supported_nvs
+    from mgs.sampler.antipodal import hand_candidates, panda_candidates, robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    from oracle import oracle as O
+    env = spread_pile(gripper, objects)
+    st = env.get_state()
+    assert env.model.nv == 32 and 32 not in supported_nvs()
+    eng = env.engine_for_state(st)
+    assert eng.specialized()
+    H, J = [], []
+    for k, o in enumerate(env.objects):
+        if gripper == "PandaGripper":
+            h, j = panda_candidates(o, 24, seed=k, gripper=env.gripper)[:2]
+        else:
+            h, j = robotiq_candidates(o, 24, seed=k)[:2]
+        H.append((env.get_obj_pose(o.name) @ SE3Pose.from_mat(h)).to_mat())
+        J.append(j)
+    poses = SE3Pose.from_mat(np.concatenate(H).astype(np.float32))
+    J = np.concatenate(J).astype(np.float64)
+    om = O.OracleModel(env.model_for(st), ncon_max=env.ncon_max, nefc_max=eng.desc.nefc_max)
+    mask = env.grasp_collision_mask(poses, J)
+    q, mp, mq = env._initial_qpos(poses, J, st)
+    ref = om.collision_free(q, mp, mq, predicate="partition_incl", nthreads=8) & env.in_bounds(poses)
+    assert np.array_equal(mask, ref)
+    idx = np.nonzero(mask)[0][:8]
+    assert len(idx) >= 2
+    plan = env.stable_plan(poses[idx], J[idx], st, nstep_lift=150, close_steps=150)
+    rg, ro = eng.rollout(plan), om.rollout(plan, nthreads=8)
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(rg[k], ro[k]), k

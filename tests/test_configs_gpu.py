@@ -98,6 +98,26 @@ def test_shadow_pile_gpu_parity(senv, scand):
 
 
 @pytest.mark.gpu
+def test_shadow_pile_reference_schedule_parity(senv, scand):
+    """C5 at the reference's own schedule: close 3000 + lift 3000 steps
+    (clutter_table.py:277,307) on two pile candidates, bit-exact against the
+    oracle"""
+    _init_torch()
+    from oracle import oracle as O
+    poses, J = scand
+    st = senv.get_state()
+    eng = senv.engine_for_state(st)
+    om = O.OracleModel(senv.model_for(st), ncon_max=senv.ncon_max, nefc_max=eng.desc.nefc_max)
+    idx = np.nonzero(senv.grasp_collision_mask(poses, J))[0][:2]
+    plan = senv.stable_plan(poses[idx], J[idx], st)
+    assert plan.nsteps == [3000, 3000]
+    rg, ro = eng.rollout(plan), om.rollout(plan, nthreads=2)
+    assert (rg["stats"][:, 2] == 0).all()
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(rg[k], ro[k]), k
+
+
+@pytest.mark.gpu
 def test_shadow_pile_capacity_escalation(senv, scand):
     """start at 16 contacts: the first pass overflows, the escalated result is
     the oracle's at full capacity."""
