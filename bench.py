@@ -541,7 +541,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
-                     "kernel": "mgs_rollout_kernel",
+                     "kernel": "mgs_special_rollout" if env.engine.static_layout() else "mgs_rollout_kernel",
                      "algorithmic_bytes_per_launch": alg},
         "cpu_baseline": None,
     }

@@ -1064,17 +1064,20 @@ DEVI int portal_choose(const SupPt& p0, const SupPt& p1, const SupPt& p2, const 
   } while (0)
 
 // On a miss that is certified by a separating direction (the support of the
-// Minkowski difference along dir is <= 0), *cm = -h(dir) >= 0 and cd = dir
-// (unit, world); else *cm = -1.
-#define MPR_CERT(P) do { *cm = -dot3((P).v, dir); cd[0] = dir[0]; cd[1] = dir[1]; cd[2] = dir[2]; } while (0)
+// Minkowski difference along dir is <= 0), *cm = -h(dir) >= 0 and dir (the
+// caller's array, the search direction throughout) is left at that unit world
+// direction; else *cm = -1.  (dir is the caller's so that no exit path stores a
+// copy of it: the compiler would merge those stores with the contact point's
+// into one store through a selected pointer and keep both arrays in scratch.)
+#define MPR_CERT(P) do { *cm = -dot3((P).v, dir); } while (0)
 DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1, int g2, double* n, double* depth,
-                         double* pos, double* cd, double* cm) {
+                         double* pos, double* dir, double* cm) {
   *cm = -1.0;
   const double tol = md.m.mpr_tolerance;
   const int32_t* ghull = IA(md, geom_hullid);
   const double* HC = DA(md, hull_center);
   SupPt p0, p1, p2, p3, p4;
-  double t[3], dir[3];
+  double t[3];
   mulmv3(t, d.geom_xmat + 9 * g1, HC + 3 * ghull[g1]);
   add3(p0.a, d.geom_xpos + 3 * g1, t);
   mulmv3(t, d.geom_xmat + 9 * g2, HC + 3 * ghull[g2]);
@@ -1154,6 +1157,7 @@ DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1,
       double su = (u1 + u2) + u3;
       if (fabs(su) < 1e-30) { u1 = u2 = u3 = 1.0 / 3.0; }
       else { double inv = 1.0 / su; u1 = u1 * inv; u2 = u2 * inv; u3 = u3 * inv; }
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         double pa = (u1 * p1.a[k] + u2 * p2.a[k]) + u3 * p3.a[k];
         double pb = (u1 * p1.b[k] + u2 * p2.b[k]) + u3 * p3.b[k];
@@ -1665,7 +1669,7 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   unsigned long long sc0 = s_prof[28];
 #endif
   pair_ctx(md, d, g1, g2, pc);
-  double cd[3] = {0.0, 0.0, 0.0}, cm;
+  double cd[3], cm;
   int hit = mpr_penetration(md, d, pc, g1, g2, n, &depth, mpos, cd, &cm);
   cert_update(md, d, pair, g1, g2, hit, cd, cm);
   PT(4);
@@ -2037,10 +2041,15 @@ DEVI void collision(const Mdl& md, Dat& d) {
       ov = 1;
       for (int k = 0; k < 3; k++)
         if (fabs(c[0][k] - c[1][k]) > (hw[0][k] + hw[1][k]) + pm[p]) ov = 0;
-      if (ov && obb_separated(d.geom_xmat + 9 * g[0], d.geom_xpos + 3 * g[0], aabb + 6 * g[0],
-                              d.geom_xmat + 9 * g[1], d.geom_xpos + 3 * g[1], aabb + 6 * g[1], pm[p]))
+    }
+    PT(59);
+    if (ov) {
+      int g1 = p1[p], g2 = p2[p];
+      if (obb_separated(d.geom_xmat + 9 * g1, d.geom_xpos + 3 * g1, aabb + 6 * g1, d.geom_xmat + 9 * g2,
+                        d.geom_xpos + 3 * g2, aabb + 6 * g2, pm[p]))
         ov = 0;
     }
+    PT(60);
     unsigned long long mask = __ballot(ov);
     mask &= ~cert_check(md, d, c0, mask);
     PT(3);

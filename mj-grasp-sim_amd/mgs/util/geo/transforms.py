@@ -10,6 +10,7 @@ from the reference's own SE3Pose) pins them (tests/test_model_and_host.py).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -28,6 +29,15 @@ def _pool():
         from concurrent.futures import ThreadPoolExecutor
         _POOL = ThreadPoolExecutor(_PAR_CHUNKS)
     return _POOL
+
+
+def _drop_pool():
+    global _POOL
+    _POOL = None
+
+
+# a forked child inherits the executor object but not its threads
+os.register_at_fork(after_in_child=_drop_pool)
 
 
 def _wxyz_to_xyzw(q):

@@ -2427,7 +2427,7 @@ static void integrate(const Mdl* md, Dat* d) {
   }
   for (int i = 0; i < nv * nv; i++) d->MI[i] = d->M[i] - dt * d->qDeriv[i];
   ldl_factor(nv, d->MI, d->LI, d->DIinv, d->Dv);
-  double rhs[128], qa[128];
+  double rhs[128] = {0}, qa[128];
   for (int k = 0; k < nv; k++) rhs[k] = d->qfrc_smooth[k] + d->qfrc_constraint[k];
   ldl_solve(nv, d->LI, d->DIinv, rhs, qa);
   for (int k = 0; k < nv; k++) d->qvel[k] = d->qvel[k] + dt * qa[k];

@@ -16,7 +16,9 @@ from mgs.core import abi
 from mgs.core.abi import ptr
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "libmgs_oracle.so")
+# MGS_ORACLE_LIB: another build of the same sources (the sanitizer build of
+# `make asan`, tools/asan_oracle.sh)
+_LIB = os.environ.get("MGS_ORACLE_LIB") or os.path.join(_HERE, "libmgs_oracle.so")
 _lib = None
 
 

@@ -181,6 +181,14 @@ def test_seeds_match_numpy_argsort():
         assert (adm.sum() >= 5) == adm[picked].all()
 
 
+def test_single_seed_nearest_is_itself():
+    """one seed has no second-nearest: the reference's sorted_indices[:, 1]
+    (sampler/contact.py:213-214) clamps to column 0, the seed itself"""
+    from oracle import oracle as O
+    nn, sel = O.contact_seeds(np.array([[0.01, 0.02, 0.03]]), 0.1, 7, 3)
+    assert list(nn) == [0]
+
+
 def _oracle_pipeline(monkeypatch):
     """the product's host logic with the device stages served by the oracle"""
     from mgs.core import engine
@@ -247,6 +255,9 @@ def test_contact_kernels_gpu_parity(kin):
     nn, sel, _ = engine.contact_seeds(seeds, 0.1, 99, 5)
     nn_o, sel_o = O.contact_seeds(seeds, 0.1, 99, 5)
     assert np.array_equal(nn, nn_o) and np.array_equal(sel, sel_o)
+    one = seeds[:1]
+    nn1, sel1, _ = engine.contact_seeds(one, 0.1, 99, 5)
+    assert list(nn1) == [0] and np.array_equal(sel1, O.contact_seeds(one, 0.1, 99, 5)[1])
     desc = C.kin_desc(kin, [2, 1, 0, 1, 2])
     n = 200
     R = np.einsum("nij,jk->nik", np.linalg.qr(rng.normal(size=(n, 3, 3)))[0], kin.align_rot)

@@ -61,14 +61,14 @@ def gravityless(gripper_name, object_ids, n, horizon="h200"):
         kr = res["kernel_ms"] if res is not None else 0.0
         per.append(dict(object=oid, candidates=n, collision_free=int(mask.sum()),
                         stable=int(res["label"].sum()) if res is not None else 0, seconds=dt,
-                        kernel_ms=km + kr))
+                        kernel_ms=km + kr, static_layout_kernel=bool(env.engine.specialized())))
         tot_n += n
         tot_t += dt
         tot_k += (km + kr) * 1e-3
     return dict(value=tot_n / tot_t, kernel_only=tot_n / tot_k, objects=per)
 
 
-def clutter(n_per_obj, steps):
+def clutter(n_per_obj, steps, cpu_sample=0, threads=16):
     from make_clutter_scene import make_env
     from mgs.sampler.antipodal import hand_candidates
     from mgs.util.geo.transforms import SE3Pose
@@ -90,11 +90,38 @@ def clutter(n_per_obj, steps):
     res = env.grasp_stable_mask(P[idx], J[idx], st, nstep_lift=steps, close_steps=steps, return_details=True)
     dt = time.perf_counter() - t0
     eng = env.engine_for_state(st)
-    return dict(value=len(P) / dt, candidates=len(P), collision_free=int(mask.sum()),
-                stable=int(res["label"].sum()), seconds=dt, rollout_kernel_ms=res["kernel_ms"],
-                overflow_rerun=int((res["stats"][:, 2] != 0).sum()), steps_per_phase=steps,
-                nv=int(env.model.nv), nefc_max=int(eng.desc.nefc_max), library=os.path.basename(eng.lib._name),
-                mean_ncon=float(res["stats"][:, 4].sum() / max(1, (2 * steps) * len(idx))))
+    out = dict(value=len(P) / dt, candidates=len(P), collision_free=int(mask.sum()),
+               stable=int(res["label"].sum()), seconds=dt, rollout_kernel_ms=res["kernel_ms"],
+               overflow_rerun=int((res["stats"][:, 2] != 0).sum()), steps_per_phase=steps,
+               nv=int(env.model.nv), nefc_max=int(eng.desc.nefc_max), library=os.path.basename(eng.lib._name),
+               static_layout_kernel=bool(eng.specialized()),
+               mean_ncon=float(res["stats"][:, 4].sum() / max(1, (2 * steps) * len(idx))))
+    if cpu_sample:
+        out["cpu_baseline"] = clutter_cpu(env, st, P, J, cpu_sample, steps, threads)
+    return out
+
+
+def clutter_cpu(env, st, P, J, sample, steps, threads):
+    """the C oracle on the host cores over a bounded sample of the same job: the
+    collision mask of `sample` evenly spaced candidates, then the close + lift
+    rollouts of the collision-free ones; candidates/s = sample / time"""
+    from oracle import oracle as O
+    sel = np.linspace(0, len(P) - 1, sample).astype(int)
+    Ps, Js = P[sel], J[sel]
+    eng = env.engine_for_state(st)
+    om = O.OracleModel(env.model_for(st), ncon_max=env.ncon_max, nefc_max=eng.desc.nefc_max)
+    t0 = time.perf_counter()
+    free = np.zeros(sample, bool)
+    inb = np.nonzero(env.in_bounds(Ps))[0]
+    q, mp, mq = env._initial_qpos(Ps[inb], Js[inb], st)
+    free[inb] = om.collision_free(q, mp, mq, predicate="partition_incl", nthreads=threads)
+    idx = np.nonzero(free)[0]
+    if len(idx):
+        om.rollout(env.stable_plan(Ps[idx], Js[idx], st, nstep_lift=steps, close_steps=steps), nthreads=threads)
+    dc = time.perf_counter() - t0
+    return dict(value=sample / dc, unit="grasp candidates/s", cores=threads, kind="port", seconds=dc,
+                sample=f"{sample} of the candidates (evenly spaced): mask + {len(idx)} collision-free "
+                       f"rollouts of {steps}+{steps} steps")
 
 
 def scenes(n=256, steps_each=900, steps_final=9000, cpu_states=16, cpu_steps=200, ncon=None):
@@ -194,9 +221,12 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c3", "c4", "c5", "sampler"])
     ap.add_argument("--c5-steps", type=int, default=600)
     ap.add_argument("--c5-per-object", type=int, default=256)
+    ap.add_argument("--c5-cpu-sample", type=int, default=0, help="candidates for the C5 CPU baseline (0: none)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--scene-piles", type=int, default=256)
     ap.add_argument("--scene-ncon", type=int, default=None)
     a = ap.parse_args()
+    os.environ.setdefault("MGS_SPECIALIZE", "1")
     import torch
     torch.cuda.init()
     from mgs.obj.ycb import ObjectYCB
@@ -211,7 +241,7 @@ def main():
             out = dict(config="c4", workload="Allegro x GSO-format stand-in (Synthetic_Mug_Body), 32768 candidates on "
                                              "one GPU, mask + h200 rollout", unit="candidates/s", **r)
         elif c == "c5":
-            r = clutter(a.c5_per_object, a.c5_steps)
+            r = clutter(a.c5_per_object, a.c5_steps, a.c5_cpu_sample, a.cpu_threads)
             out = dict(config="c5", workload=f"Shadow Hand x settled 5-object pile, {r['candidates']} candidates, "
                                              f"mask + close {a.c5_steps} + lift {a.c5_steps} (reference: 3000 + 3000)",
                        unit="candidates/s", **r)

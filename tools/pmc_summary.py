@@ -24,17 +24,17 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 PROF = os.path.join(ROOT, "profiles")
 
 
-def rows(path, kernel="mgs_rollout_kernel"):
+def rows(path, kernels=("mgs_special_rollout", "mgs_rollout_kernel")):
     with open(path) as f:
-        return [r for r in csv.DictReader(f) if kernel in r["Kernel_Name"]]
+        return [r for r in csv.DictReader(f) if any(k in r["Kernel_Name"] for k in kernels)]
 
 
-def main(d, tag="r02"):
+def main(d, tag="r03"):
     shutil.copy(os.path.join(d, "trace", "bench_kernel_stats.csv"), os.path.join(PROF, f"{tag}_rocprof_kernel_stats.csv"))
     out = {"source": "rocprofv3 --kernel-trace --pmc <counters> (separate passes) on `python3 bench.py --streams 1 "
-                     "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate` (tools/prof_r02.sh); "
+                     "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate` (tools/prof_{tag}.sh); "
                      "per rollout dispatch",
-           "kernel": "mgs_rollout_kernel<20, 1> (static-layout instantiation)"}
+           "kernel": "mgs_special_rollout (code object specialised to the headline model)"}
     sums = {}
     for name in ("fetch", "write", "sq", "valu"):
         p = os.path.join(d, f"pmc_{name}", "pmc_counter_collection.csv")

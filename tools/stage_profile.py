@@ -4,7 +4,7 @@ import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'mj-grasp-sim_amd'))
 import mgs.core.engine as E
 
-NAMES = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll: MPR', 'coll: feature+clip',
+NAMES = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: certificate checks', 'coll: MPR', 'coll: feature+clip',
          'crb', 'ldl(M)', 'act+passive+rne+smooth', 'con: J rows', 'con: G transform', 'con: params+blocks',
          'newton: setup', 'newton: hessian', 'newton: ldl+solve+jv', 'newton: linesearch', 'newton: eval+grad',
          'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
@@ -12,13 +12,14 @@ NAMES = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: broadphase', 'coll:
          'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne',
          'coll: big-hull support calls', 'coll: feature passes', 'coll: select4+add (lane 0)',
          'noslip/pgs block: residual', 'noslip/pgs block: qcqp', 'noslip/pgs block: update',
-         'coll: sort+dedup', 'coll: hull chains', 'coll: clip+depth filter']
+         'coll: sort+dedup', 'coll: hull chains', 'coll: clip+depth filter', 'coll: broadphase AABB',
+         'coll: broadphase OBB']
 
 
 def report(buf, r, ncand, horizon):
     v = np.concatenate([np.array(buf[:26], dtype=np.float64), np.array(buf[31:36], dtype=np.float64),
                         np.array(buf[39:45], dtype=np.float64),
-                        np.array(buf[47:50], dtype=np.float64)])
+                        np.array(buf[47:50], dtype=np.float64), np.array(buf[59:61], dtype=np.float64)])
     cnt = np.array(buf[26:31], dtype=np.float64)
     tot = v.sum()
     print('N=%d candidates, kernel %.1f ms, labels %d, overflow %d' % (

@@ -1,5 +1,7 @@
-"""Diagnostic: per-stage s_memtime breakdown of the wide (clutter) rollout kernel
-on the Shadow pile (libmgs_gpu_wide_prof.so, -DMGS_WIDE -DMGS_PROFILE)."""
+"""Diagnostic: per-stage s_memtime breakdown of the clutter rollout on the
+Shadow pile: the profile build (-DMGS_PROFILE) of the pile model's specialised
+code object attached in place of the product one.
+    python tools/stage_profile_clutter.py [steps] [--compile-only]"""
 import ctypes
 import os
 import sys
@@ -10,9 +12,8 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(ROOT, "mj-grasp-sim_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-import mgs.core.engine as E  # noqa: E402
+from mgs.core import special  # noqa: E402
 
-E.LIB_WIDE_PATH = E.LIB_WIDE_PATH.replace("libmgs_gpu_wide.so", "libmgs_gpu_wide_prof.so")
 from make_clutter_scene import make_env  # noqa: E402
 from mgs.sampler.antipodal import hand_candidates  # noqa: E402
 from mgs.util.geo.transforms import SE3Pose  # noqa: E402
@@ -29,15 +30,20 @@ for k, o in enumerate(env.objects):
 P = SE3Pose.from_mat(np.concatenate(H).astype(np.float32))
 J = np.concatenate(J)
 st = env.get_state()
+eng = env.engine_for_state(st)
+path = special.code_object(eng.lib, eng.desc, profile=True)
+if "--compile-only" in sys.argv:
+    print(path)
+    sys.exit(0)
 mask = env.grasp_collision_mask(P, J)
 idx = np.nonzero(mask)[0][:32]
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
 plan = env.stable_plan(P[idx], J[idx], st, nstep_lift=steps, close_steps=steps)
-eng = env.engine_for_state(st)
+eng._ck(eng.lib.mgs_model_attach_special(eng._model, path.encode()), "mgs_model_attach_special")
 L = eng.lib
-L.mgs_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+L.mgs_model_prof_read.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
 buf = (ctypes.c_ulonglong * 64)()
-L.mgs_prof_read(buf)
+L.mgs_model_prof_read(eng._model, buf)
 r = eng.rollout(plan)
-L.mgs_prof_read(buf)
+eng._ck(L.mgs_model_prof_read(eng._model, buf), "mgs_model_prof_read")
 report(buf, r, len(idx), 2 * steps)
