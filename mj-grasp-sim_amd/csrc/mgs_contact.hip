@@ -129,7 +129,8 @@ mgs_seeds_kernel(const double* __restrict__ S, int k, double radius, uint64_t rn
     // one seed: no second-nearest; the reference's sorted_indices[:, 1]
     // (sampler/contact.py:213-214) clamps to column 0, the seed itself
     out_nn[i] = n1i == 0x7fffffff ? n0i : n1i;
-    for (int a = 0; a < ntip; a++) out_sel[(size_t)i * ntip + a] = ti[a];
+    // fewer seeds than ntip (k < ntip): the empty slots take the seed itself
+    for (int a = 0; a < ntip; a++) out_sel[(size_t)i * ntip + a] = a < cnt ? ti[a] : i;
   }
 }
 

@@ -1974,44 +1974,80 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
   wsync();
 }
 
-#define OBB_FN DEVI
 /* Second broadphase stage: separating-axis test between the geoms' oriented
  * bounding boxes (their local AABBs posed in the world; 15 axes).  Each convex
  * hull lies inside its box, so separated boxes cannot produce a contact and the
  * narrowphase is skipped (MuJoCo would run MPR and find nothing; on the round-1
- * benchmark this removes ~55% of narrowphase calls).  Returns 1 if separated. */
-OBB_FN int obb_separated(const double* R1, const double* x1, const double* b1, const double* R2,
-                         const double* x2, const double* b2, double margin) {
-  double c1[3], c2[3], t[3], D[3];
-  mulmv3(t, R1, b1);
-  add3(c1, x1, t);
-  mulmv3(t, R2, b2);
-  add3(c2, x2, t);
-  sub3(D, c2, c1);
-  const double *h1 = b1 + 3, *h2 = b2 + 3;
+ * benchmark this removes ~55% of narrowphase calls).  The oracle's
+ * obb_separated tests the axes in turn; here a pair is separated iff one of its
+ * 15 axis tests is, so the axes run on lanes: one pass takes up to 4 pairs,
+ * 16 lanes each (lane q of a group = axis q; q = 15 idles).
+ *
+ * One axis test, the expressions of the oracle's loop body for axis q: D = c2 -
+ * c1 (the posed box centres), h1 / h2 the half widths, A1 / A2 the box axes
+ * (columns of R1 / R2, read from LDS).  The axis is chosen by selects with
+ * constant indices (a computed index into a register array would go through
+ * scratch). */
+DEVI int obb_axis_separated(int q, const double* R1, const double* R2, const double* D, const double* h1,
+                            const double* h2, double margin) {
   double A1[9], A2[9];  /* box axes as rows: A[k] = column k of R */
+#pragma unroll
   for (int k = 0; k < 3; k++)
+#pragma unroll
     for (int i = 0; i < 3; i++) { A1[3 * k + i] = R1[3 * i + k]; A2[3 * k + i] = R2[3 * i + k]; }
-  for (int q = 0; q < 15; q++) {
-    // the axis by cases on q, each with constant indices, so A1 / A2 stay in
-    // registers (a computed index would address them through scratch)
-    double L[3];
-    switch (q) {
-#define OBB_F(Q, A, K) case Q: L[0] = A[3 * K]; L[1] = A[3 * K + 1]; L[2] = A[3 * K + 2]; break;
-#define OBB_E(Q, a, b) case Q: cross3(L, A1 + 3 * a, A2 + 3 * b); break;
-      OBB_F(0, A1, 0) OBB_F(1, A1, 1) OBB_F(2, A1, 2) OBB_F(3, A2, 0) OBB_F(4, A2, 1) OBB_F(5, A2, 2)
-      OBB_E(6, 0, 0) OBB_E(7, 0, 1) OBB_E(8, 0, 2) OBB_E(9, 1, 0) OBB_E(10, 1, 1) OBB_E(11, 1, 2)
-      OBB_E(12, 2, 0) OBB_E(13, 2, 1) default: cross3(L, A1 + 6, A2 + 6); break;
-#undef OBB_F
-#undef OBB_E
-    }
-    double ll = dot3(L, L);
-    if (ll < 1e-20) continue;
-    double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));
-    double r2 = (h2[0] * fabs(dot3(A2, L)) + h2[1] * fabs(dot3(A2 + 3, L))) + h2[2] * fabs(dot3(A2 + 6, L));
-    if (fabs(dot3(D, L)) > (r1 + r2) + (margin + 1e-12) * sqrt(ll)) return 1;
+  // the axis' vectors straight from LDS by per-lane column (a select between
+  // register values would be folded into a select of addresses and put A1 / A2
+  // in scratch)
+  const int qa = q < 6 ? 0 : (q - 6) / 3, qb = q < 6 ? 0 : (q - 6) % 3;
+  const double* Rf = q < 3 ? R1 : R2;
+  const int kf = q < 3 ? q : (q < 6 ? q - 3 : 0);
+  double e1[3], e2[3], L[3], cx[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    e1[i] = R1[3 * i + qa];
+    e2[i] = R2[3 * i + qb];
   }
-  return 0;
+  cross3(cx, e1, e2);
+#pragma unroll
+  for (int i = 0; i < 3; i++) L[i] = q < 6 ? Rf[3 * i + kf] : cx[i];
+  double ll = dot3(L, L);
+  if (ll < 1e-20) return 0;
+  double r1 = (h1[0] * fabs(dot3(A1, L)) + h1[1] * fabs(dot3(A1 + 3, L))) + h1[2] * fabs(dot3(A1 + 6, L));
+  double r2 = (h2[0] * fabs(dot3(A2, L)) + h2[1] * fabs(dot3(A2 + 3, L))) + h2[2] * fabs(dot3(A2 + 6, L));
+  return fabs(dot3(D, L)) > (r1 + r2) + (margin + 1e-12) * sqrt(ll);
+}
+
+/* the chunk's pairs in `am` (AABB-overlapping) whose boxes are separated; lane
+ * b of the chunk holds pair b's g1, g2, D, half widths and margin */
+DEVI unsigned long long obb_separated_wave(const Dat& d, unsigned long long am, int g1, int g2, const double* D,
+                                           const double* h1, const double* h2, double margin) {
+  const int lane = lane_id(), grp = lane >> 4, q = lane & 15;
+  unsigned long long sep = 0ull;
+  while (am) {
+    unsigned long long m = am;      // this group's pair: the grp-th lowest bit
+    for (int t = 0; t < grp; t++) m &= m - 1ull;
+    int b = m ? __ffsll((long long)m) - 1 : 0;
+    int G1 = __shfl(g1, b), G2 = __shfl(g2, b);
+    double Db[3], h1b[3], h2b[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      Db[i] = __shfl(D[i], b);
+      h1b[i] = __shfl(h1[i], b);
+      h2b[i] = __shfl(h2[i], b);
+    }
+    double mb = __shfl(margin, b);
+    int s = 0;
+    if (m && q < 15) s = obb_axis_separated(q, d.geom_xmat + 9 * G1, d.geom_xmat + 9 * G2, Db, h1b, h2b, mb);
+    unsigned long long sm = __ballot(s);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (!am) break;
+      int bk = __ffsll((long long)am) - 1;
+      if ((sm >> (16 * k)) & 0x7fffull) sep |= 1ull << bk;
+      am &= am - 1ull;
+    }
+  }
+  return sep;
 }
 
 // broadphase over all admissible pairs (lanes over pairs), then narrowphase in pair order
@@ -2025,9 +2061,12 @@ DEVI void collision(const Mdl& md, Dat& d) {
   for (int c0 = 0; c0 < npair; c0 += WAVE) {
     int p = c0 + lane;
     int ov = 0;
+    int g[2] = {0, 0};
+    double c[2][3], hw[2][3], D[3] = {0.0, 0.0, 0.0}, h[2][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}}, mp = 0.0;
     if (p < npair) {
-      int g[2] = {p1[p], p2[p]};
-      double c[2][3], hw[2][3];
+      g[0] = p1[p];
+      g[1] = p2[p];
+      mp = pm[p];
       for (int s = 0; s < 2; s++) {
         const double* R = d.geom_xmat + 9 * g[s];
         const double* lc = aabb + 6 * g[s];
@@ -2035,22 +2074,20 @@ DEVI void collision(const Mdl& md, Dat& d) {
         double t[3];
         mulmv3(t, R, lc);
         add3(c[s], d.geom_xpos + 3 * g[s], t);
-        for (int k = 0; k < 3; k++)
+        for (int k = 0; k < 3; k++) {
+          h[s][k] = lh[k];
           hw[s][k] = (fabs(R[3 * k]) * lh[0] + fabs(R[3 * k + 1]) * lh[1]) + fabs(R[3 * k + 2]) * lh[2];
+        }
       }
       ov = 1;
       for (int k = 0; k < 3; k++)
-        if (fabs(c[0][k] - c[1][k]) > (hw[0][k] + hw[1][k]) + pm[p]) ov = 0;
+        if (fabs(c[0][k] - c[1][k]) > (hw[0][k] + hw[1][k]) + mp) ov = 0;
+      sub3(D, c[1], c[0]);
     }
     PT(59);
-    if (ov) {
-      int g1 = p1[p], g2 = p2[p];
-      if (obb_separated(d.geom_xmat + 9 * g1, d.geom_xpos + 3 * g1, aabb + 6 * g1, d.geom_xmat + 9 * g2,
-                        d.geom_xpos + 3 * g2, aabb + 6 * g2, pm[p]))
-        ov = 0;
-    }
-    PT(60);
     unsigned long long mask = __ballot(ov);
+    mask &= ~obb_separated_wave(d, mask, g[0], g[1], D, h[0], h[1], mp);
+    PT(60);
     mask &= ~cert_check(md, d, c0, mask);
     PT(3);
     while (mask) {

@@ -187,6 +187,7 @@ def test_single_seed_nearest_is_itself():
     from oracle import oracle as O
     nn, sel = O.contact_seeds(np.array([[0.01, 0.02, 0.03]]), 0.1, 7, 3)
     assert list(nn) == [0]
+    assert sel.tolist() == [[0, 0, 0]]          # fewer seeds than tips: the seed itself
 
 
 def _oracle_pipeline(monkeypatch):
