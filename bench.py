@@ -343,7 +343,8 @@ def main():
             # with --esc-resume the capped rollout stops an overflowing candidate
             # at that step and leaves its state in the step's resume records
             # (mgs_rollout_resumable_device), which the list re-run continues
-            self.wide = Engine(env.model, device=local, ncon_max=2 * env.ncon_max) if args.escalate else None
+            self.wide = Engine(env.model, device=local, ncon_max=2 * env.ncon_max,
+                               specialize="cached") if args.escalate else None
             self.esc_stream = torch.cuda.Stream(dev)
             self.esc = []          # per step: count, list, label, fail, objq, stats, resume records
             self.events = []

@@ -129,14 +129,20 @@ __device__ unsigned long long g_prof[64];
 static __device__ unsigned long long g_prof[64];
 #endif
 // per-workgroup accumulators in static LDS; PT(k) at wave-uniform points only
-__shared__ unsigned long long s_prof[65];
+__shared__ unsigned long long s_prof[67];
 #define PT(k) do { unsigned long long _n = __builtin_amdgcn_s_memtime(); \
     if (__lane_id() == 0) { s_prof[k] += _n - s_prof[64]; s_prof[64] = _n; } } while (0)
+// slots 61 / 62 at the flush: the workgroup's shader-clock and 100 MHz
+// real-time spans (their ratio is the clock the chip held, MI355X_MICROARCH.md
+// "DVFS give-back" item 6)
 #define PROF_DECL if (__lane_id() == 0) { for (int _k = 0; _k < 64; _k++) s_prof[_k] = 0; \
-    s_prof[64] = __builtin_amdgcn_s_memtime(); }
+    s_prof[64] = s_prof[65] = __builtin_amdgcn_s_memtime(); s_prof[66] = __builtin_amdgcn_s_memrealtime(); }
 #define PROF(k) PT(k)
 #define PCNT(k, v) do { if (__lane_id() == 0) s_prof[k] += (v); } while (0)
-#define PROF_FLUSH if (lane_id() == 0) for (int _k = 0; _k < 64; _k++) atomicAdd(&g_prof[_k], s_prof[_k]);
+#define PROF_FLUSH if (lane_id() == 0) { \
+    s_prof[61] = __builtin_amdgcn_s_memtime() - s_prof[65]; \
+    s_prof[62] = __builtin_amdgcn_s_memrealtime() - s_prof[66]; \
+    for (int _k = 0; _k < 64; _k++) atomicAdd(&g_prof[_k], s_prof[_k]); }
 #else
 #define PT(k)
 #define PROF_DECL

@@ -239,7 +239,9 @@ class ClutterTableEnv:
         key = (nc, cm.qvel0.tobytes(), cm.qacc_ws0.tobytes())
         if key not in self._engines:
             self._engines = {k: v for k, v in self._engines.items() if k[1:] == key[1:]}
-            self._engines[key] = Engine(cm, device=self.device, ncon_max=nc, nefc_max=self._nefc_max)
+            # escalation capacities re-run few candidates: specialised only if cached
+            self._engines[key] = Engine(cm, device=self.device, ncon_max=nc, nefc_max=self._nefc_max,
+                                        specialize=None if nc == self.ncon_max else "cached")
         return self._engines[key]
 
     # -- reference helpers ---------------------------------------------------

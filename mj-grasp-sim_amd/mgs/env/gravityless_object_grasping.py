@@ -155,7 +155,9 @@ class GravitylessObjectGrasping:
             self._wide = {}
         if ncon_max not in self._wide:
             from mgs.core.engine import Engine
-            self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max)
+            # the few overflowing candidates: a specialised object only if one is
+            # cached (compiling one would cost more than the re-run)
+            self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max, specialize="cached")
         return self._wide[ncon_max]
 
     def rollout(self, plan: "RolloutPlan", max_ncon: int = 40):

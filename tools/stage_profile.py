@@ -36,6 +36,9 @@ def report(buf, r, ncand, horizon):
           'qcqp iterations %.2f, block updates %.2f' % (*c2, *c3))
     c4 = np.array(buf[51:59], dtype=np.float64)
     print('per candidate-step: pairs skipped by a separation certificate %.2f' % (c4[7] / steps))
+    if buf[62]:
+        print('clock held in the kernel: %.2f GHz (shader-clock / 100 MHz real-time spans, summed over '
+              'workgroups)' % (0.1 * buf[61] / buf[62]))
     if c4[3] + c4[4] > 0:
         print('narrowphase MPR (incl. supports): missed pairs %.1f%% of ticks (%.2f support calls per step), '
               'hit pairs %.1f%% (%.2f support calls per step)' % (100 * c4[3] / tot, c4[5] / steps,
@@ -55,6 +58,14 @@ def main():
     grip = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1, 0, 0, 0]), 'wxyz'))
     obj = get_object('003_cracker_box')
     env = GravitylessObjectGrasping(grip, obj)
+    if "--compile-only" in sys.argv:
+        # the profile object of the headline engine, built here (no device needed)
+        from mgs.core import abi
+        from mgs.core.engine import library_for
+        fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+        print(special.code_object(library_for(env.model.nv, int(fields["nefc_max"])), abi.make_desc(fields),
+                                  profile=True))
+        return
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     H, J, W = robotiq_candidates(obj, 4 * N, seed=2)
     poses = SE3Pose.from_mat(H)
