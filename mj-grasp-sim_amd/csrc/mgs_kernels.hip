@@ -1036,6 +1036,98 @@ DEVI void mink_support(const PairCtx& c, const double* dir, SupPt* p) {
   if (c.n1 > WAVE || c.n2 > WAVE) PT(39); else PT(22);
 }
 
+// Two narrowphase pairs at once (collide_pair2): the MPR of pair A runs on
+// lanes 0-31 and that of pair B on lanes 32-63, each half computing exactly
+// what a whole wave computes for one pair (the MPR's control flow depends only
+// on values that are uniform within a half).  The support mappings use one
+// 16-lane row per hull: row 0 pair A's geom 1, row 1 A's geom 2, rows 2 / 3
+// B's (lane 16 s + i of a half holds vertex i), so one row-local reduction
+// serves all four hulls -- pairs whose four hulls have at most 16 vertices.
+struct PairCtx2 {
+  int n;               // this lane's hull: its vertex count,
+  double R[9], x[3];   // its geom's pose,
+  double c[3];         // the lane's vertex (lane & 15 < n)
+  double r;            // and rounding radius
+  int P;               // reduction width: next_pow2 of the largest of the four counts (<= 16)
+};
+DEVI void pair_ctx2(const Mdl& md, const Dat& d, int gA1, int gA2, int gB1, int gB2, PairCtx2& c) {
+  const int lane = lane_id(), row = lane >> 4;
+  const int32_t *ghull = IA(md, geom_hullid), *hadr = IA(md, hull_vertadr), *hnum = IA(md, hull_vertnum);
+  const int g = row == 0 ? gA1 : (row == 1 ? gA2 : (row == 2 ? gB1 : gB2));
+  const int h = ghull[g];
+  c.n = hnum[h];
+  const double* V = DA(md, hull_vert) + 3 * hadr[h];
+#pragma unroll
+  for (int k = 0; k < 9; k++) c.R[k] = d.geom_xmat[9 * g + k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) c.x[k] = d.geom_xpos[3 * g + k];
+  const int li = lane & 15, i = li < c.n ? li : 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) c.c[k] = V[k * c.n + i];
+  c.r = DA(md, geom_radius)[g];
+  int nm = __builtin_amdgcn_readlane(c.n, 0);
+  int t = __builtin_amdgcn_readlane(c.n, 16);
+  nm = t > nm ? t : nm;
+  t = __builtin_amdgcn_readlane(c.n, 32);
+  nm = t > nm ? t : nm;
+  t = __builtin_amdgcn_readlane(c.n, 48);
+  nm = t > nm ? t : nm;
+  c.P = next_pow2(nm);
+}
+
+// support_pair for both pairs: the oracle's support_geom per hull (same
+// expressions as sup_cached / sup_finish / support_pair), dir per half
+DEVI void support_pair2(const PairCtx2& c, const double* dir, double* out1, double* out2) {
+  const int lane = lane_id(), row = lane >> 4, li = lane & 15;
+  const bool second = row & 1;    // geom 2 of the pair: support along -dir
+  double sd[3] = {second ? -dir[0] : dir[0], second ? -dir[1] : dir[1], second ? -dir[2] : dir[2]};
+  double dl[3];
+  mulmtv3(dl, c.R, sd);
+  SupAcc a;
+  sup_init(a);
+  if (li < c.n) {
+    double sc = (c.c[0] * dl[0] + c.c[1] * dl[1]) + c.c[2] * dl[2];
+    if (sc > a.best) { a.best = sc; a.bi = li; a.vx = c.c[0]; a.vy = c.c[1]; a.vz = c.c[2]; }
+  }
+  const int P = c.P;
+  double m = a.best;
+  if (P > 1) m = max_f64(m, dpp_d(m, 0));
+  if (P > 2) m = max_f64(m, dpp_d(m, 1));
+  if (P > 4) m = max_f64(m, dpp_d(m, 2));
+  if (P > 8) m = max_f64(m, dpp_d(m, 3));
+  const double M0 = readlane_d(m, 0), M1 = readlane_d(m, 16), M2 = readlane_d(m, 32), M3 = readlane_d(m, 48);
+  const double M = row == 0 ? M0 : (row == 1 ? M1 : (row == 2 ? M2 : M3));
+  const unsigned long long tied = __ballot(a.bi != 0x7fffffff && a.best == M);
+  // each row's winner: its lowest tied lane (none: the row's first lane, as
+  // sup_finish falls back to lane 0)
+  int w[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const unsigned tr = (unsigned)(tied >> (16 * q)) & 0xffffu;
+    w[q] = 16 * q + (tr ? __ffs(tr) - 1 : 0);
+  }
+  const int src = row == 0 ? w[0] : (row == 1 ? w[1] : (row == 2 ? w[2] : w[3]));
+  double v[3] = {__shfl(a.vx, src), __shfl(a.vy, src), __shfl(a.vz, src)};
+  double t[3], wv[3];
+  mulmv3(t, c.R, v);
+  add3(wv, c.x, t);
+  if (c.r > 0.0) { wv[0] = wv[0] + c.r * sd[0]; wv[1] = wv[1] + c.r * sd[1]; wv[2] = wv[2] + c.r * sd[2]; }
+  const int s1 = lane & 32, s2 = s1 + 16;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    out1[k] = __shfl(wv[k], s1);
+    out2[k] = __shfl(wv[k], s2);
+  }
+}
+
+DEVI void mink_support(const PairCtx2& c, const double* dir, SupPt* p) {
+  PT(4);
+  PCNT(28, 1);
+  support_pair2(c, dir, p->a, p->b);
+  sub3(p->v, p->a, p->b);
+  PT(22);
+}
+
 DEVI void portal_normal(double* n, const SupPt* p1, const SupPt* p2, const SupPt* p3) {
   double e1[3], e2[3];
   sub3(e1, p2->v, p1->v);
@@ -1076,7 +1168,10 @@ DEVI int portal_choose(const SupPt& p0, const SupPt& p1, const SupPt& p2, const 
 // copy of it: the compiler would merge those stores with the contact point's
 // into one store through a selected pointer and keep both arrays in scratch.)
 #define MPR_CERT(P) do { *cm = -dot3((P).v, dir); } while (0)
-DEVI int mpr_penetration(const Mdl& md, const Dat& d, const PairCtx& pc, int g1, int g2, double* n, double* depth,
+// (Ctx: PairCtx for one pair on the whole wave, PairCtx2 for two pairs on the
+// two halves; g1 / g2 are then the half's geoms)
+template <class Ctx>
+DEVI int mpr_penetration(const Mdl& md, const Dat& d, const Ctx& pc, int g1, int g2, double* n, double* depth,
                          double* pos, double* dir, double* cm) {
   *cm = -1.0;
   const double tol = md.m.mpr_tolerance;
@@ -1662,9 +1757,11 @@ DEVI void cert_update(const Mdl& md, Dat& d, int pair, int g1, int g2, int hit, 
   wsync();
 }
 
+DEVI void collide_manifold(const Mdl& md, Dat& d, const PairCtx& pc, int pair, int g1, int g2, const double* n,
+                           const double* mpos);
+
 // narrowphase of one admissible pair, all lanes participate
 DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
-  int lane = lane_id();
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
   double n[3], depth, mpos[3];
   PairCtx pc;
@@ -1687,6 +1784,13 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   PCNT(hit ? 57 : 56, s_prof[28] - sc0);
 #endif
   if (!hit) return;
+  collide_manifold(md, d, pc, pair, g1, g2, n, mpos);
+}
+
+// contact manifold of a pair MPR found penetrating (normal n, MPR point mpos)
+DEVI void collide_manifold(const Mdl& md, Dat& d, const PairCtx& pc, int pair, int g1, int g2, const double* n,
+                           const double* mpos) {
+  int lane = lane_id();
   double t1[3], t2[3];
   make_frame(n, t1, t2);
   P2* fa = d.poly;                 // K_MAXPOLY each
@@ -1765,6 +1869,42 @@ DEVI void collide_pair(const Mdl& md, Dat& d, int pair) {
   }
   wsync();
   PT(41);
+}
+
+// two admissible convex pairs whose hulls all have <= 16 vertices, A before B:
+// both MPRs at once on the two halves (PairCtx2), then per pair in order the
+// certificate update and, for a hit, the manifold on the whole wave -- the
+// operations and order of collide_pair(A); collide_pair(B)
+DEVI void collide_pair2(const Mdl& md, Dat& d, int pairA, int pairB) {
+  const int lane = lane_id();
+  const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
+  const int gA1 = p1[pairA], gA2 = p2[pairA], gB1 = p1[pairB], gB2 = p2[pairB];
+  PairCtx2 q;
+  pair_ctx2(md, d, gA1, gA2, gB1, gB2, q);
+  const int g1 = lane < 32 ? gA1 : gB1, g2 = lane < 32 ? gA2 : gB2;
+  double n[3], depth, mpos[3], cd[3], cm;
+  int hit = mpr_penetration(md, d, q, g1, g2, n, &depth, mpos, cd, &cm);
+  PT(4);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int src = 32 * k, pair = k ? pairB : pairA, G1 = k ? gB1 : gA1, G2 = k ? gB2 : gA2;
+    const int hk = __builtin_amdgcn_readlane(hit, src);
+    double nk[3], mk[3], ck[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      nk[i] = readlane_d(n[i], src);
+      mk[i] = readlane_d(mpos[i], src);
+      ck[i] = readlane_d(cd[i], src);
+    }
+    cert_update(md, d, pair, G1, G2, hk, ck, readlane_d(cm, src));
+    PCNT(26, 1);
+    PCNT(27, hk);
+    if (hk) {
+      PairCtx pc;
+      pair_ctx(md, d, G1, G2, pc);
+      collide_manifold(md, d, pc, pair, G1, G2, nk, mk);
+    }
+  }
 }
 
 // Box-box pair (oracle collide_boxbox; MuJoCo's dedicated mjc_BoxBox collider
@@ -2091,6 +2231,13 @@ DEVI void collision(const Mdl& md, Dat& d) {
       sub3(D, c[1], c[0]);
     }
     PT(59);
+    // convex pairs whose four hulls fit 16-lane rows may go two at a time
+    int small2 = 0;
+    if (ov && IA(md, pair_kind)[p] != MGS_PAIR_BOXBOX) {
+      const int32_t *ghull = IA(md, geom_hullid), *hnum = IA(md, hull_vertnum);
+      small2 = hnum[ghull[g[0]]] <= 16 && hnum[ghull[g[1]]] <= 16;
+    }
+    const unsigned long long smallm = __ballot(small2);
     unsigned long long mask = __ballot(ov);
     mask &= ~obb_separated_wave(d, mask, g[0], g[1], D, h[0], h[1], mp);
     PT(60);
@@ -2099,8 +2246,15 @@ DEVI void collision(const Mdl& md, Dat& d) {
     while (mask) {
       int b = __ffsll((long long)mask) - 1;
       mask &= mask - 1ull;
-      if (IA(md, pair_kind)[c0 + b] == MGS_PAIR_BOXBOX) collide_boxbox(md, d, c0 + b);
-      else collide_pair(md, d, c0 + b);
+      if (((smallm >> b) & 1ull) && mask && ((smallm >> (__ffsll((long long)mask) - 1)) & 1ull)) {
+        int b2 = __ffsll((long long)mask) - 1;
+        mask &= mask - 1ull;
+        collide_pair2(md, d, c0 + b, c0 + b2);
+      } else if (IA(md, pair_kind)[c0 + b] == MGS_PAIR_BOXBOX) {
+        collide_boxbox(md, d, c0 + b);
+      } else {
+        collide_pair(md, d, c0 + b);
+      }
     }
   }
 }
