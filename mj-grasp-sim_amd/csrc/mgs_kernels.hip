@@ -3318,47 +3318,75 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   if (lane == 0) d.ITERS += it;
 }
 
-// noslip post-pass (both solvers): friction dims only, unregularised, normals fixed
+// noslip post-pass (both solvers): friction dims only, unregularised, normals fixed.
+// The sweep visits the rows the oracle's does work on -- friction rows and the
+// first row of each contact block of dimension 3 or 4, in ascending order --
+// from a row mask built once per call (lanes over rows), with each row's type
+// and dimension held in registers: the rows a sweep only steps over (equality,
+// limit, other contacts) cost nothing.
 DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
-  for (int ns = 0; ns < md.m.noslip_iterations && ne > 0; ns++) {
+  if (md.m.noslip_iterations <= 0 || ne <= 0) return;
+  int tk[MGS_RPL], dk[MGS_RPL];
+  unsigned long long vis[MGS_RPL];
+#pragma unroll
+  for (int h = 0; h < MGS_RPL; h++) {
+    const int r = lane + h * WAVE;
+    int t = -1, dim = 0, v = 0;
+    if (r < ne) {
+      t = d.efc_type[r];
+      dim = d.efc_dim[r];
+      v = t == MGS_EFC_FRICTION || (t == MGS_EFC_CONTACT && (dim == 3 || dim == 4) && efc_lead(d, r));
+    }
+    tk[h] = t;
+    dk[h] = dim;
+    vis[h] = __ballot(v);
+  }
+  for (int ns = 0; ns < md.m.noslip_iterations; ns++) {
     PCNT(38, 1);
     double improvement = 0.0;
     // the noslip cost drops the regulariser: count its removal at iteration 0
-    if (ns == 0)
-      for (int r = 0; r < ne; r++) {
-        double f = getf(F, r);
-        improvement = improvement + ((0.5 * f) * f) * d.efc_R[r];
+    // (row terms on their lanes, summed in row order)
+    if (ns == 0) {
+#pragma unroll
+      for (int h = 0; h < MGS_RPL; h++) {
+        const int r = lane + h * WAVE;
+        const double f = F.v[h];
+        const double term = r < ne ? ((0.5 * f) * f) * d.efc_R[r] : 0.0;
+        const int nh = ne - h * WAVE < WAVE ? ne - h * WAVE : WAVE;
+        for (int l = 0; l < nh; l++) improvement = improvement + readlane_d(term, l);
       }
-    for (int r = 0; r < ne;) {
-      int t = uni(d.efc_type[r]);
-      int dim = uni(d.efc_dim[r]);
-      if (t == MGS_EFC_FRICTION) {
-        double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
-        double res = tree_sum(g * u, P) + d.efc_b[r];
-        double fo = getf(F, r);
-        double Arr = row_sqnorm(d, r, nv);
-        double fnew[1] = {fo - res * (1.0 / Arr)};
-        project_scalar(t, row_floss(md, d, r), fnew);
-        double delta = fnew[0] - fo;
-        double ch = cost_change1(Arr, delta, res);
-        if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
-        improvement = improvement - ch;
-        if (delta != 0.0) {
-          double s = u + g * delta;
-          if (lane < nv) u = s;
-          setf(F, r, fnew[0], lane);
+    }
+#pragma unroll
+    for (int h = 0; h < MGS_RPL; h++) {
+      unsigned long long m = vis[h];
+      while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        const int r = l + h * WAVE;
+        const int t = __builtin_amdgcn_readlane(tk[h], l), dim = __builtin_amdgcn_readlane(dk[h], l);
+        if (t == MGS_EFC_FRICTION) {
+          double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
+          double res = tree_sum(g * u, P) + d.efc_b[r];
+          double fo = getf(F, r);
+          double Arr = row_sqnorm(d, r, nv);
+          double fnew[1] = {fo - res * (1.0 / Arr)};
+          project_scalar(t, row_floss(md, d, r), fnew);
+          double delta = fnew[0] - fo;
+          double ch = cost_change1(Arr, delta, res);
+          if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
+          improvement = improvement - ch;
+          if (delta != 0.0) {
+            double s = u + g * delta;
+            if (lane < nv) u = s;
+            setf(F, r, fnew[0], lane);
+          }
+        } else if (dim == 3) {
+          improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1);
+        } else {
+          improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1);
         }
-        r += 1;
-      } else if (t == MGS_EFC_CONTACT && dim == 3) {
-        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1);
-        r += 3;
-      } else if (t == MGS_EFC_CONTACT && dim == 4) {
-        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1);
-        r += 4;
-      } else {
-        r += (t == MGS_EFC_CONTACT) ? dim : 1;
       }
     }
     if (improvement * scale < md.m.noslip_tolerance) break;
