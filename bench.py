@@ -37,7 +37,17 @@ import numpy as np  # noqa: E402
 # one hardware queue per HIP stream: S pipeline streams + S escalation streams
 # (the default of 4 queues would serialise an escalation re-run with the next
 # step of the pipeline sharing its queue); set before the runtime starts
-os.environ["GPU_MAX_HW_QUEUES"] = "8"
+def _argv_streams(default=3):
+    a = sys.argv
+    for i, x in enumerate(a):
+        if x == "--streams" and i + 1 < len(a):
+            return int(a[i + 1])
+        if x.startswith("--streams="):
+            return int(x.split("=", 1)[1])
+    return default
+
+
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, 2 * _argv_streams())))
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
