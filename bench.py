@@ -246,6 +246,9 @@ def main():
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
     ap.add_argument("--esc-grid", type=int, default=1, help="workgroups of the escalation list re-run")
     ap.add_argument("--esc-side", type=int, default=1, help="1: escalation re-runs on a side stream per pipeline")
+    ap.add_argument("--fused", type=int, default=1,
+                    help="1: collision mask and rollout in one launch per step (mgs_mask_rollout_device); "
+                         "0: a mask launch, then the rollout launch over its collision-free candidates")
     ap.add_argument("--esc-resume", type=int, default=1,
                     help="1: overflowing candidates stop at the overflowing step and the escalation continues "
                          "them from there (0: re-run from the start)")
@@ -331,6 +334,7 @@ def main():
     NS = abi.MGS["MGS_NSTATS"]
     ESC_GRID = args.esc_grid
     RESUME = bool(args.escalate and args.esc_resume)
+    FUSED = bool(args.fused)
     RW = env.engine.resume_width()
 
     class Pipe:
@@ -376,11 +380,23 @@ def main():
             with torch.cuda.stream(self.stream):
                 if ev:
                     ev[0].record(self.stream)
-                self.eng.collision_free_device(N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(),
-                                               self.free.data_ptr(), predicate="any", stream=sp)
+                if not FUSED:
+                    self.eng.collision_free_device(N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(),
+                                                   self.free.data_ptr(), predicate="any", stream=sp)
                 if ev:
                     ev[1].record(self.stream)
-                if RESUME:
+                if FUSED:
+                    # mask + rollout in one launch (mgs_mask_rollout_device): each
+                    # workgroup computes its candidate's mask and, if collision-free,
+                    # its rollout; no rollout waits for a separate mask launch
+                    rec = self.esc_buffers(k)[6] if RESUME else None
+                    self.eng.mask_rollout_device(sched, N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(),
+                                                 d_ps.data_ptr(), d_pt.data_ptr(), self.free.data_ptr(),
+                                                 self.label.data_ptr(), self.fail.data_ptr(), self.objq.data_ptr(),
+                                                 self.stats.data_ptr(),
+                                                 d_resume_out=rec.data_ptr() if RESUME else None,
+                                                 predicate="any", stream=sp)
+                elif RESUME:
                     rec = self.esc_buffers(k)[6]
                     self.eng.rollout_resumable_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(),
                                                       d_pt.data_ptr(), self.label.data_ptr(), self.fail.data_ptr(),
@@ -441,6 +457,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         pipes[k % len(pipes)].step(k // len(pipes), True)
+    t_enq = time.perf_counter() - t0      # host time to enqueue the K steps (diagnostic)
     torch.cuda.synchronize(dev)
     merged = [p.merge_last() for p in pipes]
     torch.cuda.synchronize(dev)
@@ -532,6 +549,7 @@ def main():
                    "parallelism": f"batch split x{world}", "streams": len(pipes)},
         "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
                    "rollouts_per_s": float(free.sum()) * world * args.steps / dt,
+                   "host_enqueue_s": t_enq,
                    "pipelines_identical": bool(same_pipes),
                    "static_layout_kernel": env.engine.static_layout(),
                    "shard_check": shard_check,

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 14
+#define MGS_ABI_VERSION 15
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -389,6 +389,20 @@ int mgs_rollout_resumable_device(mgs_batch* batch, const mgs_schedule* sched, in
                                  const double* d_phase_target, const uint8_t* d_active, uint8_t* d_label,
                                  int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
                                  void* stream);
+/* The collision mask and the rollout in one launch (ABI 15): each workgroup
+ * computes its candidate's mask exactly as mgs_collision_free_device does
+ * (qpos_init, mocap_pos, mocap_quat, predicate) into d_free_out[i], and a
+ * collision-free candidate then runs mgs_rollout_resumable_device's rollout in
+ * the same workgroup (rejects get mgs_rollout_device's reject outputs), so no
+ * rollout waits for a separate mask launch.  The pair the reference runs as
+ * grasp_collision_mask then grasp_stability_evaluation_from_joints on the
+ * collision-free subset (mgs/cli/filter_to_stable.py:39-50); outputs are those
+ * of the two separate calls, bit for bit.  d_resume_out may be NULL. */
+int mgs_mask_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                            const double* d_mocap_pos, const double* d_mocap_quat, const double* d_phase_start,
+                            const double* d_phase_target, int predicate, uint8_t* d_free_out, uint8_t* d_label,
+                            int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
+                            void* stream);
 
 /* Antipodal candidate ray casting (AntipodalGraspGenerator.generate_grasps,
  * mgs/sampler/antipodal.py:96-172, trimesh intersects_location): for each of

@@ -360,7 +360,8 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
                           const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
                           int32_t* d_stats, const double* d_vstate, double* d_state_out, void* stream,
                           const int32_t* d_list = nullptr, const int32_t* d_count = nullptr, int grid = 0,
-                          double* d_resume_out = nullptr, const double* d_resume_in = nullptr) {
+                          double* d_resume_out = nullptr, const double* d_resume_in = nullptr,
+                          const double* d_mask_mpos = nullptr, int mask_pred = 0, uint8_t* d_mask_out = nullptr) {
   if (!b || !sched || n < 0) return fail(MGS_EINVAL, "mgs_rollout_device: bad argument%s");
   if (sched->nphase < 1 || sched->nphase > MGS_MAX_PHASES) return fail(MGS_EINVAL, "bad phase count%s");
   if (n == 0) return MGS_OK;
@@ -373,13 +374,14 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   if (lrc) return lrc;
   HIPCHK(hipEventRecord(b->e0, st));
   RolloutArgs a{md, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
-                d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in};
+                d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in,
+                d_mask_mpos, mask_pred, d_mask_out};
   if (b->m->special_rollout) {
     const int32_t* I = md.I;
     const double* D = md.D;
     void* p[] = {&a.md, &I, &D, &a.lay, &a.sc, &a.n, &a.qpos_init, &a.mocap_quat, &a.phase_start, &a.phase_target,
                  &a.active, &a.label, &a.fail_step, &a.obj_qpos, &a.stats, &a.vstate_init, &a.state_out, &a.list,
-                 &a.list_count, &a.resume_out, &a.resume_in};
+                 &a.list_count, &a.resume_out, &a.resume_in, &a.mask_mpos, &a.mask_pred, &a.mask_out};
     HIPCHK(hipModuleLaunchKernel(b->m->special_rollout, nwg, 1, 1, 64, 1, 1, b->m->lds_bytes, st, p, nullptr));
   } else {
     const KernelSet* k = kernels_for(md.m.nv);
@@ -432,6 +434,19 @@ int mgs_rollout_resumable_device(mgs_batch* b, const mgs_schedule* sched, int n,
   return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
                         d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, nullptr, nullptr, 0,
                         d_resume_out, nullptr);
+}
+
+int mgs_mask_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
+                            const double* d_mocap_pos, const double* d_mocap_quat, const double* d_phase_start,
+                            const double* d_phase_target, int predicate, uint8_t* d_free_out, uint8_t* d_label,
+                            int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
+                            void* stream) {
+  if (!d_mocap_pos || !d_free_out) return fail(MGS_EINVAL, "mgs_mask_rollout_device: mocap_pos and free_out are required%s");
+  if (predicate < MGS_PRED_ANY_CONTACT || predicate > MGS_PRED_PARTITION_INCL)
+    return fail(MGS_EINVAL, "mgs_mask_rollout_device: bad predicate%s");
+  return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, nullptr, d_label,
+                        d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, nullptr, nullptr, 0,
+                        d_resume_out, nullptr, d_mocap_pos, predicate, d_free_out);
 }
 
 int mgs_simulate_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,

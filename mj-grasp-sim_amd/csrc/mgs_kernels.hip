@@ -1302,7 +1302,12 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
   mulmtv3(nl, R, n);
   double base = dot3(x, n);
   if (rr > 0.0) base = (sign > 0) ? base + rr : base - rr;   // rounded: surface = hull (+) ball
+  // the collecting pass takes the extreme its first pass computed (*ext): the
+  // same expressions over the same vertices, so the same value
   double best = (sign > 0) ? -INFINITY : INFINITY;
+  if (collect) {
+    best = *ext;
+  } else {
   if (num <= WAVE) {
     if (lane < num) best = base + ((cv[0] * nl[0] + cv[1] * nl[1]) + cv[2] * nl[2]);
   } else {
@@ -1339,7 +1344,8 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
     best = b0;
   }
   *ext = best;
-  if (!collect) return 0;
+  return 0;
+  }
   double lim = (sign > 0) ? best - tol : best + tol;
   int cnt = 0;
   for (int c0 = 0; c0 < num && cnt < K_MAXF; c0 += WAVE) {
@@ -1802,7 +1808,7 @@ DEVI void collide_manifold(const Mdl& md, Dat& d, const PairCtx& pc, int pair, i
   double* dep = d.pdep;
   double s1, s2;
   // first pass: only the extremes are used (the oracle's first feature() pass
-  // output is overwritten by the second)
+  // output is overwritten by the second); the collecting pass starts from them
   feature(pc, 1, n, t1, t2, +1, 0.0, 0, fa, &s1);
   feature(pc, 2, n, t1, t2, -1, 0.0, 0, fb, &s2);
   double dn = s1 - s2;
@@ -4401,9 +4407,25 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
                       const uint8_t* __restrict__ active, uint8_t* __restrict__ label,
                       int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
                       const double* __restrict__ vstate_init, double* __restrict__ state_out,
-                      double* resume_out, const double* resume_in) {
+                      double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
+                      int mask_pred, uint8_t* __restrict__ mask_out) {
   int lane = lane_id();
-  if (active && !active[i]) {
+  int reject = active && !active[i];
+  if (mask_out) {
+    // fused collision mask (mgs_mask_rollout_device): collision_entry's
+    // computation for this candidate, then the rollout of the collision-free
+    // ones in the same workgroup -- no separate mask launch to wait for
+    Dat d0;
+    bind<SL>(d0, smem, lay);
+    reset(md, d0, qpos_init + (size_t)i * md.m.nq, mask_mpos + 3 * i, mocap_quat + 4 * i);
+    forward<NV>(md, d0, 0);
+    int hit = (mask_pred == MGS_PRED_ANY_CONTACT) ? (uni(d0.NCON) != 0)
+              : (mask_pred == MGS_PRED_PARTITION_INCL) ? obj_contact_incl(md, d0) : obj_contact(md, d0);
+    if (lane == 0) mask_out[i] = (uint8_t)(hit ? 0 : 1);
+    wsync();
+    reject = hit;
+  }
+  if (reject) {
     // collision-mask reject: not simulated (filter_to_stable.py:39-44)
     if (lane == 0) {
       label[i] = 0;
@@ -4572,7 +4594,8 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
                         int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
                         const double* __restrict__ vstate_init, double* __restrict__ state_out,
                         const int32_t* __restrict__ list, const int32_t* __restrict__ list_count,
-                        double* resume_out, const double* resume_in) {
+                        double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
+                        int mask_pred, uint8_t* __restrict__ mask_out) {
   Mdl md = mdarg;
   // SL: the model description is the baked one too, so sizes, table offsets and
   // options are compile-time constants (trip counts, immediate offsets)
@@ -4585,7 +4608,8 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
     int i = list ? list[s] : s;
     if (i < 0 || i >= n) continue;
     rollout_one<NV, SL>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target, active, label,
-                    fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in);
+                    fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in, mask_mpos,
+                    mask_pred, mask_out);
   }
 }
 
@@ -4601,11 +4625,12 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
                    uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
                    int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
                    double* __restrict__ state_out, const int32_t* __restrict__ list,
-                   const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in) {
+                   const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in,
+                   const double* __restrict__ mask_mpos, int mask_pred, uint8_t* __restrict__ mask_out) {
   extern __shared__ double smem[];
   rollout_entry<NV, SL>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target, active,
                         label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count, resume_out,
-                        resume_in);
+                        resume_in, mask_mpos, mask_pred, mask_out);
 }
 
 // the library's non-template kernels live in the C-ABI translation unit only

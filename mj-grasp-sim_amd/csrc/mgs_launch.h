@@ -29,6 +29,9 @@ struct RolloutArgs {
   const int32_t *list, *list_count;
   double* resume_out;
   const double* resume_in;
+  const double* mask_mpos;   // fused collision mask (mgs_mask_rollout_device): mocap positions,
+  int mask_pred;             // predicate
+  uint8_t* mask_out;         // and the mask written per candidate (nullptr: no fused mask)
 };
 
 // one dof count's runtime-layout kernels: launchers (64 lanes per workgroup,

@@ -56,6 +56,7 @@ def load_library(wide: bool = False):
     L.mgs_rollout_list_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, ctypes.c_int, vp, vp, vp, vp,
                                           vp, vp, vp, vp, vp, vp]
     L.mgs_rollout_resumable_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 11
+    L.mgs_mask_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 5 + [ctypes.c_int] + [vp] * 7
     L.mgs_rollout_resume.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
                                      P(abi.RolloutOut)]
     L.mgs_last_kernel_ms.argtypes = [vp]
@@ -359,6 +360,15 @@ class Engine:
         self._ck(self.lib.mgs_rollout_resumable_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps,
                                                      d_pt, d_active, d_label, d_fail, d_objq, d_stats,
                                                      d_resume_out, stream), "mgs_rollout_resumable_device")
+
+    def mask_rollout_device(self, sched, n, d_qpos, d_mpos, d_mquat, d_ps, d_pt, d_free, d_label, d_fail, d_objq,
+                            d_stats, d_resume_out=None, predicate="any", stream=None):
+        """collision mask and rollout in one launch (mgs_mask_rollout_device):
+        d_free gets the mask, the collision-free candidates are rolled out, the
+        outputs are those of collision_free_device + rollout_resumable_device"""
+        self._ck(self.lib.mgs_mask_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mpos, d_mquat, d_ps,
+                                                d_pt, abi.predicate_code(predicate), d_free, d_label, d_fail, d_objq,
+                                                d_stats, d_resume_out, stream), "mgs_mask_rollout_device")
 
     def rollout_list_device(self, sched, n, d_count, d_list, grid, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail,
                             d_objq, d_stats, stream=None, d_resume_in=None):

@@ -183,6 +183,46 @@ def test_device_entry_with_active_mask(env, eng, candidates, oracle_model):
     assert np.array_equal(objq.cpu().numpy()[rej], q[rej][:, plan.obj_qposadr:plan.obj_qposadr + 7])
 
 
+def test_fused_mask_rollout_equals_separate_launches(env, eng, candidates):
+    """mgs_mask_rollout_device (the bench path) = mgs_collision_free_device then
+    mgs_rollout_resumable_device over its mask, bit for bit: mask, labels, fail
+    steps, object poses, statistics and resume records"""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    plan = plan_for(env, poses, J)
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                              check_offset=getattr(plan, "check_offset", None))
+    n = len(q)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+    dq, dmp, dmq, dps, dpt = t(q), t(mp), t(mq), t(plan.phase_start), t(plan.phase_target)
+    rw = eng.resume_width()
+    outs = []
+    for fused in (False, True):
+        o = dict(free=torch.zeros(n, dtype=torch.uint8, device=dev), lab=torch.zeros(n, dtype=torch.uint8, device=dev),
+                 fail=torch.zeros(n, dtype=torch.int32, device=dev),
+                 objq=torch.zeros((n, 7), dtype=torch.float64, device=dev),
+                 st=torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev),
+                 rec=torch.zeros((n, rw), dtype=torch.float64, device=dev))
+        if fused:
+            eng.mask_rollout_device(sched, n, dq.data_ptr(), dmp.data_ptr(), dmq.data_ptr(), dps.data_ptr(),
+                                    dpt.data_ptr(), o["free"].data_ptr(), o["lab"].data_ptr(), o["fail"].data_ptr(),
+                                    o["objq"].data_ptr(), o["st"].data_ptr(), d_resume_out=o["rec"].data_ptr())
+        else:
+            eng.collision_free_device(n, dq.data_ptr(), dmp.data_ptr(), dmq.data_ptr(), o["free"].data_ptr())
+            eng.rollout_resumable_device(sched, n, dq.data_ptr(), dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
+                                         o["lab"].data_ptr(), o["fail"].data_ptr(), o["objq"].data_ptr(),
+                                         o["st"].data_ptr(), o["rec"].data_ptr(), d_active=o["free"].data_ptr())
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu().numpy() for k, v in o.items()})
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+    assert 0 < outs[1]["free"].sum() < n
+
+
 def test_device_overflow_list_and_list_rollout(env, eng, candidates):
     """mgs_overflow_list_device picks the flagged candidates; mgs_rollout_list_device
     with a grid smaller than the list (workgroups loop over it) reproduces
