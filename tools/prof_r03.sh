@@ -7,7 +7,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-prof}
 mkdir -p $OUT
-P="bench.py --streams 1 --steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate"
+P="bench.py --streams 1 --steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate --fused 0"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench -f csv -- python3 bench.py --cpu-budget 0 --e2e-steps 0 > $OUT/trace.json 2> $OUT/trace.err && \
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc_fetch -o pmc -f csv -- python3 $P > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err && \
