@@ -252,6 +252,9 @@ def main():
     ap.add_argument("--esc-resume", type=int, default=1,
                     help="1: overflowing candidates stop at the overflowing step and the escalation continues "
                          "them from there (0: re-run from the start)")
+    ap.add_argument("--queue", type=int, default=None,
+                    help="rollout launch mode (mgs_rollout_queue): 0 one workgroup per candidate, 1 the work queue "
+                         "on the resident grid (the library default)")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's layout and exit (no GPU work)")
@@ -319,6 +322,8 @@ def main():
                                   check_offset=getattr(plan, "check_offset", None))
     horizon = plan.horizon
     eng = env.engine
+    if args.queue is not None:
+        eng.lib.mgs_rollout_queue(args.queue)
     dev = torch.device("cuda", local)
     f64 = dict(dtype=torch.float64, device=dev)
     d_q = torch.as_tensor(qpos, **f64).contiguous()
@@ -552,6 +557,7 @@ def main():
                    "host_enqueue_s": t_enq,
                    "pipelines_identical": bool(same_pipes),
                    "static_layout_kernel": env.engine.static_layout(),
+                   "rollout_grid": env.engine.rollout_grid(N),
                    "shard_check": shard_check,
                    "end_to_end_api": e2e,
                    "issue": issue_summary(),

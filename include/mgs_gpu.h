@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 15
+#define MGS_ABI_VERSION 16
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -403,6 +403,21 @@ int mgs_mask_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n, 
                             const double* d_phase_target, int predicate, uint8_t* d_free_out, uint8_t* d_label,
                             int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
                             void* stream);
+/* Launch shape of the rollout calls above (ABI 16).  A rollout over n
+ * candidates runs as a work queue: the grid is the number of rollout
+ * workgroups the device holds at once (occupancy at this model's LDS size x
+ * CUs) and each workgroup takes the next candidate index from a counter when
+ * its previous rollout ends, so rejected, early-failing and full-length
+ * candidates pack the slots; outputs are independent of the order.  Returns
+ * that grid (n if n is smaller, or in mode 0 of mgs_rollout_queue: one
+ * workgroup per candidate); needs the device. */
+int mgs_rollout_grid(mgs_batch* batch, int n);
+/* Rollout launch mode for this process; returns the previous one and leaves it
+ * unchanged if mode < 0.  0: one workgroup per candidate; 1 (default): the work
+ * queue on the resident grid; k >= 2: the queue on at most k workgroups (tests
+ * exercise the queue with small batches this way).  MGS_QUEUE in the
+ * environment sets the initial mode. */
+int mgs_rollout_queue(int mode);
 
 /* Antipodal candidate ray casting (AntipodalGraspGenerator.generate_grasps,
  * mgs/sampler/antipodal.py:96-172, trimesh intersects_location): for each of

@@ -18,6 +18,10 @@
 #include "mgs_sampler.hip"
 #include "mgs_contact.hip"
 
+#include <cstdlib>
+
+#define MGS_QUEUE_RING 64
+
 namespace {
 thread_local std::string g_err;
 
@@ -169,6 +173,7 @@ struct mgs_model {
   // model-specialised code object (mgs_special.hip), if attached
   hipModule_t special_mod;
   hipFunction_t special_collision, special_rollout;
+  int resident;     // rollout workgroups the device holds at once (work-queue grid), 0 = not computed yet
 };
 
 struct mgs_batch {
@@ -180,6 +185,8 @@ struct mgs_batch {
   double* d_G;      // MGS_G_GLOBAL: per-candidate constraint rows (HBM)
   size_t g_elems;
   double* d_resume; // resume records (n * (nq + 2 nv + MGS_RESUME_EXTRA)), allocated on first use
+  int32_t* d_queue; // work-queue counters, one per launch in a ring (launches in flight on other streams
+  int qslot;        // keep their own counter)
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
@@ -256,7 +263,8 @@ int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out) {
             hipMalloc(&b->d_objq, sizeof(double) * n * 7) == hipSuccess &&
             hipMalloc(&b->d_label, n) == hipSuccess && hipMalloc(&b->d_free, n) == hipSuccess &&
             hipMalloc(&b->d_fail, sizeof(int32_t) * n) == hipSuccess &&
-            hipMalloc(&b->d_stats, sizeof(int32_t) * n * MGS_NSTATS) == hipSuccess;
+            hipMalloc(&b->d_stats, sizeof(int32_t) * n * MGS_NSTATS) == hipSuccess &&
+            hipMalloc(&b->d_queue, sizeof(int32_t) * MGS_QUEUE_RING) == hipSuccess;
   if (!ok) {
     mgs_batch_close(b);
     return fail(MGS_ENOMEM, "device allocation failed%s");
@@ -275,6 +283,7 @@ void mgs_batch_close(mgs_batch* b) {
   hipFree(b->d_objq); hipFree(b->d_label); hipFree(b->d_free); hipFree(b->d_fail); hipFree(b->d_stats);
   if (b->d_G) hipFree(b->d_G);
   if (b->d_resume) hipFree(b->d_resume);
+  if (b->d_queue) hipFree(b->d_queue);
   if (b->e0) hipEventDestroy(b->e0);
   if (b->e1) hipEventDestroy(b->e1);
   if (b->e2) hipEventDestroy(b->e2);
@@ -299,6 +308,43 @@ static int launch_layout(mgs_batch* b, int n, Lay* lay) {
   lay->gmem = b->d_G;
 #endif
   return MGS_OK;
+}
+
+// Rollout launches run as a work queue by default: the grid is the number of
+// rollout workgroups the device holds at once (occupancy of the launched
+// function at this model's LDS size x CUs) and each workgroup pulls candidate
+// indices from a zeroed counter.  Mode (mgs_rollout_queue; MGS_QUEUE in the
+// environment sets the initial one): 0 one workgroup per candidate, 1 the
+// queue on the resident grid, k >= 2 the queue on at most k workgroups (tests).
+static int g_queue_mode = -1;
+
+static int queue_mode() {
+  if (g_queue_mode < 0) {
+    const char* e = getenv("MGS_QUEUE");
+    g_queue_mode = e ? atoi(e) : 1;
+    if (g_queue_mode < 0) g_queue_mode = 1;
+  }
+  return g_queue_mode;
+}
+
+static int resident_workgroups(mgs_model* m) {
+  if (m->resident) return m->resident;
+  int per_cu = 0, cus = 0;
+  hipError_t e;
+  if (m->special_rollout) {
+    e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m->special_rollout, 64, m->lds_bytes);
+  } else {
+    const KernelSet* k = kernels_for(m->desc.nv);
+    e = k ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k->rollout_fn, 64, m->lds_bytes) : hipErrorInvalidValue;
+  }
+  if (e != hipSuccess || per_cu < 1 ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->device) != hipSuccess || cus < 1) {
+    (void)hipGetLastError();
+    m->resident = -1;       // unknown: one workgroup per candidate
+    return -1;
+  }
+  m->resident = per_cu * cus;
+  return m->resident;
 }
 
 static Mdl device_model(const mgs_model* m) {
@@ -369,19 +415,29 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   hipStream_t st = (hipStream_t)stream;
   Mdl md = device_model(b->m);
   Lay lay;
-  const int nwg = d_list ? grid : n;
+  int nwg = d_list ? grid : n;
+  int32_t* q = nullptr;
+  if (!d_list && queue_mode() > 0) {
+    int r = resident_workgroups(b->m);
+    if (queue_mode() > 1 && r > queue_mode()) r = queue_mode();
+    if (r > 0 && r < n) {
+      nwg = r;
+      q = b->d_queue + (b->qslot++ % MGS_QUEUE_RING);
+    }
+  }
   int lrc = launch_layout(b, nwg, &lay);
   if (lrc) return lrc;
+  if (q) HIPCHK(hipMemsetAsync(q, 0, sizeof(int32_t), st));
   HIPCHK(hipEventRecord(b->e0, st));
   RolloutArgs a{md, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
                 d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in,
-                d_mask_mpos, mask_pred, d_mask_out};
+                d_mask_mpos, mask_pred, d_mask_out, q};
   if (b->m->special_rollout) {
     const int32_t* I = md.I;
     const double* D = md.D;
     void* p[] = {&a.md, &I, &D, &a.lay, &a.sc, &a.n, &a.qpos_init, &a.mocap_quat, &a.phase_start, &a.phase_target,
                  &a.active, &a.label, &a.fail_step, &a.obj_qpos, &a.stats, &a.vstate_init, &a.state_out, &a.list,
-                 &a.list_count, &a.resume_out, &a.resume_in, &a.mask_mpos, &a.mask_pred, &a.mask_out};
+                 &a.list_count, &a.resume_out, &a.resume_in, &a.mask_mpos, &a.mask_pred, &a.mask_out, &a.queue};
     HIPCHK(hipModuleLaunchKernel(b->m->special_rollout, nwg, 1, 1, 64, 1, 1, b->m->lds_bytes, st, p, nullptr));
   } else {
     const KernelSet* k = kernels_for(md.m.nv);
@@ -869,7 +925,23 @@ int mgs_model_attach_special(mgs_model* m, const char* path) {
   m->special_mod = mod;
   m->special_collision = fc;
   m->special_rollout = fr;
+  m->resident = 0;          // occupancy of the new rollout function, computed at its first launch
   return MGS_OK;
+}
+
+int mgs_rollout_grid(mgs_batch* b, int n) {
+  if (!b || n < 0) return fail(MGS_EINVAL, "mgs_rollout_grid: bad argument%s");
+  if (hipSetDevice(b->m->device) != hipSuccess) return fail(MGS_EHIP, "mgs_rollout_grid: hipSetDevice failed%s");
+  if (queue_mode() == 0) return n;
+  int r = resident_workgroups(b->m);
+  if (queue_mode() > 1 && r > queue_mode()) r = queue_mode();
+  return (r > 0 && r < n) ? r : n;
+}
+
+int mgs_rollout_queue(int mode) {
+  int prev = queue_mode();
+  if (mode >= 0) g_queue_mode = mode;
+  return prev;
 }
 
 int mgs_device_count(void) {

@@ -4595,13 +4595,30 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
                         const double* __restrict__ vstate_init, double* __restrict__ state_out,
                         const int32_t* __restrict__ list, const int32_t* __restrict__ list_count,
                         double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
-                        int mask_pred, uint8_t* __restrict__ mask_out) {
+                        int mask_pred, uint8_t* __restrict__ mask_out, int32_t* queue) {
   Mdl md = mdarg;
   // SL: the model description is the baked one too, so sizes, table offsets and
   // options are compile-time constants (trip counts, immediate offsets)
   if constexpr (SL != 0) md.m = mgs_sl_desc;
   md.I = mI;
   md.D = mD;
+  if (queue) {
+    // work queue (queue != nullptr, a zeroed counter): the grid is the device's
+    // resident capacity and each workgroup takes the next candidate index when
+    // its previous one ends, so short (rejected, early-failing) and long
+    // rollouts pack the slots regardless of which XCD a workgroup landed on;
+    // the launch has a single tail
+    for (;;) {
+      int s = 0;
+      if (lane_id() == 0) s = atomicAdd(queue, 1);
+      s = __builtin_amdgcn_readfirstlane(s);
+      if (s >= n) break;
+      rollout_one<NV, SL>(md, smem, lay, sc, s, qpos_init, mocap_quat, phase_start, phase_target, active, label,
+                          fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in, mask_mpos,
+                          mask_pred, mask_out);
+    }
+    return;
+  }
   const int end = list ? *list_count : (blockIdx.x < (unsigned)n ? (int)blockIdx.x + 1 : 0);
   const int stride = list ? (int)gridDim.x : 1;
   for (int s = blockIdx.x; s < end; s += stride) {
@@ -4626,11 +4643,12 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
                    int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
                    double* __restrict__ state_out, const int32_t* __restrict__ list,
                    const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in,
-                   const double* __restrict__ mask_mpos, int mask_pred, uint8_t* __restrict__ mask_out) {
+                   const double* __restrict__ mask_mpos, int mask_pred, uint8_t* __restrict__ mask_out,
+                   int32_t* queue) {
   extern __shared__ double smem[];
   rollout_entry<NV, SL>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target, active,
                         label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count, resume_out,
-                        resume_in, mask_mpos, mask_pred, mask_out);
+                        resume_in, mask_mpos, mask_pred, mask_out, queue);
 }
 
 // the library's non-template kernels live in the C-ABI translation unit only

@@ -32,6 +32,7 @@ struct RolloutArgs {
   const double* mask_mpos;   // fused collision mask (mgs_mask_rollout_device): mocap positions,
   int mask_pred;             // predicate
   uint8_t* mask_out;         // and the mask written per candidate (nullptr: no fused mask)
+  int32_t* queue;            // work-queue counter (zeroed before the launch; nullptr: one workgroup per candidate)
 };
 
 // one dof count's runtime-layout kernels: launchers (64 lanes per workgroup,

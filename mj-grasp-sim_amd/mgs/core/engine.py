@@ -84,6 +84,10 @@ def load_library(wide: bool = False):
     L.mgs_contact_optimize.argtypes = [ctypes.c_int, P(abi.KinDesc), ctypes.c_int] + [P(c_d)] * 9
     L.mgs_supports_nv.argtypes = [ctypes.c_int]
     L.mgs_supports_nv.restype = ctypes.c_int
+    L.mgs_rollout_grid.argtypes = [vp, ctypes.c_int]
+    L.mgs_rollout_grid.restype = ctypes.c_int
+    L.mgs_rollout_queue.argtypes = [ctypes.c_int]
+    L.mgs_rollout_queue.restype = ctypes.c_int
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
         raise EngineError(f"{os.path.basename(path)} ABI version mismatch with include/mgs_gpu.h")
     _libs[path] = L
@@ -249,6 +253,14 @@ class Engine:
             self._ck(self.lib.mgs_batch_open(self._model, cap, ctypes.byref(self._batch)), "mgs_batch_open")
             self._cap = cap
         return self._batch
+
+    def rollout_grid(self, n):
+        """workgroups a rollout launch over n candidates uses (mgs_rollout_grid:
+        the device's resident capacity when the work queue runs, else n)"""
+        g = self.lib.mgs_rollout_grid(self.batch(max(1, n)), n)
+        if g < 0:
+            raise EngineError(f"mgs_rollout_grid: {self.lib.mgs_last_error().decode()}")
+        return g
 
     def collision_free(self, qpos, mocap_pos, mocap_quat, predicate="any"):
         n = len(qpos)

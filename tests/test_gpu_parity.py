@@ -223,6 +223,59 @@ def test_fused_mask_rollout_equals_separate_launches(env, eng, candidates):
     assert 0 < outs[1]["free"].sum() < n
 
 
+def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, oracle_model):
+    """The work-queue launch (mgs_rollout_queue: a grid of k workgroups pulling
+    candidate indices from a counter) gives every output of one workgroup per
+    candidate bit for bit -- fused mask, labels, fail steps, object poses,
+    statistics, resume records -- whatever the grid (k = 1, 5, 64 here; the
+    default grid is the device's resident capacity), and equals the oracle."""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    plan = plan_for(env, poses, J)
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
+                              check_offset=getattr(plan, "check_offset", None))
+    n = len(q)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+    dq, dmp, dmq, dps, dpt = t(q), t(mp), t(mq), t(plan.phase_start), t(plan.phase_target)
+    rw = eng.resume_width()
+    L = eng.lib
+    prev = L.mgs_rollout_queue(-1)
+    outs = {}
+    try:
+        for mode in (0, 1, 5, 64):
+            L.mgs_rollout_queue(mode)
+            assert eng.rollout_grid(n) == (n if mode <= 1 else mode)
+            o = dict(free=torch.zeros(n, dtype=torch.uint8, device=dev),
+                     lab=torch.zeros(n, dtype=torch.uint8, device=dev),
+                     fail=torch.zeros(n, dtype=torch.int32, device=dev),
+                     objq=torch.zeros((n, 7), dtype=torch.float64, device=dev),
+                     st=torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev),
+                     rec=torch.zeros((n, rw), dtype=torch.float64, device=dev))
+            for _ in range(2):      # two launches in a row: the counter ring restarts each one
+                eng.mask_rollout_device(sched, n, dq.data_ptr(), dmp.data_ptr(), dmq.data_ptr(), dps.data_ptr(),
+                                        dpt.data_ptr(), o["free"].data_ptr(), o["lab"].data_ptr(),
+                                        o["fail"].data_ptr(), o["objq"].data_ptr(), o["st"].data_ptr(),
+                                        d_resume_out=o["rec"].data_ptr())
+            torch.cuda.synchronize()
+            outs[mode] = {k: v.cpu().numpy() for k, v in o.items()}
+    finally:
+        L.mgs_rollout_queue(prev)
+    for mode in (1, 5, 64):
+        for k in outs[0]:
+            assert np.array_equal(outs[0][k], outs[mode][k]), (mode, k)
+    free = outs[5]["free"].astype(bool)
+    assert np.array_equal(free, oracle_model.collision_free(q, mp, mq, nthreads=8))
+    idx = np.nonzero(free)[0]
+    ro = oracle_model.rollout(plan_for(env, poses[idx], J[idx]), nthreads=8)
+    assert np.array_equal(outs[5]["lab"].astype(bool)[idx], ro["label"])
+    assert np.array_equal(outs[5]["fail"][idx], ro["fail_step"])
+    assert np.array_equal(outs[5]["objq"][idx], ro["obj_qpos"])
+
+
 def test_device_overflow_list_and_list_rollout(env, eng, candidates):
     """mgs_overflow_list_device picks the flagged candidates; mgs_rollout_list_device
     with a grid smaller than the list (workgroups loop over it) reproduces
