@@ -10,7 +10,7 @@ resident in HBM when the timed region starts; each step runs the mask, the
 rollout (which reads the mask on the device) and the device-built list of
 capacity overflows on one HIP stream with no host round trip; the listed
 candidates are re-run wider on a side stream (the env's escalation).  Steps rotate over
-`--streams` pipelines (engine + stream each, default 3), so one batch's
+`--streams` pipelines (engine + stream each, default 4), so one batch's
 rollout tail overlaps the next batches' work; every step is a whole batch.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--candidates 8192]
@@ -37,7 +37,7 @@ import numpy as np  # noqa: E402
 # one hardware queue per HIP stream: S pipeline streams + S escalation streams
 # (the default of 4 queues would serialise an escalation re-run with the next
 # step of the pipeline sharing its queue); set before the runtime starts
-def _argv_streams(default=3):
+def _argv_streams(default=4):
     a = sys.argv
     for i, x in enumerate(a):
         if x == "--streams" and i + 1 < len(a):
@@ -241,7 +241,7 @@ def main():
                     help="also time the drop-in API on the batch repeated this many times in one call (0 = skip)")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
     ap.add_argument("--esc-grid", type=int, default=1, help="workgroups of the escalation list re-run")
@@ -255,6 +255,9 @@ def main():
     ap.add_argument("--queue", type=int, default=None,
                     help="rollout launch mode (mgs_rollout_queue): 0 one workgroup per candidate, 1 the work queue "
                          "on the resident grid (the library default)")
+    ap.add_argument("--slice", type=int, default=None,
+                    help="time slices of the queue's items (mgs_rollout_slicing): 0 none, 1 auto (the library "
+                         "default), k >= 2 k steps")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's layout and exit (no GPU work)")
@@ -324,6 +327,8 @@ def main():
     eng = env.engine
     if args.queue is not None:
         eng.lib.mgs_rollout_queue(args.queue)
+    if args.slice is not None:
+        eng.lib.mgs_rollout_slicing(args.slice)
     dev = torch.device("cuda", local)
     f64 = dict(dtype=torch.float64, device=dev)
     d_q = torch.as_tensor(qpos, **f64).contiguous()
@@ -558,6 +563,7 @@ def main():
                    "pipelines_identical": bool(same_pipes),
                    "static_layout_kernel": env.engine.static_layout(),
                    "rollout_grid": env.engine.rollout_grid(N),
+                   "slice_steps": env.engine.lib.mgs_rollout_slice_steps(horizon),
                    "shard_check": shard_check,
                    "end_to_end_api": e2e,
                    "issue": issue_summary(),

@@ -32,7 +32,9 @@ struct RolloutArgs {
   const double* mask_mpos;   // fused collision mask (mgs_mask_rollout_device): mocap positions,
   int mask_pred;             // predicate
   uint8_t* mask_out;         // and the mask written per candidate (nullptr: no fused mask)
-  int32_t* queue;            // work-queue counter (zeroed before the launch; nullptr: one workgroup per candidate)
+  uint32_t* queue;           // work-queue counter (nullptr: one workgroup per candidate)
+  uint32_t qbase;            // its value when the launch starts
+  Slc slc;                   // time slices of the queue's items (slc.steps 0: none)
 };
 
 // one dof count's runtime-layout kernels: launchers (64 lanes per workgroup,
