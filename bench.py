@@ -255,9 +255,6 @@ def main():
     ap.add_argument("--queue", type=int, default=None,
                     help="rollout launch mode (mgs_rollout_queue): 0 one workgroup per candidate, 1 the work queue "
                          "on the resident grid (the library default)")
-    ap.add_argument("--slice", type=int, default=None,
-                    help="time slices of the queue's items (mgs_rollout_slicing): 0 none, 1 auto (the library "
-                         "default), k >= 2 k steps")
     ap.add_argument("--no-escalate", dest="escalate", action="store_false",
                     help="skip the contact-capacity re-run of overflowed candidates")
     ap.add_argument("--dry-run", action="store_true", help="print each rank's layout and exit (no GPU work)")
@@ -327,8 +324,6 @@ def main():
     eng = env.engine
     if args.queue is not None:
         eng.lib.mgs_rollout_queue(args.queue)
-    if args.slice is not None:
-        eng.lib.mgs_rollout_slicing(args.slice)
     dev = torch.device("cuda", local)
     f64 = dict(dtype=torch.float64, device=dev)
     d_q = torch.as_tensor(qpos, **f64).contiguous()
@@ -563,7 +558,6 @@ def main():
                    "pipelines_identical": bool(same_pipes),
                    "static_layout_kernel": env.engine.static_layout(),
                    "rollout_grid": env.engine.rollout_grid(N),
-                   "slice_steps": env.engine.lib.mgs_rollout_slice_steps(horizon),
                    "shard_check": shard_check,
                    "end_to_end_api": e2e,
                    "issue": issue_summary(),

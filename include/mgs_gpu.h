@@ -272,8 +272,8 @@ typedef struct mgs_rollout_out {
                               qacc_warmstart, time) and the schedule position / partial stats, from
                               which mgs_rollout_resume continues it with more capacity */
 } mgs_rollout_out;
-#define MGS_RESUME_EXTRA 10        /* time, phase, step in phase, global step, max ncon, max nefc,
-                                      sum ncon, sum nefc, solver iterations, stats flags so far */
+#define MGS_RESUME_EXTRA 9         /* time, phase, step in phase, global step, max ncon, max nefc,
+                                      sum ncon, sum nefc, solver iterations */
 
 typedef struct mgs_model mgs_model;
 typedef struct mgs_batch mgs_batch;
@@ -418,22 +418,6 @@ int mgs_rollout_grid(mgs_batch* batch, int n);
  * exercise the queue with small batches this way).  MGS_QUEUE in the
  * environment sets the initial mode. */
 int mgs_rollout_queue(int mode);
-/* Time slices of a work-queue launch (ABI 16).  The queue's items are then
- * (candidate, slice) pairs, slice-major: an item runs at most k steps of its
- * candidate, leaves the state in a per-candidate slice record (the resume
- * record layout) and the next slice's item continues it, so the rollouts of a
- * launch share every slot round-robin instead of the last ones starting when
- * the first ones end (a launch with more rollouts than slots finishes near
- * total work / slots instead of a whole rollout later).  Outputs equal the
- * unsliced launch bit for bit.  Mode: returns the previous one, unchanged if
- * mode < 0; 0 no slicing; 1 (default) k = max(25, horizon / 32); k >= 2 fixed
- * k steps.  A launch slices when the queue runs and the horizon exceeds k;
- * with a forced queue grid (mgs_rollout_queue k >= 2) also when n is smaller
- * than the resident capacity.  MGS_SLICE in the environment sets the initial
- * mode.  mgs_rollout_slice_steps(horizon): k for a schedule of `horizon`
- * steps under the current mode (0: not sliced); host-only. */
-int mgs_rollout_slicing(int mode);
-int mgs_rollout_slice_steps(int horizon);
 
 /* Antipodal candidate ray casting (AntipodalGraspGenerator.generate_grasps,
  * mgs/sampler/antipodal.py:96-172, trimesh intersects_location): for each of

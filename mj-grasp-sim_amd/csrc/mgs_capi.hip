@@ -188,10 +188,6 @@ struct mgs_batch {
   uint32_t* d_queue;                // work-queue counters, one per launch in a ring (launches in flight on
   int qslot;                        // other streams keep their own counter), never reset: each launch
   uint32_t qbase[MGS_QUEUE_RING];   // advances its counter by n + grid, the next launch's base
-  uint32_t* d_progress;             // time slices (Slc): per-candidate progress words and slice records,
-  double* d_slice_rec;              // grown on demand to slice_n candidates
-  int slice_n;
-  uint32_t epoch;                   // the last sliced launch's tag
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
@@ -293,8 +289,6 @@ void mgs_batch_close(mgs_batch* b) {
   if (b->d_G) hipFree(b->d_G);
   if (b->d_resume) hipFree(b->d_resume);
   if (b->d_queue) hipFree(b->d_queue);
-  if (b->d_progress) hipFree(b->d_progress);
-  if (b->d_slice_rec) hipFree(b->d_slice_rec);
   if (b->e0) hipEventDestroy(b->e0);
   if (b->e1) hipEventDestroy(b->e1);
   if (b->e2) hipEventDestroy(b->e2);
@@ -328,29 +322,6 @@ static int launch_layout(mgs_batch* b, int n, Lay* lay) {
 // environment sets the initial one): 0 one workgroup per candidate, 1 the
 // queue on the resident grid, k >= 2 the queue on at most k workgroups (tests).
 static int g_queue_mode = -1;
-// Time slices of the queue's items (Slc in mgs_kernels.hip): 0 none, 1 auto
-// (max(25, horizon / 32) steps per slice), k >= 2 k steps per slice.  MGS_SLICE
-// in the environment sets the initial mode.
-static int g_slice_mode = -1;
-
-static int slice_mode() {
-  if (g_slice_mode < 0) {
-    const char* e = getenv("MGS_SLICE");
-    g_slice_mode = e ? atoi(e) : 1;
-    if (g_slice_mode < 0) g_slice_mode = 1;
-  }
-  return g_slice_mode;
-}
-
-// steps per slice for a schedule of `horizon` steps (0: one slice)
-static int slice_steps(int horizon) {
-  const int m = slice_mode();
-  if (m == 0 || horizon < 2) return 0;
-  int k = (m == 1) ? (horizon + 31) / 32 : m;
-  if (m == 1 && k < 25) k = 25;
-  if ((horizon + k - 1) / k > 250) k = (horizon + 249) / 250;   // progress words count slices in 8 bits
-  return k < horizon ? k : 0;
-}
 
 static int queue_mode() {
   if (g_queue_mode < 0) {
@@ -379,26 +350,6 @@ static int resident_workgroups(mgs_model* m) {
   }
   m->resident = per_cu * cus;
   return m->resident;
-}
-
-// slice buffers for n candidates (device entry points take any n): grown, zeroed
-// and synchronised before the launch that needs them (a one-off stall)
-static int ensure_slices(mgs_batch* b, int n) {
-  if (n <= b->slice_n) return MGS_OK;
-  if (b->d_progress) HIPCHK(hipFree(b->d_progress));
-  if (b->d_slice_rec) HIPCHK(hipFree(b->d_slice_rec));
-  b->d_progress = nullptr;
-  b->d_slice_rec = nullptr;
-  b->slice_n = 0;
-  const mgs_model_desc& d = b->m->desc;
-  const size_t rs = (size_t)d.nq + 2 * (size_t)d.nv + MGS_RESUME_EXTRA;
-  if (hipMalloc(&b->d_progress, sizeof(uint32_t) * (size_t)n) != hipSuccess ||
-      hipMalloc(&b->d_slice_rec, sizeof(double) * (size_t)n * rs) != hipSuccess)
-    return fail(MGS_ENOMEM, "slice buffer allocation failed%s");
-  HIPCHK(hipMemset(b->d_progress, 0, sizeof(uint32_t) * (size_t)n));
-  HIPCHK(hipDeviceSynchronize());
-  b->slice_n = n;
-  return MGS_OK;
 }
 
 static Mdl device_model(const mgs_model* m) {
@@ -472,31 +423,13 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   int nwg = d_list ? grid : n;
   uint32_t* q = nullptr;
   int slot = 0;
-  Slc slc;
-  memset(&slc, 0, sizeof(slc));
   if (!d_list && queue_mode() > 0) {
     int r = resident_workgroups(b->m);
     if (queue_mode() > 1 && r > queue_mode()) r = queue_mode();
-    int horizon = 0;
-    for (int p = 0; p < sched->nphase; p++) horizon += sched->nsteps[p];
-    const int k = slice_steps(horizon);
-    // slicing pays off once the rollouts outnumber the slots; a forced grid
-    // (mode >= 2, tests) slices whenever asked
-    if (r > 0 && (r < n || (k > 0 && queue_mode() > 1 && n > 1))) {
-      nwg = r < n ? r : n;
+    if (r > 0 && r < n) {
+      nwg = r;
       slot = b->qslot++ % MGS_QUEUE_RING;
       q = b->d_queue + slot;
-      if (k > 0) {
-        int src = ensure_slices(b, n);
-        if (src) return src;
-        b->epoch = (b->epoch + 1) & 0xffffffu;
-        if (b->epoch == 0) b->epoch = 1;
-        slc.steps = k;
-        slc.nslice = (horizon + k - 1) / k;
-        slc.epoch = b->epoch;
-        slc.progress = b->d_progress;
-        slc.rec = b->d_slice_rec;
-      }
     }
   }
   int lrc = launch_layout(b, nwg, &lay);
@@ -504,14 +437,14 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   HIPCHK(hipEventRecord(b->e0, st));
   RolloutArgs a{md, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
                 d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in,
-                d_mask_mpos, mask_pred, d_mask_out, q, q ? b->qbase[slot] : 0u, slc};
+                d_mask_mpos, mask_pred, d_mask_out, q, q ? b->qbase[slot] : 0u};
   if (b->m->special_rollout) {
     const int32_t* I = md.I;
     const double* D = md.D;
     void* p[] = {&a.md, &I, &D, &a.lay, &a.sc, &a.n, &a.qpos_init, &a.mocap_quat, &a.phase_start, &a.phase_target,
                  &a.active, &a.label, &a.fail_step, &a.obj_qpos, &a.stats, &a.vstate_init, &a.state_out, &a.list,
                  &a.list_count, &a.resume_out, &a.resume_in, &a.mask_mpos, &a.mask_pred, &a.mask_out, &a.queue,
-                 &a.qbase, &a.slc};
+                 &a.qbase};
     HIPCHK(hipModuleLaunchKernel(b->m->special_rollout, nwg, 1, 1, 64, 1, 1, b->m->lds_bytes, st, p, nullptr));
   } else {
     const KernelSet* k = kernels_for(md.m.nv);
@@ -519,8 +452,7 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
     k->rollout(dim3(nwg), b->m->lds_bytes, st, a);
   }
   HIPCHK(hipGetLastError());
-  // every item popped once, plus one failing pop per workgroup
-  if (q) b->qbase[slot] += (uint32_t)n * (uint32_t)(slc.steps ? slc.nslice : 1) + (uint32_t)nwg;
+  if (q) b->qbase[slot] += (uint32_t)n + (uint32_t)nwg;   // every index popped once, plus one failing pop per workgroup
   HIPCHK(hipEventRecord(b->e1, st));
   return MGS_OK;
 }
@@ -1019,14 +951,6 @@ int mgs_rollout_queue(int mode) {
   if (mode >= 0) g_queue_mode = mode;
   return prev;
 }
-
-int mgs_rollout_slicing(int mode) {
-  int prev = slice_mode();
-  if (mode >= 0) g_slice_mode = mode;
-  return prev;
-}
-
-int mgs_rollout_slice_steps(int horizon) { return slice_steps(horizon); }
 
 int mgs_device_count(void) {
   int n = 0;

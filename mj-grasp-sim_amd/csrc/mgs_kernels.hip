@@ -4411,56 +4411,19 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   collision_entry<NV, SL>(smem, mdarg, mI, mD, lay, n, qpos_init, mocap_pos, mocap_quat, predicate, out);
 }
 
-// Time slices of a work-queue rollout launch (steps > 0): the queue's items
-// are (candidate, slice) pairs, slice-major, and an item runs at most `steps`
-// steps of its candidate.  An unfinished candidate leaves its state in its
-// slice record (rec, the resume-record layout, flags included) and advances
-// progress[i] to (epoch << 8) | slices done; a finished one writes its outputs
-// and sets (epoch << 8) | MGS_SLICE_DONE.  The item of slice s waits for
-// slice s - 1 (popped n items earlier by a running workgroup), so long
-// rollouts spread over every slot instead of the last ones starting when the
-// first ones end.  epoch: a per-launch tag, so progress needs no reset.
-#define MGS_SLICE_DONE 0xffu
-struct Slc {
-  int steps;            // steps per slice, 0 = no slicing
-  int nslice;           // slices per candidate (horizon / steps, rounded up)
-  uint32_t epoch;       // this launch's tag (24 bits)
-  uint32_t* progress;   // n words
-  double* rec;          // n slice records
-};
-
-// state entering step t of phase p, the schedule position and the partial
-// stats: a resume record (capacity escalation) or a slice record
-DEVI void save_record(double* rec, const Dat& d, int nq, int nvr, int p, int t, int gstep, int maxcon, int maxefc,
-                      int sumcon, int sumefc) {
-  const int lane = lane_id();
-  for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
-  for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
-  if (lane == 0) {
-    double* tail = rec + nq + 2 * nvr;
-    tail[0] = d.time[0];
-    tail[1] = p; tail[2] = t; tail[3] = gstep;
-    tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
-    tail[8] = d.ITERS;
-    tail[9] = d.OVERFLOW;
-  }
-}
-
-// one candidate's rollout (the body of mgs_rollout_kernel); with a slice
-// descriptor, slice `slice` of it: returns 1 if the candidate finished
-// (outputs written), 0 if it stopped at the slice's step budget
+// one candidate's rollout (the body of mgs_rollout_kernel)
 template <int NV, int SL>
-DEVI int rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_schedule& sc, int i,
+DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_schedule& sc, int i,
                       const double* __restrict__ qpos_init, const double* __restrict__ mocap_quat,
                       const double* __restrict__ phase_start, const double* __restrict__ phase_target,
                       const uint8_t* __restrict__ active, uint8_t* __restrict__ label,
                       int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
                       const double* __restrict__ vstate_init, double* __restrict__ state_out,
                       double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
-                      int mask_pred, uint8_t* __restrict__ mask_out, const Slc* slc = nullptr, int slice = 0) {
+                      int mask_pred, uint8_t* __restrict__ mask_out) {
   int lane = lane_id();
-  int reject = active && !active[i] && slice == 0;
-  if (mask_out && slice == 0) {
+  int reject = active && !active[i];
+  if (mask_out) {
     // fused collision mask (mgs_mask_rollout_device): collision_entry's
     // computation for this candidate, then the rollout of the collision-free
     // ones in the same workgroup -- no separate mask launch to wait for
@@ -4485,7 +4448,7 @@ DEVI int rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sche
     // no object joint reported (obj_qposadr < 0): zeros, as the oracle's output
     if (obj_qpos && lane < 7)
       obj_qpos[7 * i + lane] = sc.obj_qposadr >= 0 ? qpos_init[(size_t)i * md.m.nq + sc.obj_qposadr + lane] : 0.0;
-    return 1;
+    return;
   }
   Dat d;
   bind<SL>(d, smem, lay);
@@ -4497,42 +4460,24 @@ DEVI int rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sche
   int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
   const int nq = md.m.nq, nvr = md.m.nv, RS = nq + 2 * nvr + MGS_RESUME_EXTRA;
   int p0 = 0, t0 = 0;
-  // a later slice continues from its slice record (stats flags included); a
-  // capacity escalation from a capped run's resume record (flags restart)
-  const double* rin = (slc && slice > 0) ? slc->rec : resume_in;
-  if (rin) {
+  if (resume_in) {
     // continue a capacity-capped run from its last step before the overflow
-    // (the capped run and a wider one are identical up to that step), or the
-    // previous slice from its last step
-    const double* rec = rin + (size_t)i * RS;
+    // (the capped run and a wider one are identical up to that step)
+    const double* rec = resume_in + (size_t)i * RS;
     for (int k = lane; k < nq; k += WAVE) d.qpos[k] = rec[k];
     for (int k = lane; k < nvr; k += WAVE) { d.qvel[k] = rec[nq + k]; d.qacc_ws[k] = rec[nq + nvr + k]; }
     const double* tail = rec + nq + 2 * nvr;
-    if (lane == 0) {
-      d.time[0] = tail[0];
-      d.ITERS = (int)tail[8];
-      if (rin != resume_in) d.OVERFLOW = (int)tail[9];
-    }
+    if (lane == 0) { d.time[0] = tail[0]; d.ITERS = (int)tail[8]; }
     p0 = (int)tail[1]; t0 = (int)tail[2]; gstep = (int)tail[3];
     maxcon = (int)tail[4]; maxefc = (int)tail[5]; sumcon = (int)tail[6]; sumefc = (int)tail[7];
     wsync();
   }
-  const int budget = slc ? slc->steps : 0;
-  int done_steps = 0;
   PROF_DECL
   for (int p = p0; p < np && ok; p++) {
     if (lane == 0)
       for (int u = 0; u < md.m.nu; u++) d.ctrl[u] = sc.ctrl[p * 32 + u];
     int ns = sc.nsteps[p];
     for (int t = (p == p0 ? t0 : 0); t < ns && ok; t++) {
-      if (budget && done_steps == budget) {
-        // the slice's step budget is spent: the state entering this step goes
-        // to the slice record and the next slice continues from it
-        save_record(slc->rec + (size_t)i * RS, d, nq, nvr, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
-        PROF_FLUSH
-        return 0;
-      }
-      done_steps++;
       double frac = (double)t / (double)ns;
       if (lane == 0)
         for (int k = 0; k < 3; k++) d.mocap_pos[k] = ps[3 * p + k] + (pt[3 * p + k] - ps[3 * p + k]) * frac;
@@ -4569,7 +4514,16 @@ DEVI int rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sche
         // state entering the step, the schedule position and the partial stats
         // go to the candidate's resume record and the candidate stops (the
         // escalation continues it from here with more capacity)
-        save_record(resume_out + (size_t)i * RS, d, nq, nvr, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
+        double* rec = resume_out + (size_t)i * RS;
+        for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
+        for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
+        if (lane == 0) {
+          double* tail = rec + nq + 2 * nvr;
+          tail[0] = d.time[0];
+          tail[1] = p; tail[2] = t; tail[3] = gstep;
+          tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
+          tail[8] = d.ITERS;
+        }
         ok = 0;
         fstep = -3;
         break;
@@ -4632,7 +4586,6 @@ DEVI int rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sche
     for (int k = lane; k < nv; k += WAVE) { so[nq + k] = d.qvel[k]; so[nq + nv + k] = d.qacc_ws[k]; }
   }
   PROF_FLUSH
-  return 1;
 }
 
 // One workgroup (one wave) per candidate: candidate blockIdx.x, or -- list mode
@@ -4654,8 +4607,7 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
                         const double* __restrict__ vstate_init, double* __restrict__ state_out,
                         const int32_t* __restrict__ list, const int32_t* __restrict__ list_count,
                         double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
-                        int mask_pred, uint8_t* __restrict__ mask_out, uint32_t* queue, uint32_t qbase,
-                        const Slc& slc) {
+                        int mask_pred, uint8_t* __restrict__ mask_out, uint32_t* queue, uint32_t qbase) {
   Mdl md = mdarg;
   // SL: the model description is the baked one too, so sizes, table offsets and
   // options are compile-time constants (trip counts, immediate offsets)
@@ -4671,44 +4623,14 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
     // starts and every workgroup's pops (the last one failing) advance it, so
     // the launch leaves it at qbase + n + gridDim.x (the host's next base;
     // unsigned wrap-around keeps the differences exact)
-    const int lane = lane_id();
-    const uint32_t nitems = slc.steps ? (uint32_t)n * (uint32_t)slc.nslice : (uint32_t)n;
     for (;;) {
       uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(queue, 1u);
-      const uint32_t j = __builtin_amdgcn_readfirstlane(t) - qbase;
-      if (j >= nitems) break;
-      const int i = (int)(j % (uint32_t)n), slice = (int)(j / (uint32_t)n);
-      if (!slc.steps) {
-        rollout_one<NV, SL>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target, active, label,
-                            fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in, mask_mpos,
-                            mask_pred, mask_out);
-        continue;
-      }
-      if (slice > 0) {
-        // wait for the candidate's previous slice (its item was popped n items
-        // earlier by a resident workgroup, so it completes); skip a finished one
-        uint32_t pr = 0;
-        if (lane == 0) {
-          for (uint32_t it = 0;; it++) {
-            pr = __hip_atomic_load(slc.progress + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if ((pr >> 8) == slc.epoch && (pr & 0xffu) >= (uint32_t)slice) break;
-            if (it == (1u << 26)) { pr = (slc.epoch << 8) | MGS_SLICE_DONE; break; }   // bounded: never hang
-            __builtin_amdgcn_s_sleep(8);
-          }
-        }
-        pr = __builtin_amdgcn_readfirstlane(pr);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if ((pr & 0xffu) == MGS_SLICE_DONE) continue;
-      }
-      const int fin = rollout_one<NV, SL>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target,
-                                          active, label, fail_step, obj_qpos, stats, vstate_init, state_out,
-                                          resume_out, resume_in, mask_mpos, mask_pred, mask_out, &slc, slice);
-      // the slice record (or outputs) visible device-wide before the progress word
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      if (lane == 0)
-        __hip_atomic_store(slc.progress + i, (slc.epoch << 8) | (fin ? MGS_SLICE_DONE : (uint32_t)(slice + 1)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane_id() == 0) t = atomicAdd(queue, 1u);
+      const int s = (int)(__builtin_amdgcn_readfirstlane(t) - qbase);
+      if ((uint32_t)s >= (uint32_t)n) break;
+      rollout_one<NV, SL>(md, smem, lay, sc, s, qpos_init, mocap_quat, phase_start, phase_target, active, label,
+                          fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in, mask_mpos,
+                          mask_pred, mask_out);
     }
     return;
   }
@@ -4737,11 +4659,11 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
                    double* __restrict__ state_out, const int32_t* __restrict__ list,
                    const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in,
                    const double* __restrict__ mask_mpos, int mask_pred, uint8_t* __restrict__ mask_out,
-                   uint32_t* queue, uint32_t qbase, Slc slc) {
+                   uint32_t* queue, uint32_t qbase) {
   extern __shared__ double smem[];
   rollout_entry<NV, SL>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target, active,
                         label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count, resume_out,
-                        resume_in, mask_mpos, mask_pred, mask_out, queue, qbase, slc);
+                        resume_in, mask_mpos, mask_pred, mask_out, queue, qbase);
 }
 
 // the library's non-template kernels live in the C-ABI translation unit only

@@ -34,7 +34,6 @@ struct RolloutArgs {
   uint8_t* mask_out;         // and the mask written per candidate (nullptr: no fused mask)
   uint32_t* queue;           // work-queue counter (nullptr: one workgroup per candidate)
   uint32_t qbase;            // its value when the launch starts
-  Slc slc;                   // time slices of the queue's items (slc.steps 0: none)
 };
 
 // one dof count's runtime-layout kernels: launchers (64 lanes per workgroup,

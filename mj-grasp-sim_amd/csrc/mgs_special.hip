@@ -53,11 +53,11 @@ mgs_special_rollout(Mdl mdarg, const int32_t* __restrict__ mI, const double* __r
                     double* __restrict__ state_out, const int32_t* __restrict__ list,
                     const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in,
                     const double* __restrict__ mask_mpos, int mask_pred, uint8_t* __restrict__ mask_out,
-                    uint32_t* queue, uint32_t qbase, Slc slc) {
+                    uint32_t* queue, uint32_t qbase) {
   extern __shared__ double smem[];
   rollout_entry<MGS_SL_NV, 1>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target,
                               active, label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count,
-                              resume_out, resume_in, mask_mpos, mask_pred, mask_out, queue, qbase, slc);
+                              resume_out, resume_in, mask_mpos, mask_pred, mask_out, queue, qbase);
 }
 
 }  // extern "C"

@@ -88,10 +88,6 @@ def load_library(wide: bool = False):
     L.mgs_rollout_grid.restype = ctypes.c_int
     L.mgs_rollout_queue.argtypes = [ctypes.c_int]
     L.mgs_rollout_queue.restype = ctypes.c_int
-    L.mgs_rollout_slicing.argtypes = [ctypes.c_int]
-    L.mgs_rollout_slicing.restype = ctypes.c_int
-    L.mgs_rollout_slice_steps.argtypes = [ctypes.c_int]
-    L.mgs_rollout_slice_steps.restype = ctypes.c_int
     if L.mgs_abi_version() != abi.MGS["MGS_ABI_VERSION"]:
         raise EngineError(f"{os.path.basename(path)} ABI version mismatch with include/mgs_gpu.h")
     _libs[path] = L

@@ -128,24 +128,3 @@ def test_headline_specialised_object_is_built(env):
     if not os.path.isdir(special.CACHE):
         pytest.skip("build() ran without the specialised objects")
     assert os.path.isfile(path), "headline specialised object missing: run __graft_entry__.build()"
-
-
-def test_slice_steps_host_only(lib):
-    """mgs_rollout_slice_steps: the time-slice length a work-queue launch uses
-    for a schedule of `horizon` steps under each slicing mode (no device)"""
-    lib.mgs_rollout_slicing.restype = ctypes.c_int
-    lib.mgs_rollout_slicing.argtypes = [ctypes.c_int]
-    lib.mgs_rollout_slice_steps.restype = ctypes.c_int
-    lib.mgs_rollout_slice_steps.argtypes = [ctypes.c_int]
-    prev = lib.mgs_rollout_slicing(1)
-    try:
-        # auto: max(25, horizon / 32), no slicing when one slice covers the horizon
-        assert [lib.mgs_rollout_slice_steps(h) for h in (20, 25, 200, 6000, 8000)] == [0, 0, 25, 188, 250]
-        lib.mgs_rollout_slicing(7)
-        assert lib.mgs_rollout_slice_steps(200) == 7 and lib.mgs_rollout_slice_steps(5) == 0
-        lib.mgs_rollout_slicing(2)          # at most 250 slices per candidate
-        assert lib.mgs_rollout_slice_steps(1000) == 4
-        lib.mgs_rollout_slicing(0)
-        assert lib.mgs_rollout_slice_steps(8000) == 0
-    finally:
-        lib.mgs_rollout_slicing(prev)

@@ -223,15 +223,12 @@ def test_fused_mask_rollout_equals_separate_launches(env, eng, candidates):
     assert 0 < outs[1]["free"].sum() < n
 
 
-@pytest.mark.parametrize("slicing", [0, 7, 1])
-def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, oracle_model, slicing):
+def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, oracle_model):
     """The work-queue launch (mgs_rollout_queue: a grid of k workgroups pulling
-    candidate indices from a counter), with or without time slices
-    (mgs_rollout_slicing: 0 none, 7-step slices, auto = 25-step slices of the
-    h200 schedule), gives every output of one workgroup per candidate bit for
-    bit -- fused mask, labels, fail steps, object poses, statistics, capacity
-    resume records -- whatever the grid (k = 1, 5, 64 here; the default grid
-    is the device's resident capacity), and equals the oracle."""
+    candidate indices from a counter) gives every output of one workgroup per
+    candidate bit for bit -- fused mask, labels, fail steps, object poses,
+    statistics, resume records -- whatever the grid (k = 1, 5, 64 here; the
+    default grid is the device's resident capacity), and equals the oracle."""
     import torch
     from conftest import plan_for
     from mgs.core import abi
@@ -246,12 +243,11 @@ def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, ora
     dq, dmp, dmq, dps, dpt = t(q), t(mp), t(mq), t(plan.phase_start), t(plan.phase_target)
     rw = eng.resume_width()
     L = eng.lib
-    prev, prev_s = L.mgs_rollout_queue(-1), L.mgs_rollout_slicing(-1)
+    prev = L.mgs_rollout_queue(-1)
     outs = {}
     try:
         for mode in (0, 1, 5, 64):
             L.mgs_rollout_queue(mode)
-            L.mgs_rollout_slicing(slicing if mode else 0)
             assert eng.rollout_grid(n) == (n if mode <= 1 else mode)
             o = dict(free=torch.zeros(n, dtype=torch.uint8, device=dev),
                      lab=torch.zeros(n, dtype=torch.uint8, device=dev),
@@ -268,9 +264,6 @@ def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, ora
             outs[mode] = {k: v.cpu().numpy() for k, v in o.items()}
     finally:
         L.mgs_rollout_queue(prev)
-        L.mgs_rollout_slicing(prev_s)
-    if slicing:
-        assert L.mgs_rollout_slice_steps(plan.horizon) == (7 if slicing == 7 else 25)
     for mode in (1, 5, 64):
         for k in outs[0]:
             assert np.array_equal(outs[0][k], outs[mode][k]), (mode, k)
@@ -281,26 +274,6 @@ def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, ora
     assert np.array_equal(outs[5]["lab"].astype(bool)[idx], ro["label"])
     assert np.array_equal(outs[5]["fail"][idx], ro["fail_step"])
     assert np.array_equal(outs[5]["objq"][idx], ro["obj_qpos"])
-
-
-def test_sliced_reference_horizon(env, eng, candidates, oracle_model):
-    """The reference's 8000-step schedule through the host API with the queue
-    forced onto 2 workgroups and auto slices (250 steps, 32 slices per
-    candidate): equal to the oracle"""
-    from conftest import plan_for
-    poses, J = candidates
-    q, mp, mq, _ = env.initial_state(poses, J)
-    idx = np.nonzero(oracle_model.collision_free(q, mp, mq, nthreads=8))[0][:3]
-    plan = plan_for(env, poses[idx], J[idx], horizon="ref8000")
-    L = eng.lib
-    prev, prev_s = L.mgs_rollout_queue(2), L.mgs_rollout_slicing(1)
-    try:
-        assert L.mgs_rollout_slice_steps(plan.horizon) == 250
-        rg = eng.rollout(plan)
-    finally:
-        L.mgs_rollout_queue(prev)
-        L.mgs_rollout_slicing(prev_s)
-    _assert_same(rg, oracle_model.rollout(plan, nthreads=8), "ref8000 sliced")
 
 
 def test_device_overflow_list_and_list_rollout(env, eng, candidates):
