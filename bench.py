@@ -6,10 +6,11 @@ One step = the reference's filter_to_stable pipeline (mgs/cli/filter_to_stable.p
 39-50) over one batch: collision mask of every candidate, then the close ->
 lift -> shake rollout of the collision-free ones (h200 horizon).  Inputs are
 host-prepared once (float32 SE3 processing, mocap schedule), uploaded, and
-resident in HBM when the timed region starts; each step runs the mask, the
-rollout (which reads the mask on the device) and the device-built list of
-capacity overflows on one HIP stream with no host round trip; the listed
-candidates are re-run wider on a side stream (the env's escalation).  Steps rotate over
+resident in HBM when the timed region starts; each step runs the fused mask +
+rollout launch (mgs_mask_rollout_device, a work queue on the resident grid)
+on its pipeline's HIP stream with no host round trip; the device-built list of
+capacity overflows and the wider re-run of the listed candidates (the env's
+escalation) follow on a side stream.  Steps rotate over
 `--streams` pipelines (engine + stream each, default 4), so one batch's
 rollout tail overlaps the next batches' work; every step is a whole batch.
 
@@ -368,6 +369,7 @@ def main():
             self.esc = []          # per step: count, list, label, fail, objq, stats, resume records
             self.events = []
             self.last = -1
+            self.listed = None     # the side stream has read this pipeline's stats (overflow list built)
 
         def esc_buffers(self, k):
             while len(self.esc) <= k:
@@ -383,6 +385,9 @@ def main():
             sp = self.stream.cuda_stream
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
             with torch.cuda.stream(self.stream):
+                if self.listed is not None:
+                    # the previous step's overflow list (side stream) has read stats
+                    self.stream.wait_event(self.listed)
                 if ev:
                     ev[0].record(self.stream)
                 if not FUSED:
@@ -416,12 +421,20 @@ def main():
                     ev[2].record(self.stream)
                     self.events.append(ev)
                 if self.wide is not None:
+                    # the escalation bookkeeping (zeroing the count, the overflow
+                    # list) runs on the side stream: any kernel between two
+                    # rollouts of this pipeline's stream waits for a free slot
+                    # behind the other pipelines' persistent grids (50-110 ms in
+                    # the round-3 traces) and held the next rollout back
                     cnt, lst, el, ef, eo, es, rec = self.esc_buffers(k)
-                    self.eng.overflow_list_device(N, self.stats.data_ptr(), cnt.data_ptr(), lst.data_ptr(), stream=sp)
                     done = torch.cuda.Event()
                     done.record(self.stream)
                     es_ = self.esc_stream if args.esc_side else self.stream
                     es_.wait_event(done)
+                    self.eng.overflow_list_device(N, self.stats.data_ptr(), cnt.data_ptr(), lst.data_ptr(),
+                                                  stream=es_.cuda_stream)
+                    self.listed = torch.cuda.Event()
+                    self.listed.record(es_)
                     self.wide.rollout_list_device(sched, N, cnt.data_ptr(), lst.data_ptr(), ESC_GRID, d_q.data_ptr(),
                                                   d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(), el.data_ptr(),
                                                   ef.data_ptr(), eo.data_ptr(), es.data_ptr(),
