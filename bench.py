@@ -253,6 +253,9 @@ def main():
     ap.add_argument("--esc-resume", type=int, default=1,
                     help="1: overflowing candidates stop at the overflowing step and the escalation continues "
                          "them from there (0: re-run from the start)")
+    ap.add_argument("--warmup-s", type=float, default=0.0,
+                    help="untimed warm-up continues past --warmup steps until this much wall time has passed "
+                         "(probe of the fresh-box first-process deficit, profiles/r03q_first_process.txt)")
     ap.add_argument("--queue", type=int, default=None,
                     help="rollout launch mode (mgs_rollout_queue): 0 one workgroup per candidate, 1 the work queue "
                          "on the resident grid (the library default)")
@@ -466,9 +469,18 @@ def main():
         if p.wide is not None:
             p.esc_buffers(per_pipe)
     torch.cuda.synchronize(dev)
-    for k in range(max(args.warmup, len(pipes))):       # every pipeline (and its escalation) warmed up
+    tw = time.perf_counter()
+    nwarm = max(args.warmup, len(pipes))
+    for k in range(nwarm):       # every pipeline (and its escalation) warmed up
         pipes[k % len(pipes)].step(k // len(pipes), False)
     torch.cuda.synchronize(dev)
+    # optional warm-up floor in wall time: further untimed rounds over the
+    # pipelines (outputs overwritten by the timed steps; nothing carries over)
+    while time.perf_counter() - tw < args.warmup_s:
+        for p in pipes:
+            p.step(0, False)
+        nwarm += len(pipes)
+        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -568,6 +580,7 @@ def main():
         "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
                    "rollouts_per_s": float(free.sum()) * world * args.steps / dt,
                    "host_enqueue_s": t_enq,
+                   "warmup_steps_executed": nwarm,
                    "pipelines_identical": bool(same_pipes),
                    "static_layout_kernel": env.engine.static_layout(),
                    "rollout_grid": env.engine.rollout_grid(N),
