@@ -8,9 +8,9 @@ lift -> shake rollout of the collision-free ones (h200 horizon).  Inputs are
 host-prepared once (float32 SE3 processing, mocap schedule), uploaded, and
 resident in HBM when the timed region starts; each step runs the fused mask +
 rollout launch (mgs_mask_rollout_device, a work queue on the resident grid)
-on its pipeline's HIP stream with no host round trip; the device-built list of
-capacity overflows and the wider re-run of the listed candidates (the env's
-escalation) follow on a side stream.  Steps rotate over
+on its pipeline's HIP stream with no host round trip; the launch lists its
+capacity overflows itself and the wider re-run of the listed candidates (the
+env's escalation) follows on a side stream.  Steps rotate over
 `--streams` pipelines (engine + stream each, default 4), so one batch's
 rollout tail overlaps the next batches' work; every step is a whole batch.
 
@@ -345,6 +345,7 @@ def main():
     RESUME = bool(args.escalate and args.esc_resume)
     FUSED = bool(args.fused)
     RW = env.engine.resume_width()
+    LH = abi.MGS["MGS_LIST_HEADER"]
 
     class Pipe:
         def __init__(self, s):
@@ -358,26 +359,25 @@ def main():
             self.stats = torch.zeros((N, NS), dtype=torch.int32, device=dev)
             # contact-capacity escalation (GravitylessObjectGrasping.rollout: the
             # candidates whose contacts / rows exceeded the capacity are re-run
-            # with twice the capacity): after each step's rollout the overflowed
-            # candidates are listed on the device (mgs_overflow_list_device) and
-            # re-run from that list on this pipeline's escalation stream
-            # (mgs_rollout_list_device, ESC_GRID workgroups looping over it) into
-            # the step's own escalation outputs, so the next step never waits;
-            # with --esc-resume the capped rollout stops an overflowing candidate
-            # at that step and leaves its state in the step's resume records
-            # (mgs_rollout_resumable_device), which the list re-run continues
+            # with twice the capacity): the step's rollout appends each
+            # overflowing candidate to the step's device list itself (ABI 17:
+            # a list header + n indices, zeroed once here and left zeroed by
+            # each list re-run) and stops it at that step, leaving its state in
+            # the step's resume records; the list re-run (mgs_rollout_list_device,
+            # ESC_GRID workgroups looping over the list) continues them on this
+            # pipeline's escalation stream into the step's own escalation
+            # outputs.  Nothing runs between two rollouts of a pipeline's
+            # stream, and the pipeline never waits for its side stream.
             self.wide = Engine(env.model, device=local, ncon_max=2 * env.ncon_max,
                                specialize="cached") if args.escalate else None
             self.esc_stream = torch.cuda.Stream(dev)
-            self.esc = []          # per step: count, list, label, fail, objq, stats, resume records
+            self.esc = []          # per step: list (header + indices), label, fail, objq, stats, resume records
             self.events = []
             self.last = -1
-            self.listed = None     # the side stream has read this pipeline's stats (overflow list built)
 
         def esc_buffers(self, k):
             while len(self.esc) <= k:
-                self.esc.append((torch.zeros(1, dtype=torch.int32, device=dev),
-                                 torch.zeros(N, dtype=torch.int32, device=dev),
+                self.esc.append((torch.zeros(LH + N, dtype=torch.int32, device=dev),
                                  torch.zeros(N, dtype=torch.uint8, device=dev),
                                  torch.zeros(N, dtype=torch.int32, device=dev), torch.zeros((N, 7), **f64),
                                  torch.zeros((N, NS), dtype=torch.int32, device=dev),
@@ -387,10 +387,9 @@ def main():
         def step(self, k, timed):
             sp = self.stream.cuda_stream
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
+            ovf, el, ef, eo, es, rec = self.esc_buffers(k) if self.wide is not None else (None,) * 6
+            d_ovf = ovf.data_ptr() if ovf is not None else None
             with torch.cuda.stream(self.stream):
-                if self.listed is not None:
-                    # the previous step's overflow list (side stream) has read stats
-                    self.stream.wait_event(self.listed)
                 if ev:
                     ev[0].record(self.stream)
                 if not FUSED:
@@ -402,59 +401,50 @@ def main():
                     # mask + rollout in one launch (mgs_mask_rollout_device): each
                     # workgroup computes its candidate's mask and, if collision-free,
                     # its rollout; no rollout waits for a separate mask launch
-                    rec = self.esc_buffers(k)[6] if RESUME else None
                     self.eng.mask_rollout_device(sched, N, d_q.data_ptr(), d_mp.data_ptr(), d_mq.data_ptr(),
                                                  d_ps.data_ptr(), d_pt.data_ptr(), self.free.data_ptr(),
                                                  self.label.data_ptr(), self.fail.data_ptr(), self.objq.data_ptr(),
                                                  self.stats.data_ptr(),
                                                  d_resume_out=rec.data_ptr() if RESUME else None,
-                                                 predicate="any", stream=sp)
-                elif RESUME:
-                    rec = self.esc_buffers(k)[6]
+                                                 predicate="any", stream=sp, d_ovf=d_ovf)
+                else:
                     self.eng.rollout_resumable_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(),
                                                       d_pt.data_ptr(), self.label.data_ptr(), self.fail.data_ptr(),
-                                                      self.objq.data_ptr(), self.stats.data_ptr(), rec.data_ptr(),
-                                                      d_active=self.free.data_ptr(), stream=sp)
-                else:
-                    self.eng.rollout_device(sched, N, d_q.data_ptr(), d_mq.data_ptr(), d_ps.data_ptr(),
-                                            d_pt.data_ptr(), self.label.data_ptr(), self.fail.data_ptr(),
-                                            self.objq.data_ptr(), self.stats.data_ptr(),
-                                            d_active=self.free.data_ptr(), stream=sp)
+                                                      self.objq.data_ptr(), self.stats.data_ptr(),
+                                                      (rec if RESUME else self.res_scratch()).data_ptr(),
+                                                      d_active=self.free.data_ptr(), stream=sp, d_ovf=d_ovf)
                 if ev:
                     ev[2].record(self.stream)
                     self.events.append(ev)
                 if self.wide is not None:
-                    # the escalation bookkeeping (zeroing the count, the overflow
-                    # list) runs on the side stream: any kernel between two
-                    # rollouts of this pipeline's stream waits for a free slot
-                    # behind the other pipelines' persistent grids (50-110 ms in
-                    # the round-3 traces) and held the next rollout back
-                    cnt, lst, el, ef, eo, es, rec = self.esc_buffers(k)
                     done = torch.cuda.Event()
                     done.record(self.stream)
                     es_ = self.esc_stream if args.esc_side else self.stream
                     es_.wait_event(done)
-                    self.eng.overflow_list_device(N, self.stats.data_ptr(), cnt.data_ptr(), lst.data_ptr(),
-                                                  stream=es_.cuda_stream)
-                    self.listed = torch.cuda.Event()
-                    self.listed.record(es_)
-                    self.wide.rollout_list_device(sched, N, cnt.data_ptr(), lst.data_ptr(), ESC_GRID, d_q.data_ptr(),
+                    self.wide.rollout_list_device(sched, N, d_ovf, d_ovf + 4 * LH, ESC_GRID, d_q.data_ptr(),
                                                   d_mq.data_ptr(), d_ps.data_ptr(), d_pt.data_ptr(), el.data_ptr(),
                                                   ef.data_ptr(), eo.data_ptr(), es.data_ptr(),
                                                   stream=es_.cuda_stream,
                                                   d_resume_in=rec.data_ptr() if RESUME else None)
             self.last = k
 
+        def res_scratch(self):
+            # the non-resumed escalation (--esc-resume 0) re-runs from the start:
+            # the capped launch still needs somewhere to put its records
+            if not hasattr(self, "_rs"):
+                self._rs = torch.zeros((N, RW), **f64)
+            return self._rs
+
         def merge_last(self):
             """this pipeline's last step with its escalated candidates merged;
             returns (escalated count, still capped after escalation)"""
             if self.wide is None or self.last < 0:
                 return 0, 0
-            cnt, lst, el, ef, eo, es, _ = self.esc[self.last]
-            m = int(cnt.item())
+            ovf, el, ef, eo, es, _ = self.esc[self.last]
+            m = int(ovf[2].item())        # the count the list re-run ran
             if m == 0:
                 return 0, 0
-            idx = lst[:m].long()
+            idx = ovf[LH:LH + m].long()
             self.label[idx] = el[idx]
             self.fail[idx] = ef[idx]
             self.objq[idx] = eo[idx]

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 16
+#define MGS_ABI_VERSION 17
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -363,17 +363,25 @@ int mgs_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n,
 
 /* Capacity escalation on the device (GravitylessObjectGrasping.rollout's
  * re-run of the candidates that overflowed the contact / constraint-row
- * capacity, with no host round trip): mgs_overflow_list_device zeroes *d_count
- * and writes the indices i < n with stats[i * MGS_NSTATS + 2] & flag_mask into
- * d_list (n ints; arrival order), asynchronously on `stream`;
- * mgs_rollout_list_device re-runs exactly those candidates (as
- * mgs_rollout_device would, outputs written at their indices, other entries
- * untouched) with `grid` workgroups that loop over the list, so an empty or
- * short list costs a handful of workgroups instead of one per batch entry.
- * grid <= the batch capacity. */
+ * capacity, with no host round trip).  A device list is a header of
+ * MGS_LIST_HEADER int32 words -- [0] count, [1] workgroup exits (internal),
+ * [2] the count the last mgs_rollout_list_device over it ran, [3] reserved --
+ * followed by up to n int32 candidate indices (arrival order; each re-run is
+ * independent of the order).  A header starts zeroed (the caller's
+ * allocation) and mgs_rollout_list_device leaves words 0 and 1 zeroed again,
+ * so one header serves launch after launch with no fill in between (ABI 17).
+ *
+ * mgs_overflow_list_device zeroes words 0 and 1 of *d_count and writes the
+ * indices i < n with stats[i * MGS_NSTATS + 2] & flag_mask into d_list,
+ * asynchronously on `stream`.  mgs_rollout_list_device re-runs exactly the
+ * listed candidates (as mgs_rollout_device would, outputs written at their
+ * indices, other entries untouched) with `grid` workgroups that loop over the
+ * list, so an empty or short list costs a handful of workgroups instead of one
+ * per batch entry; d_count is the list's header, grid <= the batch capacity. */
+#define MGS_LIST_HEADER 4
 int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32_t* d_count, int32_t* d_list,
                              void* stream);
-int mgs_rollout_list_device(mgs_batch* batch, const mgs_schedule* sched, int n, const int32_t* d_count,
+int mgs_rollout_list_device(mgs_batch* batch, const mgs_schedule* sched, int n, int32_t* d_count,
                             const int32_t* d_list, int grid, const double* d_qpos_init, const double* d_mocap_quat,
                             const double* d_phase_start, const double* d_phase_target, const double* d_resume_in,
                             uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats,
@@ -383,12 +391,15 @@ int mgs_rollout_list_device(mgs_batch* batch, const mgs_schedule* sched, int n, 
  * mgs_rollout_out.resume); mgs_rollout_list_device with d_resume_in != NULL
  * continues the listed candidates from those records (the capped run and the
  * wider one are identical up to that step), so the escalation costs only the
- * remaining steps. */
+ * remaining steps.  d_ovf (may be NULL; ABI 17): a device list (header +
+ * n entries, see above) each capacity-capped candidate appends itself to, so
+ * mgs_rollout_list_device(d_count = d_ovf, d_list = d_ovf + MGS_LIST_HEADER)
+ * can follow with no list kernel in between. */
 int mgs_rollout_resumable_device(mgs_batch* batch, const mgs_schedule* sched, int n, const double* d_qpos_init,
                                  const double* d_mocap_quat, const double* d_phase_start,
                                  const double* d_phase_target, const uint8_t* d_active, uint8_t* d_label,
                                  int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
-                                 void* stream);
+                                 int32_t* d_ovf, void* stream);
 /* The collision mask and the rollout in one launch (ABI 15): each workgroup
  * computes its candidate's mask exactly as mgs_collision_free_device does
  * (qpos_init, mocap_pos, mocap_quat, predicate) into d_free_out[i], and a
@@ -397,12 +408,13 @@ int mgs_rollout_resumable_device(mgs_batch* batch, const mgs_schedule* sched, in
  * rollout waits for a separate mask launch.  The pair the reference runs as
  * grasp_collision_mask then grasp_stability_evaluation_from_joints on the
  * collision-free subset (mgs/cli/filter_to_stable.py:39-50); outputs are those
- * of the two separate calls, bit for bit.  d_resume_out may be NULL. */
+ * of the two separate calls, bit for bit.  d_resume_out and d_ovf (the
+ * overflow list, as in mgs_rollout_resumable_device) may be NULL. */
 int mgs_mask_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n, const double* d_qpos_init,
                             const double* d_mocap_pos, const double* d_mocap_quat, const double* d_phase_start,
                             const double* d_phase_target, int predicate, uint8_t* d_free_out, uint8_t* d_label,
                             int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
-                            void* stream);
+                            int32_t* d_ovf, void* stream);
 /* Launch shape of the rollout calls above (ABI 16).  A rollout over n
  * candidates runs as a work queue: the grid is the number of rollout
  * workgroups the device holds at once (occupancy at this model's LDS size x

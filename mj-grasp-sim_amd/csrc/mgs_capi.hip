@@ -185,9 +185,9 @@ struct mgs_batch {
   double* d_G;      // MGS_G_GLOBAL: per-candidate constraint rows (HBM)
   size_t g_elems;
   double* d_resume; // resume records (n * (nq + 2 nv + MGS_RESUME_EXTRA)), allocated on first use
-  uint32_t* d_queue;                // work-queue counters, one per launch in a ring (launches in flight on
-  int qslot;                        // other streams keep their own counter), never reset: each launch
-  uint32_t qbase[MGS_QUEUE_RING];   // advances its counter by n + grid, the next launch's base
+  uint32_t* d_queue;                // work-queue counter pairs (next index, exits), one per launch in a
+  int qslot;                        // ring (launches in flight on other streams keep their own pair);
+                                    // each launch's last workgroup returns its pair to zero
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
@@ -265,8 +265,8 @@ int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out) {
             hipMalloc(&b->d_label, n) == hipSuccess && hipMalloc(&b->d_free, n) == hipSuccess &&
             hipMalloc(&b->d_fail, sizeof(int32_t) * n) == hipSuccess &&
             hipMalloc(&b->d_stats, sizeof(int32_t) * n * MGS_NSTATS) == hipSuccess &&
-            hipMalloc(&b->d_queue, sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
-            hipMemset(b->d_queue, 0, sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
+            hipMalloc(&b->d_queue, 2 * sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
+            hipMemset(b->d_queue, 0, 2 * sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
             // the counters must be zero before any stream's launch reads them
             // (hipMemset may still be in flight on the null stream otherwise)
             hipDeviceSynchronize() == hipSuccess;
@@ -318,7 +318,7 @@ static int launch_layout(mgs_batch* b, int n, Lay* lay) {
 // Rollout launches run as a work queue by default: the grid is the number of
 // rollout workgroups the device holds at once (occupancy of the launched
 // function at this model's LDS size x CUs) and each workgroup pulls candidate
-// indices from a counter (never reset, see rollout_entry).  Mode (mgs_rollout_queue; MGS_QUEUE in the
+// indices from a counter (reset by the launch's last workgroup, see rollout_entry).  Mode (mgs_rollout_queue; MGS_QUEUE in the
 // environment sets the initial one): 0 one workgroup per candidate, 1 the
 // queue on the resident grid, k >= 2 the queue on at most k workgroups (tests).
 static int g_queue_mode = -1;
@@ -410,9 +410,10 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
                           const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
                           const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
                           int32_t* d_stats, const double* d_vstate, double* d_state_out, void* stream,
-                          const int32_t* d_list = nullptr, const int32_t* d_count = nullptr, int grid = 0,
+                          const int32_t* d_list = nullptr, int32_t* d_count = nullptr, int grid = 0,
                           double* d_resume_out = nullptr, const double* d_resume_in = nullptr,
-                          const double* d_mask_mpos = nullptr, int mask_pred = 0, uint8_t* d_mask_out = nullptr) {
+                          const double* d_mask_mpos = nullptr, int mask_pred = 0, uint8_t* d_mask_out = nullptr,
+                          int32_t* d_ovf = nullptr) {
   if (!b || !sched || n < 0) return fail(MGS_EINVAL, "mgs_rollout_device: bad argument%s");
   if (sched->nphase < 1 || sched->nphase > MGS_MAX_PHASES) return fail(MGS_EINVAL, "bad phase count%s");
   if (n == 0) return MGS_OK;
@@ -429,7 +430,7 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
     if (r > 0 && r < n) {
       nwg = r;
       slot = b->qslot++ % MGS_QUEUE_RING;
-      q = b->d_queue + slot;
+      q = b->d_queue + 2 * slot;
     }
   }
   int lrc = launch_layout(b, nwg, &lay);
@@ -437,14 +438,14 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   HIPCHK(hipEventRecord(b->e0, st));
   RolloutArgs a{md, lay, *sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
                 d_fail_step, d_obj_qpos, d_stats, d_vstate, d_state_out, d_list, d_count, d_resume_out, d_resume_in,
-                d_mask_mpos, mask_pred, d_mask_out, q, q ? b->qbase[slot] : 0u};
+                d_mask_mpos, mask_pred, d_mask_out, q, d_ovf, d_ovf ? d_ovf + MGS_LIST_HEADER : nullptr};
   if (b->m->special_rollout) {
     const int32_t* I = md.I;
     const double* D = md.D;
     void* p[] = {&a.md, &I, &D, &a.lay, &a.sc, &a.n, &a.qpos_init, &a.mocap_quat, &a.phase_start, &a.phase_target,
                  &a.active, &a.label, &a.fail_step, &a.obj_qpos, &a.stats, &a.vstate_init, &a.state_out, &a.list,
                  &a.list_count, &a.resume_out, &a.resume_in, &a.mask_mpos, &a.mask_pred, &a.mask_out, &a.queue,
-                 &a.qbase};
+                 &a.ovf_count, &a.ovf_list};
     HIPCHK(hipModuleLaunchKernel(b->m->special_rollout, nwg, 1, 1, 64, 1, 1, b->m->lds_bytes, st, p, nullptr));
   } else {
     const KernelSet* k = kernels_for(md.m.nv);
@@ -452,7 +453,6 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
     k->rollout(dim3(nwg), b->m->lds_bytes, st, a);
   }
   HIPCHK(hipGetLastError());
-  if (q) b->qbase[slot] += (uint32_t)n + (uint32_t)nwg;   // every index popped once, plus one failing pop per workgroup
   HIPCHK(hipEventRecord(b->e1, st));
   return MGS_OK;
 }
@@ -469,7 +469,7 @@ int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32
                              void* stream) {
   if (n < 0 || !d_stats || !d_count || !d_list) return fail(MGS_EINVAL, "mgs_overflow_list_device: bad argument%s");
   hipStream_t st = (hipStream_t)stream;
-  HIPCHK(hipMemsetAsync(d_count, 0, sizeof(int32_t), st));
+  HIPCHK(hipMemsetAsync(d_count, 0, 2 * sizeof(int32_t), st));   // count and exits of the list header
   if (n == 0) return MGS_OK;
   hipLaunchKernelGGL(mgs_overflow_list_kernel, dim3((n + 255) / 256), dim3(256), 0, st, d_stats, n, flag_mask, d_count,
                      d_list);
@@ -477,7 +477,7 @@ int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32
   return MGS_OK;
 }
 
-int mgs_rollout_list_device(mgs_batch* b, const mgs_schedule* sched, int n, const int32_t* d_count,
+int mgs_rollout_list_device(mgs_batch* b, const mgs_schedule* sched, int n, int32_t* d_count,
                             const int32_t* d_list, int grid, const double* d_qpos_init, const double* d_mocap_quat,
                             const double* d_phase_start, const double* d_phase_target, const double* d_resume_in,
                             uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats,
@@ -493,24 +493,24 @@ int mgs_rollout_resumable_device(mgs_batch* b, const mgs_schedule* sched, int n,
                                  const double* d_mocap_quat, const double* d_phase_start,
                                  const double* d_phase_target, const uint8_t* d_active, uint8_t* d_label,
                                  int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
-                                 void* stream) {
+                                 int32_t* d_ovf, void* stream) {
   if (!d_resume_out) return fail(MGS_EINVAL, "mgs_rollout_resumable_device: null resume buffer%s");
   return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, d_active, d_label,
                         d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, nullptr, nullptr, 0,
-                        d_resume_out, nullptr);
+                        d_resume_out, nullptr, nullptr, 0, nullptr, d_ovf);
 }
 
 int mgs_mask_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
                             const double* d_mocap_pos, const double* d_mocap_quat, const double* d_phase_start,
                             const double* d_phase_target, int predicate, uint8_t* d_free_out, uint8_t* d_label,
                             int32_t* d_fail_step, double* d_obj_qpos, int32_t* d_stats, double* d_resume_out,
-                            void* stream) {
+                            int32_t* d_ovf, void* stream) {
   if (!d_mocap_pos || !d_free_out) return fail(MGS_EINVAL, "mgs_mask_rollout_device: mocap_pos and free_out are required%s");
   if (predicate < MGS_PRED_ANY_CONTACT || predicate > MGS_PRED_PARTITION_INCL)
     return fail(MGS_EINVAL, "mgs_mask_rollout_device: bad predicate%s");
   return launch_rollout(b, sched, n, d_qpos_init, d_mocap_quat, d_phase_start, d_phase_target, nullptr, d_label,
                         d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream, nullptr, nullptr, 0,
-                        d_resume_out, nullptr, d_mocap_pos, predicate, d_free_out);
+                        d_resume_out, nullptr, d_mocap_pos, predicate, d_free_out, d_ovf);
 }
 
 int mgs_simulate_device(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,

@@ -30,7 +30,7 @@ void launch_rollout(dim3 grid, size_t shmem, hipStream_t st, const RolloutArgs& 
   hipLaunchKernelGGL(mgs_rollout_kernel<MGS_INST_NV>, grid, dim3(64), shmem, st, a.md, a.md.I, a.md.D, a.lay, a.sc,
                      a.n, a.qpos_init, a.mocap_quat, a.phase_start, a.phase_target, a.active, a.label, a.fail_step,
                      a.obj_qpos, a.stats, a.vstate_init, a.state_out, a.list, a.list_count, a.resume_out,
-                     a.resume_in, a.mask_mpos, a.mask_pred, a.mask_out, a.queue, a.qbase);
+                     a.resume_in, a.mask_mpos, a.mask_pred, a.mask_out, a.queue, a.ovf_count, a.ovf_list);
 }
 #ifdef MGS_PROFILE
 int prof_read(unsigned long long* acc) {

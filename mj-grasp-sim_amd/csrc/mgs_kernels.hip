@@ -4420,7 +4420,7 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
                       int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
                       const double* __restrict__ vstate_init, double* __restrict__ state_out,
                       double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
-                      int mask_pred, uint8_t* __restrict__ mask_out) {
+                      int mask_pred, uint8_t* __restrict__ mask_out, int32_t* ovf_count, int32_t* ovf_list) {
   int lane = lane_id();
   int reject = active && !active[i];
   if (mask_out) {
@@ -4577,6 +4577,10 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       int32_t* st = stats + MGS_NSTATS * i;
       st[0] = maxcon; st[1] = maxefc; st[2] = d.OVERFLOW; st[3] = d.ITERS; st[4] = sumcon; st[5] = sumefc;
     }
+    // the launch's overflow list (ABI 17): a capacity-capped candidate appends
+    // itself, so the escalation re-run needs no list kernel (nor a fill of its
+    // count) between this launch and the next one on the stream
+    if (ovf_list && (d.OVERFLOW & MGS_FLAG_CAPACITY)) ovf_list[atomicAdd(ovf_count, 1)] = i;
   }
   if (obj_qpos && lane < 7) obj_qpos[7 * i + lane] = sc.obj_qposadr >= 0 ? d.qpos[sc.obj_qposadr + lane] : 0.0;
   if (state_out) {
@@ -4605,9 +4609,10 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
                         const uint8_t* __restrict__ active, uint8_t* __restrict__ label,
                         int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
                         const double* __restrict__ vstate_init, double* __restrict__ state_out,
-                        const int32_t* __restrict__ list, const int32_t* __restrict__ list_count,
+                        const int32_t* __restrict__ list, int32_t* list_count,
                         double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
-                        int mask_pred, uint8_t* __restrict__ mask_out, uint32_t* queue, uint32_t qbase) {
+                        int mask_pred, uint8_t* __restrict__ mask_out, uint32_t* queue, int32_t* ovf_count,
+                        int32_t* ovf_list) {
   Mdl md = mdarg;
   // SL: the model description is the baked one too, so sizes, table offsets and
   // options are compile-time constants (trip counts, immediate offsets)
@@ -4619,29 +4624,43 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
     // and each workgroup takes the next candidate index when its previous one
     // ends, so short (rejected, early-failing) and long rollouts pack the slots
     // regardless of which XCD a workgroup landed on; the launch has a single
-    // tail.  The counter is never reset: it stands at qbase when the launch
-    // starts and every workgroup's pops (the last one failing) advance it, so
-    // the launch leaves it at qbase + n + gridDim.x (the host's next base;
-    // unsigned wrap-around keeps the differences exact)
+    // tail.  queue[0] is the next index, queue[1] counts the workgroups that
+    // have made their one failing pop: the last of them returns both words to
+    // zero (every pop of this launch is behind it), so each launch on this slot
+    // starts from zero with no fill kernel and no host-tracked base (ABI 17)
     for (;;) {
       uint32_t t = 0;
-      if (lane_id() == 0) t = atomicAdd(queue, 1u);
-      const int s = (int)(__builtin_amdgcn_readfirstlane(t) - qbase);
-      if ((uint32_t)s >= (uint32_t)n) break;
-      rollout_one<NV, SL>(md, smem, lay, sc, s, qpos_init, mocap_quat, phase_start, phase_target, active, label,
+      if (lane_id() == 0) t = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t s = __builtin_amdgcn_readfirstlane(t);
+      if (s >= (uint32_t)n) break;
+      rollout_one<NV, SL>(md, smem, lay, sc, (int)s, qpos_init, mocap_quat, phase_start, phase_target, active, label,
                           fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in, mask_mpos,
-                          mask_pred, mask_out);
+                          mask_pred, mask_out, ovf_count, ovf_list);
+    }
+    if (lane_id() == 0 &&
+        __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
-  const int end = list ? *list_count : (blockIdx.x < (unsigned)n ? (int)blockIdx.x + 1 : 0);
+  const int end = list ? list_count[0] : (blockIdx.x < (unsigned)n ? (int)blockIdx.x + 1 : 0);
   const int stride = list ? (int)gridDim.x : 1;
   for (int s = blockIdx.x; s < end; s += stride) {
     int i = list ? list[s] : s;
     if (i < 0 || i >= n) continue;
     rollout_one<NV, SL>(md, smem, lay, sc, i, qpos_init, mocap_quat, phase_start, phase_target, active, label,
                     fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in, mask_mpos,
-                    mask_pred, mask_out);
+                    mask_pred, mask_out, ovf_count, ovf_list);
+  }
+  if (list && lane_id() == 0 &&
+      __hip_atomic_fetch_add(list_count + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+    // list header (MGS_LIST_HEADER words: count, exits, consumed): the last
+    // workgroup out records the count it ran and leaves the header zeroed for
+    // the next launch that appends to it
+    __hip_atomic_store(list_count + 2, list_count[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(list_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(list_count + 1, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -4657,13 +4676,13 @@ mgs_rollout_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __re
                    uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
                    int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
                    double* __restrict__ state_out, const int32_t* __restrict__ list,
-                   const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in,
+                   int32_t* list_count, double* resume_out, const double* resume_in,
                    const double* __restrict__ mask_mpos, int mask_pred, uint8_t* __restrict__ mask_out,
-                   uint32_t* queue, uint32_t qbase) {
+                   uint32_t* queue, int32_t* ovf_count, int32_t* ovf_list) {
   extern __shared__ double smem[];
   rollout_entry<NV, SL>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target, active,
                         label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count, resume_out,
-                        resume_in, mask_mpos, mask_pred, mask_out, queue, qbase);
+                        resume_in, mask_mpos, mask_pred, mask_out, queue, ovf_count, ovf_list);
 }
 
 // the library's non-template kernels live in the C-ABI translation unit only

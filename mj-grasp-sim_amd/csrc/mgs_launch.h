@@ -26,14 +26,16 @@ struct RolloutArgs {
   int32_t* stats;
   const double* vstate_init;
   double* state_out;
-  const int32_t *list, *list_count;
+  const int32_t* list;
+  int32_t* list_count;       // list header (MGS_LIST_HEADER words, see mgs_rollout_list_device)
   double* resume_out;
   const double* resume_in;
   const double* mask_mpos;   // fused collision mask (mgs_mask_rollout_device): mocap positions,
   int mask_pred;             // predicate
   uint8_t* mask_out;         // and the mask written per candidate (nullptr: no fused mask)
-  uint32_t* queue;           // work-queue counter (nullptr: one workgroup per candidate)
-  uint32_t qbase;            // its value when the launch starts
+  uint32_t* queue;           // work-queue counter pair (nullptr: one workgroup per candidate)
+  int32_t* ovf_count;        // overflow list the capped candidates append to (nullptr: none):
+  int32_t* ovf_list;         // its header (count first) and its entries
 };
 
 // one dof count's runtime-layout kernels: launchers (64 lanes per workgroup,

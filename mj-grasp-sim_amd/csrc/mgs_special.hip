@@ -51,13 +51,13 @@ mgs_special_rollout(Mdl mdarg, const int32_t* __restrict__ mI, const double* __r
                     uint8_t* __restrict__ label, int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos,
                     int32_t* __restrict__ stats, const double* __restrict__ vstate_init,
                     double* __restrict__ state_out, const int32_t* __restrict__ list,
-                    const int32_t* __restrict__ list_count, double* resume_out, const double* resume_in,
+                    int32_t* list_count, double* resume_out, const double* resume_in,
                     const double* __restrict__ mask_mpos, int mask_pred, uint8_t* __restrict__ mask_out,
-                    uint32_t* queue, uint32_t qbase) {
+                    uint32_t* queue, int32_t* ovf_count, int32_t* ovf_list) {
   extern __shared__ double smem[];
   rollout_entry<MGS_SL_NV, 1>(smem, mdarg, mI, mD, lay, sc, n, qpos_init, mocap_quat, phase_start, phase_target,
                               active, label, fail_step, obj_qpos, stats, vstate_init, state_out, list, list_count,
-                              resume_out, resume_in, mask_mpos, mask_pred, mask_out, queue, qbase);
+                              resume_out, resume_in, mask_mpos, mask_pred, mask_out, queue, ovf_count, ovf_list);
 }
 
 }  // extern "C"

@@ -55,8 +55,8 @@ def load_library(wide: bool = False):
     L.mgs_overflow_list_device.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp, vp]
     L.mgs_rollout_list_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int, vp, vp, ctypes.c_int, vp, vp, vp, vp,
                                           vp, vp, vp, vp, vp, vp]
-    L.mgs_rollout_resumable_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 11
-    L.mgs_mask_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 5 + [ctypes.c_int] + [vp] * 7
+    L.mgs_rollout_resumable_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 12
+    L.mgs_mask_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 5 + [ctypes.c_int] + [vp] * 8
     L.mgs_rollout_resume.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
                                      P(abi.RolloutOut)]
     L.mgs_last_kernel_ms.argtypes = [vp]
@@ -361,32 +361,38 @@ class Engine:
                "mgs_rollout_device")
 
     def overflow_list_device(self, n, d_stats, d_count, d_list, stream=None, mask=None):
-        """device list of the candidates whose stats flag a capacity overflow"""
+        """device list of the candidates whose stats flag a capacity overflow
+        (d_count: a list header of MGS_LIST_HEADER int32 words)"""
         m = abi.MGS["MGS_FLAG_CAPACITY"] if mask is None else int(mask)
         self._ck(self.lib.mgs_overflow_list_device(n, d_stats, m, d_count, d_list, stream), "mgs_overflow_list_device")
 
     def rollout_resumable_device(self, sched, n, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail, d_objq, d_stats,
-                                 d_resume_out, d_active=None, stream=None):
+                                 d_resume_out, d_active=None, stream=None, d_ovf=None):
         """rollout_device whose overflowing candidates stop at the overflowing
-        step and leave a resume record (n x resume_width() doubles)"""
+        step and leave a resume record (n x resume_width() doubles); d_ovf: a
+        zeroed device list (MGS_LIST_HEADER + n int32) the capped candidates
+        append themselves to"""
         self._ck(self.lib.mgs_rollout_resumable_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mquat, d_ps,
                                                      d_pt, d_active, d_label, d_fail, d_objq, d_stats,
-                                                     d_resume_out, stream), "mgs_rollout_resumable_device")
+                                                     d_resume_out, d_ovf, stream), "mgs_rollout_resumable_device")
 
     def mask_rollout_device(self, sched, n, d_qpos, d_mpos, d_mquat, d_ps, d_pt, d_free, d_label, d_fail, d_objq,
-                            d_stats, d_resume_out=None, predicate="any", stream=None):
+                            d_stats, d_resume_out=None, predicate="any", stream=None, d_ovf=None):
         """collision mask and rollout in one launch (mgs_mask_rollout_device):
         d_free gets the mask, the collision-free candidates are rolled out, the
-        outputs are those of collision_free_device + rollout_resumable_device"""
+        outputs are those of collision_free_device + rollout_resumable_device
+        (d_ovf: the overflow list, as there)"""
         self._ck(self.lib.mgs_mask_rollout_device(self.batch(1), ctypes.byref(sched), n, d_qpos, d_mpos, d_mquat, d_ps,
                                                 d_pt, abi.predicate_code(predicate), d_free, d_label, d_fail, d_objq,
-                                                d_stats, d_resume_out, stream), "mgs_mask_rollout_device")
+                                                d_stats, d_resume_out, d_ovf, stream), "mgs_mask_rollout_device")
 
     def rollout_list_device(self, sched, n, d_count, d_list, grid, d_qpos, d_mquat, d_ps, d_pt, d_label, d_fail,
                             d_objq, d_stats, stream=None, d_resume_in=None):
         """re-run the candidates of a device list with `grid` workgroups looping
-        over it (outputs at their batch indices); d_resume_in: continue each
-        from its resume record instead of from the start"""
+        over it (outputs at their batch indices); d_count is the list header
+        (MGS_LIST_HEADER int32: the count ran ends in word 2, words 0-1 are left
+        zeroed); d_resume_in: continue each from its resume record instead of
+        from the start"""
         self._ck(self.lib.mgs_rollout_list_device(self.batch(grid), ctypes.byref(sched), n, d_count, d_list, grid,
                                                 d_qpos, d_mquat, d_ps, d_pt, d_resume_in, d_label, d_fail, d_objq,
                                                 d_stats, stream), "mgs_rollout_list_device")

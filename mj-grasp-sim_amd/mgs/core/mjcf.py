@@ -159,35 +159,76 @@ def load_mesh_bytes(data: bytes, fname: str):
     raise ValueError(f"unsupported mesh file {fname}")
 
 
-def mesh_mass_properties(verts, faces):
-    """volume, centroid, inertia about centroid (density 1) of a closed mesh.
-    Falls back to the convex hull when the mesh has no faces."""
-    if faces is None or len(faces) == 0:
-        from scipy.spatial import ConvexHull
-        h = ConvexHull(verts)
-        faces = h.simplices
-        # orient outward
-        c = verts[h.vertices].mean(0)
-        a, b, cc = verts[faces[:, 0]], verts[faces[:, 1]], verts[faces[:, 2]]
-        flip = np.einsum("ij,ij->i", np.cross(b - a, cc - a), a - c) < 0
-        faces = faces.copy()
-        faces[flip] = faces[flip][:, [0, 2, 1]]
+def _hull_faces(verts):
+    """outward-oriented triangles of the convex hull"""
+    from scipy.spatial import ConvexHull
+    h = ConvexHull(verts)
+    faces = h.simplices.copy()
+    c = verts[h.vertices].mean(0)
+    a, b, cc = verts[faces[:, 0]], verts[faces[:, 1]], verts[faces[:, 2]]
+    flip = np.einsum("ij,ij->i", np.cross(b - a, cc - a), a - c) < 0
+    faces[flip] = faces[flip][:, [0, 2, 1]]
+    return faces
+
+
+# products of inertia accumulated per tetrahedron: xx, yy, zz, xy, xz, yz
+_PI = ((0, 0), (1, 1), (2, 2), (0, 1), (0, 2), (1, 2))
+
+
+def mesh_mass_properties(verts, faces, inertia="legacy"):
+    """volume, centroid, inertia about centroid (density 1) of a mesh, as
+    MuJoCo 3.2's mesh compiler computes them (user_mesh.cc) for
+    <mesh inertia=...> (default "legacy", the value MuJoCo 3.2.2 uses when the
+    attribute is absent):
+
+      * a pyramid per face with its apex at the area-weighted centroid of the
+        face centres: signed volume dot(cen - facecen, n) * area / 3; "legacy"
+        takes its absolute value (a non-convex mesh is over-counted: the
+        Robotiq base_mount mesh by 2.16x), "exact" keeps the sign;
+      * centre of mass: pyramid volumes times pyramid centroids
+        (3/4 face centre + 1/4 apex);
+      * inertia: a tetrahedron per face with its apex at the centre of mass
+        (again |volume| for "legacy"), the standard second-moment formula;
+      * "convex": the same over the convex hull's faces (a mesh given by
+        vertices only is its hull, so every inertia mode agrees on it).
+    """
+    verts = np.asarray(verts, np.float64)
+    if faces is None or len(faces) == 0 or inertia == "convex":
+        faces = _hull_faces(verts)
+    faces = np.asarray(faces)
     a, b, c = verts[faces[:, 0]], verts[faces[:, 1]], verts[faces[:, 2]]
-    det = np.einsum("ij,ij->i", a, np.cross(b, c))
-    vol = det.sum() / 6.0
-    if vol < 0:
-        vol, det = -vol, -det
-    if vol < 1e-20:
+    cr = np.cross(b - a, c - a)
+    nn = np.linalg.norm(cr, axis=1)
+    keep = nn > 0
+    a, b, c, cr, nn = a[keep], b[keep], c[keep], cr[keep], nn[keep]
+    area = 0.5 * nn
+    nrm = cr / nn[:, None]
+    cen = (a + b + c) / 3.0
+    facecen = (area[:, None] * cen).sum(0) / area.sum()
+    vol = np.einsum("ij,ij->i", cen - facecen, nrm) * area / 3.0
+    if inertia == "legacy":
+        vol = np.abs(vol)
+    V = vol.sum()
+    if V < 0:
+        V, vol = -V, -vol
+    if V < 1e-20:
         return 0.0, verts.mean(0), np.zeros((3, 3))
-    com = ((a + b + c) * det[:, None]).sum(0) / (24.0 * vol)
-    cov = np.zeros((3, 3))
-    for i in range(3):
-        for j in range(3):
-            s = (a[:, i] * a[:, j] + b[:, i] * b[:, j] + c[:, i] * c[:, j]
-                 + (a[:, i] + b[:, i] + c[:, i]) * (a[:, j] + b[:, j] + c[:, j]))
-            cov[i, j] = (det * s).sum() / 120.0
-    cov_c = cov - vol * np.outer(com, com)
-    return vol, com, np.trace(cov_c) * np.eye(3) - cov_c
+    com = (vol[:, None] * (0.75 * cen + 0.25 * facecen)).sum(0) / V
+    D, E, F = a - com, b - com, c - com
+    v2 = np.einsum("ij,ij->i", (D + E + F) / 3.0, nrm) * area / 3.0
+    if inertia == "legacy":
+        v2 = np.abs(v2)
+    elif v2.sum() < 0:
+        v2 = -v2
+    P = np.zeros(6)
+    for j, (k0, k1) in enumerate(_PI):
+        P[j] = (v2 / 20.0 * (2.0 * (D[:, k0] * D[:, k1] + E[:, k0] * E[:, k1] + F[:, k0] * F[:, k1])
+                             + D[:, k0] * E[:, k1] + D[:, k1] * E[:, k0] + D[:, k0] * F[:, k1]
+                             + D[:, k1] * F[:, k0] + E[:, k0] * F[:, k1] + E[:, k1] * F[:, k0])).sum()
+    I = np.array([[P[1] + P[2], -P[3], -P[4]],
+                  [-P[3], P[0] + P[2], -P[5]],
+                  [-P[4], -P[5], P[0] + P[1]]])
+    return V, com, I
 
 
 def convex_hull_vertices(verts):
@@ -417,7 +458,8 @@ class Compiler:
             verts, faces = load_mesh_bytes(data, fname)
         verts = (verts * scale).astype(np.float32).astype(np.float64)
         name = attrs.get("name") or os.path.splitext(os.path.basename(fname))[0]
-        self.meshes[name] = dict(verts=verts, faces=faces, hull=None, mass=None)
+        self.meshes[name] = dict(verts=verts, faces=faces, hull=None, mass=None,
+                                 inertia=attrs.get("inertia", "legacy"))
 
     def _mesh_hull(self, name):
         m = self.meshes[name]
@@ -451,7 +493,7 @@ class Compiler:
     def _mesh_massprops(self, name):
         m = self.meshes[name]
         if m["mass"] is None:
-            m["mass"] = mesh_mass_properties(m["verts"], m["faces"])
+            m["mass"] = mesh_mass_properties(m["verts"], m["faces"], m.get("inertia", "legacy"))
         return m["mass"]
 
     def _parse_body_children(self, el, parent, childclass):

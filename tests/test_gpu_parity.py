@@ -255,7 +255,16 @@ def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, ora
                      objq=torch.zeros((n, 7), dtype=torch.float64, device=dev),
                      st=torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev),
                      rec=torch.zeros((n, rw), dtype=torch.float64, device=dev))
-            for _ in range(2):      # two launches in a row: the counter ring restarts each one
+            for _ in range(2):      # two launches in a row: each leaves its counter pair zeroed
+                if mode > 0:
+                    # a call refused before its launch (bad predicate) leaves no trace
+                    import ctypes
+                    rc = L.mgs_mask_rollout_device(eng.batch(1), ctypes.byref(sched), n, dq.data_ptr(),
+                                                   dmp.data_ptr(), dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
+                                                   99, o["free"].data_ptr(), o["lab"].data_ptr(),
+                                                   o["fail"].data_ptr(), o["objq"].data_ptr(), o["st"].data_ptr(),
+                                                   None, None, None)
+                    assert rc != 0
                 eng.mask_rollout_device(sched, n, dq.data_ptr(), dmp.data_ptr(), dmq.data_ptr(), dps.data_ptr(),
                                         dpt.data_ptr(), o["free"].data_ptr(), o["lab"].data_ptr(),
                                         o["fail"].data_ptr(), o["objq"].data_ptr(), o["st"].data_ptr(),
@@ -304,14 +313,17 @@ def test_device_overflow_list_and_list_rollout(env, eng, candidates):
     flags = torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev)
     pick = np.arange(3, n, 7)
     flags[torch.as_tensor(pick, device=dev), 2] = abi.MGS["MGS_FLAG_CONTACTS"]
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(abi.MGS["MGS_LIST_HEADER"], dtype=torch.int32, device=dev)
     lst = torch.zeros(n, dtype=torch.int32, device=dev)
     eng.overflow_list_device(n, flags.data_ptr(), cnt.data_ptr(), lst.data_ptr())
     sub = outs(5)
     eng.rollout_list_device(sched, n, cnt.data_ptr(), lst.data_ptr(), 3, dq.data_ptr(), dmq.data_ptr(),
                             dps.data_ptr(), dpt.data_ptr(), *[x.data_ptr() for x in sub])
     torch.cuda.synchronize()
-    k = int(cnt.item())
+    # the list run records the count it ran (word 2) and leaves count / exits zeroed
+    hdr = cnt.cpu().numpy()
+    k = int(hdr[2])
+    assert hdr[0] == 0 and hdr[1] == 0
     assert k == len(pick) and sorted(lst.cpu().numpy()[:k]) == list(pick)
     for a, b in zip(full, sub):
         a, b = a.cpu().numpy(), b.cpu().numpy()
@@ -319,11 +331,11 @@ def test_device_overflow_list_and_list_rollout(env, eng, candidates):
     rest = np.setdiff1d(np.arange(n), pick)
     assert np.all(sub[0].cpu().numpy()[rest] == 5) and np.all(sub[1].cpu().numpy()[rest] == -7)
     # an empty list launches and changes nothing
-    cnt.zero_()
     eng.rollout_list_device(sched, n, cnt.data_ptr(), lst.data_ptr(), 3, dq.data_ptr(), dmq.data_ptr(),
                             dps.data_ptr(), dpt.data_ptr(), *[x.data_ptr() for x in sub])
     torch.cuda.synchronize()
     assert np.all(sub[0].cpu().numpy()[rest] == 5)
+    assert cnt.cpu().numpy().tolist()[:3] == [0, 0, 0]
 
 
 def test_full_size_properties(env, eng, oracle_model):
@@ -424,16 +436,38 @@ def test_resumed_escalation_equals_wide_run(env, candidates):
     rec = torch.zeros((n, e4.engine.resume_width()), dtype=torch.float64, device=dev)
     e4.engine.rollout_resumable_device(sched, n, dq.data_ptr(), dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
                                        *[x.data_ptr() for x in main], rec.data_ptr())
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(abi.MGS["MGS_LIST_HEADER"], dtype=torch.int32, device=dev)
     lst = torch.zeros(n, dtype=torch.int32, device=dev)
     e4.engine.overflow_list_device(n, main[3].data_ptr(), cnt.data_ptr(), lst.data_ptr())
     e4.engine_for(40).rollout_list_device(sched, n, cnt.data_ptr(), lst.data_ptr(), 5, dq.data_ptr(),
                                           dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
                                           *[x.data_ptr() for x in esc], d_resume_in=rec.data_ptr())
     torch.cuda.synchronize()
-    k = int(cnt.item())
+    k = int(cnt[2].item())
     lo = np.sort(lst.cpu().numpy()[:k])
     assert np.array_equal(lo, stopped)
+    # ABI 17: the capped launch appends its overflowing candidates to a list
+    # itself (no list kernel); the list re-run over it gives the same outputs,
+    # twice in a row on the same header (left zeroed by each re-run)
+    H = abi.MGS["MGS_LIST_HEADER"]
+    ovf = torch.zeros(H + n, dtype=torch.int32, device=dev)
+    for _ in range(2):
+        main2, esc2 = outs(), outs()
+        rec2 = torch.zeros_like(rec)
+        e4.engine.rollout_resumable_device(sched, n, dq.data_ptr(), dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
+                                           *[x.data_ptr() for x in main2], rec2.data_ptr(), d_ovf=ovf.data_ptr())
+        e4.engine_for(40).rollout_list_device(sched, n, ovf.data_ptr(), ovf.data_ptr() + 4 * H, 5, dq.data_ptr(),
+                                              dmq.data_ptr(), dps.data_ptr(), dpt.data_ptr(),
+                                              *[x.data_ptr() for x in esc2], d_resume_in=rec2.data_ptr())
+        torch.cuda.synchronize()
+        o = ovf.cpu().numpy()
+        assert o[0] == 0 and o[1] == 0 and o[2] == k
+        assert np.array_equal(np.sort(o[H:H + k]), stopped)
+        for a, b in zip(main, main2):
+            assert torch.equal(a, b)
+        for a, b in zip(esc, esc2):
+            a, b = a.cpu().numpy(), b.cpu().numpy()
+            assert np.array_equal(a[lo], b[lo])
     got = [x.cpu().numpy() for x in main]
     for a, e in zip(got, [x.cpu().numpy() for x in esc]):
         a[lo] = e[lo]

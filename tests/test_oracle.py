@@ -1,63 +1,186 @@
 """The CPU oracle (oracle/mgs_oracle.c): the checker the GPU path is compared
 with.  Pinned here by (1) the reference's own known answer for the physics,
 Robotiq's recorded closed state `state_close` (mgs/cli/config/gripper/
-robotiq_2f_85.yaml:11, values copied as data below), (2) its arithmetic
-primitives, (3) determinism and solver consistency."""
+robotiq_2f_85.yaml:11, values copied as data below), run in the model it was
+recorded in, (2) its arithmetic primitives, (3) determinism and solver
+consistency."""
 import copy
 
 import numpy as np
 import pytest
 
 # state_close (robotiq_2f_85.yaml:11): right driver, coupler, spring link,
-# follower, then the left chain, after a long ctrl=255 close in free space.
+# follower, then the left chain, after a long ctrl=255 close in free space
+# (time 223.376 s, |qvel| <= 2e-14).
 KAT_JOINTS = np.array([7.93116751e-01, 3.48441304e-04, 7.89591521e-01, -7.76735418e-01,
                        7.93117030e-01, 3.47173334e-04, 7.89598436e-01, -7.76696653e-01])
+# rest state of the oracle minus KAT_JOINTS (rad) in the scan-env model, MuJoCo
+# 3.2.2's legacy mesh inertia (see test_state_close_offset_is_the_base_mount_mass):
+# drivers +1.09e-4, couplers -3.2e-6 / -0.7e-6, spring links -2.93e-4 / -3.17e-4,
+# followers +3.1e-5 / -6.5e-5.  Per-joint bounds are ~1.3x those offsets.
+KAT_TOL = np.array([1.5e-4, 1.0e-5, 4.0e-4, 1.0e-4, 1.5e-4, 1.0e-5, 4.2e-4, 1.0e-4])
+
+# GripperScanEnv's model (reference mgs/env/gripper_scan.py:26-49), the model
+# state_close was recorded in (its 22 qpos = 15 gripper + 7 of the free
+# camera body): the option sequence, the gripper, a world-fixed 1e-6 m sphere
+# at the origin and a free camera body 0.4 m above it (lights and the camera
+# element do not enter the physics and are left out)
+SCAN_XML = r"""
+<mujoco>
+  <compiler angle="radian" autolimits="true" />
+  <option integrator="implicitfast" timestep="0.001"/>
+  <compiler discardvisual="false"/>
+  <option noslip_iterations="1"> </option>
+  <option><flag multiccd="enable"/> </option>
+  <option cone="elliptic" gravity="0 0 -9.81" impratio="3" timestep="0.001" noslip_iterations="2"
+          noslip_tolerance="1e-8" tolerance="1e-8"/>
+  <option gravity="0 0 0" />
+  {gripper}
+  <option gravity="0 0 0" />
+  <worldbody>
+    <body name="center" pos="0.0 0.0 0.0" quat="1.0 0.0 0 0">
+      <geom name="geom:center" size="0.000001" rgba="0 0 0 1.0"/>
+    </body>
+    <body name="body:camera" pos="0.0 0.0 .4" quat="1.0 0.0 0 0">
+      <freejoint name="camera:joint"/>
+      <geom name="geom:camera" size="0.01" />
+    </body>
+  </worldbody>
+</mujoco>
+"""
 
 
-def free_close(env, solver, noslip, nsteps):
-    from oracle import oracle as O
+@pytest.fixture(scope="module")
+def scan_model():
+    from mgs.core.mjcf import compile_xml
+    from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
     from mgs.util.geo.transforms import SE3Pose
-    cm = copy.copy(env.model)
-    cm.options = dict(env.model.options)
+    g = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz"))
+    gx, ga = g.to_xml()
+    cm = compile_xml(SCAN_XML.format(gripper=gx), ga)
+    # GripperScanEnv.__init__ (gripper_scan.py:86-91): identity pose @ b2c
+    pose = SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz") @ g.base_to_contact_transform()
+    q = np.array(cm.qpos0, np.float64).copy()
+    q[0:3], q[3:7] = pose.pos, pose.quat
+    return cm, q, np.array(pose.pos, np.float64), np.array(pose.quat, np.float64)
+
+
+def scan_close(scan_model, solver="Newton", noslip=2, nsteps=6000, cm=None):
+    from oracle import oracle as O
+    cm0, q, mp, mq = scan_model
+    cm = copy.copy(cm0 if cm is None else cm)
+    cm.options = dict(cm.options)
     cm.options["solver"] = solver
     om = O.OracleModel(cm)
     om.desc.noslip_iterations = noslip
-    pose = SE3Pose(np.array([[0.0, 0.0, 0.0]]), np.array([[1.0, 0, 0, 0]]), "wxyz")
-    q, mp, mq, _ = env.initial_state(pose, np.zeros((1, 8)))
-    q[0, 17] = 0.4      # object out of reach, as in the recorded state
-    tr, nc, qv = om.trace(q[0], mp[0], mq[0], np.array([255.0]), nsteps)
-    return tr, qv
+    tr, nc, qv = om.trace(q, mp, mq, np.array([255.0]), nsteps)
+    return tr, nc, qv, om
+
+
+def test_scan_model_is_the_recorded_one(scan_model):
+    """state_close's layout: 22 qpos (15 gripper + 7 camera), 20 dofs; the
+    scan env's options after the gripper's own <option> (impratio 10)"""
+    cm = scan_model[0]
+    assert (cm.nq, cm.nv) == (22, 20)
+    o = cm.options
+    assert (o["impratio"], o["noslip_iterations"], o["tolerance"], o["cone"]) == (10.0, 2, 1e-8, "elliptic")
+    assert np.all(o["gravity"] == 0.0)
 
 
 @pytest.mark.parametrize("solver", ["Newton", "PGS"])
-def test_state_close_known_answer(env, solver):
-    """Free-space close settles within 1.5e-3 rad of MuJoCo's recorded state
-    (noslip off: MuJoCo reached rest, |qvel| ~ 1e-14)."""
-    tr, qv = free_close(env, solver, noslip=0, nsteps=4000)
-    assert np.abs(tr[-1, 7:15] - KAT_JOINTS).max() < 1.5e-3
+def test_state_close_known_answer(scan_model, solver):
+    """Free-space close in GripperScanEnv's model (noslip off: MuJoCo reached
+    rest): every joint within ~1.3x its known offset (KAT_TOL) of the recorded
+    state.  The world-fixed 1e-6 m sphere stays 16 mm below the pads' contact
+    line and the camera sphere 0.55 m away: the pads touch only each other."""
+    cm = scan_model[0]
+    tr, nc, qv, om = scan_close(scan_model, solver, noslip=0, nsteps=6000)
+    assert np.all(np.abs(tr[-1, 7:15] - KAT_JOINTS) < KAT_TOL)
     assert np.abs(qv).max() < (1e-9 if solver == "Newton" else 1e-4)   # PGS: 100 iterations, not converged
+    _, _, _, _, g = om.contacts(tr[-1], scan_model[2], scan_model[3])
+    names = {cm.geom_names[i] for i in g.ravel()}
+    assert names == {"right_pad1", "left_pad1"}
+    assert np.array_equal(tr[-1, 15:22], scan_model[1][15:22])       # the camera body never moves
 
 
-def test_state_close_with_noslip(env):
-    """With the reference's noslip_iterations=2 (gravityless_object_grasping.py:41)
-    the close comes to rest at the recorded state.  Before MuJoCo's costChange
-    rule was restated (a block update that raises the dual cost by > 1e-10 is
-    undone), noslip kept the pad1-pad1 edge contact in a limit cycle at
-    |qvel| = 0.19 rad/s; now the residual is the unregularised noslip sweep's
-    jitter on the two redundant edge contacts, < 1e-6 rad/s."""
-    tr, qv = free_close(env, "Newton", noslip=2, nsteps=4000)
-    assert np.abs(tr[-1, 7:15] - KAT_JOINTS).max() < 1.5e-3
-    assert np.abs(qv).max() < 2e-6
-    v = np.abs(np.diff(tr[2000:, 7:15], axis=0)).max() / 1e-3      # finite-difference joint speed
-    assert v < 2e-6
+def test_state_close_with_noslip(scan_model):
+    """With the scan env's noslip_iterations=2 the close comes to rest at the
+    same joints.  MuJoCo's recorded |qvel| is <= 2e-14; here a 40 Hz limit cycle
+    of ~6e-7 rad/s (joint amplitude ~3e-9 rad) remains: the two pad-pad contact
+    points lie on one edge, so their tangent rows along that edge are identical
+    and the unregularised noslip sweep has no unique split between them (noslip
+    off, the same rest state is reached at 5e-14, test_state_close_known_answer;
+    noslip iterations 1 or 50 give the same cycle)."""
+    tr, nc, qv, _ = scan_close(scan_model, noslip=2, nsteps=6000)
+    assert np.all(np.abs(tr[-1, 7:15] - KAT_JOINTS) < KAT_TOL)
+    assert np.abs(qv).max() < 1e-6
+    amp = np.abs(tr[-2000:, 7:15] - tr[-2000:, 7:15].mean(0)).max()
+    assert amp < 1e-8
 
 
-def test_pgs_cost_change_revert_noslip_free_close(env):
+def test_pgs_cost_change_revert_noslip_free_close(scan_model):
     """PGS main solver + noslip, same rest criterion (PGS at 100 iterations is
     not converged, so the bound is the solver's, not the revert rule's)."""
-    tr, qv = free_close(env, "PGS", noslip=2, nsteps=4000)
-    assert np.abs(tr[-1, 7:15] - KAT_JOINTS).max() < 1.5e-3
+    tr, nc, qv, _ = scan_close(scan_model, "PGS", noslip=2, nsteps=6000)
+    assert np.all(np.abs(tr[-1, 7:15] - KAT_JOINTS) < KAT_TOL)
     assert np.abs(qv).max() < 1e-3
+
+
+def test_state_close_offset_is_the_base_mount_mass(scan_model):
+    """Which modelled term the state_close offset came from.  The rest state is
+    a static balance of soft constraints whose stiffness is
+    K imp^2 / ((1 - imp) diagApprox), and diagApprox is built from the qpos0
+    inverse weights, which every gripper body inherits from the free base.
+    base_mount has no <inertial>, so its mass comes from its two mesh geoms at
+    density 1000, and MuJoCo 3.2.2's default <mesh inertia="legacy"> sums
+    |volume| per face pyramid: 74.98 cm^3 for this non-convex mesh against its
+    34.77 cm^3 exact volume.  With the exact volume (the round-3 model) the
+    drivers rest 4.7e-4 rad and the followers 5.8e-4 / 6.9e-4 rad off the
+    recorded state; with the legacy mass 1.1e-4 and 3.1e-5 / 6.5e-5.  The spring
+    links (-2.9e-4 / -3.2e-4) are the remaining, unexplained term."""
+    from mgs.core.mjcf import _invweight0, mesh_mass_properties
+    from mgs.gripper.robotiq2f85 import _ASSET
+    cm = scan_model[0]
+    b = cm.body_names.index("base_mount")
+    d = np.load(_ASSET)
+    vol = float(d["vol_base_mount"])
+    assert abs(cm.body_mass[b] - 2 * 1000.0 * vol) < 1e-12
+    # the exact-volume variant of the same body (the mesh's own vertices are
+    # not shipped: scale the legacy properties to the exact volume 34.769 cm^3
+    # and centroid, which is what the round-3 model carried)
+    ex = copy.copy(cm)
+    ex.body_mass = cm.body_mass.copy()
+    ex.body_mass[b] = 2 * 1000.0 * 3.4769031848943e-05
+    ex.body_inertia = cm.body_inertia.copy()
+    ex.body_inertia[b] = cm.body_inertia[b] * (3.4769031848943e-05 / vol)
+    ex.body_ipos = cm.body_ipos.copy()
+    ex.body_ipos[b] = [-1.41673786e-03, -3.79796273e-05, -8.98408191e-04]
+    ex.body_invweight0, ex.dof_invweight0, ex.meaninertia = _invweight0(ex)
+    tr_l, *_ = scan_close(scan_model, noslip=0)
+    tr_e, *_ = scan_close(scan_model, noslip=0, cm=ex)
+    off_l = np.abs(tr_l[-1, 7:15] - KAT_JOINTS)
+    off_e = np.abs(tr_e[-1, 7:15] - KAT_JOINTS)
+    drv, fol = [0, 4], [3, 7]
+    assert off_e[drv].min() > 4e-4 and off_e[fol].min() > 5e-4
+    assert off_l[drv].max() < 1.2e-4 and off_l[fol].max() < 7e-5
+    assert (off_l[drv] < off_e[drv] / 4).all() and (off_l[fol] < off_e[fol] / 8).all()
+    # the legacy rule itself (mgs.core.mjcf.mesh_mass_properties): a convex
+    # mesh is unchanged, a non-convex one is over-counted
+    cube = np.array([[x, y, z] for x in (0, 1) for y in (0, 1) for z in (0, 1)], float)
+    assert abs(mesh_mass_properties(cube, None)[0] - 1.0) < 1e-12
+    # a U-shaped prism (volume 7): its area-weighted face centroid lies in the
+    # notch, outside the solid, so some face pyramids are negative and legacy
+    # counts them positive
+    P = np.array([[0, 0], [1, 0], [2, 0], [3, 0], [3, 3], [2, 3], [2, 1], [1, 1], [1, 3], [0, 3]], float)
+    verts = np.vstack([np.c_[P, np.zeros(10)], np.c_[P, np.ones(10)]])
+    up = [[0, 1, 8], [0, 8, 9], [1, 2, 6], [1, 6, 7], [2, 3, 4], [2, 4, 5]]   # CCW seen from +z
+    faces = [[a, c, b] for a, b, c in up] + [[10 + a, 10 + b, 10 + c] for a, b, c in up]
+    for i in range(10):
+        j = (i + 1) % 10
+        faces += [[i, j, 10 + j], [i, 10 + j, 10 + i]]
+    faces = np.array(faces)
+    assert abs(mesh_mass_properties(verts, faces, "exact")[0] - 7.0) < 1e-12
+    assert mesh_mass_properties(verts, faces, "legacy")[0] > 7.0 + 1e-3
 
 
 def test_sincos_and_tree_primitives():

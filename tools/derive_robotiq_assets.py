@@ -12,7 +12,9 @@ Output: mj-grasp-sim_amd/mgs/assets/robotiq2f85.npz — DERIVED DATA only:
     mesh vertices),
   * for every mesh whose body has no <inertial> (base_mount, silicone_pad),
     its volume, centroid and inertia tensor about the centroid (density 1),
-    from exact signed-volume integration over the closed triangle mesh.
+    as MuJoCo 3.2.2's mesh compiler computes them with its default
+    <mesh inertia="legacy"> (mgs.core.mjcf.mesh_mass_properties: |volume| per
+    face pyramid, so the non-convex base_mount counts 2.16x its volume).
 
 No STL file and no reference source is copied into the repository.
 Reference: mgs/gripper/robotiq2f85.py:32-225 (template), asset/robotiq2f85/*.stl.
@@ -23,6 +25,9 @@ import sys
 
 import numpy as np
 from scipy.spatial import ConvexHull
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "mj-grasp-sim_amd"))
+from mgs.core.mjcf import mesh_mass_properties  # noqa: E402
 
 SRC = "/root/reference/asset/robotiq2f85"
 DST = os.path.join(os.path.dirname(__file__), "..", "mj-grasp-sim_amd", "mgs",
@@ -40,27 +45,6 @@ def load_stl(path):
     return arr["v"].astype(np.float64)
 
 
-def mesh_mass_properties(tri):
-    """Volume, centroid and inertia about the centroid of a closed mesh (rho=1)."""
-    a, b, c = tri[:, 0], tri[:, 1], tri[:, 2]
-    det = np.einsum("ij,ij->i", a, np.cross(b, c))
-    vol = det.sum() / 6.0
-    sign = 1.0 if vol > 0 else -1.0
-    vol *= sign
-    det = det * sign
-    com = ((a + b + c) * det[:, None]).sum(0) / (24.0 * vol)
-    # second moments of each tetrahedron (origin, a, b, c)
-    cov = np.zeros((3, 3))
-    for i in range(3):
-        for j in range(3):
-            s = (a[:, i] * a[:, j] + b[:, i] * b[:, j] + c[:, i] * c[:, j]
-                 + (a[:, i] + b[:, i] + c[:, i]) * (a[:, j] + b[:, j] + c[:, j]))
-            cov[i, j] = (det * s).sum() / 120.0
-    cov_c = cov - vol * np.outer(com, com)
-    inertia = np.trace(cov_c) * np.eye(3) - cov_c
-    return vol, com, inertia
-
-
 def main():
     if not os.path.isdir(SRC):
         print("reference meshes not found at", SRC)
@@ -73,8 +57,9 @@ def main():
         verts = np.unique(pts[hull.vertices], axis=0)
         out["hull_" + name] = verts
     for name in MASS_MESHES:
-        tri = load_stl(os.path.join(SRC, name + ".stl")) * SCALE
-        vol, com, inertia = mesh_mass_properties(tri)
+        tri = (load_stl(os.path.join(SRC, name + ".stl")) * SCALE).astype(np.float32).astype(np.float64)
+        v = tri.reshape(-1, 3)
+        vol, com, inertia = mesh_mass_properties(v, np.arange(len(v)).reshape(-1, 3))
         out["vol_" + name] = np.array(vol)
         out["com_" + name] = com
         out["inertia_" + name] = inertia

@@ -1,0 +1,106 @@
+#!/bin/bash
+# One GPU call (gpurun), any sequence of steps; each step has its own time
+# limit, the chain stops at the first failure and prints what it left.
+#
+#   bash tools/gpu.sh <tag> <step> [<step> ...]
+#
+# steps:
+#   tests     the GPU suite (pytest -m gpu)
+#   smoke     __graft_entry__.smoke()
+#   bench     the driver's command, `bench.py --gpus 1 --steps 20 --warmup 5`
+#             (full line: e2e API, CPU baseline); first process of the call
+#   rep       the driver's command without CPU baseline / e2e, 3 processes
+#   n2        2-rank launcher rehearsal on one GPU (gloo) with the shard check
+#   trace     rocprofv3 --kernel-trace --stats of the driver's command
+#   pmc       PMC passes (FETCH / WRITE / SQ / VALU) on a one-pipeline bench
+#   stages    stage timers (MGS_PROFILE builds): headline and Shadow pile
+#   configs   tools/bench_configs.py (C3, C4, C5)
+#   py:<file> python3 <file> (a probe script under tools/)
+# Outputs: gpurun_out/<tag>/
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+DRIVER="bench.py --gpus 1 --steps 20 --warmup 5"
+P1="bench.py --streams 1 --steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate --fused 0"
+
+summ() {   # one-line summary of a bench JSON line
+  python3 - "$1" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+x = d["detail"]
+e = x.get("end_to_end_api") or {}
+c = d.get("cpu_baseline") or {}
+print(sys.argv[1], "value", round(d["value"]), "ms/step", round(d["ms_per_step"], 2),
+      "roll ms", round(x["rollout_kernel_ms"], 2), "frac", round(d["roofline"]["frac"], 5),
+      "e2e", round(e.get("candidates_per_s", 0)), "cpu", round(c.get("value", 0)),
+      "shard", (x.get("shard_check") or {}).get("labels_identical_to_single_rank"))
+EOF
+}
+
+fail() { echo "FAILED step $1"; tail -40 "$2"; exit 1; }
+
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 1200 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > $O/tests.log 2>&1 || fail tests $O/tests.log
+      tail -1 $O/tests.log ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 600 python3 $DRIVER > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+      summ $O/bench.json ;;
+    rep)
+      for r in 1 2 3; do
+        timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 0 > $O/rep$r.json 2> $O/rep$r.err || fail rep $O/rep$r.err
+        summ $O/rep$r.json
+      done ;;
+    n2)
+      timeout -k 10 300 python3 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-budget 0 --e2e-steps 0 \
+        > $O/n2.json 2> $O/n2.err || fail n2 $O/n2.err
+      summ $O/n2.json ;;
+    trace)
+      (cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o bench -f csv -- python3 $DRIVER \
+          --cpu-budget 0 --e2e-steps 0 > $O/trace.json 2> $O/trace.err) || fail trace $O/trace.err
+      summ $O/trace.json ;;
+    pmc)
+      export TMPDIR=/tmp
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc -f csv -- python3 $P1 \
+        > $O/pmc_fetch.json 2> $O/pmc_fetch.err || fail pmc_fetch $O/pmc_fetch.err
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o pmc -f csv -- python3 $P1 \
+        > $O/pmc_write.json 2> $O/pmc_write.err || fail pmc_write $O/pmc_write.err
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM -d $O/pmc_sq -o pmc -f csv -- python3 $P1 \
+        > $O/pmc_sq.json 2> $O/pmc_sq.err || fail pmc_sq $O/pmc_sq.err
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES \
+        SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_VALU \
+        SQ_INSTS_SALU -d $O/pmc_valu -o pmc -f csv -- python3 $P1 > $O/pmc_valu.json 2> $O/pmc_valu.err \
+        || fail pmc_valu $O/pmc_valu.err
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES \
+        SQ_WAVES -d $O/pmc_lane -o pmc -f csv -- python3 $P1 > $O/pmc_lane.json 2> $O/pmc_lane.err \
+        || fail pmc_lane $O/pmc_lane.err
+      echo "pmc ok" ;;
+    stages)
+      timeout -k 10 300 python3 tools/stage_profile.py 160 > $O/stages.txt 2>&1 || fail stages $O/stages.txt
+      tail -3 $O/stages.txt
+      timeout -k 10 400 python3 tools/stage_profile_clutter.py 300 > $O/stages_clutter.txt 2>&1 \
+        || fail stages_clutter $O/stages_clutter.txt
+      tail -3 $O/stages_clutter.txt ;;
+    configs)
+      timeout -k 10 900 python3 tools/bench_configs.py > $O/configs.jsonl 2> $O/configs.err || fail configs $O/configs.err
+      cat $O/configs.jsonl | cut -c1-300 ;;
+    py:*)
+      f=${step#py:}
+      b=$(basename "$f" .py)
+      timeout -k 10 600 python3 -u "$f" > $O/$b.txt 2>&1 || fail "$step" $O/$b.txt
+      tail -20 $O/$b.txt ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done

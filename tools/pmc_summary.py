@@ -1,4 +1,4 @@
-"""Summarise a tools/prof_r0N.sh output directory into profiles/:
+"""Summarise a tools/gpu.sh pmc / trace output directory into profiles/:
 
   profiles/<tag>_rocprof_kernel_stats.csv kernel-trace --stats of the bench command
   profiles/<tag>_pmc_{fetch,write,sq}.csv the rollout kernel's counter rows
