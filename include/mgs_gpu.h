@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 17
+#define MGS_ABI_VERSION 18
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -83,6 +83,8 @@ extern "C" {
 #define MGS_FLAG_CAPACITY 3        /* either capacity flag */
 #define MGS_FLAG_DIVERGED 4        /* qpos / qvel / qacc NaN or beyond 1e10 (MuJoCo mj_checkPos /
                                       mj_checkVel / mj_checkAcc, mjMAXVAL): the candidate stops, label 0 */
+#define MGS_FLAG_PAUSED 8          /* reached mgs_schedule.pause_step unfinished: stopped there with a
+                                      resume record (fail_step -4), continued by a later launch */
 #define MGS_MAXVAL 1e10
 
 /* narrowphase of a geom pair (pair_kind) */
@@ -190,6 +192,10 @@ typedef struct mgs_model_desc {
                                radius (sphere: 1 vertex, capsule: 2 vertices on z; 0 otherwise) */
   int32_t d_geom_rbound;    /* 1: largest vertex norm of the geom's hull (geom frame): bounds how
                                far a rotation moves its supports (separation certificates) */
+  int32_t d_geom_cyl;       /* 2: cylinder radius and half-height, (0, 0) for other geoms (ABI
+                               18).  A cylinder's supports and contact features are the exact
+                               ones; its hull, a 16-sided prism inscribed in it (rim vertices
+                               on the true circle), serves the broadphase and the cap polygon */
   /* convex hulls */
   int32_t i_hull_vertadr;
   int32_t i_hull_vertnum;
@@ -257,6 +263,14 @@ typedef struct mgs_schedule {
   double ctrl[MGS_MAX_PHASES * 32];
   double vclip;          /* > 0: clip every qvel entry to [-vclip, vclip] after each step
                             (ClutterTableEnv.gen_clutter, clutter_table.py:215-221); 0 = off */
+  int32_t pause_step;    /* > 0 (with resume records): a candidate that has executed this many
+                            steps (global step count, resumed runs included) stops before the
+                            next one with its resume record, MGS_FLAG_PAUSED and fail_step -4,
+                            so a long batch runs as time slices of several launches (ABI 18);
+                            0 = run to the end */
+  int32_t capped_continue; /* 1: with resume records, a candidate over the contact / row capacity
+                            runs on capped and flagged instead of stopping (the last stage of an
+                            escalation); 0 = stop there (fail_step -3) */
 } mgs_schedule;
 
 /* per-candidate rollout outputs */

@@ -954,6 +954,7 @@ struct PairCtx {
   double R1[9], R2[9], x1[3], x2[3];
   double c1[3], c2[3];
   double r1, r2;   // rounding radii (sphere / capsule: hull (+) ball), 0 for hulls
+  double cy1[2], cy2[2];   // cylinder radius / half-height (exact solid), 0 0 for others
 };
 DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   int lane = lane_id();
@@ -969,6 +970,25 @@ DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   for (int k = 0; k < 3; k++) { c.c1[k] = c.V1[k * c.n1 + i1]; c.c2[k] = c.V2[k * c.n2 + i2]; }
   c.r1 = DA(md, geom_radius)[g1];
   c.r2 = DA(md, geom_radius)[g2];
+  const double* cy = DA(md, geom_cyl);
+  c.cy1[0] = cy[2 * g1]; c.cy1[1] = cy[2 * g1 + 1];
+  c.cy2[0] = cy[2 * g2]; c.cy2[1] = cy[2 * g2 + 1];
+}
+
+// exact cylinder support in the geom frame (oracle cyl_support; MuJoCo's ccd
+// support of mjGEOM_CYLINDER): the rim point along dl's radial part on the cap
+// dl points to, (0, 0, +-h) along the axis; dl is uniform, so is the result
+DEVI void cyl_support(double* v, const double* cy, const double* dl) {
+  double rho = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+  if (rho > K_MINVAL) {
+    double s = cy[0] / rho;
+    v[0] = dl[0] * s;
+    v[1] = dl[1] * s;
+  } else {
+    v[0] = 0.0;
+    v[1] = 0.0;
+  }
+  v[2] = dl[2] >= 0.0 ? cy[1] : -cy[1];
 }
 
 DEVI void sup_cached(SupAcc& a, int n, const double* cached, const double* dl) {
@@ -1030,6 +1050,8 @@ DEVI void support_pair(const PairCtx& c, const double* dir, double* out1, double
   double v1[3], v2[3], t[3];
   sup_finish(a1, v1, c.n1);
   sup_finish(a2, v2, c.n2);
+  if (c.cy1[0] > 0.0) cyl_support(v1, c.cy1, dl1);
+  if (c.cy2[0] > 0.0) cyl_support(v2, c.cy2, dl2);
   mulmv3(t, c.R1, v1);
   add3(out1, c.x1, t);
   mulmv3(t, c.R2, v2);
@@ -1310,10 +1332,27 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
   const double* cv = which == 1 ? c.c1 : c.c2;
   int num = which == 1 ? c.n1 : c.n2;
   double rr = which == 1 ? c.r1 : c.r2;
+  const double* cy = which == 1 ? c.cy1 : c.cy2;
   double nl[3];
   mulmtv3(nl, R, n);
   double base = dot3(x, n);
   if (rr > 0.0) base = (sign > 0) ? base + rr : base - rr;   // rounded: surface = hull (+) ball
+  // exact cylinder (oracle feature()): its rim polygons turned about the axis
+  // so that vertex 0 of each cap is the true rim extreme along n; n along the
+  // axis keeps the prism (a cap face).  The prism has 32 <= WAVE vertices, so
+  // every vertex comes from the lane cache and is turned in registers
+  const bool cyl = cy[0] > 0.0;
+  double c0 = 1.0, s0 = 0.0;
+  if (cyl) {
+    double rho = sqrt(nl[0] * nl[0] + nl[1] * nl[1]);
+    if (rho > K_MINVAL) {
+      double sg = (sign > 0) ? 1.0 : -1.0;
+      c0 = sg * (nl[0] / rho);
+      s0 = sg * (nl[1] / rho);
+    }
+  }
+  double cvx = cv[0], cvy = cv[1];
+  if (cyl) { double tx = c0 * cvx - s0 * cvy; cvy = s0 * cvx + c0 * cvy; cvx = tx; }
   // the collecting pass takes the extreme its first pass computed (*ext): the
   // same expressions over the same vertices, so the same value
   double best = (sign > 0) ? -INFINITY : INFINITY;
@@ -1321,7 +1360,7 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
     best = *ext;
   } else {
   if (num <= WAVE) {
-    if (lane < num) best = base + ((cv[0] * nl[0] + cv[1] * nl[1]) + cv[2] * nl[2]);
+    if (lane < num) best = base + ((cvx * nl[0] + cvy * nl[1]) + cv[2] * nl[2]);
   } else {
     for (int b0 = 0; b0 < num; b0 += SUP_CH * WAVE) {
       SupChunk k;
@@ -1365,7 +1404,7 @@ DEVI int feature(const PairCtx& c, int which, const double* n, const double* t1,
     double s = 0.0, vx = 0.0, vy = 0.0, vz = 0.0;
     int pred = 0;
     if (i < num) {
-      if (num <= WAVE) { vx = cv[0]; vy = cv[1]; vz = cv[2]; }
+      if (num <= WAVE) { vx = cvx; vy = cvy; vz = cv[2]; }
       else { vx = V[i]; vy = V[num + i]; vz = V[2 * num + i]; }
       s = base + ((vx * nl[0] + vy * nl[1]) + vz * nl[2]);
       pred = sign > 0 ? (s >= lim) : (s <= lim);
@@ -4411,6 +4450,23 @@ mgs_collision_kernel(Mdl mdarg, const int32_t* __restrict__ mI, const double* __
   collision_entry<NV, SL>(smem, mdarg, mI, mD, lay, n, qpos_init, mocap_pos, mocap_quat, predicate, out);
 }
 
+// a candidate's resume record: the state entering step (p, t) -- qpos, qvel,
+// qacc_warmstart, time -- the schedule position and the partial stats
+// (mgs_rollout_out.resume)
+DEVI void save_record(const Mdl& md, Dat& d, double* rec, int p, int t, int gstep, int maxcon, int maxefc,
+                      int sumcon, int sumefc) {
+  const int lane = lane_id(), nq = md.m.nq, nvr = md.m.nv;
+  for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
+  for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
+  if (lane == 0) {
+    double* tail = rec + nq + 2 * nvr;
+    tail[0] = d.time[0];
+    tail[1] = p; tail[2] = t; tail[3] = gstep;
+    tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
+    tail[8] = d.ITERS;
+  }
+}
+
 // one candidate's rollout (the body of mgs_rollout_kernel)
 template <int NV, int SL>
 DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_schedule& sc, int i,
@@ -4478,6 +4534,17 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       for (int u = 0; u < md.m.nu; u++) d.ctrl[u] = sc.ctrl[p * 32 + u];
     int ns = sc.nsteps[p];
     for (int t = (p == p0 ? t0 : 0); t < ns && ok; t++) {
+      if (sc.pause_step > 0 && gstep >= sc.pause_step && resume_out) {
+        // time slice (ABI 18): the state entering this step, the schedule
+        // position and the partial stats go to the resume record, exactly as
+        // for a capacity stop, and a later launch continues from there
+        save_record(md, d, resume_out + (size_t)i * RS, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
+        if (lane == 0) d.OVERFLOW |= MGS_FLAG_PAUSED;
+        wsync();
+        ok = 0;
+        fstep = -4;
+        break;
+      }
       double frac = (double)t / (double)ns;
       if (lane == 0)
         for (int k = 0; k < 3; k++) d.mocap_pos[k] = ps[3 * p + k] + (pt[3 * p + k] - ps[3 * p + k]) * frac;
@@ -4508,22 +4575,13 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
 #else
       forward_rows<NV>(md, d);
 #endif
-      if (resume_out && (uni(d.OVERFLOW) & MGS_FLAG_CAPACITY)) {
+      if (resume_out && !sc.capped_continue && (uni(d.OVERFLOW) & MGS_FLAG_CAPACITY)) {
         // capacity exceeded in this step (contacts in collision, rows in
         // make_constraints, both before anything of the state moved): the
         // state entering the step, the schedule position and the partial stats
         // go to the candidate's resume record and the candidate stops (the
         // escalation continues it from here with more capacity)
-        double* rec = resume_out + (size_t)i * RS;
-        for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
-        for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
-        if (lane == 0) {
-          double* tail = rec + nq + 2 * nvr;
-          tail[0] = d.time[0];
-          tail[1] = p; tail[2] = t; tail[3] = gstep;
-          tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
-          tail[8] = d.ITERS;
-        }
+        save_record(md, d, resume_out + (size_t)i * RS, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
         ok = 0;
         fstep = -3;
         break;
@@ -4568,7 +4626,7 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       gstep++;
     }
     if (ok && sc.check_at_end[p] && !obj_contact(md, d)) { ok = 0; fstep = gstep - 1; }
-    if (fstep == -3) break;
+    if (fstep <= -3) break;
   }
   if (lane == 0) {
     label[i] = (uint8_t)ok;

@@ -280,14 +280,22 @@ class Engine:
         """doubles per resume record (mgs_rollout_out.resume)"""
         return self.cm.nq + 2 * self.cm.nv + abi.MGS["MGS_RESUME_EXTRA"]
 
-    def rollout(self, plan, resumable=False, resume_from=None):
+    def rollout(self, plan, resumable=False, resume_from=None, pause_step=0, capped_continue=False):
         """mgs_rollout.  resumable: candidates overflowing the capacity stop at
         that step (fail_step -3) and result["resume"] holds their records;
         resume_from: records of such a capped run, continued here
-        (mgs_rollout_resume) instead of restarting from the plan."""
+        (mgs_rollout_resume) instead of restarting from the plan.
+        pause_step > 0 (needs resumable): candidates that have run that many
+        steps stop there (fail_step -4, MGS_FLAG_PAUSED) with a record, a time
+        slice a later call continues; capped_continue: over-capacity candidates
+        run on capped and flagged instead of stopping."""
         n = len(plan.qpos_init)
         sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
                                   check_offset=getattr(plan, "check_offset", None))
+        sched.pause_step = int(pause_step)
+        sched.capped_continue = int(bool(capped_continue))
+        if pause_step and not resumable:
+            raise ValueError("pause_step needs resumable=True (the paused state goes to the resume records)")
         label = np.zeros(n, np.uint8)
         fail = np.zeros(n, np.int32)
         objq = np.zeros((n, 7), np.float64)

@@ -752,7 +752,8 @@ class Compiler:
                 hulls.append(np.zeros((1, 3)) if t == "sphere" else np.array([[0, 0, -s[1]], [0, 0, s[1]]]))
             elif t == "cylinder":
                 # a CYL_SIDES-sided prism inscribed in the cylinder (vertices on the
-                # true rim): documented approximation of MuJoCo's smooth support
+                # true rim): the broadphase box and the cap polygon; supports and
+                # contact features use the exact cylinder (geom_cyl)
                 s = _f(g["size"], 3)
                 a = 2 * np.pi * np.arange(CYL_SIDES) / CYL_SIDES
                 rim = np.stack([s[0] * np.cos(a), s[0] * np.sin(a)], 1)
@@ -762,6 +763,7 @@ class Compiler:
             else:
                 raise MJCFError(f"collision geom type {t} not supported yet")
             radius = float(_f(g["size"], 3)[0]) if t in ("sphere", "capsule") else 0.0
+            cyl = _f(g["size"], 3)[:2].copy() if t == "cylinder" else np.zeros(2)
             side = 0 if partition is None else int(np.sign(gid - partition))
             fr = _fv(g, "friction")
             cgeoms.append(dict(gid=gid, body=bi, hull=hid, pos=gpos, quat=gquat, contype=ct,
@@ -769,7 +771,7 @@ class Compiler:
                                solref=_fv(g, "solref"), solimp=_fv(g, "solimp"),
                                margin=float(g.get("margin", "0")), gap=float(g.get("gap", "0")),
                                priority=int(g.get("priority", "0")), solmix=float(g.get("solmix", "1")),
-                               side=side, name=g.get("name", ""), radius=radius, type=t))
+                               side=side, name=g.get("name", ""), radius=radius, type=t, cyl=cyl))
         # --- admissible pairs
         excl = set()
         for b1, b2 in self.excludes:
@@ -963,6 +965,7 @@ class Compiler:
             aabb.append(np.concatenate([(lo + hi) / 2, (hi - lo) / 2]))
         cm.geom_aabb = np.array(aabb).reshape(-1, 6)
         cm.geom_radius = np.array([g["radius"] for g in cgeoms], np.float64)
+        cm.geom_cyl = np.array([g["cyl"] for g in cgeoms], np.float64).reshape(-1, 2)
         cm.geom_rbound = np.array([float(np.max(np.linalg.norm(hulls[g["hull"]], axis=1)))
                                    for g in cgeoms], np.float64)
         cm.hull_vertnum = np.array([len(h) for h in hulls], np.int32)
@@ -1166,7 +1169,7 @@ class CompiledModel:
               else np.zeros(self.nv))
         for n in ["geom_bodyid", "geom_hullid", "geom_side"]:
             put_i(n, getattr(self, n))
-        for n in ["geom_pos", "geom_quat", "geom_aabb", "geom_radius", "geom_rbound"]:
+        for n in ["geom_pos", "geom_quat", "geom_aabb", "geom_radius", "geom_rbound", "geom_cyl"]:
             put_d(n, getattr(self, n))
         put_i("hull_vertadr", self.hull_vertadr)
         put_i("hull_vertnum", self.hull_vertnum)

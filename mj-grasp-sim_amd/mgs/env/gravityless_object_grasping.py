@@ -160,29 +160,69 @@ class GravitylessObjectGrasping:
             self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max, specialize="cached")
         return self._wide[ncon_max]
 
-    def rollout(self, plan: "RolloutPlan", max_ncon: int = 40):
-        """engine.rollout with capacity escalation: MuJoCo has no contact cap, the
-        kernel's per-candidate contact arrays do (ncon_max, LDS-resident).  A
-        candidate that exceeds it (stats[:, 2] & FLAG_CAPACITY) stops at that step
-        and is continued from the state entering it with twice the capacity
-        (constraint rows capped at 128) -- the capped and the wider run are
-        identical up to there -- until none overflows or max_ncon is reached (the
-        last stage runs on capped, flagged); its results replace the capped
-        run's.  res['overflow'] counts candidates still capped."""
-        cap = self.ncon_max
-        res = self.engine.rollout(plan, resumable=cap < max_ncon)
-        rec = res.pop("resume", None)
-        ov = np.nonzero(res["stats"][:, 2] & FLAG_CAPACITY)[0]
+    # a batch with more rollouts than the device holds at once runs as this
+    # many time slices (launches): each launch then ends about one slice after
+    # its last candidate started, instead of one whole rollout after it
+    SLICES = 4
+
+    def _escalate(self, plan, res, rec, ov, cap, max_ncon):
+        """continue the over-capacity candidates ov (their records rec[ov]) at
+        twice the capacity, to the end, until none overflows or max_ncon is
+        reached (the last stage runs on capped, flagged); results replace res's"""
         while len(ov) and cap < max_ncon:
             cap = min(2 * cap, max_ncon)
-            sub = self.engine_for(cap).rollout(plan.subset(ov), resumable=cap < max_ncon, resume_from=rec[ov])
+            last = cap >= max_ncon
+            sub = self.engine_for(cap).rollout(plan.subset(ov), resumable=True, resume_from=rec[ov],
+                                               capped_continue=last)
             for k in ("label", "fail_step", "obj_qpos", "stats"):
                 res[k][ov] = sub[k]
-            keep = np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0]
+            keep = np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0] if not last else np.zeros(0, np.int64)
+            rec[ov[keep]] = sub["resume"][keep]
             ov = ov[keep]
-            if "resume" in sub:
-                rec[ov] = sub["resume"][keep]
-        res["overflow"] = len(ov)
+        return int(((res["stats"][:, 2] & FLAG_CAPACITY) != 0).sum()) if len(res["label"]) else 0
+
+    def rollout(self, plan: "RolloutPlan", max_ncon: int = 40, slices: Optional[int] = None):
+        """engine.rollout with capacity escalation and time slices.
+
+        Capacity: MuJoCo has no contact cap, the kernel's per-candidate contact
+        arrays do (ncon_max, LDS-resident).  A candidate that exceeds it
+        (stats[:, 2] & FLAG_CAPACITY) stops at that step and is continued from
+        the state entering it with twice the capacity -- the capped and the
+        wider run are identical up to there -- until none overflows or max_ncon
+        is reached (the last stage runs on capped, flagged); its results
+        replace the capped run's.  res['overflow'] counts candidates capped.
+
+        Slices: when the batch has more rollouts than the device runs at once
+        (the work queue's resident grid), the horizon is cut into `slices`
+        (default SLICES) launches: every unfinished candidate stops at the
+        slice boundary with a resume record (MGS_FLAG_PAUSED) and the next
+        launch continues the survivors, so a launch never waits for a whole
+        rollout that started late.  Records carry the complete state, so the
+        results equal one launch's bit for bit."""
+        cap = self.ncon_max
+        n = len(plan.qpos_init)
+        H = plan.horizon
+        if slices is None:
+            slices = self.SLICES if n and self.engine.rollout_grid(n) < n else 1
+        slices = max(1, min(int(slices), H))
+        bounds = [int(round(H * (j + 1) / slices)) for j in range(slices - 1)] + [0]
+        res = self.engine.rollout(plan, resumable=True, pause_step=bounds[0], capped_continue=cap >= max_ncon)
+        rec = res.pop("resume")
+        live = np.arange(n)
+        for j, b in enumerate(bounds):
+            if j > 0:
+                sub = self.engine.rollout(plan.subset(live), resumable=True, resume_from=rec[live], pause_step=b,
+                                          capped_continue=cap >= max_ncon)
+                for k in ("label", "fail_step", "obj_qpos", "stats"):
+                    res[k][live] = sub[k]
+                rec[live] = sub["resume"]
+            flags = res["stats"][live, 2]
+            ov = live[(flags & FLAG_CAPACITY) != 0] if cap < max_ncon else live[:0]
+            self._escalate(plan, res, rec, ov, cap, max_ncon)
+            live = live[(flags & MGS["MGS_FLAG_PAUSED"]) != 0]
+            if not len(live):
+                break
+        res["overflow"] = int(((res["stats"][:, 2] & FLAG_CAPACITY) != 0).sum())
         return res
 
     # -- host-side bookkeeping (exactly the reference's arithmetic) ------------

@@ -640,6 +640,22 @@ double* oracle_sep_vals(void) { return g_sep_val; }
 int* oracle_sep_pairs(void) { return g_sep_pair; }
 long oracle_sep_count(void) { return g_sep_n; }
 void oracle_sep_enable(int on) { g_sep_log = on; g_sep_n = 0; }
+/* exact cylinder support in the geom frame (MuJoCo's ccd support of
+ * mjGEOM_CYLINDER, engine_collision_convex.c): the rim point along the radial
+ * part of dl, on the cap dl points to; (0, 0, +-h) when dl is along the axis */
+static void cyl_support(double* v, const double* cy, const double* dl) {
+  double rho = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+  if (rho > O_MINVAL) {
+    double s = cy[0] / rho;
+    v[0] = dl[0] * s;
+    v[1] = dl[1] * s;
+  } else {
+    v[0] = 0.0;
+    v[1] = 0.0;
+  }
+  v[2] = dl[2] >= 0.0 ? cy[1] : -cy[1];
+}
+
 static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, double* out) {
   int h = IA(md, geom_hullid)[g];
   int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
@@ -654,6 +670,8 @@ static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, d
     if (s > best) { best = s; bi = i; }
   }
   double t[3], vb[3] = {V[bi], V[num + bi], V[2 * num + bi]};
+  const double* cy = DA(md, geom_cyl) + 2 * g;
+  if (cy[0] > 0.0) cyl_support(vb, cy, dl);
   mulmv3(t, R, vb);
   add3(out, d->geom_xpos + 3 * g, t);
   /* rounded geoms (sphere, capsule): hull (+) ball; dir is a unit vector */
@@ -836,18 +854,35 @@ static int feature(const Mdl* md, const Dat* d, int g, const double* n, const do
   double base = dot3(x, n);
   double r = DA(md, geom_radius)[g];
   if (r > 0.0) base = (sign > 0) ? base + r : base - r;   /* rounded: surface = hull (+) ball */
+  /* exact cylinder: its rim polygons turned about the axis so that vertex 0
+   * of each cap is the true rim extreme along n (the generator through the
+   * surface's extreme); n along the axis keeps the prism (a cap face) */
+  double c0 = 1.0, s0 = 0.0;
+  const double* cy = DA(md, geom_cyl) + 2 * g;
+  if (cy[0] > 0.0) {
+    double rho = sqrt(nl[0] * nl[0] + nl[1] * nl[1]);
+    if (rho > O_MINVAL) {
+      double sg = (sign > 0) ? 1.0 : -1.0;
+      c0 = sg * (nl[0] / rho);
+      s0 = sg * (nl[1] / rho);
+    }
+  }
   double best = (sign > 0) ? -INFINITY : INFINITY;
   for (int i = 0; i < num; i++) {
-    double s = base + ((V[i] * nl[0] + V[num + i] * nl[1]) + V[2 * num + i] * nl[2]);
+    double vx = V[i], vy = V[num + i];
+    if (cy[0] > 0.0) { double tx = c0 * vx - s0 * vy; vy = s0 * vx + c0 * vy; vx = tx; }
+    double s = base + ((vx * nl[0] + vy * nl[1]) + V[2 * num + i] * nl[2]);
     if (sign > 0 ? (s > best) : (s < best)) best = s;
   }
   *ext = best;
   int cnt = 0;
   double lim = (sign > 0) ? best - tol : best + tol;
   for (int i = 0; i < num && cnt < O_MAXF; i++) {
-    double s = base + ((V[i] * nl[0] + V[num + i] * nl[1]) + V[2 * num + i] * nl[2]);
+    double vx = V[i], vy = V[num + i];
+    if (cy[0] > 0.0) { double tx = c0 * vx - s0 * vy; vy = s0 * vx + c0 * vy; vx = tx; }
+    double s = base + ((vx * nl[0] + vy * nl[1]) + V[2 * num + i] * nl[2]);
     if (sign > 0 ? (s >= lim) : (s <= lim)) {
-      double t[3], P[3], vi[3] = {V[i], V[num + i], V[2 * num + i]};
+      double t[3], P[3], vi[3] = {vx, vy, V[2 * num + i]};
       mulmv3(t, R, vi);
       add3(P, x, t);
       out[cnt].x = dot3(P, t1);

@@ -179,23 +179,7 @@ def test_oversized_pile_fails_clearly():
         ClutterTableEnv(grip, objs)
 
 
-def spread_pile(gripper_name, object_ids):
-    """a pile scene of any size with its objects set apart on the table (the
-    parity of the kernels does not need a settled pile)"""
-    import sys
-    sys.path.insert(0, os.path.join(HERE, "golden"))
-    from make_clutter_scene import make_env
-    env = make_env(gripper_name, object_ids)
-    parts = env.split_state(env.get_state())
-    q = parts["qpos"].copy()
-    for i, (n, qs, vs) in enumerate(env._obj_slices()):
-        q[qs] = [0.12 * (i - 1.5), 0.06 * (i % 2), 0.06, 1.0, 0.0, 0.0, 0.0]
-    env.set_state(env.join_state(dict(parts, qpos=q)))
-    return env
-
-
-SPREAD_PILES = [("Robotiq2f85Gripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can"]),
-                ("PandaGripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange"])]
+from mgs.core.shipped import SPREAD_PILES, spread_pile  # noqa: E402  (the shipped pile scenes)
 
 
 @pytest.mark.gpu

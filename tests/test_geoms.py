@@ -1,5 +1,6 @@
-"""Rounded and prism collision geoms (sphere / capsule = hull (+) ball; cylinder
-= 16-sided inscribed prism) in the oracle's narrowphase, pinned by analytic
+"""Rounded and cylinder collision geoms (sphere / capsule = hull (+) ball;
+cylinder = the exact solid: analytic support in MPR, rim polygons turned onto
+the true extreme for the contact features) in the oracle's narrowphase, pinned by analytic
 contact geometry: MuJoCo's sphere-box and capsule-box colliders
 (engine_collision_primitive.c in MuJoCo 3.2.2, not vendored) return the deepest
 point (sphere) and the two segment-end points of a capsule lying on a face, with
@@ -52,12 +53,82 @@ def test_capsule_upright_one_contact():
 
 
 def test_cylinder_standing_on_box_four_contacts():
-    # 16-sided prism cap: the manifold keeps 4 rim points, depth 1 mm
+    # the cap face: 16 rim points on the true circle, the manifold keeps 4, depth 1 mm
     n, p, fr, dist = contacts('<geom type="cylinder" size="0.02 0.03"/>', "0 0 0.049")
     assert n == 4
     assert np.allclose(dist, -0.001, atol=1e-12)
     assert np.allclose(np.hypot(p[:, 0], p[:, 1]), 0.02, atol=1e-12)
     assert np.allclose(p[:, 2], 0.0195, atol=1e-12)
+
+
+@pytest.mark.parametrize("spin", [0.0, 0.3, 0.7])
+def test_cylinder_lying_on_box_two_generator_contacts(spin):
+    # axis along world x, turned about its own axis by `spin` (0.3 / 0.7 rad put
+    # no vertex of an inscribed 16-gon at the bottom: a prism would rest up to
+    # r (1 - cos(pi / 16)) = 0.38 mm higher), 0.4 mm into the floor: the exact
+    # cylinder touches along its bottom generator, contacts at its two ends
+    from scipy.spatial.transform import Rotation
+    r, h, depth = 0.02, 0.03, 0.0004
+    R = Rotation.from_euler("y", np.pi / 2) * Rotation.from_euler("z", spin)
+    x, y, z, w = R.as_quat()
+    n, p, fr, dist = contacts(f'<geom type="cylinder" size="{r} {h}"/>', f"0 0.003 {0.02 + r - depth}",
+                              f"{w} {x} {y} {z}")
+    assert n == 2
+    # MPR's normal (mpr_tolerance 1e-6) carries into the feature heights, as
+    # for the capsule (test_capsule_lying_on_box_two_contacts)
+    assert np.allclose(dist, -depth, atol=1e-7)
+    assert np.allclose(np.abs(fr[:, 2]), 1.0, atol=1e-6)
+    assert np.allclose(sorted(p[:, 0]), [-h, h], atol=1e-7)
+    assert np.allclose(p[:, 1], 0.003, atol=1e-6)
+    assert np.allclose(p[:, 2], 0.02 - depth / 2, atol=1e-7)
+
+
+def test_cylinder_tilted_on_box_rim_contact():
+    # axis tilted 0.4 rad about x and spun 0.2 rad: one rim point is lowest;
+    # exact depth and position (the point midway between it and the face)
+    from scipy.spatial.transform import Rotation
+    r, h, depth = 0.02, 0.03, 0.0005
+    R = Rotation.from_euler("x", 0.4) * Rotation.from_euler("z", 0.2)
+    low = R.apply([0.0, -r, -h])            # rim point on the low side: local (0, -r, -h)
+    # the lowest point of the tilted solid: rim point towards -y of the bottom cap
+    zs = [R.apply([r * np.cos(a), r * np.sin(a), -h])[2] for a in np.linspace(0, 2 * np.pi, 20001)]
+    zlow = min(zs)
+    assert abs(zlow - low[2]) < 1e-12 or zlow <= low[2]
+    c = np.array([0.001, 0.002, 0.02 - zlow - depth])
+    x, y, z, w = R.as_quat()
+    n, p, fr, dist = contacts(f'<geom type="cylinder" size="{r} {h}"/>', " ".join(map(str, c)), f"{w} {x} {y} {z}")
+    assert n == 1
+    assert np.allclose(dist, [-depth], atol=1e-8)
+    assert np.allclose(np.abs(fr[0, :3]), [0, 0, 1], atol=1e-6)
+    lowest = c + R.apply([0.0, -r, -h]) if abs(zlow - low[2]) < 1e-12 else None
+    assert np.allclose(p[0, 2], 0.02 - depth / 2, atol=1e-8)
+    if lowest is not None:
+        assert np.allclose(p[0, :2], lowest[:2], atol=1e-6)
+
+
+def test_cylinder_support_is_exact():
+    # the oracle's MPR support of a cylinder reaches the true surface: a sphere
+    # touching the curved side at 45 deg between two prism vertices collides
+    # (0.2 mm deep) although it is 0.15 mm clear of the inscribed 16-gon prism
+    r, h, rs = 0.02, 0.03, 0.005
+    a = np.pi / 16                          # midway between prism vertices
+    depth = 0.0002
+    dxy = (r + rs - depth) * np.array([np.cos(a), np.sin(a)])
+    xml = f"""
+<mujoco><option gravity="0 0 0" cone="elliptic" integrator="implicitfast"/>
+<worldbody>
+  <body name="cyl" pos="0 0 0"><geom type="cylinder" size="{r} {h}"/></body>
+  <body name="s" pos="{dxy[0]} {dxy[1]} 0.001"><freejoint name="fj"/><geom type="sphere" size="{rs}"/></body>
+</worldbody></mujoco>"""
+    from mgs.core.mjcf import compile_xml
+    from oracle import oracle as O
+    cm = compile_xml(xml)
+    assert np.allclose(cm.geom_cyl, [[r, h], [0, 0]])
+    om = O.OracleModel(cm)
+    n, p, fr, dist, g = om.contacts(cm.qpos0, np.zeros(3), np.array([1.0, 0, 0, 0]))
+    assert n == 1
+    assert np.allclose(dist, [-depth], atol=2e-6)          # MPR, mpr_tolerance 1e-6
+    assert np.allclose(np.abs(fr[0, :2]), [np.cos(a), np.sin(a)], atol=5e-3)   # MPR normal on a curved face
 
 
 def test_rounded_aabb_includes_radius():

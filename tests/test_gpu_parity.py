@@ -537,3 +537,41 @@ def test_row_capacity_overflow_parity(env, candidates, nefc_max):
     rg, ro = e.rollout(plan), om.rollout(plan, nthreads=8)
     _assert_same(rg, ro, f"nefc_max={nefc_max}")
     assert (rg["stats"][:, 2] & 2).any()
+
+
+@pytest.mark.parametrize("horizon,n,slices", [("h200", 256, [2, 3, 7]), ("ref8000", 4, [5])])
+def test_time_slices_equal_one_launch(env, candidates, oracle_model, horizon, n, slices):
+    """GravitylessObjectGrasping.rollout in time slices (mgs_schedule.pause_step:
+    every unfinished candidate stops at the slice boundary with its resume
+    record, MGS_FLAG_PAUSED, and the next launch continues the survivors) gives
+    every output of one launch bit for bit, and equals the oracle; a pause
+    right at a phase boundary and inside the lift's check cadence included
+    (h200: phases end at 76 / 152 / 164 / 176)"""
+    from conftest import plan_for
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(oracle_model.collision_free(q, mp, mq, nthreads=8))[0][:n]
+    plan = plan_for(env, poses[idx], J[idx], horizon)
+    one = env.rollout(plan, slices=1)
+    assert one["overflow"] == 0
+    for k in slices:
+        r = env.rollout(plan, slices=k)
+        _assert_same(r, one, f"{k} slices")
+    # a boundary on a phase end (76) and one on a lift check (76 + 25)
+    for b in (76, 101):
+        e = env.engine
+        a = e.rollout(plan, resumable=True, pause_step=b)
+        live = np.nonzero(a["stats"][:, 2] & abi_flag("MGS_FLAG_PAUSED"))[0]
+        assert np.all(a["fail_step"][live] == -4)
+        if len(live):
+            sub = e.rollout(plan.subset(live), resumable=True, resume_from=a["resume"][live])
+            for k in ("label", "fail_step", "obj_qpos", "stats"):
+                a[k][live] = sub[k]
+        _assert_same(a, one, f"pause at {b}")
+    ro = oracle_model.rollout(plan, nthreads=8)
+    _assert_same(one, ro, "oracle")
+
+
+def abi_flag(name):
+    from mgs.core.abi import MGS
+    return MGS[name]
