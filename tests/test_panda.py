@@ -106,3 +106,38 @@ def test_panda_gpu_parity(penv, pcand, pom):
     rg, ro = penv.engine.rollout(plan), pom.rollout(plan, nthreads=8)
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(rg[k], ro[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("obj_id", ["005_tomato_soup_can", "010_potted_meat_can", "017_orange", "061_foam_brick"])
+def test_panda_ycb_set_gpu_parity(obj_id):
+    """C3 covers the YCB set: every shipped YCB-format object besides the
+    cracker box (test_panda_gpu_parity), mask and h200 rollouts bit-exact
+    against the oracle through the C-ABI (with the env's capacity escalation)"""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+    from conftest import plan_for
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    from mgs.gripper.selector import get_gripper
+    from mgs.obj.selector import get_object
+    from mgs.sampler.antipodal import panda_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    from oracle import oracle as O
+    env = GravitylessObjectGrasping(get_gripper({"name": "PandaGripper"}), get_object(obj_id))
+    H, J, _ = panda_candidates(env.obj, 512, seed=1)
+    poses, J = SE3Pose.from_mat(H), np.asarray(J, np.float64)
+    q, mp, mq, _ = env.initial_state(poses, J)
+    om = O.OracleModel(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+    fg = env.engine.collision_free(q, mp, mq)
+    assert np.array_equal(fg, om.collision_free(q, mp, mq, nthreads=8))
+    idx = np.nonzero(fg)[0][:96]
+    assert len(idx) >= 8
+    plan = plan_for(env, poses[idx], J[idx])
+    rg = env.rollout(plan, max_ncon=env.ncon_max)
+    ro = om.rollout(plan, nthreads=8)
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(rg[k], ro[k]), k
