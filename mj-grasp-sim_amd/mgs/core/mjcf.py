@@ -125,6 +125,57 @@ def _normq(q):
     return np.array([1.0, 0, 0, 0]) if n < _MINVAL else q / n
 
 
+def eig3(mat):
+    """MuJoCo's mju_eig3 (engine_util_solve.c): eigen-decomposition of a
+    symmetric 3x3 matrix by Jacobi rotations accumulated in a quaternion
+    (at most 500 sweeps of the largest off-diagonal element, eps 1e-12), then
+    the eigenvalues sorted in decreasing order by quarter-turn rotations of the
+    quaternion.  Returns (eigenvalues, quaternion wxyz); the columns of
+    quat2mat(quaternion) are the eigenvectors.  MuJoCo's mesh compiler takes
+    the mesh frame (mesh_quat) from it, so principal axes of degenerate
+    inertias (axisymmetric meshes) are chosen as MuJoCo chooses them rather
+    than as a LAPACK solver would."""
+    eps = 1e-12
+    A = np.asarray(mat, np.float64).reshape(3, 3)
+    quat = np.array([1.0, 0.0, 0.0, 0.0])
+    ev = np.zeros(3)
+    for _ in range(500):
+        V = quat2mat(quat)
+        D = V.T @ A @ V
+        ev = np.array([D[0, 0], D[1, 1], D[2, 2]])
+        d1, d2, d5 = D.flat[1], D.flat[2], D.flat[5]
+        if abs(d1) > abs(d2) and abs(d1) > abs(d5):
+            rk, ck, rotk = 0, 1, 2
+        elif abs(d2) > abs(d5):
+            rk, ck, rotk = 0, 2, 1
+        else:
+            rk, ck, rotk = 1, 2, 0
+        off = D.flat[3 * rk + ck]
+        if abs(off) < eps:
+            break
+        tau = (D.flat[4 * ck] - D.flat[4 * rk]) / (2 * off)
+        t = 1.0 / (tau + np.sqrt(1 + tau * tau)) if tau >= 0 else -1.0 / (-tau + np.sqrt(1 + tau * tau))
+        c = 1.0 / np.sqrt(1 + t * t)
+        if c > 1.0 - eps:
+            break
+        r = np.zeros(4)
+        r[rotk + 1] = -np.sqrt(0.5 - 0.5 * c) if tau >= 0 else np.sqrt(0.5 - 0.5 * c)
+        if rotk == 1:
+            r[rotk + 1] = -r[rotk + 1]
+        r[0] = np.sqrt(1.0 - r[rotk + 1] * r[rotk + 1])
+        r = _normq(r)
+        quat = _normq(quat_mul(quat, r))
+    for j in range(3):
+        j1 = j % 2
+        if ev[j1] < ev[j1 + 1]:
+            ev[j1], ev[j1 + 1] = ev[j1 + 1], ev[j1]
+            r = np.zeros(4)
+            r[0] = 0.707106781186548
+            r[(j1 + 2) % 3 + 1] = r[0]
+            quat = _normq(quat_mul(quat, r))
+    return ev, quat
+
+
 # ----------------------------------------------------------------------------
 # meshes
 def load_mesh_bytes(data: bytes, fname: str):
@@ -473,21 +524,19 @@ class Compiler:
         y, z (mesh_pos, mesh_quat) -- and its vertices are stored as float32
         (mesh_vert).  Returns (mesh_pos, mesh_quat, float32-rounded hull
         vertices in that frame as float64).  The principal axes come from
-        numpy's symmetric eigensolver (MuJoCo: mju_eig3), so roundings agree
-        with MuJoCo's only as far as the two frames do."""
+        MuJoCo's own eigensolver restated (eig3: decreasing moments, MuJoCo's
+        choice of axes for equal moments)."""
         m = self.meshes[name]
         if m.get("frame") is None:
             vol, com, I = self._mesh_massprops(name)
             if vol > 0 and np.any(I):
-                _, V = np.linalg.eigh(I)
-                V = V[:, ::-1].copy()          # decreasing principal moments
-                if np.linalg.det(V) < 0:
-                    V[:, 2] = -V[:, 2]
+                _, q = eig3(I)
             else:
-                V = np.eye(3)
+                q = np.array([1.0, 0.0, 0.0, 0.0])
+            V = quat2mat(q)
             hull = self._mesh_hull(name)
             local = ((hull - com) @ V).astype(np.float32).astype(np.float64)
-            m["frame"] = (np.asarray(com, np.float64), _normq(mat2quat(V)), local)
+            m["frame"] = (np.asarray(com, np.float64), q, local)
         return m["frame"]
 
     def _mesh_massprops(self, name):

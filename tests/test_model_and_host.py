@@ -117,3 +117,26 @@ def test_se3_pose_against_reference_golden():
     assert np.array_equal(inv.pos, g["inv_pos"]) and np.array_equal(inv.quat, g["inv_quat"])
     assert c.pos.dtype == g["self_pos"].dtype and np.array_equal(c.pos, g["self_pos"])
     assert c.quat.dtype == g["self_quat"].dtype and np.array_equal(c.quat, g["self_quat"])
+
+
+def test_eig3_mesh_frame():
+    """mgs.core.mjcf.eig3 (MuJoCo's mju_eig3 restated, the mesh compiler's
+    principal axes): eigenvalues in decreasing order, the quaternion's matrix
+    diagonalises the tensor to MuJoCo's own stopping rule (cosine within 1e-12
+    of 1, i.e. off-diagonals ~1e-6 relative), and a degenerate (axisymmetric)
+    tensor gets a fixed frame: the identity for an already diagonal one"""
+    from mgs.core.mjcf import eig3, quat2mat
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        A = rng.standard_normal((3, 3))
+        A = A @ A.T
+        ev, q = eig3(A)
+        V = quat2mat(q)
+        D = V.T @ A @ V
+        assert np.abs(D - np.diag(np.diag(D))).max() < 1e-5 * np.abs(A).max()
+        assert np.allclose(ev, np.sort(np.linalg.eigvalsh(A))[::-1], atol=1e-9 * np.abs(A).max())
+    ev, q = eig3(np.diag([3.0, 2.0, 2.0]))
+    assert np.array_equal(q, [1.0, 0.0, 0.0, 0.0]) and np.array_equal(ev, [3.0, 2.0, 2.0])
+    ev, q = eig3(np.diag([1.0, 2.0, 2.0]))        # sorted by quarter turns
+    assert np.allclose(ev, [2.0, 2.0, 1.0])
+    assert np.allclose(quat2mat(q).T @ np.diag([1.0, 2.0, 2.0]) @ quat2mat(q), np.diag(ev), atol=1e-12)
