@@ -248,6 +248,8 @@ def main():
                     help="also time the drop-in API on the batch repeated this many times in one call (0 = skip)")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
+    ap.add_argument("--e2e-slices", type=int, default=None,
+                    help="time slices of the env API's rollout launches (default: the env's SLICES rule)")
     ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
@@ -508,6 +510,8 @@ def main():
     fail = d_fail.cpu().numpy()
     stats = d_stats.cpu().numpy()
     e2e = None
+    if args.e2e_slices is not None:
+        env.SLICES = args.e2e_slices
     if args.e2e_steps > 0:
         m2, l2, t2 = e2e_api(env, poses, J, h, args.e2e_steps)
         large = None
@@ -522,6 +526,7 @@ def main():
                      "labels_identical_to_device_run": bool(np.array_equal(mk, np.tile(free, k)) and
                                                             np.array_equal(lk, np.tile(labels, k)))}
         e2e = {"candidates_per_s": N / t2, "ms_per_batch": t2 * 1e3, "batches": args.e2e_steps,
+               "rollout_slices": getattr(env, "SLICES", 1),
                "one_call_over_repeated_batch": large,
                "labels_identical_to_device_run": bool(np.array_equal(m2, free) and np.array_equal(l2, labels)),
                "what": "env.grasp_collision_mask + grasp_stability_evaluation_from_joints on host arrays "

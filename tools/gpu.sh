@@ -10,6 +10,7 @@
 #   bench     the driver's command, `bench.py --gpus 1 --steps 20 --warmup 5`
 #             (full line: e2e API, CPU baseline); first process of the call
 #   rep       the driver's command without CPU baseline / e2e, 3 processes
+#   api       the drop-in env API per call, one rollout launch vs 4 time slices
 #   n2        2-rank launcher rehearsal on one GPU (gloo) with the shard check
 #   trace     rocprofv3 --kernel-trace --stats of the driver's command
 #   pmc       PMC passes (FETCH / WRITE / SQ / VALU) on a one-pipeline bench
@@ -59,6 +60,13 @@ for step in "$@"; do
       for r in 1 2 3; do
         timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 0 > $O/rep$r.json 2> $O/rep$r.err || fail rep $O/rep$r.err
         summ $O/rep$r.json
+      done ;;
+    api)
+      # the drop-in env API per 8192-candidate call: one rollout launch vs time slices
+      for sl in 1 4; do
+        timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 4 --e2e-slices $sl > $O/api$sl.json \
+          2> $O/api$sl.err || fail api $O/api$sl.err
+        summ $O/api$sl.json
       done ;;
     n2)
       timeout -k 10 300 python3 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-budget 0 --e2e-steps 0 \
