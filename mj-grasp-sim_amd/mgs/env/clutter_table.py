@@ -33,7 +33,7 @@ import numpy as np
 
 from mgs.core.abi import MGS
 from mgs.core.mjcf import CompiledModel, compile_xml
-from mgs.env.gravityless_object_grasping import RolloutPlan, apply_enough_stable
+from mgs.env.gravityless_object_grasping import RolloutPlan, apply_enough_stable, sliced_rollout
 from mgs.util.geo.transforms import SE3Pose
 
 # stats[:, 2] flags that a wider re-run resolves (contacts / rows over capacity);
@@ -363,20 +363,15 @@ class ClutterTableEnv:
                            phase_target=np.ascontiguousarray(np.stack([mp, target_lift], 1)),
                            obj_qposadr=-1, check_offset=[0, 1])
 
-    def rollout(self, plan: RolloutPlan, env_state, max_ncon: int = 128):
-        """engine rollout with contact-capacity escalation (see
-        GravitylessObjectGrasping.rollout)."""
-        res = self.engine_for_state(env_state).rollout(plan)
-        cap = self.ncon_max
-        ov = np.nonzero(res["stats"][:, 2] & FLAG_CAPACITY)[0]
-        while len(ov) and cap < max_ncon:
-            cap = min(2 * cap, max_ncon)
-            sub = self.engine_for_state(env_state, ncon_max=cap).rollout(plan.subset(ov))
-            for k in ("label", "fail_step", "obj_qpos", "stats"):
-                res[k][ov] = sub[k]
-            ov = ov[np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0]]
-        res["overflow"] = len(ov)
-        return res
+    SLICES = 4
+
+    def rollout(self, plan: RolloutPlan, env_state, max_ncon: int = 128, slices: Optional[int] = None):
+        """engine rollout with contact-capacity escalation (continued from the
+        overflowing step) and time slices, as GravitylessObjectGrasping.rollout
+        (sliced_rollout)."""
+        return sliced_rollout(plan, self.engine_for_state(env_state),
+                              lambda c: self.engine_for_state(env_state, ncon_max=c), self.ncon_max, max_ncon,
+                              self.SLICES if slices is None else slices, auto=slices is None)
 
     def grasp_stable_mask(self, poses: SE3Pose, joints: np.ndarray, env_state, nstep_lift: int = 3000,
                           lift_dist: float = 0.3, enough_stable=None, *, close_steps: Optional[int] = None,

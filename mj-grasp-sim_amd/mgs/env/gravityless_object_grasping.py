@@ -165,65 +165,11 @@ class GravitylessObjectGrasping:
     # its last candidate started, instead of one whole rollout after it
     SLICES = 4
 
-    def _escalate(self, plan, res, rec, ov, cap, max_ncon):
-        """continue the over-capacity candidates ov (their records rec[ov]) at
-        twice the capacity, to the end, until none overflows or max_ncon is
-        reached (the last stage runs on capped, flagged); results replace res's"""
-        while len(ov) and cap < max_ncon:
-            cap = min(2 * cap, max_ncon)
-            last = cap >= max_ncon
-            sub = self.engine_for(cap).rollout(plan.subset(ov), resumable=True, resume_from=rec[ov],
-                                               capped_continue=last)
-            for k in ("label", "fail_step", "obj_qpos", "stats"):
-                res[k][ov] = sub[k]
-            keep = np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0] if not last else np.zeros(0, np.int64)
-            rec[ov[keep]] = sub["resume"][keep]
-            ov = ov[keep]
-        return int(((res["stats"][:, 2] & FLAG_CAPACITY) != 0).sum()) if len(res["label"]) else 0
-
     def rollout(self, plan: "RolloutPlan", max_ncon: int = 40, slices: Optional[int] = None):
-        """engine.rollout with capacity escalation and time slices.
-
-        Capacity: MuJoCo has no contact cap, the kernel's per-candidate contact
-        arrays do (ncon_max, LDS-resident).  A candidate that exceeds it
-        (stats[:, 2] & FLAG_CAPACITY) stops at that step and is continued from
-        the state entering it with twice the capacity -- the capped and the
-        wider run are identical up to there -- until none overflows or max_ncon
-        is reached (the last stage runs on capped, flagged); its results
-        replace the capped run's.  res['overflow'] counts candidates capped.
-
-        Slices: when the batch has more rollouts than the device runs at once
-        (the work queue's resident grid), the horizon is cut into `slices`
-        (default SLICES) launches: every unfinished candidate stops at the
-        slice boundary with a resume record (MGS_FLAG_PAUSED) and the next
-        launch continues the survivors, so a launch never waits for a whole
-        rollout that started late.  Records carry the complete state, so the
-        results equal one launch's bit for bit."""
-        cap = self.ncon_max
-        n = len(plan.qpos_init)
-        H = plan.horizon
-        if slices is None:
-            slices = self.SLICES if n and self.engine.rollout_grid(n) < n else 1
-        slices = max(1, min(int(slices), H))
-        bounds = [int(round(H * (j + 1) / slices)) for j in range(slices - 1)] + [0]
-        res = self.engine.rollout(plan, resumable=True, pause_step=bounds[0], capped_continue=cap >= max_ncon)
-        rec = res.pop("resume")
-        live = np.arange(n)
-        for j, b in enumerate(bounds):
-            if j > 0:
-                sub = self.engine.rollout(plan.subset(live), resumable=True, resume_from=rec[live], pause_step=b,
-                                          capped_continue=cap >= max_ncon)
-                for k in ("label", "fail_step", "obj_qpos", "stats"):
-                    res[k][live] = sub[k]
-                rec[live] = sub["resume"]
-            flags = res["stats"][live, 2]
-            ov = live[(flags & FLAG_CAPACITY) != 0] if cap < max_ncon else live[:0]
-            self._escalate(plan, res, rec, ov, cap, max_ncon)
-            live = live[(flags & MGS["MGS_FLAG_PAUSED"]) != 0]
-            if not len(live):
-                break
-        res["overflow"] = int(((res["stats"][:, 2] & FLAG_CAPACITY) != 0).sum())
-        return res
+        """engine.rollout with capacity escalation and time slices
+        (sliced_rollout below)."""
+        return sliced_rollout(plan, self.engine, self.engine_for, self.ncon_max, max_ncon,
+                              self.SLICES if slices is None else slices, auto=slices is None)
 
     # -- host-side bookkeeping (exactly the reference's arithmetic) ------------
     def _check_inputs(self, poses, joints, check_width=True):
@@ -344,3 +290,59 @@ def apply_enough_stable(labels: np.ndarray, enough_stable) -> np.ndarray:
     cum = np.cumsum(labels)
     labels[(cum > enough_stable)] = False
     return labels
+
+
+def sliced_rollout(plan: "RolloutPlan", engine, engine_for, cap: int, max_ncon: int, slices: int,
+                   auto: bool = True):
+    """A batch's rollouts on `engine` (capacity `cap` contacts) with capacity
+    escalation and time slices; results equal one launch at unlimited capacity.
+
+    Capacity: MuJoCo has no contact cap, the kernel's per-candidate contact
+    arrays do (ncon_max, LDS-resident).  A candidate that exceeds it
+    (stats[:, 2] & FLAG_CAPACITY) stops at that step and is continued from the
+    state entering it on engine_for(2 cap) -- the capped and the wider run are
+    identical up to there -- until none overflows or max_ncon is reached (the
+    last stage runs on capped, flagged); its results replace the capped run's.
+    res['overflow'] counts candidates capped.
+
+    Slices: when the batch has more rollouts than the device runs at once
+    (the work queue's resident grid; auto) or `slices` is given, the horizon
+    is cut into `slices` launches: every unfinished candidate stops at the
+    slice boundary with a resume record (MGS_FLAG_PAUSED) and the next launch
+    continues the survivors, so a launch never waits for a whole rollout that
+    started late.  Records carry the complete state, so the results equal one
+    launch's bit for bit."""
+    n = len(plan.qpos_init)
+    H = plan.horizon
+    if auto:
+        slices = slices if n and engine.rollout_grid(n) < n else 1
+    slices = max(1, min(int(slices), max(H, 1)))
+    bounds = [int(round(H * (j + 1) / slices)) for j in range(slices - 1)] + [0]
+    last_cap = cap >= max_ncon
+    res = engine.rollout(plan, resumable=True, pause_step=bounds[0], capped_continue=last_cap)
+    rec = res.pop("resume")
+    live = np.arange(n)
+    for j, b in enumerate(bounds):
+        if j > 0:
+            sub = engine.rollout(plan.subset(live), resumable=True, resume_from=rec[live], pause_step=b,
+                                 capped_continue=last_cap)
+            for k in ("label", "fail_step", "obj_qpos", "stats"):
+                res[k][live] = sub[k]
+            rec[live] = sub["resume"]
+        flags = res["stats"][live, 2]
+        ov = live[(flags & FLAG_CAPACITY) != 0] if not last_cap else live[:0]
+        c = cap
+        while len(ov) and c < max_ncon:
+            c = min(2 * c, max_ncon)
+            last = c >= max_ncon
+            sub = engine_for(c).rollout(plan.subset(ov), resumable=True, resume_from=rec[ov], capped_continue=last)
+            for k in ("label", "fail_step", "obj_qpos", "stats"):
+                res[k][ov] = sub[k]
+            keep = np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0] if not last else np.zeros(0, np.int64)
+            rec[ov[keep]] = sub["resume"][keep]
+            ov = ov[keep]
+        live = live[(flags & MGS["MGS_FLAG_PAUSED"]) != 0]
+        if not len(live):
+            break
+    res["overflow"] = int(((res["stats"][:, 2] & FLAG_CAPACITY) != 0).sum()) if n else 0
+    return res
