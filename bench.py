@@ -98,11 +98,12 @@ def cpu_baseline(env, poses, joints, h, budget_s, threads):
     dt_pilot = max(time.perf_counter() - t0, 1e-6)
     want = n_pilot * budget_s / dt_pilot
     n = int(min(len(poses), max(n_pilot, want)))
-    # a block shorter than the budget is timed over whole repeated passes, so
-    # the sample is ~budget_s of CPU work either way
-    reps = max(1, int(want / len(poses))) if n == len(poses) else 1
+    reps = 0
     t0 = time.perf_counter()
-    for r in range(reps):
+    # whole passes until the budget is spent (at least one): a block shorter
+    # than the budget is timed over repeated passes
+    while reps == 0 or (n == len(poses) and time.perf_counter() - t0 < budget_s):
+        reps += 1
         free = om.collision_free(q[:n], mp[:n], mq[:n], nthreads=threads)
         idx = np.nonzero(free)[0]
         labels = np.zeros(n, bool)

@@ -160,9 +160,9 @@ class GravitylessObjectGrasping:
             self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max, specialize="cached")
         return self._wide[ncon_max]
 
-    # a batch with more rollouts than the device holds at once runs as this
-    # many time slices (launches): each launch then ends about one slice after
-    # its last candidate started, instead of one whole rollout after it
+    # a batch with more than four grids' worth of rollouts runs as this many
+    # time slices (launches): each launch then ends about one slice after its
+    # last candidate started, instead of one whole rollout after it
     SLICES = 4
 
     def rollout(self, plan: "RolloutPlan", max_ncon: int = 40, slices: Optional[int] = None):
@@ -305,8 +305,8 @@ def sliced_rollout(plan: "RolloutPlan", engine, engine_for, cap: int, max_ncon: 
     last stage runs on capped, flagged); its results replace the capped run's.
     res['overflow'] counts candidates capped.
 
-    Slices: when the batch has more rollouts than the device runs at once
-    (the work queue's resident grid; auto) or `slices` is given, the horizon
+    Slices: when the batch has more than four times the rollouts the device
+    runs at once (the work queue's resident grid; auto) or `slices` is given, the horizon
     is cut into `slices` launches: every unfinished candidate stops at the
     slice boundary with a resume record (MGS_FLAG_PAUSED) and the next launch
     continues the survivors, so a launch never waits for a whole rollout that
@@ -315,7 +315,10 @@ def sliced_rollout(plan: "RolloutPlan", engine, engine_for, cap: int, max_ncon: 
     n = len(plan.qpos_init)
     H = plan.horizon
     if auto:
-        slices = slices if n and engine.rollout_grid(n) < n else 1
+        # measured (profiles/r04b_api.txt): a batch a little over the grid
+        # (1173 rollouts on 1024 slots) loses more to the extra round trips
+        # than its tail costs; one of many grids' worth gains
+        slices = slices if n and 4 * engine.rollout_grid(n) < n else 1
     slices = max(1, min(int(slices), max(H, 1)))
     bounds = [int(round(H * (j + 1) / slices)) for j in range(slices - 1)] + [0]
     last_cap = cap >= max_ncon
