@@ -11,6 +11,7 @@
 #             (full line: e2e API, CPU baseline); first process of the call
 #   rep       the driver's command without CPU baseline / e2e, 3 processes
 #   api       the drop-in env API per call, one rollout launch vs 4 time slices
+#   streams   the driver's command with 2 / 6 / 8 pipelines in flight
 #   n2        2-rank launcher rehearsal on one GPU (gloo) with the shard check
 #   trace     rocprofv3 --kernel-trace --stats of the driver's command
 #   pmc       PMC passes (FETCH / WRITE / SQ / VALU) on a one-pipeline bench
@@ -67,6 +68,13 @@ for step in "$@"; do
         timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 4 --e2e-slices $sl > $O/api$sl.json \
           2> $O/api$sl.err || fail api $O/api$sl.err
         summ $O/api$sl.json
+      done ;;
+    streams)
+      # pipelines in flight (bench --streams): 2, 6, 8 against the default 4
+      for k in 2 6 8; do
+        timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 0 --streams $k > $O/streams$k.json \
+          2> $O/streams$k.err || fail streams $O/streams$k.err
+        summ $O/streams$k.json
       done ;;
     n2)
       timeout -k 10 300 python3 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-budget 0 --e2e-steps 0 \

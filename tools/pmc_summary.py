@@ -30,13 +30,16 @@ def rows(path, kernels=("mgs_special_rollout", "mgs_rollout_kernel")):
 
 
 def main(d, tag="r03"):
-    shutil.copy(os.path.join(d, "trace", "bench_kernel_stats.csv"), os.path.join(PROF, f"{tag}_rocprof_kernel_stats.csv"))
+    tr = os.path.join(d, "trace", "bench_kernel_stats.csv")
+    if os.path.isfile(tr):
+        shutil.copy(tr, os.path.join(PROF, f"{tag}_rocprof_kernel_stats.csv"))
     out = {"source": "rocprofv3 --kernel-trace --pmc <counters> (separate passes) on `python3 bench.py --streams 1 "
-                     "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate` (tools/prof_{tag}.sh); "
+                     "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate --fused 0` (tools/gpu.sh pmc, "
+                     f"{tag}); "
                      "per rollout dispatch",
            "kernel": "mgs_special_rollout (code object specialised to the headline model)"}
     sums = {}
-    for name in ("fetch", "write", "sq", "valu"):
+    for name in ("fetch", "write", "sq", "valu", "lane"):
         p = os.path.join(d, f"pmc_{name}", "pmc_counter_collection.csv")
         if not os.path.isfile(p):
             continue
@@ -46,8 +49,11 @@ def main(d, tag="r03"):
             w.writeheader()
             w.writerows(rr)
         ndisp = len({r["Dispatch_Id"] for r in rr}) or 1
+        part = {}
         for r in rr:
-            sums[r["Counter_Name"]] = sums.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) / ndisp
+            part[r["Counter_Name"]] = part.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) / ndisp
+        for k, v in part.items():       # a counter repeated in a later pass: the first pass's value
+            sums.setdefault(k, v)
     with open(os.path.join(d, "pmc_fetch.json")) as f:
         steps = json.loads(f.read().strip().splitlines()[-1])["detail"]["executed_candidate_steps"]
     hbm = (2.0 * sums["FETCH_SIZE"] + sums["WRITE_SIZE"]) * 1024.0
@@ -56,6 +62,11 @@ def main(d, tag="r03"):
                correction="FETCH_SIZE x 2 (gfx950 half-count, MI355X_MICROARCH.md), WRITE_SIZE as reported; both KiB",
                executed_candidate_steps=steps, hbm_bytes_per_candidate_step=hbm / steps,
                sq={k: v for k, v in sums.items() if k.startswith("SQ_")})
+    if "SQ_THREAD_CYCLES_VALU" in sums and sums.get("SQ_ACTIVE_INST_VALU"):
+        # rocprof-compute's "VALU active threads": lanes doing work per VALU
+        # instruction issued (of 64)
+        out["valu_active_threads"] = sums["SQ_THREAD_CYCLES_VALU"] / sums["SQ_ACTIVE_INST_VALU"]
+        out["valu_lane_utilisation"] = out["valu_active_threads"] / 64.0
     with open(os.path.join(PROF, "pmc_rollout.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
