@@ -250,7 +250,13 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
     ap.add_argument("--e2e-slices", type=int, default=None,
-                    help="time slices of the env API's rollout launches (default: the env's SLICES rule)")
+                    help="time slices by relaunch of the env API's rollout calls (default: the env's SLICES)")
+    ap.add_argument("--e2e-yield", type=int, default=None,
+                    help="in-launch rotation of the env API's rollout launches, steps per slice (default: the "
+                         "env's YIELD_EVERY; 0 = off)")
+    ap.add_argument("--yield-every", type=int, default=0,
+                    help="in-launch rotation (mgs_schedule.yield_every) of the timed pipelines' launches, steps "
+                         "per slice (0 = off; needs the resume records of --esc-resume 1)")
     ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
@@ -333,6 +339,7 @@ def main():
                             close_steps=h["close_steps"], lift_check_every=h["lift_check_every"])
     sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
                                   check_offset=getattr(plan, "check_offset", None))
+    sched.yield_every = int(args.yield_every)
     horizon = plan.horizon
     eng = env.engine
     if args.queue is not None:
@@ -513,6 +520,8 @@ def main():
     e2e = None
     if args.e2e_slices is not None:
         env.SLICES = args.e2e_slices
+    if args.e2e_yield is not None:
+        env.YIELD_EVERY = args.e2e_yield
     if args.e2e_steps > 0:
         m2, l2, t2 = e2e_api(env, poses, J, h, args.e2e_steps)
         large = None
@@ -528,6 +537,7 @@ def main():
                                                             np.array_equal(lk, np.tile(labels, k)))}
         e2e = {"candidates_per_s": N / t2, "ms_per_batch": t2 * 1e3, "batches": args.e2e_steps,
                "rollout_slices": getattr(env, "SLICES", 1),
+               "rollout_yield_every": getattr(env, "YIELD_EVERY", 0),
                "one_call_over_repeated_batch": large,
                "labels_identical_to_device_run": bool(np.array_equal(m2, free) and np.array_equal(l2, labels)),
                "what": "env.grasp_collision_mask + grasp_stability_evaluation_from_joints on host arrays "
@@ -578,7 +588,8 @@ def main():
         "config": {"workload": f"Robotiq2F85 x YCB 003_cracker_box, {N} candidates/GPU, collision mask + "
                                f"{args.horizon} close-lift-shake rollout ({horizon} steps, dt 1 ms)",
                    "candidates_per_gpu": N, "horizon_steps": horizon, "solver": env.model.options.get("solver"),
-                   "parallelism": f"batch split x{world}", "streams": len(pipes)},
+                   "parallelism": f"batch split x{world}", "streams": len(pipes),
+                   "yield_every": int(args.yield_every)},
         "detail": {"collision_free": int(free.sum()), "stable": int(labels.sum()),
                    "rollouts_per_s": float(free.sum()) * world * args.steps / dt,
                    "host_enqueue_s": t_enq,

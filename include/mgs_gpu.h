@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 18
+#define MGS_ABI_VERSION 19
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -271,6 +271,14 @@ typedef struct mgs_schedule {
   int32_t capped_continue; /* 1: with resume records, a candidate over the contact / row capacity
                             runs on capped and flagged instead of stopping (the last stage of an
                             escalation); 0 = stop there (fail_step -3) */
+  int32_t yield_every;   /* > 0 (with resume records, on a work-queue launch): in-launch rotation
+                            (ABI 19).  Every yield_every steps a candidate checks whether another
+                            one waits for a slot (not started yet, or yielded); if so it writes
+                            its resume record, joins the launch's ring of yielded candidates and
+                            its workgroup takes the waiting one.  A launch with more rollouts
+                            than resident workgroups then runs them round robin and ends about
+                            one slice after the last one finishes; outputs are those of one
+                            uninterrupted run (the record is the complete state).  0 = off */
 } mgs_schedule;
 
 /* per-candidate rollout outputs */
@@ -286,8 +294,8 @@ typedef struct mgs_rollout_out {
                               qacc_warmstart, time) and the schedule position / partial stats, from
                               which mgs_rollout_resume continues it with more capacity */
 } mgs_rollout_out;
-#define MGS_RESUME_EXTRA 9         /* time, phase, step in phase, global step, max ncon, max nefc,
-                                      sum ncon, sum nefc, solver iterations */
+#define MGS_RESUME_EXTRA 10        /* time, phase, step in phase, global step, max ncon, max nefc,
+                                      sum ncon, sum nefc, solver iterations, flags */
 
 typedef struct mgs_model mgs_model;
 typedef struct mgs_batch mgs_batch;

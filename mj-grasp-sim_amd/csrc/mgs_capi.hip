@@ -185,9 +185,12 @@ struct mgs_batch {
   double* d_G;      // MGS_G_GLOBAL: per-candidate constraint rows (HBM)
   size_t g_elems;
   double* d_resume; // resume records (n * (nq + 2 nv + MGS_RESUME_EXTRA)), allocated on first use
-  uint32_t* d_queue;                // work-queue counter pairs (next index, exits), one per launch in a
-  int qslot;                        // ring (launches in flight on other streams keep their own pair);
-                                    // each launch's last workgroup returns its pair to zero
+  uint32_t* d_queue;                // work-queue headers (MGS_QHDR words: next index, exits, rotation
+  int qslot;                        // ring head / tail, ring address), one per launch in a ring of
+                                    // MGS_QUEUE_RING (launches in flight on other streams keep their
+                                    // own); each launch's last workgroup returns its counters to zero
+  uint32_t* d_rings;                // rotation rings (ABI 19), MGS_QRING_F(cap) words per header,
+                                    // allocated on the first launch with yield_every > 0
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
@@ -265,8 +268,8 @@ int mgs_batch_open(mgs_model* model, int capacity, mgs_batch** out) {
             hipMalloc(&b->d_label, n) == hipSuccess && hipMalloc(&b->d_free, n) == hipSuccess &&
             hipMalloc(&b->d_fail, sizeof(int32_t) * n) == hipSuccess &&
             hipMalloc(&b->d_stats, sizeof(int32_t) * n * MGS_NSTATS) == hipSuccess &&
-            hipMalloc(&b->d_queue, 2 * sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
-            hipMemset(b->d_queue, 0, 2 * sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
+            hipMalloc(&b->d_queue, MGS_QHDR * sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
+            hipMemset(b->d_queue, 0, MGS_QHDR * sizeof(uint32_t) * MGS_QUEUE_RING) == hipSuccess &&
             // the counters must be zero before any stream's launch reads them
             // (hipMemset may still be in flight on the null stream otherwise)
             hipDeviceSynchronize() == hipSuccess;
@@ -289,6 +292,7 @@ void mgs_batch_close(mgs_batch* b) {
   if (b->d_G) hipFree(b->d_G);
   if (b->d_resume) hipFree(b->d_resume);
   if (b->d_queue) hipFree(b->d_queue);
+  if (b->d_rings) hipFree(b->d_rings);
   if (b->e0) hipEventDestroy(b->e0);
   if (b->e1) hipEventDestroy(b->e1);
   if (b->e2) hipEventDestroy(b->e2);
@@ -406,6 +410,24 @@ int mgs_collision_free(mgs_batch* b, int n, const double* qpos_init, const doubl
   return MGS_OK;
 }
 
+// the rotation rings of every queue header (zeroed; each header's words 4-5
+// get its ring's address).  Synchronous, once per batch.
+static int alloc_rings(mgs_batch* b) {
+  const size_t per = MGS_QRING_F(b->cap);
+  HIPCHK(hipDeviceSynchronize());   // no launch holds a header's cache line while words 4-5 are written
+  if (hipMalloc(&b->d_rings, sizeof(uint32_t) * per * MGS_QUEUE_RING) != hipSuccess) {
+    b->d_rings = nullptr;
+    return fail(MGS_ENOMEM, "rotation ring allocation failed%s");
+  }
+  HIPCHK(hipMemset(b->d_rings, 0, sizeof(uint32_t) * per * MGS_QUEUE_RING));
+  for (int k = 0; k < MGS_QUEUE_RING; k++) {
+    uint64_t a = (uint64_t)(uintptr_t)(b->d_rings + per * k);
+    HIPCHK(hipMemcpy(b->d_queue + MGS_QHDR * k + 4, &a, sizeof(a), hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipDeviceSynchronize());
+  return MGS_OK;
+}
+
 static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
                           const double* d_mocap_quat, const double* d_phase_start, const double* d_phase_target,
                           const uint8_t* d_active, uint8_t* d_label, int32_t* d_fail_step, double* d_obj_qpos,
@@ -430,7 +452,11 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
     if (r > 0 && r < n) {
       nwg = r;
       slot = b->qslot++ % MGS_QUEUE_RING;
-      q = b->d_queue + 2 * slot;
+      q = b->d_queue + MGS_QHDR * slot;
+      if (sched->yield_every > 0 && d_resume_out && !b->d_rings) {
+        int rrc = alloc_rings(b);
+        if (rrc) return rrc;
+      }
     }
   }
   int lrc = launch_layout(b, nwg, &lay);

@@ -4464,7 +4464,92 @@ DEVI void save_record(const Mdl& md, Dat& d, double* rec, int p, int t, int gste
     tail[1] = p; tail[2] = t; tail[3] = gstep;
     tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
     tail[8] = d.ITERS;
+    tail[9] = d.OVERFLOW;
   }
+}
+
+// ---------------------------------------------------------------------------
+// In-launch rotation (ABI 19).  A work-queue launch whose schedule sets
+// yield_every keeps, next to its candidate counter, a ring of yielded
+// candidates: every yield_every steps a candidate checks whether anyone is
+// waiting (a candidate not started yet, or one in the ring); if so it writes
+// its resume record, appends itself to the ring and its workgroup takes the
+// next un-started candidate, else the ring's oldest.  So a launch with more
+// rollouts than slots runs them round robin and ends about one slice after
+// the last one finishes, instead of one whole rollout after the last one
+// started.  No workgroup ever waits for another's candidate: the only waits
+// are for a ring slot between a producer's two atomics (tail, then the slot),
+// a few instructions of a running wave.  Queue header (MGS_QHDR words): [0]
+// next candidate, [1] exits, [2] ring head, [3] ring tail, [4..5] the ring's
+// address (set by the host when it allocates the rings; MGS_QRING_F(n) words,
+// candidate + 1, 0 = empty).
+#define MGS_QHDR 8
+#define MGS_QRING_F(n) (2u * (uint32_t)(n))
+#define MGS_SPIN_MAX (1u << 22)
+
+DEVI uint32_t* ring_of(const uint32_t* q) { return (uint32_t*)((const uint64_t*)q)[2]; }
+
+// is any candidate waiting for a slot (un-started, or yielded to the ring)?
+DEVI int queue_waiting(const uint32_t* q, int n) {
+  uint32_t w = 0;
+  if (lane_id() == 0) {
+    uint32_t nx = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t h = __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t t = __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w = (nx < (uint32_t)n) || (h < t);
+  }
+  return (int)__builtin_amdgcn_readfirstlane(w);
+}
+
+// append candidate i (its record already written by the whole wave) to the
+// ring; 0 if the slot never emptied (then the caller keeps the candidate)
+DEVI int ring_push(uint32_t* q, int n, int i) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // every lane's record stores
+  wsync();
+  uint32_t ok = 0;
+  if (lane_id() == 0) {
+    const uint32_t F = MGS_QRING_F(n);
+    uint32_t t = __hip_atomic_fetch_add(q + 3, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t* slot = ring_of(q) + (t % F);
+    for (uint32_t it = 0; it < MGS_SPIN_MAX; it++) {
+      uint32_t z = 0;
+      if (__hip_atomic_compare_exchange_strong(slot, &z, (uint32_t)i + 1u, __ATOMIC_RELEASE, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        ok = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    if (!ok) printf("mgs: ring slot %u of the work queue never emptied (candidate %d kept)\n", t % F, i);
+  }
+  return (int)__builtin_amdgcn_readfirstlane(ok);
+}
+
+// the ring's oldest candidate, or -1 if the ring is empty
+DEVI int ring_pop(uint32_t* q, int n) {
+  int c = -1;
+  if (lane_id() == 0) {
+    const uint32_t F = MGS_QRING_F(n);
+    for (;;) {
+      uint32_t h = __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t t = __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (h >= t) break;
+      if (!__hip_atomic_compare_exchange_strong(q + 2, &h, h + 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT))
+        continue;
+      uint32_t* slot = ring_of(q) + (h % F);
+      for (uint32_t it = 0; it < MGS_SPIN_MAX; it++) {
+        uint32_t v = __hip_atomic_exchange(slot, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (v) { c = (int)(v - 1u); break; }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      if (c < 0) printf("mgs: ring slot %u of the work queue never filled\n", h % F);
+      break;
+    }
+  }
+  c = (int)__builtin_amdgcn_readfirstlane(c);
+  if (c >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the record, for every lane
+  return c;
 }
 
 // one candidate's rollout (the body of mgs_rollout_kernel)
@@ -4476,8 +4561,16 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
                       int32_t* __restrict__ fail_step, double* __restrict__ obj_qpos, int32_t* __restrict__ stats,
                       const double* __restrict__ vstate_init, double* __restrict__ state_out,
                       double* resume_out, const double* resume_in, const double* __restrict__ mask_mpos,
-                      int mask_pred, uint8_t* __restrict__ mask_out, int32_t* ovf_count, int32_t* ovf_list) {
+                      int mask_pred, uint8_t* __restrict__ mask_out, int32_t* ovf_count, int32_t* ovf_list,
+                      uint32_t* yq = nullptr, int n = 0, int from_ring = 0) {
   int lane = lane_id();
+  if (from_ring) {
+    // a candidate that yielded earlier in this launch: accepted, and its
+    // record (in resume_out) holds the state to continue from
+    active = nullptr;
+    mask_out = nullptr;
+    resume_in = resume_out;
+  }
   int reject = active && !active[i];
   if (mask_out) {
     // fused collision mask (mgs_mask_rollout_device): collision_entry's
@@ -4523,17 +4616,38 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
     for (int k = lane; k < nq; k += WAVE) d.qpos[k] = rec[k];
     for (int k = lane; k < nvr; k += WAVE) { d.qvel[k] = rec[nq + k]; d.qacc_ws[k] = rec[nq + nvr + k]; }
     const double* tail = rec + nq + 2 * nvr;
-    if (lane == 0) { d.time[0] = tail[0]; d.ITERS = (int)tail[8]; }
+    if (lane == 0) {
+      d.time[0] = tail[0];
+      d.ITERS = (int)tail[8];
+      // a yielded candidate keeps its flags; a capacity escalation or a time
+      // slice by relaunch starts the continued run's flags afresh
+      if (from_ring) d.OVERFLOW = (int)tail[9];
+    }
     p0 = (int)tail[1]; t0 = (int)tail[2]; gstep = (int)tail[3];
     maxcon = (int)tail[4]; maxefc = (int)tail[5]; sumcon = (int)tail[6]; sumefc = (int)tail[7];
     wsync();
   }
   PROF_DECL
+  int since = 0;     // steps run since this candidate (re)started in this launch
   for (int p = p0; p < np && ok; p++) {
     if (lane == 0)
       for (int u = 0; u < md.m.nu; u++) d.ctrl[u] = sc.ctrl[p * 32 + u];
     int ns = sc.nsteps[p];
     for (int t = (p == p0 ? t0 : 0); t < ns && ok; t++) {
+      if (yq && since >= sc.yield_every) {
+        // in-launch rotation (ABI 19): the state entering this step goes to the
+        // record and the candidate to the ring if anyone waits for a slot
+        since = 0;
+        if (queue_waiting(yq, n)) {
+          save_record(md, d, resume_out + (size_t)i * RS, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
+          if (ring_push(yq, n, i)) {
+            ok = 0;
+            fstep = -5;
+            break;
+          }
+        }
+      }
+      since++;
       if (sc.pause_step > 0 && gstep >= sc.pause_step && resume_out) {
         // time slice (ABI 18): the state entering this step, the schedule
         // position and the partial stats go to the resume record, exactly as
@@ -4628,6 +4742,10 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
     if (ok && sc.check_at_end[p] && !obj_contact(md, d)) { ok = 0; fstep = gstep - 1; }
     if (fstep <= -3) break;
   }
+  if (fstep == -5) {   // yielded: another workgroup of this launch continues it
+    PROF_FLUSH
+    return;
+  }
   if (lane == 0) {
     label[i] = (uint8_t)ok;
     if (fail_step) fail_step[i] = fstep;
@@ -4686,18 +4804,34 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
     // have made their one failing pop: the last of them returns both words to
     // zero (every pop of this launch is behind it), so each launch on this slot
     // starts from zero with no fill kernel and no host-tracked base (ABI 17)
+    // rotation (sc.yield_every > 0 with resume records): un-started candidates
+    // first, then the ring of yielded ones; a workgroup leaves when both are
+    // empty (a candidate pushed later is taken by its pusher's own next pop)
+    uint32_t* yq = (sc.yield_every > 0 && resume_out && ring_of(queue)) ? queue : nullptr;
+    int fresh = 1;
     for (;;) {
-      uint32_t t = 0;
-      if (lane_id() == 0) t = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t s = __builtin_amdgcn_readfirstlane(t);
-      if (s >= (uint32_t)n) break;
-      rollout_one<NV, SL>(md, smem, lay, sc, (int)s, qpos_init, mocap_quat, phase_start, phase_target, active, label,
+      int s = -1, ring = 0;
+      if (fresh) {
+        uint32_t t = 0;
+        if (lane_id() == 0) t = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t u = __builtin_amdgcn_readfirstlane(t);
+        if (u < (uint32_t)n) s = (int)u;
+        else fresh = 0;
+      }
+      if (s < 0 && yq) {
+        s = ring_pop(yq, n);
+        ring = 1;
+      }
+      if (s < 0) break;
+      rollout_one<NV, SL>(md, smem, lay, sc, s, qpos_init, mocap_quat, phase_start, phase_target, active, label,
                           fail_step, obj_qpos, stats, vstate_init, state_out, resume_out, resume_in, mask_mpos,
-                          mask_pred, mask_out, ovf_count, ovf_list);
+                          mask_pred, mask_out, ovf_count, ovf_list, yq, n, ring);
     }
     if (lane_id() == 0 &&
         __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
       __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(queue + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(queue + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;

@@ -280,7 +280,7 @@ class Engine:
         """doubles per resume record (mgs_rollout_out.resume)"""
         return self.cm.nq + 2 * self.cm.nv + abi.MGS["MGS_RESUME_EXTRA"]
 
-    def rollout(self, plan, resumable=False, resume_from=None, pause_step=0, capped_continue=False):
+    def rollout(self, plan, resumable=False, resume_from=None, pause_step=0, capped_continue=False, yield_every=0):
         """mgs_rollout.  resumable: candidates overflowing the capacity stop at
         that step (fail_step -3) and result["resume"] holds their records;
         resume_from: records of such a capped run, continued here
@@ -288,12 +288,17 @@ class Engine:
         pause_step > 0 (needs resumable): candidates that have run that many
         steps stop there (fail_step -4, MGS_FLAG_PAUSED) with a record, a time
         slice a later call continues; capped_continue: over-capacity candidates
-        run on capped and flagged instead of stopping."""
+        run on capped and flagged instead of stopping.  yield_every > 0 (needs
+        resumable): in-launch rotation (mgs_schedule.yield_every) when the batch
+        has more rollouts than the resident grid; outputs are unchanged."""
         n = len(plan.qpos_init)
         sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
                                   check_offset=getattr(plan, "check_offset", None))
         sched.pause_step = int(pause_step)
         sched.capped_continue = int(bool(capped_continue))
+        sched.yield_every = int(yield_every)
+        if yield_every and not resumable:
+            raise ValueError("yield_every needs resumable=True (a yielded state goes to the resume records)")
         if pause_step and not resumable:
             raise ValueError("pause_step needs resumable=True (the paused state goes to the resume records)")
         label = np.zeros(n, np.uint8)

@@ -363,15 +363,19 @@ class ClutterTableEnv:
                            phase_target=np.ascontiguousarray(np.stack([mp, target_lift], 1)),
                            obj_qposadr=-1, check_offset=[0, 1])
 
-    SLICES = 4
+    # in-launch rotation and explicit relaunch slices, as GravitylessObjectGrasping
+    YIELD_EVERY = 32
+    SLICES = 1
 
-    def rollout(self, plan: RolloutPlan, env_state, max_ncon: int = 128, slices: Optional[int] = None):
+    def rollout(self, plan: RolloutPlan, env_state, max_ncon: int = 128, slices: Optional[int] = None,
+                yield_every: Optional[int] = None):
         """engine rollout with contact-capacity escalation (continued from the
-        overflowing step) and time slices, as GravitylessObjectGrasping.rollout
-        (sliced_rollout)."""
+        overflowing step), in-launch rotation and optional time slices by
+        relaunch, as GravitylessObjectGrasping.rollout (sliced_rollout)."""
         return sliced_rollout(plan, self.engine_for_state(env_state),
                               lambda c: self.engine_for_state(env_state, ncon_max=c), self.ncon_max, max_ncon,
-                              self.SLICES if slices is None else slices, auto=slices is None)
+                              self.SLICES if slices is None else slices,
+                              yield_every=self.YIELD_EVERY if yield_every is None else yield_every)
 
     def grasp_stable_mask(self, poses: SE3Pose, joints: np.ndarray, env_state, nstep_lift: int = 3000,
                           lift_dist: float = 0.3, enough_stable=None, *, close_steps: Optional[int] = None,

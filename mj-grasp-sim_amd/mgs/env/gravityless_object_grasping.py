@@ -160,16 +160,22 @@ class GravitylessObjectGrasping:
             self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max, specialize="cached")
         return self._wide[ncon_max]
 
-    # a batch with more than four grids' worth of rollouts runs as this many
-    # time slices (launches): each launch then ends about one slice after its
-    # last candidate started, instead of one whole rollout after it
-    SLICES = 4
+    # in-launch rotation (mgs_schedule.yield_every, ABI 19): a batch with more
+    # rollouts than resident workgroups runs them round robin in slices of this
+    # many steps, so the launch ends about one slice after its last rollout
+    # finishes instead of one whole rollout after its last one started
+    YIELD_EVERY = 32
+    # explicit time slices by relaunch (rollout(slices=k)): every k-th part of
+    # the horizon is its own launch (pause_step); the default is one launch
+    SLICES = 1
 
-    def rollout(self, plan: "RolloutPlan", max_ncon: int = 40, slices: Optional[int] = None):
-        """engine.rollout with capacity escalation and time slices
-        (sliced_rollout below)."""
+    def rollout(self, plan: "RolloutPlan", max_ncon: int = 40, slices: Optional[int] = None,
+                yield_every: Optional[int] = None):
+        """engine.rollout with capacity escalation, in-launch rotation and
+        optional time slices by relaunch (sliced_rollout below)."""
         return sliced_rollout(plan, self.engine, self.engine_for, self.ncon_max, max_ncon,
-                              self.SLICES if slices is None else slices, auto=slices is None)
+                              self.SLICES if slices is None else slices,
+                              yield_every=self.YIELD_EVERY if yield_every is None else yield_every)
 
     # -- host-side bookkeeping (exactly the reference's arithmetic) ------------
     def _check_inputs(self, poses, joints, check_width=True):
@@ -292,8 +298,8 @@ def apply_enough_stable(labels: np.ndarray, enough_stable) -> np.ndarray:
     return labels
 
 
-def sliced_rollout(plan: "RolloutPlan", engine, engine_for, cap: int, max_ncon: int, slices: int,
-                   auto: bool = True):
+def sliced_rollout(plan: "RolloutPlan", engine, engine_for, cap: int, max_ncon: int, slices: int = 1,
+                   yield_every: int = 0):
     """A batch's rollouts on `engine` (capacity `cap` contacts) with capacity
     escalation and time slices; results equal one launch at unlimited capacity.
 
@@ -305,30 +311,30 @@ def sliced_rollout(plan: "RolloutPlan", engine, engine_for, cap: int, max_ncon: 
     last stage runs on capped, flagged); its results replace the capped run's.
     res['overflow'] counts candidates capped.
 
-    Slices: when the batch has more than four times the rollouts the device
-    runs at once (the work queue's resident grid; auto) or `slices` is given, the horizon
-    is cut into `slices` launches: every unfinished candidate stops at the
-    slice boundary with a resume record (MGS_FLAG_PAUSED) and the next launch
-    continues the survivors, so a launch never waits for a whole rollout that
-    started late.  Records carry the complete state, so the results equal one
-    launch's bit for bit."""
+    Rotation (yield_every > 0): inside each launch, a candidate that has run
+    yield_every steps hands its slot to a waiting one (mgs_schedule.yield_every),
+    so the launch ends about one slice after its last rollout finishes.
+
+    Slices by relaunch (slices > 1): the horizon is cut into `slices`
+    launches: every unfinished candidate stops at the slice boundary with a
+    resume record (MGS_FLAG_PAUSED) and the next launch continues the
+    survivors (one host round trip per slice; profiles/r04b_api.txt).
+
+    Records carry the complete state, so either way the results equal one
+    uninterrupted launch's bit for bit."""
     n = len(plan.qpos_init)
     H = plan.horizon
-    if auto:
-        # measured (profiles/r04b_api.txt): a batch a little over the grid
-        # (1173 rollouts on 1024 slots) loses more to the extra round trips
-        # than its tail costs; one of many grids' worth gains
-        slices = slices if n and 4 * engine.rollout_grid(n) < n else 1
     slices = max(1, min(int(slices), max(H, 1)))
     bounds = [int(round(H * (j + 1) / slices)) for j in range(slices - 1)] + [0]
     last_cap = cap >= max_ncon
-    res = engine.rollout(plan, resumable=True, pause_step=bounds[0], capped_continue=last_cap)
+    res = engine.rollout(plan, resumable=True, pause_step=bounds[0], capped_continue=last_cap,
+                         yield_every=yield_every)
     rec = res.pop("resume")
     live = np.arange(n)
     for j, b in enumerate(bounds):
         if j > 0:
             sub = engine.rollout(plan.subset(live), resumable=True, resume_from=rec[live], pause_step=b,
-                                 capped_continue=last_cap)
+                                 capped_continue=last_cap, yield_every=yield_every)
             for k in ("label", "fail_step", "obj_qpos", "stats"):
                 res[k][live] = sub[k]
             rec[live] = sub["resume"]
@@ -338,7 +344,8 @@ def sliced_rollout(plan: "RolloutPlan", engine, engine_for, cap: int, max_ncon: 
         while len(ov) and c < max_ncon:
             c = min(2 * c, max_ncon)
             last = c >= max_ncon
-            sub = engine_for(c).rollout(plan.subset(ov), resumable=True, resume_from=rec[ov], capped_continue=last)
+            sub = engine_for(c).rollout(plan.subset(ov), resumable=True, resume_from=rec[ov], capped_continue=last,
+                                        yield_every=yield_every)
             for k in ("label", "fail_step", "obj_qpos", "stats"):
                 res[k][ov] = sub[k]
             keep = np.nonzero(sub["stats"][:, 2] & FLAG_CAPACITY)[0] if not last else np.zeros(0, np.int64)

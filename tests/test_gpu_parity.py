@@ -285,6 +285,82 @@ def test_work_queue_equals_one_workgroup_per_candidate(env, eng, candidates, ora
     assert np.array_equal(outs[5]["objq"][idx], ro["obj_qpos"])
 
 
+@pytest.mark.parametrize("grid,yield_every", [(5, 1), (5, 7), (64, 7), (64, 32)])
+def test_rotation_equals_one_workgroup_per_candidate(env, eng, candidates, grid, yield_every):
+    """In-launch rotation (mgs_schedule.yield_every, ABI 19): on a work-queue
+    grid smaller than the batch, a candidate that has run yield_every steps
+    hands its slot to a waiting one (its record to the launch's ring, another
+    workgroup continues it).  Every output -- fused mask, labels, fail steps,
+    object poses, statistics -- equals one workgroup per candidate without
+    rotation bit for bit, for two launches in a row on the same queue slot
+    ring (each leaves its counters and ring zeroed); yield_every 1 rotates at
+    every step."""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    plan = plan_for(env, poses, J)
+    n = len(q)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+    dq, dmp, dmq, dps, dpt = t(q), t(mp), t(mq), t(plan.phase_start), t(plan.phase_target)
+    rw = eng.resume_width()
+    L = eng.lib
+    prev = L.mgs_rollout_queue(-1)
+    outs = {}
+    try:
+        for mode, ye in ((0, 0), (grid, yield_every)):
+            L.mgs_rollout_queue(mode)
+            sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl,
+                                      plan.obj_qposadr, check_offset=getattr(plan, "check_offset", None))
+            sched.yield_every = ye
+            for rep in range(2):
+                o = dict(free=torch.zeros(n, dtype=torch.uint8, device=dev),
+                         lab=torch.zeros(n, dtype=torch.uint8, device=dev),
+                         fail=torch.zeros(n, dtype=torch.int32, device=dev),
+                         objq=torch.zeros((n, 7), dtype=torch.float64, device=dev),
+                         st=torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev),
+                         rec=torch.zeros((n, rw), dtype=torch.float64, device=dev))
+                eng.mask_rollout_device(sched, n, dq.data_ptr(), dmp.data_ptr(), dmq.data_ptr(), dps.data_ptr(),
+                                        dpt.data_ptr(), o["free"].data_ptr(), o["lab"].data_ptr(),
+                                        o["fail"].data_ptr(), o["objq"].data_ptr(), o["st"].data_ptr(),
+                                        d_resume_out=o["rec"].data_ptr())
+                torch.cuda.synchronize()
+                outs[(mode, rep)] = {k: v.cpu().numpy() for k, v in o.items() if k != "rec"}
+    finally:
+        L.mgs_rollout_queue(prev)
+    ref = outs[(0, 0)]
+    assert 0 < ref["free"].sum() < n
+    for rep in range(2):
+        for k in ref:
+            assert np.array_equal(ref[k], outs[(grid, rep)][k]), (grid, yield_every, rep, k)
+
+
+def test_env_rotation_equals_one_launch(env, candidates, oracle_model):
+    """GravitylessObjectGrasping.rollout with its default in-launch rotation
+    on a small queue grid equals the same call without rotation, and the
+    oracle (h200 and ref8000)."""
+    from conftest import plan_for
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(oracle_model.collision_free(q, mp, mq, nthreads=8))[0]
+    L = env.engine.lib
+    prev = L.mgs_rollout_queue(-1)
+    try:
+        for horizon, sub in (("h200", idx[:128]), ("ref8000", idx[:6])):
+            plan = plan_for(env, poses[sub], J[sub], horizon)
+            L.mgs_rollout_queue(0)
+            one = env.rollout(plan, yield_every=0)
+            L.mgs_rollout_queue(4 if horizon == "ref8000" else 16)
+            rot = env.rollout(plan, yield_every=64 if horizon == "ref8000" else 16)
+            _assert_same(rot, one, f"rotation {horizon}")
+            if horizon == "h200":
+                _assert_same(one, oracle_model.rollout(plan, nthreads=8), "oracle")
+    finally:
+        L.mgs_rollout_queue(prev)
+
+
 def test_device_overflow_list_and_list_rollout(env, eng, candidates):
     """mgs_overflow_list_device picks the flagged candidates; mgs_rollout_list_device
     with a grid smaller than the list (workgroups loop over it) reproduces

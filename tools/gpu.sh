@@ -6,11 +6,13 @@
 #
 # steps:
 #   tests     the GPU suite (pytest -m gpu)
+#   tk:<expr> the GPU tests matching a pytest -k expression
 #   smoke     __graft_entry__.smoke()
 #   bench     the driver's command, `bench.py --gpus 1 --steps 20 --warmup 5`
 #             (full line: e2e API, CPU baseline); first process of the call
 #   rep       the driver's command without CPU baseline / e2e, 3 processes
 #   api       the drop-in env API per call, one rollout launch vs 4 time slices
+#   rot       in-launch rotation A/B (bench --yield-every, env API --e2e-yield)
 #   streams   the driver's command with 2 / 6 / 8 pipelines in flight
 #   n2        2-rank launcher rehearsal on one GPU (gloo) with the shard check
 #   trace     rocprofv3 --kernel-trace --stats of the driver's command
@@ -51,6 +53,12 @@ for step in "$@"; do
       timeout -k 10 1200 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         > $O/tests.log 2>&1 || fail tests $O/tests.log
       tail -1 $O/tests.log ;;
+    tk:*)
+      # a subset of the GPU suite (pytest -k expression), before the whole suite
+      k=${step#tk:}
+      timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$k" \
+        > $O/tk.log 2>&1 || fail "$step" $O/tk.log
+      tail -1 $O/tk.log ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
       tail -1 $O/smoke.log ;;
@@ -68,6 +76,19 @@ for step in "$@"; do
         timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 4 --e2e-slices $sl > $O/api$sl.json \
           2> $O/api$sl.err || fail api $O/api$sl.err
         summ $O/api$sl.json
+      done ;;
+    rot)
+      # in-launch rotation A/B: the driver's command with --yield-every 0 / 16 / 32 / 64,
+      # then the env API per call with its rotation off and on
+      for y in 0 16 32 64; do
+        timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 0 --yield-every $y > $O/rot$y.json \
+          2> $O/rot$y.err || fail rot $O/rot$y.err
+        summ $O/rot$y.json
+      done
+      for y in 0 32; do
+        timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 4 --e2e-yield $y > $O/apiy$y.json \
+          2> $O/apiy$y.err || fail rot $O/apiy$y.err
+        summ $O/apiy$y.json
       done ;;
     streams)
       # pipelines in flight (bench --streams): 2, 6, 8 against the default 4
