@@ -29,6 +29,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import numpy as np  # noqa: E402
 
+YIELD = None    # --yield: the envs' in-launch rotation (steps per slice; None = the env default)
+
 
 def gravityless(gripper_name, object_ids, n, horizon="h200"):
     from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, HORIZONS
@@ -42,6 +44,8 @@ def gravityless(gripper_name, object_ids, n, horizon="h200"):
     for oid in object_ids:
         g = get_gripper({"name": gripper_name})
         env = GravitylessObjectGrasping(g, get_object(oid))
+        if YIELD is not None:
+            env.YIELD_EVERY = YIELD
         if gripper_name == "PandaGripper":
             H, J, _ = antipodal.panda_candidates(env.obj, n, seed=0, gripper=g)
         else:
@@ -74,6 +78,8 @@ def clutter(n_per_obj, steps, cpu_sample=0, threads=16):
     from mgs.util.geo.transforms import SE3Pose
     z = np.load(os.path.join(ROOT, "tests", "golden", "clutter_scene_shadow.npz"))
     env = make_env("ShadowHand")
+    if YIELD is not None:
+        env.YIELD_EVERY = YIELD
     env.set_state(z["state"])
     H, J = [], []
     for k, o in enumerate(env.objects):
@@ -223,9 +229,13 @@ def main():
     ap.add_argument("--c5-per-object", type=int, default=256)
     ap.add_argument("--c5-cpu-sample", type=int, default=0, help="candidates for the C5 CPU baseline (0: none)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--yield", dest="yield_every", type=int, default=None,
+                    help="in-launch rotation of the envs' rollout launches, steps per slice (0 = off)")
     ap.add_argument("--scene-piles", type=int, default=256)
     ap.add_argument("--scene-ncon", type=int, default=None)
     a = ap.parse_args()
+    global YIELD
+    YIELD = a.yield_every
     os.environ.setdefault("MGS_SPECIALIZE", "1")
     import torch
     torch.cuda.init()
@@ -257,6 +267,7 @@ def main():
                        **sampler())
         else:
             raise SystemExit(f"unknown config {c}")
+        out["yield_every"] = "env default" if YIELD is None else YIELD
         print(json.dumps(out), flush=True)
 
 

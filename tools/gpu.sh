@@ -18,7 +18,9 @@
 #   trace     rocprofv3 --kernel-trace --stats of the driver's command
 #   pmc       PMC passes (FETCH / WRITE / SQ / VALU) on a one-pipeline bench
 #   stages    stage timers (MGS_PROFILE builds): headline and Shadow pile
+#   heavy     stage timers over the 64 heaviest rollouts of the headline batch
 #   configs   tools/bench_configs.py (C3, C4, C5)
+#   c5big     C5 at 3000 + 3000 steps on 10 240 candidates, rotation on / off
 #   py:<file> python3 <file> (a probe script under tools/)
 # Outputs: gpurun_out/<tag>/
 set -o pipefail
@@ -129,9 +131,21 @@ for step in "$@"; do
       timeout -k 10 400 python3 tools/stage_profile_clutter.py 300 > $O/stages_clutter.txt 2>&1 \
         || fail stages_clutter $O/stages_clutter.txt
       tail -3 $O/stages_clutter.txt ;;
+    heavy)
+      # stage timers over the 64 heaviest rollouts of the headline batch (the single launch's critical path)
+      timeout -k 10 300 python3 tools/stage_profile.py 64 --heavy > $O/stages_heavy.txt 2>&1 \
+        || fail heavy $O/stages_heavy.txt
+      tail -8 $O/stages_heavy.txt ;;
     configs)
       timeout -k 10 900 python3 tools/bench_configs.py > $O/configs.jsonl 2> $O/configs.err || fail configs $O/configs.err
       cat $O/configs.jsonl | cut -c1-300 ;;
+    c5big)
+      # C5 at the reference's schedule (3000 + 3000) on 10 240 candidates, rotation on and off
+      for y in 32 0; do
+        timeout -k 10 600 python3 tools/bench_configs.py c5 --c5-per-object 2048 --c5-steps 3000 --yield $y \
+          > $O/c5big_y$y.jsonl 2> $O/c5big_y$y.err || fail c5big $O/c5big_y$y.err
+        cut -c1-400 $O/c5big_y$y.jsonl
+      done ;;
     py:*)
       f=${step#py:}
       b=$(basename "$f" .py)

@@ -66,16 +66,28 @@ def main():
         print(special.code_object(library_for(env.model.nv, int(fields["nefc_max"])), abi.make_desc(fields),
                                   profile=True))
         return
-    N = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-    H, J, W = robotiq_candidates(obj, 4 * N, seed=2)
+    N = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64
+    heavy = "--heavy" in sys.argv
+    # --heavy: the N candidates with the most constraint rows over their rollout
+    # among the collision-free ones of the headline's 8192-candidate batch (the
+    # critical path of a single launch, tools/probes/critical_path_probe.py)
+    H, J, W = robotiq_candidates(obj, 8192 if heavy else 4 * N, seed=0 if heavy else 2)
     poses = SE3Pose.from_mat(H)
     q, mp, mq, _ = env.initial_state(poses, J)
     eng = env.engine
     free = eng.collision_free(q, mp, mq)
-    idx = np.nonzero(free)[0][:N]
+    idx = np.nonzero(free)[0]
     h = HORIZONS['h200']
-    plan = env.rollout_plan(poses[idx], J[idx], nstep_lift=h['nstep_lift'], shake_steps=h['shake_steps'],
-                            close_steps=h['close_steps'], lift_check_every=h['lift_check_every'])
+
+    def plan_of(sel):
+        return env.rollout_plan(poses[sel], J[sel], nstep_lift=h['nstep_lift'], shake_steps=h['shake_steps'],
+                                close_steps=h['close_steps'], lift_check_every=h['lift_check_every'])
+    if heavy:
+        st = eng.rollout(plan_of(idx))["stats"]
+        idx = idx[np.argsort(-st[:, 5], kind="stable")[:N]]
+    else:
+        idx = idx[:N]
+    plan = plan_of(idx)
     path = special.code_object(eng.lib, eng.desc, profile=True)
     eng._ck(eng.lib.mgs_model_attach_special(eng._model, path.encode()), 'mgs_model_attach_special')
     L = eng.lib
