@@ -254,9 +254,10 @@ def main():
     ap.add_argument("--e2e-yield", type=int, default=None,
                     help="in-launch rotation of the env API's rollout launches, steps per slice (default: the "
                          "env's YIELD_EVERY; 0 = off)")
-    ap.add_argument("--yield-every", type=int, default=0,
-                    help="in-launch rotation (mgs_schedule.yield_every) of the timed pipelines' launches, steps "
-                         "per slice (0 = off; needs the resume records of --esc-resume 1)")
+    ap.add_argument("--yield-every", type=int, default=32,
+                    help="in-launch rotation (mgs_schedule.yield_every, the env API's default too) of the timed "
+                         "pipelines' launches, steps per slice (0 = off; needs the resume records of "
+                         "--esc-resume 1); profiles/r04e_rotation_ab.txt")
     ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")

@@ -446,6 +446,11 @@ int mgs_mask_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n, 
  * that grid (n if n is smaller, or in mode 0 of mgs_rollout_queue: one
  * workgroup per candidate); needs the device. */
 int mgs_rollout_grid(mgs_batch* batch, int n);
+/* In-launch rotation counters of a batch (ABI 19), cumulative over its
+ * launches: out[0] yields (a candidate handed its slot to a waiting one),
+ * out[1] expired ring spins (0 unless the rotation protocol is broken; see
+ * mgs_schedule.yield_every).  Synchronises the device. */
+int mgs_queue_stats(mgs_batch* batch, uint64_t* out);
 /* Rollout launch mode for this process; returns the previous one and leaves it
  * unchanged if mode < 0.  0: one workgroup per candidate; 1 (default): the work
  * queue on the resident grid; k >= 2: the queue on at most k workgroups (tests

@@ -491,6 +491,20 @@ int mgs_rollout_device(mgs_batch* b, const mgs_schedule* sched, int n, const dou
                         d_fail_step, d_obj_qpos, d_stats, nullptr, nullptr, stream);
 }
 
+int mgs_queue_stats(mgs_batch* b, uint64_t* out) {
+  if (!b || !out) return fail(MGS_EINVAL, "mgs_queue_stats: null argument%s");
+  HIPCHK(hipSetDevice(b->m->device));
+  uint32_t h[MGS_QHDR * MGS_QUEUE_RING];
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(h, b->d_queue, sizeof(h), hipMemcpyDeviceToHost));
+  out[0] = out[1] = 0;
+  for (int k = 0; k < MGS_QUEUE_RING; k++) {
+    out[0] += h[MGS_QHDR * k + 6];
+    out[1] += h[MGS_QHDR * k + 7];
+  }
+  return MGS_OK;
+}
+
 int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32_t* d_count, int32_t* d_list,
                              void* stream) {
   if (n < 0 || !d_stats || !d_count || !d_list) return fail(MGS_EINVAL, "mgs_overflow_list_device: bad argument%s");

@@ -4482,7 +4482,10 @@ DEVI void save_record(const Mdl& md, Dat& d, double* rec, int p, int t, int gste
 // a few instructions of a running wave.  Queue header (MGS_QHDR words): [0]
 // next candidate, [1] exits, [2] ring head, [3] ring tail, [4..5] the ring's
 // address (set by the host when it allocates the rings; MGS_QRING_F(n) words,
-// candidate + 1, 0 = empty).
+// candidate + 1, 0 = empty), [6] yields and [7] expired spins, both
+// cumulative over the batch's launches (mgs_queue_stats; an expired spin --
+// a bug, never seen -- keeps the candidate on its workgroup or, on the pop
+// side, loses the slot's candidate, whose outputs then stay unwritten).
 #define MGS_QHDR 8
 #define MGS_QRING_F(n) (2u * (uint32_t)(n))
 #define MGS_SPIN_MAX (1u << 22)
@@ -4520,7 +4523,8 @@ DEVI int ring_push(uint32_t* q, int n, int i) {
       }
       __builtin_amdgcn_s_sleep(4);
     }
-    if (!ok) printf("mgs: ring slot %u of the work queue never emptied (candidate %d kept)\n", t % F, i);
+    if (ok) __hip_atomic_fetch_add(q + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(q + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return (int)__builtin_amdgcn_readfirstlane(ok);
 }
@@ -4543,7 +4547,7 @@ DEVI int ring_pop(uint32_t* q, int n) {
         if (v) { c = (int)(v - 1u); break; }
         __builtin_amdgcn_s_sleep(4);
       }
-      if (c < 0) printf("mgs: ring slot %u of the work queue never filled\n", h % F);
+      if (c < 0) __hip_atomic_fetch_add(q + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
   }

@@ -59,6 +59,7 @@ def load_library(wide: bool = False):
     L.mgs_mask_rollout_device.argtypes = [vp, P(abi.Schedule), ctypes.c_int] + [vp] * 5 + [ctypes.c_int] + [vp] * 8
     L.mgs_rollout_resume.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
                                      P(abi.RolloutOut)]
+    L.mgs_queue_stats.argtypes = [vp, P(ctypes.c_uint64)]
     L.mgs_last_kernel_ms.argtypes = [vp]
     L.mgs_last_kernel_ms.restype = ctypes.c_double
     L.mgs_last_collision_ms.argtypes = [vp]
@@ -409,6 +410,13 @@ class Engine:
         self._ck(self.lib.mgs_rollout_list_device(self.batch(grid), ctypes.byref(sched), n, d_count, d_list, grid,
                                                 d_qpos, d_mquat, d_ps, d_pt, d_resume_in, d_label, d_fail, d_objq,
                                                 d_stats, stream), "mgs_rollout_list_device")
+
+    def queue_stats(self):
+        """(yields, expired ring spins) of this engine's batch, cumulative
+        (mgs_queue_stats; synchronises the device)"""
+        out = (ctypes.c_uint64 * 2)()
+        self._ck(self.lib.mgs_queue_stats(self.batch(1), out), "mgs_queue_stats")
+        return int(out[0]), int(out[1])
 
     def last_collision_ms(self):
         return self.lib.mgs_last_collision_ms(self._batch)

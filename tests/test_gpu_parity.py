@@ -309,8 +309,12 @@ def test_rotation_equals_one_workgroup_per_candidate(env, eng, candidates, grid,
     L = eng.lib
     prev = L.mgs_rollout_queue(-1)
     outs = {}
+    yields, spins = [], []
     try:
         for mode, ye in ((0, 0), (grid, yield_every)):
+            y0, s0 = eng.queue_stats()
+            yields.append(y0)
+            spins.append(s0)
             L.mgs_rollout_queue(mode)
             sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl,
                                       plan.obj_qposadr, check_offset=getattr(plan, "check_offset", None))
@@ -328,6 +332,10 @@ def test_rotation_equals_one_workgroup_per_candidate(env, eng, candidates, grid,
                                         d_resume_out=o["rec"].data_ptr())
                 torch.cuda.synchronize()
                 outs[(mode, rep)] = {k: v.cpu().numpy() for k, v in o.items() if k != "rec"}
+        y1, s1 = eng.queue_stats()
+        yields.append(y1)
+        spins.append(s1)
+        yields, spins = yields[1:], spins[1:]
     finally:
         L.mgs_rollout_queue(prev)
     ref = outs[(0, 0)]
@@ -335,6 +343,8 @@ def test_rotation_equals_one_workgroup_per_candidate(env, eng, candidates, grid,
     for rep in range(2):
         for k in ref:
             assert np.array_equal(ref[k], outs[(grid, rep)][k]), (grid, yield_every, rep, k)
+    # the rotation ran (candidates yielded) and its ring protocol never timed out
+    assert yields[1] > yields[0] and spins[1] == spins[0] == 0, (yields, spins)
 
 
 def test_env_rotation_equals_one_launch(env, candidates, oracle_model):
