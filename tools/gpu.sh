@@ -18,7 +18,6 @@
 #   trace     rocprofv3 --kernel-trace --stats of the driver's command
 #   pmc       PMC passes (FETCH / WRITE / SQ / VALU) on a one-pipeline bench
 #   stages    stage timers (MGS_PROFILE builds): headline and Shadow pile
-#   pcs       rocprofv3 PC sampling on the line-table variant of the headline object
 #   heavy     stage timers over the 64 heaviest rollouts of the headline batch
 #   configs   tools/bench_configs.py (C3, C4, C5)
 #   c5big     C5 at 3000 + 3000 steps on 10 240 candidates, rotation on / off
@@ -132,21 +131,6 @@ for step in "$@"; do
       timeout -k 10 400 python3 tools/stage_profile_clutter.py 300 > $O/stages_clutter.txt 2>&1 \
         || fail stages_clutter $O/stages_clutter.txt
       tail -3 $O/stages_clutter.txt ;;
-    pcs)
-      # PC sampling (rocprofv3, stochastic, cycles) of a one-pipeline bench on the
-      # line-table variant of the headline object (tools/ab_variant.py pcs -gline-tables-only)
-      export TMPDIR=/tmp
-      MGS_SPECIAL_OBJECT=$PWD/mj-grasp-sim_amd/mgs/_lib/ab/pcs.hsaco timeout -s KILL 180 rocprofv3 \
-        --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles \
-        --pc-sampling-interval 1048576 -d $O/pcs -o pcs -f csv -- python3 bench.py --streams 1 --steps 2 \
-        --warmup 1 --cpu-budget 0 --e2e-steps 0 --no-escalate > $O/pcs.json 2> $O/pcs.err \
-        || { echo "stochastic failed, trying host_trap"; tail -5 $O/pcs.err; \
-             MGS_SPECIAL_OBJECT=$PWD/mj-grasp-sim_amd/mgs/_lib/ab/pcs.hsaco timeout -s KILL 180 rocprofv3 \
-             --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
-             --pc-sampling-interval 100 -d $O/pcs_ht -o pcs -f csv -- python3 bench.py --streams 1 --steps 2 \
-             --warmup 1 --cpu-budget 0 --e2e-steps 0 --no-escalate > $O/pcs_ht.json 2> $O/pcs_ht.err \
-             || fail pcs $O/pcs_ht.err; }
-      find $O -name '*pc_sampling*' | head ;;
     heavy)
       # stage timers over the 64 heaviest rollouts of the headline batch (the single launch's critical path)
       timeout -k 10 300 python3 tools/stage_profile.py 64 --heavy > $O/stages_heavy.txt 2>&1 \
