@@ -677,6 +677,14 @@ DEVI void ldl_factor_lds(double* A, double* Dv, double* Dinv) {
     // paid once per four terms instead of once per term); the FMA chain and
     // its ascending-k order are unchanged
     int k = 0;
+    // eight at a time first (one LDS latency per eight terms), then four
+    for (; k + 8 <= c; k += 8) {
+      double a[8], b[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) { a[q] = A[li * NV + k + q]; b[q] = A[(k + q) * NV + c]; }
+#pragma unroll
+      for (int q = 0; q < 8; q++) s = __builtin_fma(-a[q], b[q], s);
+    }
     for (; k + 4 <= c; k += 4) {
       const double a0 = A[li * NV + k], a1 = A[li * NV + k + 1], a2 = A[li * NV + k + 2], a3 = A[li * NV + k + 3];
       const double b0 = A[k * NV + c], b1 = A[(k + 1) * NV + c], b2 = A[(k + 2) * NV + c], b3 = A[(k + 3) * NV + c];
@@ -3136,14 +3144,16 @@ DEVI double cost_change(const double* A, const double* delta, const double* res)
 
 // one PGS update of the contact block starting at row r with DIM rows
 template <int DIM>
-DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u, Frc& F, int noslip) {
+DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u, Frc& F, int noslip,
+                        const double* gpre = nullptr) {
   double g[DIM], res[DIM], old[DIM], nw[DIM];
   const int c = uni(d.efc_con[r]);
   const double* blk = d.con_blk + BLKSTRIDE * c;
   const double* mu = d.con_mu + 5 * c;
 #pragma unroll
   for (int i = 0; i < DIM; i++) {
-    g[i] = (lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
+    // gpre: the block's G rows loaded ahead by the caller (lanes over dofs)
+    g[i] = gpre ? gpre[i] : ((lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0);
     old[i] = getf(F, r + i);
     // noslip never reads the normal row's residual: its reduction is skipped
     if (noslip && i == 0) { res[i] = 0.0; continue; }
@@ -3380,8 +3390,140 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
 // first row of each contact block of dimension 3 or 4, in ascending order --
 // from a row mask built once per call (lanes over rows), with each row's type
 // and dimension held in registers: the rows a sweep only steps over (equality,
-// limit, other contacts) cost nothing.
-DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+// limit, other contacts) cost nothing.  noslip_prefetch: per call, a friction row's A_rr (its
+// row_sqnorm, the same ascending sum) and frictionloss are formed once on the
+// row's lane instead of once per sweep, and each visited block's G rows are
+// loaded while the previous block is processed (wide build: G is in HBM, a
+// round trip per block otherwise).  Same values and order as the oracle.
+template <int N>
+DEVI int sel_i(const int (&a)[N], int r) {
+  int out = 0;
+#pragma unroll
+  for (int h = 0; h < N; h++)
+    if ((r >> 6) == h) out = __builtin_amdgcn_readlane(a[h], r & (WAVE - 1));
+  return out;
+}
+template <int N>
+DEVI double sel_d(const double (&a)[N], int r) {
+  double out = 0.0;
+#pragma unroll
+  for (int h = 0; h < N; h++)
+    if ((r >> 6) == h) out = readlane_d(a[h], r & (WAVE - 1));
+  return out;
+}
+// the first visited row after r (r = -1: the first one), -1 if none
+template <int N>
+DEVI int next_visited(const unsigned long long (&vis)[N], int r) {
+  const int s = r + 1;
+  int out = -1;
+#pragma unroll
+  for (int h = N - 1; h >= 0; h--) {
+    if (h < (s >> 6)) continue;
+    unsigned long long m = vis[h];
+    if (h == (s >> 6)) m &= ~0ull << (s & (WAVE - 1));
+    if (m) out = h * WAVE + __ffsll((long long)m) - 1;
+  }
+  return out;
+}
+DEVI void load_block_rows(const Dat& d, int r, int dim, int nv, int lane, double (&g)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) g[i] = (i < dim && lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
+}
+
+DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+  int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
+  int P = next_pow2(nv);
+  if (md.m.noslip_iterations <= 0 || ne <= 0) return;
+  int tk[MGS_RPL], dk[MGS_RPL];
+  unsigned long long vis[MGS_RPL];
+  double Ak[MGS_RPL], Fk[MGS_RPL];
+#pragma unroll
+  for (int h = 0; h < MGS_RPL; h++) {
+    const int r = lane + h * WAVE;
+    int t = -1, dim = 0, v = 0;
+    if (r < ne) {
+      t = d.efc_type[r];
+      dim = d.efc_dim[r];
+      v = t == MGS_EFC_FRICTION || (t == MGS_EFC_CONTACT && (dim == 3 || dim == 4) && efc_lead(d, r));
+    }
+    tk[h] = t;
+    dk[h] = dim;
+    vis[h] = __ballot(v);
+    Ak[h] = 0.0;
+    Fk[h] = 0.0;
+    if (v && t == MGS_EFC_FRICTION) {
+      Ak[h] = row_sqnorm(d, r, nv);
+      Fk[h] = row_floss(md, d, r);
+    }
+  }
+  for (int ns = 0; ns < md.m.noslip_iterations; ns++) {
+    PCNT(38, 1);
+    double improvement = 0.0;
+    // the noslip cost drops the regulariser: count its removal at iteration 0
+    // (row terms on their lanes, summed in row order)
+    if (ns == 0) {
+#pragma unroll
+      for (int h = 0; h < MGS_RPL; h++) {
+        const int r = lane + h * WAVE;
+        const double f = F.v[h];
+        const double term = r < ne ? ((0.5 * f) * f) * d.efc_R[r] : 0.0;
+        const int nh = ne - h * WAVE < WAVE ? ne - h * WAVE : WAVE;
+        for (int l = 0; l < nh; l++) improvement = improvement + readlane_d(term, l);
+      }
+    }
+    int r = next_visited(vis, -1);
+    int t = 0, dim = 0;
+    double gc[4];
+    if (r >= 0) {
+      t = sel_i(tk, r);
+      dim = t == MGS_EFC_FRICTION ? 1 : sel_i(dk, r);
+      load_block_rows(d, r, dim, nv, lane, gc);
+    }
+    while (r >= 0) {
+      const int rn = next_visited(vis, r);
+      int tn = 0, dimn = 0;
+      double gn[4] = {0.0, 0.0, 0.0, 0.0};
+      if (rn >= 0) {
+        tn = sel_i(tk, rn);
+        dimn = tn == MGS_EFC_FRICTION ? 1 : sel_i(dk, rn);
+        load_block_rows(d, rn, dimn, nv, lane, gn);
+      }
+      if (t == MGS_EFC_FRICTION) {
+        double g = gc[0];
+        double res = tree_sum(g * u, P) + d.efc_b[r];
+        double fo = getf(F, r);
+        double Arr = sel_d(Ak, r);
+        double fnew[1] = {fo - res * (1.0 / Arr)};
+        project_scalar(t, sel_d(Fk, r), fnew);
+        double delta = fnew[0] - fo;
+        double ch = cost_change1(Arr, delta, res);
+        if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
+        improvement = improvement - ch;
+        if (delta != 0.0) {
+          double s = u + g * delta;
+          if (lane < nv) u = s;
+          setf(F, r, fnew[0], lane);
+        }
+      } else if (dim == 3) {
+        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1, gc);
+      } else {
+        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1, gc);
+      }
+      r = rn;
+      t = tn;
+      dim = dimn;
+#pragma unroll
+      for (int i = 0; i < 4; i++) gc[i] = gn[i];
+    }
+    if (improvement * scale < md.m.noslip_tolerance) break;
+  }
+}
+
+// G in LDS (main build): rows are a few LDS loads away, the sweep reads them
+// in place; G in HBM (wide build): noslip_prefetch (C5 pile rollout 2148 ->
+// 2058 ms, profiles/r04m_noslip_ab.txt; the main build measured 1 % slower
+// with it)
+DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   if (md.m.noslip_iterations <= 0 || ne <= 0) return;
@@ -3448,6 +3590,14 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     }
     if (improvement * scale < md.m.noslip_tolerance) break;
   }
+}
+
+DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+#ifdef MGS_G_GLOBAL
+  noslip_prefetch(md, d, scale, F, u);
+#else
+  noslip_inplace(md, d, scale, F, u);
+#endif
 }
 
 // qacc = qacc_smooth + L^-T D^-1/2 u ; qfrc_constraint = L D^1/2 u, lane i owns
@@ -3743,6 +3893,17 @@ DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
   if (lane < NV) {
     double s = 0.0;
     int r = 0;
+#ifdef MGS_G_GLOBAL
+    // G in HBM: sixteen rows' loads in flight per step (one memory latency per
+    // sixteen terms), same ascending FMA chain
+    for (; r + 16 <= ne; r += 16) {
+      double g[16], f[16];
+#pragma unroll
+      for (int q = 0; q < 16; q++) { g[q] = d.G[(r + q) * GS + lane]; f[q] = d.efc_f[r + q]; }
+#pragma unroll
+      for (int q = 0; q < 16; q++) s = __builtin_fma(g[q], f[q], s);
+    }
+#endif
     // rows in order, four loads in flight per step
     for (; r + 4 <= ne; r += 4) {
       double g0 = d.G[r * GS + lane], g1 = d.G[(r + 1) * GS + lane], g2 = d.G[(r + 2) * GS + lane],

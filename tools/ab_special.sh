@@ -8,5 +8,5 @@ O=gpurun_out/ab
 mkdir -p $O
 for r in a b c; do for v in "$@"; do
   MGS_SPECIAL_OBJECT=$PWD/mj-grasp-sim_amd/mgs/_lib/ab/$v.hsaco timeout -k 10 120 python3 bench.py --cpu-budget 0 --e2e-steps 0 --steps 20 > $O/$v.$r.json 2>$O/$v.$r.err || { tail $O/$v.$r.err; exit 1; }
-  python3 -c "import json; d=json.loads(open('$O/$v.$r.json').read().strip().splitlines()[-1]); print('$v.$r', round(d['value']), round(d['detail']['rollout_kernel_ms'],1), d['detail']['static_layout_kernel'])"
+  python3 -c "import json; d=json.loads(open('$O/$v.$r.json').read().strip().splitlines()[-1]); print('$v.$r', round(d['value']), round(d['detail']['rollout_kernel_ms'],1), d['detail']['static_layout_kernel'], 'stable', d['detail']['stable'], 'free', d['detail']['collision_free'])"
 done; done

@@ -3,7 +3,7 @@ call (mgs/cli/filter_to_stable.py:39-50): host pose processing, the mask
 launch, the stability call's plan building, its rollout launch(es), the rest.
 GPU box; prints one line per stage (median of 5 calls after 2 warm-up calls).
 
-    python tools/api_breakdown.py [slices]"""
+    python tools/api_breakdown.py [yield_every]"""
 import os
 import sys
 import time
@@ -24,7 +24,7 @@ def main():
     env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
                                     get_object("003_cracker_box"))
     if len(sys.argv) > 1:
-        env.SLICES = int(sys.argv[1])
+        env.YIELD_EVERY = int(sys.argv[1])
     h = HORIZONS["h200"]
     H, J, _ = robotiq_candidates(env.obj, 8192, seed=0)
     poses = SE3Pose.from_mat(H)
@@ -45,7 +45,7 @@ def main():
             rows.append(np.diff(t) * 1e3)
     m = np.median(np.array(rows), 0)
     names = ["initial_state (host SE3, 8192)", "collision_free (upload, launch, download)",
-             "rollout_plan (host SE3 + schedule, %d)" % len(idx), "env.rollout (%d slices)" % env.SLICES]
+             "rollout_plan (host SE3 + schedule, %d)" % len(idx), "env.rollout (rotation every %d steps)" % env.YIELD_EVERY]
     for n, v in zip(names, m):
         print(f"{n:48s} {v:8.2f} ms")
     print(f"{'total':48s} {m.sum():8.2f} ms  -> {8192 / m.sum() * 1e3:.0f} candidates/s; "

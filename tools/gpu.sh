@@ -17,10 +17,12 @@
 #   n2        2-rank launcher rehearsal on one GPU (gloo) with the shard check
 #   trace     rocprofv3 --kernel-trace --stats of the driver's command
 #   pmc       PMC passes (FETCH / WRITE / SQ / VALU) on a one-pipeline bench
+#   pmclds    PMC passes on LDS conflicts / waits and scalar work (one-pipeline bench)
 #   stages    stage timers (MGS_PROFILE builds): headline and Shadow pile
 #   heavy     stage timers over the 64 heaviest rollouts of the headline batch
 #   configs   tools/bench_configs.py (C3, C4, C5)
 #   c5big     C5 at 3000 + 3000 steps on 10 240 candidates, rotation on / off
+#   c5ab:a,b  C5 (600 + 600) on the listed mgs/_lib/ab objects (MGS_SPECIAL_OBJECT)
 #   py:<file> python3 <file> (a probe script under tools/)
 # Outputs: gpurun_out/<tag>/
 set -o pipefail
@@ -125,6 +127,16 @@ for step in "$@"; do
         SQ_WAVES -d $O/pmc_lane -o pmc -f csv -- python3 $P1 > $O/pmc_lane.json 2> $O/pmc_lane.err \
         || fail pmc_lane $O/pmc_lane.err
       echo "pmc ok" ;;
+    pmclds)
+      # LDS pressure of the rollout kernel: bank / address conflicts, waits, in-flight level
+      export TMPDIR=/tmp
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT \
+        SQ_LDS_UNALIGNED_STALL SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INST_LEVEL_LDS SQ_WAVE_CYCLES \
+        -d $O/pmc_lds -o pmc -f csv -- python3 $P1 > $O/pmc_lds.json 2> $O/pmc_lds.err || fail pmc_lds $O/pmc_lds.err
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM \
+        SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC \
+        -d $O/pmc_sca -o pmc -f csv -- python3 $P1 > $O/pmc_sca.json 2> $O/pmc_sca.err || fail pmc_sca $O/pmc_sca.err
+      echo "pmclds ok" ;;
     stages)
       timeout -k 10 300 python3 tools/stage_profile.py 160 > $O/stages.txt 2>&1 || fail stages $O/stages.txt
       tail -3 $O/stages.txt
@@ -146,6 +158,15 @@ for step in "$@"; do
           > $O/c5big_y$y.jsonl 2> $O/c5big_y$y.err || fail c5big $O/c5big_y$y.err
         cut -c1-400 $O/c5big_y$y.jsonl
       done ;;
+    c5ab:*)
+      # C5 (600 + 600, 1280 candidates: one round of 48 rollouts, i.e. their latency) on
+      # each listed object of mgs/_lib/ab (MGS_SPECIAL_OBJECT), interleaved twice
+      objs=${step#c5ab:}
+      for r in a b; do for v in ${objs//,/ }; do
+        MGS_SPECIAL_OBJECT=$PWD/mj-grasp-sim_amd/mgs/_lib/ab/$v.hsaco timeout -k 10 300 python3 tools/bench_configs.py c5 \
+          > $O/c5ab_$v.$r.jsonl 2> $O/c5ab_$v.$r.err || fail "$step" $O/c5ab_$v.$r.err
+        python3 -c "import json; d=json.loads(open('$O/c5ab_$v.$r.jsonl').read().strip().splitlines()[-1]); print('$v.$r', round(d['value'],1), 'cand/s, rollout ms', round(d['rollout_kernel_ms'],1), 'stable', d['stable'], 'free', d['collision_free'])"
+      done; done ;;
     py:*)
       f=${step#py:}
       b=$(basename "$f" .py)
