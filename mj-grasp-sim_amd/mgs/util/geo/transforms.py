@@ -19,23 +19,10 @@ from scipy.spatial.transform import Rotation
 from mgs.util.geo.operations import quaternion_apply, quaternion_invert
 
 
-def _host_threads():
-    """CPUs this process may use: the affinity mask, capped by a cgroup CPU
-    quota when one is set (the GPU boxes show 256 CPUs under a quota of 16)"""
-    n = len(os.sched_getaffinity(0))
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, per = f.read().split()[:2]
-        if q != "max":
-            n = min(n, max(1, int(int(q) // int(per))))
-    except (OSError, ValueError):
-        pass
-    return n
-
-
 # large pose batches: scipy's from_matrix (an SVD per float32 matrix) over
-# row blocks on up to 8 threads (np.linalg.svd releases the GIL)
-_PAR_MIN, _PAR_CHUNKS = 2048, max(1, min(8, _host_threads()))
+# row blocks on 4 threads; 8 measured slower on the GPU box (GIL contention:
+# 12.3 -> 18.4 ms for 8192 poses, profiles/r04o_api_breakdown.txt)
+_PAR_MIN, _PAR_CHUNKS = 2048, 4
 _POOL = None
 
 
