@@ -140,6 +140,45 @@ def test_shadow_pile_capacity_escalation(senv, scand):
         assert np.array_equal(res[k], ro[k]), k
 
 
+@pytest.mark.gpu
+def test_shadow_pile_rotation_and_escalation(senv, scand):
+    """the wide build's in-launch rotation (G in HBM, four rows per lane): a
+    work-queue grid of 3 workgroups over the pile candidates with a yield every
+    7 steps, starting at 16 contacts so the escalation continues the capped
+    candidates from their records -- every output equals one workgroup per
+    candidate without rotation, candidates yielded and no ring spin expired"""
+    _init_torch()
+    from mgs.env.clutter_table import ClutterTableEnv
+    poses, J = scand
+    st = senv.get_state()
+    small = ClutterTableEnv.from_dict(senv.to_dict(), ncon_max=16)
+    idx = np.nonzero(senv.grasp_collision_mask(poses, J))[0][:8]
+    plan = small.stable_plan(poses[idx], J[idx], st, nstep_lift=60, close_steps=60)
+    # the main engine (16 contacts) and the escalation's (32 .. 128): the
+    # capped candidates stop within a few steps at 16, so the later stages
+    # are the ones that run long enough to rotate
+    engines = [small.engine_for_state(st, ncon_max=c) for c in (16, 32, 64, 128)]
+    L = engines[0].lib
+
+    def stats():
+        q = [e.queue_stats() for e in engines]
+        return sum(a for a, _ in q), sum(b for _, b in q)
+    prev = L.mgs_rollout_queue(-1)
+    try:
+        L.mgs_rollout_queue(0)
+        one = small.rollout(plan, st, yield_every=0)
+        y0, s0 = stats()
+        L.mgs_rollout_queue(3)
+        rot = small.rollout(plan, st, yield_every=7)
+        y1, s1 = stats()
+    finally:
+        L.mgs_rollout_queue(prev)
+    assert len(idx) > 3
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(rot[k], one[k]), k
+    assert y1 > y0 and s1 == s0 == 0
+
+
 @pytest.fixture(scope="module")
 def genv():
     from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
