@@ -150,7 +150,14 @@ __shared__ unsigned long long s_prof[67];
 #define PCNT(k, v)
 #define PROF_FLUSH
 #endif
-#ifdef MGS_WSYNC_FENCE
+// Lane-to-lane hand-off inside the one-wave workgroup.  Main build: every
+// such hand-off goes through LDS, whose operations a wave issues and the LDS
+// processes in order, so a wavefront-scope fence (it keeps the compiler from
+// moving memory operations across it) is enough: +1 % on the bench, -1 % on
+// one API launch (profiles/r04v_wavefront_fence_ab.txt).  Wide build (G in
+// HBM: rows written by lanes over rows and read by lanes over dofs through
+// global memory): the workgroup barrier, which waits for the stores.
+#if defined(MGS_WSYNC_FENCE) || (!defined(MGS_G_GLOBAL) && !defined(MGS_WSYNC_BARRIER))
 DEVI void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 #else
 DEVI void wsync() { __syncthreads(); }
