@@ -68,14 +68,26 @@ def executed_steps(labels, fail_step, active, horizon):
     return int(np.sum(np.where(active, s, 0)))
 
 
+def pmc_record():
+    """the committed PMC pass (profiles/pmc_rollout.json) and a label of where it
+    came from -- its numbers are read from that file, not measured in this run"""
+    p = os.path.join(ROOT, "profiles", "pmc_rollout.json")
+    if not os.path.isfile(p):
+        return None, None
+    with open(p) as f:
+        j = json.load(f)
+    m = j.get("measured") or {}
+    label = ("stored: profiles/pmc_rollout.json, rocprofv3 PMC pass %s (commit %s, %s) on a one-pipeline bench, "
+             "per candidate-step scaled to this launch" % (m.get("tag", "?"), m.get("commit", "?"), m.get("date", "?")))
+    return j, label
+
+
 def load_traffic(launch_steps):
     """HBM bytes per rollout launch from the committed PMC pass (profiles/), scaled
     to this launch's candidate-steps; None if no PMC summary is present."""
-    p = os.path.join(ROOT, "profiles", "pmc_rollout.json")
-    if not os.path.isfile(p):
+    j, _ = pmc_record()
+    if j is None:
         return None
-    with open(p) as f:
-        j = json.load(f)
     per_cs = j.get("hbm_bytes_per_candidate_step")
     return None if per_cs is None else float(per_cs) * launch_steps
 
@@ -152,11 +164,9 @@ def issue_summary():
     """latency / issue view of the rollout kernel from the committed PMC pass
     (profiles/pmc_rollout.json): instructions and wave cycles per executed
     candidate-step; None if absent"""
-    p = os.path.join(ROOT, "profiles", "pmc_rollout.json")
-    if not os.path.isfile(p):
+    j, label = pmc_record()
+    if j is None:
         return None
-    with open(p) as f:
-        j = json.load(f)
     sq, cs = j.get("sq", {}), j.get("executed_candidate_steps")
     if not sq or not cs:
         return None
@@ -183,7 +193,7 @@ def issue_summary():
                                         "SQ_INSTS_VALU_TRANS_F64"))
     if f64 and sq.get("SQ_INSTS_VALU"):
         out["f64_arith_share_of_valu"] = f64 / sq["SQ_INSTS_VALU"]
-    out["source"] = "profiles/pmc_rollout.json (" + j.get("kernel", "") + ")"
+    out["source"] = label + " (" + j.get("kernel", "") + ")"
     return out
 
 
@@ -386,7 +396,7 @@ def main():
             # outputs.  Nothing runs between two rollouts of a pipeline's
             # stream, and the pipeline never waits for its side stream.
             self.wide = Engine(env.model, device=local, ncon_max=2 * env.ncon_max,
-                               specialize="cached") if args.escalate else None
+                               specialize="cached", role="escalation") if args.escalate else None
             self.esc_stream = torch.cuda.Stream(dev)
             self.esc = []          # per step: list (header + indices), label, fail, objq, stats, resume records
             self.events = []
@@ -501,6 +511,15 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # in-launch rotation audit (outside the timed region): no ring spin expired
+    # in any pipeline's launches and no candidate kept the MGS_FAIL_YIELDED
+    # sentinel (a lost candidate) -- else the line is not printed
+    from mgs.core.engine import check_no_lost_candidates
+    qs = [p.eng.queue_stats() for p in pipes]
+    for p in pipes:
+        check_no_lost_candidates(p.fail.cpu().numpy(), sum(x[1] for x in qs))
+    rotation = {"yields": int(sum(x[0] for x in qs)), "expired_spins": int(sum(x[1] for x in qs)),
+                "lost_candidates": 0}
     t = torch.tensor([dt], dtype=torch.float64, device="cpu" if shared else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -572,6 +591,10 @@ def main():
     alg = algorithmic_bytes(env.model, steps_exec, int(stats[:, 4].sum()), int(stats[:, 5].sum()))
     roll_avg = float(np.mean(roll_ms))
     achieved = alg / (roll_avg * 1e-3) / 1e9
+    # the same bytes over the step time: the device-level rate with the
+    # --streams launches in flight (a launch's span overlaps the others')
+    achieved_device = alg / (dt / args.steps) / 1e9
+    _, pmc_label = pmc_record()
     traffic = load_traffic(steps_exec)
     out = {
         "metric": "grasp candidates evaluated/sec at 200-step horizon, Robotiq2F85xYCB",
@@ -601,6 +624,7 @@ def main():
                    "shard_check": shard_check,
                    "end_to_end_api": e2e,
                    "issue": issue_summary(),
+                   "rotation": rotation,
                    "rollout_kernel_ms": roll_avg, "collision_kernel_ms": float(np.mean(coll_ms)),
                    "executed_candidate_steps": steps_exec,
                    "mean_ncon": float(stats[:, 4].sum() / max(1, steps_exec)),
@@ -616,8 +640,17 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
+                     "traffic_source": pmc_label,
                      "kernel": "mgs_special_rollout" if env.engine.static_layout() else "mgs_rollout_kernel",
-                     "algorithmic_bytes_per_launch": alg},
+                     "algorithmic_bytes_per_launch": alg,
+                     "launch_ms_hip_events": roll_avg,
+                     "launches_in_flight": len(pipes),
+                     "achieved_device": achieved_device,
+                     "frac_device": achieved_device / HBM_PEAK_GBS,
+                     "what": "achieved = SURVEY 8(d) bytes of one main rollout launch (its executed "
+                             "candidate-steps) / that launch's mean duration from HIP events on its stream; "
+                             "achieved_device = the same bytes / ms_per_step (launches overlap); the escalation "
+                             "re-runs are mgs_special_rollout_esc in a trace"},
         "cpu_baseline": None,
     }
     if world == 1 and args.cpu_budget > 0:

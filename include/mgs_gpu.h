@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 19
+#define MGS_ABI_VERSION 20
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -51,6 +51,9 @@ extern "C" {
 #define MGS_EHIP (-2)
 #define MGS_ECAPACITY (-3)
 #define MGS_ENOMEM (-4)
+#define MGS_EQUEUE (-5)     /* a rotating launch's ring protocol timed out (an expired spin, see
+                               mgs_queue_stats): a candidate may have been lost; the outputs of
+                               that launch are not valid (the rings are reset) */
 
 /* joint types (MuJoCo mjtJoint numbering) */
 #define MGS_JNT_FREE 0
@@ -86,6 +89,13 @@ extern "C" {
 #define MGS_FLAG_PAUSED 8          /* reached mgs_schedule.pause_step unfinished: stopped there with a
                                       resume record (fail_step -4), continued by a later launch */
 #define MGS_MAXVAL 1e10
+
+/* fail_step values below -1 (label 0): -2 collision-mask reject (not simulated), -3 stopped at a
+ * capacity overflow with a resume record, -4 paused at mgs_schedule.pause_step, and
+ * MGS_FAIL_YIELDED: the sentinel a yielding candidate writes before it joins the launch's rotation
+ * ring (ABI 20).  Its continuation overwrites it, so it survives a launch only if the candidate was
+ * lost -- never in a correct run; callers of the device entries treat it as an error. */
+#define MGS_FAIL_YIELDED (-5)
 
 /* narrowphase of a geom pair (pair_kind) */
 #define MGS_PAIR_CONVEX 0          /* general convex path: MPR + feature clipping (mjc_Convex role) */
@@ -449,7 +459,13 @@ int mgs_rollout_grid(mgs_batch* batch, int n);
 /* In-launch rotation counters of a batch (ABI 19), cumulative over its
  * launches: out[0] yields (a candidate handed its slot to a waiting one),
  * out[1] expired ring spins (0 unless the rotation protocol is broken; see
- * mgs_schedule.yield_every).  Synchronises the device. */
+ * mgs_schedule.yield_every).  Synchronises the device.  The synchronous
+ * entries (mgs_rollout, mgs_rollout_resume) check out[1] after their launch
+ * themselves and fail with MGS_EQUEUE if it grew (ABI 20); callers of the
+ * device entries check it (or the MGS_FAIL_YIELDED sentinel) after theirs.
+ * The rotation rings are sized for the largest n a batch has launched with
+ * rotation (grown, with a device synchronisation, when a launch's n exceeds
+ * it), whatever the batch capacity. */
 int mgs_queue_stats(mgs_batch* batch, uint64_t* out);
 /* Rollout launch mode for this process; returns the previous one and leaves it
  * unchanged if mode < 0.  0: one workgroup per candidate; 1 (default): the work

@@ -189,8 +189,11 @@ struct mgs_batch {
   int qslot;                        // ring head / tail, ring address), one per launch in a ring of
                                     // MGS_QUEUE_RING (launches in flight on other streams keep their
                                     // own); each launch's last workgroup returns its counters to zero
-  uint32_t* d_rings;                // rotation rings (ABI 19), MGS_QRING_F(cap) words per header,
-                                    // allocated on the first launch with yield_every > 0
+  uint32_t* d_rings;                // rotation rings (ABI 19), MGS_QRING_F(ring_n) words per header,
+  int ring_n;                       // allocated on the first launch with yield_every > 0 and grown
+                                    // when a launch's n exceeds ring_n (the kernel indexes a ring by
+                                    // its launch's n, which may exceed the batch capacity: ADVICE r4)
+  uint64_t spins_seen;              // expired ring spins already reported (mgs_queue_stats word 7)
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
 };
@@ -410,13 +413,25 @@ int mgs_collision_free(mgs_batch* b, int n, const double* qpos_init, const doubl
   return MGS_OK;
 }
 
-// the rotation rings of every queue header (zeroed; each header's words 4-5
-// get its ring's address).  Synchronous, once per batch.
-static int alloc_rings(mgs_batch* b) {
-  const size_t per = MGS_QRING_F(b->cap);
-  HIPCHK(hipDeviceSynchronize());   // no launch holds a header's cache line while words 4-5 are written
+// the rotation rings of every queue header for launches of up to n
+// candidates (zeroed; each header's words 4-5 get its ring's address; a
+// launch over n indexes MGS_QRING_F(n) words of its ring).  Synchronous: on
+// the first rotating launch, and again whenever a launch's n exceeds the n the
+// rings were sized for (the old rings are freed once no launch uses them).
+static int alloc_rings(mgs_batch* b, int n) {
+  if (b->d_rings && b->ring_n >= n) return MGS_OK;
+  const size_t per = MGS_QRING_F(n);
+  HIPCHK(hipDeviceSynchronize());   // no launch holds a header or a ring while they are replaced
+  if (b->d_rings) {
+    HIPCHK(hipFree(b->d_rings));
+    b->d_rings = nullptr;
+    b->ring_n = 0;
+  }
   if (hipMalloc(&b->d_rings, sizeof(uint32_t) * per * MGS_QUEUE_RING) != hipSuccess) {
     b->d_rings = nullptr;
+    uint64_t z = 0;
+    for (int k = 0; k < MGS_QUEUE_RING; k++)      // no header may point at the freed rings
+      HIPCHK(hipMemcpy(b->d_queue + MGS_QHDR * k + 4, &z, sizeof(z), hipMemcpyHostToDevice));
     return fail(MGS_ENOMEM, "rotation ring allocation failed%s");
   }
   HIPCHK(hipMemset(b->d_rings, 0, sizeof(uint32_t) * per * MGS_QUEUE_RING));
@@ -425,7 +440,38 @@ static int alloc_rings(mgs_batch* b) {
     HIPCHK(hipMemcpy(b->d_queue + MGS_QHDR * k + 4, &a, sizeof(a), hipMemcpyHostToDevice));
   }
   HIPCHK(hipDeviceSynchronize());
+  b->ring_n = n;
   return MGS_OK;
+}
+
+// the expired-spin counters (word 7 of every queue header), summed
+static int expired_spins(mgs_batch* b, uint64_t* out) {
+  uint32_t h[MGS_QHDR * MGS_QUEUE_RING];
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(h, b->d_queue, sizeof(h), hipMemcpyDeviceToHost));
+  uint64_t e = 0;
+  for (int k = 0; k < MGS_QUEUE_RING; k++) e += h[MGS_QHDR * k + 7];
+  *out = e;
+  return MGS_OK;
+}
+
+// after a rotating launch of a synchronous entry: an expired ring spin (a
+// candidate possibly lost, a ring slot possibly written after its launch
+// ended) fails the call with MGS_EQUEUE and resets every ring and ring
+// head / tail, so the next launch starts from a clean protocol state
+static int check_rotation(mgs_batch* b) {
+  if (!b->d_rings) return MGS_OK;
+  uint64_t e = 0;
+  int rc = expired_spins(b, &e);
+  if (rc) return rc;
+  if (e == b->spins_seen) return MGS_OK;
+  b->spins_seen = e;
+  HIPCHK(hipMemset(b->d_rings, 0, sizeof(uint32_t) * MGS_QRING_F(b->ring_n) * MGS_QUEUE_RING));
+  for (int k = 0; k < MGS_QUEUE_RING; k++)
+    HIPCHK(hipMemset(b->d_queue + MGS_QHDR * k + 2, 0, 2 * sizeof(uint32_t)));
+  HIPCHK(hipDeviceSynchronize());
+  return fail(MGS_EQUEUE, "rotation ring protocol timed out (expired spin): a candidate may have been lost; "
+                          "the launch's outputs are invalid%s");
 }
 
 static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const double* d_qpos_init,
@@ -453,8 +499,8 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
       nwg = r;
       slot = b->qslot++ % MGS_QUEUE_RING;
       q = b->d_queue + MGS_QHDR * slot;
-      if (sched->yield_every > 0 && d_resume_out && !b->d_rings) {
-        int rrc = alloc_rings(b);
+      if (sched->yield_every > 0 && d_resume_out) {
+        int rrc = alloc_rings(b, n);
         if (rrc) return rrc;
       }
     }
@@ -640,6 +686,7 @@ static int rollout_host(mgs_batch* b, const mgs_schedule* sched, int n, const do
                           b->d_objq, b->d_stats, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                           out->resume ? b->d_resume : nullptr, resume_in ? b->d_resume : nullptr);
   if (rc) return rc;
+  if (sched->yield_every > 0 && (rc = check_rotation(b))) return rc;
   HIPCHK(hipMemcpy(out->label, b->d_label, n, hipMemcpyDeviceToHost));
   if (out->fail_step) HIPCHK(hipMemcpy(out->fail_step, b->d_fail, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   if (out->obj_qpos) HIPCHK(hipMemcpy(out->obj_qpos, b->d_objq, sizeof(double) * n * 7, hipMemcpyDeviceToHost));
@@ -962,9 +1009,15 @@ int mgs_model_attach_special(mgs_model* m, const char* path) {
   };
   int rc = check();
   hipFunction_t fc = nullptr, fr = nullptr;
-  if (rc == MGS_OK && (hipModuleGetFunction(&fc, mod, "mgs_special_collision") != hipSuccess ||
-                       hipModuleGetFunction(&fr, mod, "mgs_special_rollout") != hipSuccess))
+  // main-role objects name their kernels mgs_special_*, escalation-role ones
+  // mgs_special_*_esc (mgs_special.hip)
+  if (rc == MGS_OK && !((hipModuleGetFunction(&fc, mod, "mgs_special_collision") == hipSuccess &&
+                         hipModuleGetFunction(&fr, mod, "mgs_special_rollout") == hipSuccess) ||
+                        (hipModuleGetFunction(&fc, mod, "mgs_special_collision_esc") == hipSuccess &&
+                         hipModuleGetFunction(&fr, mod, "mgs_special_rollout_esc") == hipSuccess))) {
+    (void)hipGetLastError();
     rc = fail(MGS_EINVAL, "code object %s lacks the specialised kernels", path);
+  }
   if (rc != MGS_OK) {
     hipModuleUnload(mod);
     return rc;

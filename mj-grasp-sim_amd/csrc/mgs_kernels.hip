@@ -994,16 +994,16 @@ DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
 // support of mjGEOM_CYLINDER): the rim point along dl's radial part on the cap
 // dl points to, (0, 0, +-h) along the axis; dl is uniform, so is the result
 DEVI void cyl_support(double* v, const double* cy, const double* dl) {
+  // MuJoCo's operation order (dir / length * size) and mju_sign (0 at 0)
   double rho = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
   if (rho > K_MINVAL) {
-    double s = cy[0] / rho;
-    v[0] = dl[0] * s;
-    v[1] = dl[1] * s;
+    v[0] = dl[0] / rho * cy[0];
+    v[1] = dl[1] / rho * cy[0];
   } else {
     v[0] = 0.0;
     v[1] = 0.0;
   }
-  v[2] = dl[2] >= 0.0 ? cy[1] : -cy[1];
+  v[2] = dl[2] > 0.0 ? cy[1] : (dl[2] < 0.0 ? -cy[1] : 0.0);
 }
 
 DEVI void sup_cached(SupAcc& a, int n, const double* cached, const double* dl) {
@@ -2178,8 +2178,16 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
         for (int i = 0; i < 3; i++) pos[i] = deep_c[i] - (0.5 * deep) * nr[i];
         add_contact(d, ncmax, pair, g1, g2, pos, n, t1, t2, deep);
       } else {
+        // an edge on a face (exactly two penetrating vertices): one contact at
+        // the deeper vertex (oracle collide_boxbox, round 5: the set that
+        // reproduces MuJoCo's recorded Robotiq state_close)
         int sel[4], ns;
-        select4(pts, dep, np, sel, &ns);
+        if (np == 2) {
+          ns = 1;
+          sel[0] = dep[1] > dep[0] ? 1 : 0;
+        } else {
+          select4(pts, dep, np, sel, &ns);
+        }
         for (int q = 0; q < ns; q++) {
           const P2* p = &pts[sel[q]];
           double pos[3];
@@ -2528,12 +2536,13 @@ DEVI int add_row(const Mdl& md, Dat& d, int type, double pos, double margin, int
   return r;
 }
 
-// lane 0 only
+// lane 0 only; ipos: the violation the impedance is taken at (the row's own
+// efc_pos, or an equality constraint's violation norm, eq_violation_norm)
 DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, const double* si,
-                           const double* mu, int elliptic_contact) {
+                           const double* mu, int elliptic_contact, double ipos) {
   const double dt = md.m.timestep;
   double tc = sr[0], dr = sr[1];
-  double imp = impedance(si, d.efc_pos[r], d.efc_margin[r]);
+  double imp = impedance(si, ipos, d.efc_margin[r]);
   double dmax = si[1];
   double B, Kc;
   if (tc > 0.0) {
@@ -2562,6 +2571,23 @@ DEVI void row_params(const Mdl& md, Dat& d, int r, int dim, const double* sr, co
       d.efc_R[r + j] = Rj < K_MINVAL ? K_MINVAL : Rj;
     }
   }
+}
+
+// the norm of an equality constraint's violation over all of its rows (a
+// connect's 3, a weld's 6, a joint equality's 1), summed in row order: the
+// impedance of every row of the constraint is taken at it (oracle
+// eq_violation_norm; round 5, the choice that reproduces MuJoCo's recorded
+// Robotiq state_close)
+DEVI double eq_violation_norm(const Dat& d, int r) {
+  const int id = d.efc_con[r];
+  int q = r;
+  while (q > 0 && d.efc_type[q - 1] == MGS_EFC_EQUALITY && d.efc_con[q - 1] == id) q--;
+  double s2 = 0.0;
+  for (; d.efc_type[q] == MGS_EFC_EQUALITY && d.efc_con[q] == id; q++) {
+    s2 = s2 + d.efc_pos[q] * d.efc_pos[q];
+    if (q + 1 >= d.NEFC) break;
+  }
+  return sqrt(s2);
 }
 
 // MuJoCo mj_diagApprox from the qpos0 inverse weights (oracle diag_approx()); lane 0
@@ -2990,15 +3016,16 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   for (int r = lane; r < ne; r += WAVE) {
     int t = d.efc_type[r], id = d.efc_con[r];
     if (t == MGS_EFC_EQUALITY) {
-      row_params(md, d, r, 1, DA(md, eq_solref) + 2 * id, DA(md, eq_solimp) + 5 * id, nullptr, 0);
+      row_params(md, d, r, 1, DA(md, eq_solref) + 2 * id, DA(md, eq_solimp) + 5 * id, nullptr, 0,
+                 eq_violation_norm(d, r));
     } else if (t == MGS_EFC_FRICTION) {
-      row_params(md, d, r, 1, DA(md, dof_solref) + 2 * id, DA(md, dof_solimp) + 5 * id, nullptr, 0);
+      row_params(md, d, r, 1, DA(md, dof_solref) + 2 * id, DA(md, dof_solimp) + 5 * id, nullptr, 0, d.efc_pos[r]);
     } else if (t == MGS_EFC_LIMIT) {
-      row_params(md, d, r, 1, DA(md, jnt_solref) + 2 * id, DA(md, jnt_solimp) + 5 * id, nullptr, 0);
+      row_params(md, d, r, 1, DA(md, jnt_solref) + 2 * id, DA(md, jnt_solimp) + 5 * id, nullptr, 0, d.efc_pos[r]);
     } else if (efc_lead(d, r)) {
       int p = d.con_pair[id];
       row_params(md, d, r, d.efc_dim[r], DA(md, pair_solref) + 2 * p, DA(md, pair_solimp) + 5 * p,
-                 d.con_mu + 5 * id, 1);
+                 d.con_mu + 5 * id, 1, d.efc_pos[r]);
     }
   }
   wsync();
@@ -4651,12 +4678,20 @@ DEVI void save_record(const Mdl& md, Dat& d, double* rec, int p, int t, int gste
 // next candidate, [1] exits, [2] ring head, [3] ring tail, [4..5] the ring's
 // address (set by the host when it allocates the rings; MGS_QRING_F(n) words,
 // candidate + 1, 0 = empty), [6] yields and [7] expired spins, both
-// cumulative over the batch's launches (mgs_queue_stats; an expired spin --
-// a bug, never seen -- keeps the candidate on its workgroup or, on the pop
-// side, loses the slot's candidate, whose outputs then stay unwritten).
+// cumulative over the batch's launches (mgs_queue_stats).  An expired spin
+// -- a protocol error, never seen -- keeps the candidate on its workgroup
+// (push side) or loses the slot's candidate (pop side).  A lost candidate is
+// never silent (ABI 20): a yielding candidate marks its outputs with the
+// MGS_FAIL_YIELDED sentinel before it joins the ring (its continuation
+// overwrites them), and the host entries compare word 7 after every launch
+// and fail with MGS_EQUEUE when it grew.  The ring holds MGS_QRING_F(n)
+// words for the launch's n (the host sizes the rings for the largest n it
+// launched, so a ring slot index never leaves its allocation).
 #define MGS_QHDR 8
 #define MGS_QRING_F(n) (2u * (uint32_t)(n))
+#ifndef MGS_SPIN_MAX
 #define MGS_SPIN_MAX (1u << 22)
+#endif
 
 DEVI uint32_t* ring_of(const uint32_t* q) { return (uint32_t*)((const uint64_t*)q)[2]; }
 
@@ -4715,6 +4750,9 @@ DEVI int ring_pop(uint32_t* q, int n) {
         if (v) { c = (int)(v - 1u); break; }
         __builtin_amdgcn_s_sleep(4);
       }
+#ifdef MGS_TEST_DROP_POP
+      c = -1;     // fault injection (tests only): every pop expires and loses its candidate
+#endif
       if (c < 0) __hip_atomic_fetch_add(q + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -4791,9 +4829,13 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
     if (lane == 0) {
       d.time[0] = tail[0];
       d.ITERS = (int)tail[8];
-      // a yielded candidate keeps its flags; a capacity escalation or a time
-      // slice by relaunch starts the continued run's flags afresh
-      if (from_ring) d.OVERFLOW = (int)tail[9];
+      // a yielded candidate keeps its flags, a paused one (time slice by
+      // relaunch) keeps them without the pause (a capacity flag of a capped
+      // run that paused stays, as in one launch); a capacity escalation starts
+      // the continued run's flags afresh (the wider run is not capped there)
+      const int fl = (int)tail[9];
+      if (from_ring) d.OVERFLOW = fl;
+      else if (fl & MGS_FLAG_PAUSED) d.OVERFLOW = fl & ~MGS_FLAG_PAUSED;
     }
     p0 = (int)tail[1]; t0 = (int)tail[2]; gstep = (int)tail[3];
     maxcon = (int)tail[4]; maxefc = (int)tail[5]; sumcon = (int)tail[6]; sumefc = (int)tail[7];
@@ -4812,6 +4854,12 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
         since = 0;
         if (queue_waiting(yq, n)) {
           save_record(md, d, resume_out + (size_t)i * RS, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
+          // the sentinel a lost candidate would keep (its continuation, ordered
+          // after the push's release, overwrites it)
+          if (lane == 0) {
+            label[i] = 0;
+            if (fail_step) fail_step[i] = MGS_FAIL_YIELDED;
+          }
           if (ring_push(yq, n, i)) {
             ok = 0;
             fstep = -5;
@@ -4824,9 +4872,10 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
         // time slice (ABI 18): the state entering this step, the schedule
         // position and the partial stats go to the resume record, exactly as
         // for a capacity stop, and a later launch continues from there
-        save_record(md, d, resume_out + (size_t)i * RS, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
+        // (the record carries the pause flag: its relaunch keeps the flags)
         if (lane == 0) d.OVERFLOW |= MGS_FLAG_PAUSED;
         wsync();
+        save_record(md, d, resume_out + (size_t)i * RS, p, t, gstep, maxcon, maxefc, sumcon, sumefc);
         ok = 0;
         fstep = -4;
         break;

@@ -25,6 +25,18 @@
 #error "mgs_special.hip is compiled with -DMGS_SPECIAL=<generated header>"
 #endif
 
+// kernel symbols by role: an escalation engine's object (mgs/core/special.py,
+// role "escalation": -DMGS_SPECIAL_ESC) names its kernels *_esc, so a trace
+// tells the capacity escalation's re-runs from the main launches
+// (mgs_model_attach_special accepts either)
+#ifdef MGS_SPECIAL_ESC
+#define MGS_SPECIAL_COLLISION mgs_special_collision_esc
+#define MGS_SPECIAL_ROLLOUT mgs_special_rollout_esc
+#else
+#define MGS_SPECIAL_COLLISION mgs_special_collision
+#define MGS_SPECIAL_ROLLOUT mgs_special_rollout
+#endif
+
 extern "C" {
 
 // what the object was compiled for, read back by mgs_model_attach_special
@@ -36,7 +48,7 @@ __device__ mgs_model_desc mgs_special_desc = mgs_sl_desc;
 __device__ int mgs_special_words[L_COUNT + U_COUNT + 4] = MGS_SL_WORDS_INIT;
 
 __global__ void __launch_bounds__(64)
-mgs_special_collision(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
+MGS_SPECIAL_COLLISION(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay, int n,
                       const double* __restrict__ qpos_init, const double* __restrict__ mocap_pos,
                       const double* __restrict__ mocap_quat, int predicate, uint8_t* __restrict__ out) {
   extern __shared__ double smem[];
@@ -44,7 +56,7 @@ mgs_special_collision(Mdl mdarg, const int32_t* __restrict__ mI, const double* _
 }
 
 __global__ void __launch_bounds__(64) MGS_ROLL_ATTR
-mgs_special_rollout(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
+MGS_SPECIAL_ROLLOUT(Mdl mdarg, const int32_t* __restrict__ mI, const double* __restrict__ mD, Lay lay,
                     mgs_schedule sc, int n, const double* __restrict__ qpos_init,
                     const double* __restrict__ mocap_quat, const double* __restrict__ phase_start,
                     const double* __restrict__ phase_target, const uint8_t* __restrict__ active,

@@ -189,15 +189,28 @@ def _check(rc, what, lib=None):
         raise EngineError(f"{what} failed ({rc}): {msg}")
 
 
+def check_no_lost_candidates(fail_step, expired_spins=0):
+    """raise if a rotating launch lost a candidate: its fail_step still holds
+    the MGS_FAIL_YIELDED sentinel it wrote when it joined the ring (ABI 20), or
+    the batch's expired-spin counter grew (mgs_queue_stats out[1]; callers of
+    the device entries pass the growth over their launches)"""
+    lost = np.nonzero(np.asarray(fail_step) == abi.MGS["MGS_FAIL_YIELDED"])[0]
+    if len(lost) or expired_spins:
+        raise EngineError(f"in-launch rotation lost {len(lost)} candidate(s) (first {lost[:8].tolist()}), "
+                          f"{int(expired_spins)} expired ring spin(s): the launch's outputs are invalid")
+
+
 class Engine:
     """One compiled model resident on one GPU plus a reusable batch."""
 
-    def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None, specialize=None):
+    def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None, specialize=None, role="main"):
         """specialize: True = attach the model-specialised code object, compiling
         it if it is not cached; "cached" = attach it only if cached; False = the
         library's runtime-layout kernels.  Default (None): MGS_SPECIALIZE from the
         environment ("1" / "cached" / "0"), else "cached".  A dof count the
-        library has no kernel for always specialises (compiling if needed)."""
+        library has no kernel for always specialises (compiling if needed).
+        role: the object's role (mgs.core.special.ROLE_FLAGS): "escalation" for
+        the capacity escalation's engines (kernel symbols *_esc in traces)."""
         if nefc_max is None:
             nefc_max = default_rows(cm, int(cm.pack(ncon_max=ncon_max)[0]["nefc_max"]))
         fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
@@ -224,7 +237,7 @@ class Engine:
                 specialize = False
         if specialize:
             from mgs.core import special
-            path = special.code_object(self.lib, self.desc, compile=specialize is True)
+            path = special.code_object(self.lib, self.desc, compile=specialize is True, role=role)
             if path is not None:
                 self._ck(self.lib.mgs_model_attach_special(self._model, path.encode()), "mgs_model_attach_special")
 
@@ -328,6 +341,9 @@ class Engine:
                                                ptr(mq, ctypes.c_double), ptr(ps, ctypes.c_double),
                                                ptr(pt, ctypes.c_double), ptr(rs, ctypes.c_double),
                                                ctypes.byref(out)), "mgs_rollout_resume")
+        # (an expired rotation spin already failed the call with MGS_EQUEUE; the
+        # sentinel is the second, independent guard against a lost candidate)
+        check_no_lost_candidates(fail)
         res = dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats,
                    kernel_ms=self.lib.mgs_last_kernel_ms(self._batch))
         if rec is not None:

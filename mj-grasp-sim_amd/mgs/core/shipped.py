@@ -56,9 +56,10 @@ def spread_pile(gripper_name: str, object_ids: Sequence[str]):
     return env
 
 
-def shipped_engines() -> List[Tuple[object, int, object]]:
-    """(compiled model, ncon_max, nefc_max or None) of the engines the shipped
-    configurations and the GPU tests create first"""
+def shipped_engines() -> List[Tuple[object, int, object, str]]:
+    """(compiled model, ncon_max, nefc_max or None, object role) of the engines
+    the shipped configurations and the GPU tests create first (role: see
+    mgs.core.special.ROLE_FLAGS)"""
     from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
     from mgs.gripper.selector import get_gripper
     from mgs.obj.selector import get_object
@@ -69,15 +70,18 @@ def shipped_engines() -> List[Tuple[object, int, object]]:
                        ("AllegroGripper", ["Synthetic_Mug_Body"])):
         for o in objs:
             env = GravitylessObjectGrasping(get_gripper({"name": grip}), get_object(o))
-            out.append((env.model, env.ncon_max, env.nefc_max))
+            out.append((env.model, env.ncon_max, env.nefc_max, "main"))
             if grip == "Robotiq2f85Gripper":
                 # the headline's escalation engine (twice the contacts, rows as
                 # Engine() sizes them): its re-runs then run specialised too
-                out.append((env.model, 2 * env.ncon_max, None))
+                out.append((env.model, 2 * env.ncon_max, None, "escalation"))
+                # the rotation fault-injection object of the GPU tests (every
+                # ring pop expires: the product must raise, not return labels)
+                out.append((env.model, env.ncon_max, env.nefc_max, "fault"))
     env = pile_env("ShadowHand")
     if os.path.isfile(C5_SCENE):
         env.set_state(np.load(C5_SCENE)["state"])
     scenes = [env] + [spread_pile(g, objs) for g, objs in SPREAD_PILES]
     for env in scenes:
-        out.append((env.model_for(env.get_state()), env.ncon_max, env._nefc_max))
+        out.append((env.model_for(env.get_state()), env.ncon_max, env._nefc_max, "main"))
     return out

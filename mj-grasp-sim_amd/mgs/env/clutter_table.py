@@ -241,7 +241,8 @@ class ClutterTableEnv:
             self._engines = {k: v for k, v in self._engines.items() if k[1:] == key[1:]}
             # escalation capacities re-run few candidates: specialised only if cached
             self._engines[key] = Engine(cm, device=self.device, ncon_max=nc, nefc_max=self._nefc_max,
-                                        specialize=None if nc == self.ncon_max else "cached")
+                                        specialize=None if nc == self.ncon_max else "cached",
+                                        role="main" if nc == self.ncon_max else "escalation")
         return self._engines[key]
 
     # -- reference helpers ---------------------------------------------------

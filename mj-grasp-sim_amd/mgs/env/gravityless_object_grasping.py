@@ -157,7 +157,8 @@ class GravitylessObjectGrasping:
             from mgs.core.engine import Engine
             # the few overflowing candidates: a specialised object only if one is
             # cached (compiling one would cost more than the re-run)
-            self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max, specialize="cached")
+            self._wide[ncon_max] = Engine(self.model, device=self.device, ncon_max=ncon_max, specialize="cached",
+                                          role="escalation")
         return self._wide[ncon_max]
 
     # in-launch rotation (mgs_schedule.yield_every, ABI 19): a batch with more

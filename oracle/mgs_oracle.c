@@ -644,16 +644,16 @@ void oracle_sep_enable(int on) { g_sep_log = on; g_sep_n = 0; }
  * mjGEOM_CYLINDER, engine_collision_convex.c): the rim point along the radial
  * part of dl, on the cap dl points to; (0, 0, +-h) when dl is along the axis */
 static void cyl_support(double* v, const double* cy, const double* dl) {
+  // MuJoCo's operation order (dir / length * size) and mju_sign (0 at 0)
   double rho = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
   if (rho > O_MINVAL) {
-    double s = cy[0] / rho;
-    v[0] = dl[0] * s;
-    v[1] = dl[1] * s;
+    v[0] = dl[0] / rho * cy[0];
+    v[1] = dl[1] / rho * cy[0];
   } else {
     v[0] = 0.0;
     v[1] = 0.0;
   }
-  v[2] = dl[2] >= 0.0 ? cy[1] : -cy[1];
+  v[2] = dl[2] > 0.0 ? cy[1] : (dl[2] < 0.0 ? -cy[1] : 0.0);
 }
 
 static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, double* out) {
@@ -1199,6 +1199,20 @@ static int bb_clip(P2* Q, int nq, int axis, double lim, double sgn) {
   return no;
 }
 
+/* Which points a face contact of the box-box collider emits.  0 = the
+ * contract (the kernels' collide_boxbox): the penetrating clipped vertices of
+ * the incident face, reduced to <= 4 by select4, except that an edge on a face
+ * (exactly two penetrating vertices) gives one contact at the deeper vertex --
+ * the set that reproduces MuJoCo's recorded Robotiq state_close (round 5,
+ * tests/test_oracle.py::test_state_close_contact_set_study).
+ * Study variants (never the product's): 1 = the round-4 contract (both edge
+ * vertices kept), 2 = every clipped vertex of the incident face at its own
+ * signed distance (the face-overlap corners, non-penetrating ones included),
+ * 3 = the single deepest vertex always, 4 = one contact at the centroid of
+ * the penetrating vertices at the deepest depth. */
+static int g_bbmode = 0;
+void oracle_set_bbmode(int mode) { g_bbmode = mode; }
+
 static void collide_boxbox(const Mdl* md, Dat* d, int pair) {
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
   const double *R1 = d->geom_xmat + 9 * g1, *R2 = d->geom_xmat + 9 * g2;
@@ -1318,7 +1332,7 @@ static void collide_boxbox(const Mdl* md, Dat* d, int pair) {
   double mtol = BB_MERGE * (hA[ku] > hA[kv] ? hA[ku] : hA[kv]);
   mtol = mtol * mtol;
   for (int i = 0; i < nq; i++) {
-    if (!(poly[i].h < margin)) continue;
+    if (!(poly[i].h < margin) && g_bbmode != 2) continue;
     int dup = 0;
     for (int q = 0; q < np; q++) if (dist2d(&pts[q], &poly[i]) < mtol) dup = 1;
     if (!dup) { pts[np] = poly[i]; dep[np] = -poly[i].h; np++; }
@@ -1331,8 +1345,29 @@ static void collide_boxbox(const Mdl* md, Dat* d, int pair) {
     add_contact(md, d, pair, g1, g2, pos, n, t1, t2, deep);
     return;
   }
-  int sel[4], ns;
-  select4(pts, dep, np, sel, &ns);
+  int sel[16], ns;
+  if (g_bbmode == 0 && np == 2) {
+    ns = 1;
+    sel[0] = dep[1] > dep[0] ? 1 : 0;
+  } else if (g_bbmode == 2) {
+    ns = np;
+    for (int q = 0; q < np; q++) sel[q] = q;
+  } else if (g_bbmode == 3) {
+    ns = 1;
+    sel[0] = 0;
+    for (int q = 1; q < np; q++) if (dep[q] > dep[sel[0]]) sel[0] = q;
+  } else if (g_bbmode == 4) {
+    /* one contact at the centroid of the penetrating vertices, deepest depth */
+    P2 c = pts[0];
+    double dm = dep[0];
+    for (int q = 1; q < np; q++) { c.x = c.x + pts[q].x; c.y = c.y + pts[q].y; if (dep[q] > dm) dm = dep[q]; }
+    c.x = c.x / np; c.y = c.y / np; c.h = -dm;
+    pts[0] = c;
+    ns = 1;
+    sel[0] = 0;
+  } else {
+    select4(pts, dep, np, sel, &ns);
+  }
   for (int q = 0; q < ns; q++) {
     const P2* p = &pts[sel[q]];
     double pos[3];
@@ -1481,11 +1516,29 @@ static int add_row(Dat* d, int type, double pos, double margin, int dim, int con
 }
 
 /* reference acceleration and regularizer for rows r..r+dim-1 sharing solref/solimp */
+/* The violation an equality row's impedance is taken at.  0 = the contract
+ * (the kernels' eq_violation_norm): the norm of its constraint's violation over
+ * all of the constraint's rows (a connect's 3, a weld's 6, a joint equality's
+ * 1), summed in row order -- with the box-box edge rule above, the choice that
+ * reproduces MuJoCo's recorded Robotiq state_close (round 5).  1 = the round-4
+ * contract, each row's own violation (study variant). */
+static int g_eqimp = 0;
+void oracle_set_eqimp(int mode) { g_eqimp = mode; }
+
+static double eq_violation_norm(const Dat* d, int r, int neqrows) {
+  int e = d->efc_con[r];
+  double s2 = 0.0;
+  for (int q = 0; q < neqrows; q++)
+    if (d->efc_con[q] == e) s2 = s2 + d->efc_pos[q] * d->efc_pos[q];
+  return sqrt(s2);
+}
+
+/* ipos: the violation the impedance is taken at */
 static void row_params(const Mdl* md, Dat* d, int r, int dim, const double* sr, const double* si,
-                       const double* mu, int elliptic_contact) {
+                       const double* mu, int elliptic_contact, double ipos) {
   const double dt = md->m->timestep;
   double tc = sr[0], dr = sr[1];
-  double imp = impedance(si, d->efc_pos[r], d->efc_margin[r]);
+  double imp = impedance(si, ipos, d->efc_margin[r]);
   double dmax = si[1];
   double B, Kc;
   if (tc > 0.0) {
@@ -1704,24 +1757,25 @@ static void make_constraints(const Mdl* md, Dat* d) {
   const double *eqsr = DA(md, eq_solref), *eqsi = DA(md, eq_solimp);
   for (int r = 0; r < neqrows; r++) {
     int e = d->efc_con[r];
-    row_params(md, d, r, 1, eqsr + 2 * e, eqsi + 5 * e, NULL, 0);
+    row_params(md, d, r, 1, eqsr + 2 * e, eqsi + 5 * e, NULL, 0,
+               g_eqimp == 1 ? d->efc_pos[r] : eq_violation_norm(d, r, neqrows));
   }
   const double *dsr = DA(md, dof_solref), *dsi = DA(md, dof_solimp);
   for (int r = fr0; r < fr1; r++) {
     int k = d->efc_con[r];
-    row_params(md, d, r, 1, dsr + 2 * k, dsi + 5 * k, NULL, 0);
+    row_params(md, d, r, 1, dsr + 2 * k, dsi + 5 * k, NULL, 0, d->efc_pos[r]);
   }
   const double *jsr = DA(md, jnt_solref), *jsi = DA(md, jnt_solimp);
   for (int r = lr0; r < lr1; r++) {
     int j = d->efc_con[r];
-    row_params(md, d, r, 1, jsr + 2 * j, jsi + 5 * j, NULL, 0);
+    row_params(md, d, r, 1, jsr + 2 * j, jsi + 5 * j, NULL, 0, d->efc_pos[r]);
   }
   const double *psr = DA(md, pair_solref), *psi = DA(md, pair_solimp);
   for (int r = cr0; r < cr1;) {
     int c = d->efc_con[r];
     int p = d->con_pair[c];
     int dim = d->efc_dim[r];
-    row_params(md, d, r, dim, psr + 2 * p, psi + 5 * p, d->efc_mu + 5 * r, 1);
+    row_params(md, d, r, dim, psr + 2 * p, psi + 5 * p, d->efc_mu + 5 * r, 1, d->efc_pos[r]);
     r += dim;
   }
   for (int r = 0; r < ne; r++) {
@@ -2780,11 +2834,13 @@ double oracle_tree_dot(const double* a, const double* b, int n) { return tree_do
 
 /* Debug hook: one forward() at a given state with a given solver; returns
  * nefc and copies efc_f (nefc), qacc (nv), types/dims and the Newton/PGS
- * iteration count. */
+ * iteration count; optionally the rows' G, aref, R | b, and pos | margin |
+ * diagApprox | vel (4 nefc). */
 int oracle_forward_debug(const mgs_model_desc* desc, const int32_t* I, const double* D, const double* qpos,
                          const double* qvel, const double* qacc_ws, const double* mocap_pos,
                          const double* mocap_quat, const double* ctrl, int solver, double* f_out, double* qacc_out,
-                         int32_t* type_out, int32_t* iters_out, double* G_out, double* aref_out, double* R_out) {
+                         int32_t* type_out, int32_t* iters_out, double* G_out, double* aref_out, double* R_out,
+                         double* pos_out) {
   mgs_model_desc m2 = *desc;
   m2.solver = solver;
   Mdl md = {&m2, I, D};
@@ -2801,6 +2857,12 @@ int oracle_forward_debug(const mgs_model_desc* desc, const int32_t* I, const dou
   if (G_out) memcpy(G_out, d->K, sizeof(double) * ne * desc->nv);
   if (aref_out) memcpy(aref_out, d->efc_aref, sizeof(double) * ne);
   if (R_out) { memcpy(R_out, d->efc_R, sizeof(double) * ne); memcpy(R_out + ne, d->efc_b, sizeof(double) * ne); }
+  if (pos_out) {   /* efc_pos, efc_margin, efc_diagApprox, efc_vel */
+    memcpy(pos_out, d->efc_pos, sizeof(double) * ne);
+    memcpy(pos_out + ne, d->efc_margin, sizeof(double) * ne);
+    memcpy(pos_out + 2 * ne, d->efc_dA, sizeof(double) * ne);
+    memcpy(pos_out + 3 * ne, d->efc_vel, sizeof(double) * ne);
+  }
   *iters_out = d->iters;
   dat_free(d);
   return ne;

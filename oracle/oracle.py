@@ -46,6 +46,8 @@ def lib():
         L.oracle_sincos.argtypes = [P(c_d), ctypes.c_int, P(c_d), P(c_d)]
         L.oracle_tree_dot.argtypes = [P(c_d), P(c_d), ctypes.c_int]
         L.oracle_tree_dot.restype = c_d
+        L.oracle_set_bbmode.argtypes = [ctypes.c_int]
+        L.oracle_set_eqimp.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
 
@@ -130,6 +132,25 @@ class OracleModel:
                                phase_start=mp, phase_target=mp)
         r = self.simulate_batch(plan, vclip=vclip)
         return r["qpos"][0], r["qvel"][0], r["qacc_warmstart"][0]
+
+    def forward_debug(self, qpos, mocap_pos, mocap_quat, ctrl, qvel=None, qacc_ws=None, solver=2):
+        """one forward() at a state (oracle_forward_debug): the constraint rows'
+        forces, types (efc_type), dims, R, b, aref, and qacc"""
+        L = lib()
+        P, d, i32 = ctypes.POINTER, ctypes.c_double, ctypes.c_int32
+        L.oracle_forward_debug.argtypes = [P(abi.ModelDesc), P(i32), P(d)] + [P(d)] * 6 + [ctypes.c_int] + \
+            [P(d), P(d), P(i32), P(i32), P(d), P(d), P(d), P(d)]
+        nv, cap = self.cm.nv, int(self.desc.nefc_max)
+        f, qa, ty, it = np.zeros(cap), np.zeros(nv), np.zeros(cap, np.int32), np.zeros(1, np.int32)
+        R, ar, pm = np.zeros(2 * cap), np.zeros(cap), np.zeros(4 * cap)
+        z = np.zeros(nv)
+        a = [np.ascontiguousarray(x, np.float64) for x in
+             (qpos, z if qvel is None else qvel, z if qacc_ws is None else qacc_ws, mocap_pos, mocap_quat, ctrl)]
+        ne = L.oracle_forward_debug(*self._args(), *[ptr(x, d) for x in a], int(solver), ptr(f, d), ptr(qa, d),
+                                    ptr(ty, i32), ptr(it, i32), None, ptr(ar, d), ptr(R, d), ptr(pm, d))
+        return dict(nefc=ne, force=f[:ne], type=ty[:ne] // 16, dim=ty[:ne] % 16, R=R[:ne], b=R[ne:2 * ne],
+                    aref=ar[:ne], pos=pm[:ne], margin=pm[ne:2 * ne], diag=pm[2 * ne:3 * ne],
+                    vel=pm[3 * ne:4 * ne], qacc=qa, iters=int(it[0]))
 
     def contacts(self, qpos, mocap_pos, mocap_quat, maxc=64):
         pos = np.zeros((maxc, 3)); fr = np.zeros((maxc, 9)); dist = np.zeros(maxc); g = np.zeros((maxc, 2), np.int32)
@@ -251,3 +272,10 @@ def contact_loss_grad(desc, prm, targets, normals):
     g = np.zeros(len(p))
     loss = _contact_lib().oracle_contact_loss_grad(ctypes.byref(desc), ptr(p, d), ptr(T, d), ptr(N, d), ptr(g, d))
     return loss, g
+
+
+def set_study_variant(bbmode=0, eqimp=0):
+    """the state_close study's model variants (mgs_oracle.c oracle_set_bbmode /
+    oracle_set_eqimp); (0, 0) is the contract the kernels follow"""
+    lib().oracle_set_bbmode(int(bbmode))
+    lib().oracle_set_eqimp(int(eqimp))

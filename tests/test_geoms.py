@@ -161,8 +161,12 @@ def test_box_resting_on_box_four_corners():
     assert np.allclose(p[:, 2], 0.01975, atol=1e-15)
 
 
-def test_tilted_box_edge_on_face_two_contacts():
-    # box rotated about x by 0.2 rad: its lowest edge (along x) is the contact
+def test_tilted_box_edge_on_face_one_contact():
+    # box rotated about x by 0.2 rad: its lowest edge (along x) is the contact.
+    # An edge on a face (two penetrating clipped vertices) gives one contact at
+    # the deeper vertex (round 5: the set that reproduces MuJoCo's recorded
+    # Robotiq state_close, tests/test_oracle.py::test_state_close_contact_set_study);
+    # both are equally deep here, so the first in clipping order
     a = 0.2
     hz, hy = 0.005, 0.015
     zlow = -(hy * np.sin(a) + hz * np.cos(a))
@@ -170,11 +174,21 @@ def test_tilted_box_edge_on_face_two_contacts():
     z = 0.02 - zlow - depth
     q = f"{np.cos(a / 2)} {np.sin(a / 2)} 0 0"
     n, p, fr, dist = contacts('<geom type="box" size="0.01 0.015 0.005"/>', f"0 0 {z}", q)
-    assert n == 2
+    assert n == 1
     assert np.allclose(dist, -depth, atol=1e-12)
     assert np.allclose(fr[:, :3], [0, 0, 1], atol=1e-12)
-    assert np.allclose(sorted(p[:, 0]), [-0.01, 0.01], atol=1e-12)
+    assert np.isclose(abs(p[0, 0]), 0.01, atol=1e-12)
     assert np.allclose(p[:, 2], 0.02 - depth / 2, atol=1e-12)
+    # tilted about y as well: the deeper end of the edge
+    b = 0.01
+    qa = np.array([np.cos(a / 2), np.sin(a / 2), 0, 0])
+    qb = np.array([np.cos(b / 2), 0, np.sin(b / 2), 0])
+    w1, x1, y1, z1 = qb
+    w2, x2, y2, z2 = qa
+    qq = [w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+          w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2]
+    n, p, fr, dist = contacts('<geom type="box" size="0.01 0.015 0.005"/>', f"0 0 {z}", " ".join(map(str, qq)))
+    assert n == 1 and dist[0] < -depth and p[0, 0] > 0.0
 
 
 def test_crossed_ridges_edge_edge_contact():

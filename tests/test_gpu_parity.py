@@ -662,3 +662,128 @@ def test_time_slices_equal_one_launch(env, candidates, oracle_model, horizon, n,
 def abi_flag(name):
     from mgs.core.abi import MGS
     return MGS[name]
+
+
+def test_time_slices_keep_capacity_flags(env, candidates):
+    """with the last escalation stage from the first launch
+    (ncon_max = max_ncon = 4, capped_continue), a capped candidate that pauses
+    at a slice boundary keeps its capacity flag in the relaunch (the record
+    carries MGS_FLAG_PAUSED and the resumed run restores its flags without it),
+    so slices equal one launch in every output, res['overflow'] included"""
+    from conftest import plan_for
+    from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping
+    e4 = GravitylessObjectGrasping(env.gripper, env.obj, ncon_max=4)
+    poses, J = candidates
+    q, mp, mq, _ = e4.initial_state(poses, J)
+    idx = np.nonzero(e4.engine.collision_free(q, mp, mq))[0][:96]
+    plan = plan_for(e4, poses[idx], J[idx])
+    one = e4.rollout(plan, max_ncon=4, slices=1)
+    assert one["overflow"] > 0
+    for k in (2, 3, 7):
+        r = e4.rollout(plan, max_ncon=4, slices=k)
+        _assert_same(r, one, f"{k} slices, capped")
+        assert r["overflow"] == one["overflow"]
+
+
+def _device_run(eng, plan, q, mp, n, sched, dev):
+    import torch
+    from mgs.core import abi
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+    o = dict(free=torch.zeros(n, dtype=torch.uint8, device=dev), lab=torch.zeros(n, dtype=torch.uint8, device=dev),
+             fail=torch.zeros(n, dtype=torch.int32, device=dev),
+             objq=torch.zeros((n, 7), dtype=torch.float64, device=dev),
+             st=torch.zeros((n, abi.MGS["MGS_NSTATS"]), dtype=torch.int32, device=dev))
+    rec = torch.zeros((n, eng.resume_width()), dtype=torch.float64, device=dev)
+    ins = [t(a) for a in (q, mp, plan.mocap_quat, plan.phase_start, plan.phase_target)]
+    eng.mask_rollout_device(sched, n, *[x.data_ptr() for x in ins], o["free"].data_ptr(), o["lab"].data_ptr(),
+                            o["fail"].data_ptr(), o["objq"].data_ptr(), o["st"].data_ptr(),
+                            d_resume_out=rec.data_ptr())
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in o.items()}
+
+
+def test_rotation_rings_sized_by_launch_n(env):
+    """a fresh engine's batch holds 256 candidates, but a
+    device launch over n = 1024 rotates through rings indexed modulo 2n; the
+    rings are sized for the launch's n (grown on demand), so a rotating launch
+    over more candidates than the batch capacity equals one workgroup per
+    candidate bit for bit with no expired spin"""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi
+    from mgs.core.engine import Engine, check_no_lost_candidates
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    n = 1024
+    H, J, _ = robotiq_candidates(env.obj, n, seed=3)
+    P = SE3Pose.from_mat(H)
+    q, mp, mq, _ = env.initial_state(P, J)
+    plan = plan_for(env, P, J)
+    fresh = Engine(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+    assert fresh.specialized()
+    sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr)
+    dev = torch.device("cuda", 0)
+    L = fresh.lib
+    prev = L.mgs_rollout_queue(-1)
+    try:
+        L.mgs_rollout_queue(0)
+        ref = _device_run(fresh, plan, q, mp, n, sched, dev)
+        sched.yield_every = 5
+        L.mgs_rollout_queue(48)
+        for _ in range(2):
+            got = _device_run(fresh, plan, q, mp, n, sched, dev)
+            for k in ref:
+                assert np.array_equal(ref[k], got[k]), k
+    finally:
+        L.mgs_rollout_queue(prev)
+    y, s = fresh.queue_stats()
+    assert y > 0 and s == 0
+    check_no_lost_candidates(got["fail"], s)
+    fresh.close()
+
+
+def test_lost_rotation_candidate_raises(env, candidates):
+    """verdict r4 item 3: a rotation that loses a candidate must not return
+    stale labels.  A fault-injection object (role "fault", -DMGS_TEST_DROP_POP:
+    every ring pop expires and drops the candidate it took) makes the env's
+    rollout raise EngineError (mgs_rollout fails with MGS_EQUEUE), and on the
+    device path the lost candidates keep the MGS_FAIL_YIELDED sentinel that
+    check_no_lost_candidates reports; the same engine runs correctly after
+    the reset (rotation off)"""
+    import torch
+    from conftest import plan_for
+    from mgs.core import abi, special
+    from mgs.core.engine import Engine, EngineError, check_no_lost_candidates
+    from mgs.env.gravityless_object_grasping import sliced_rollout
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(env.engine.collision_free(q, mp, mq))[0][:64]
+    plan = plan_for(env, poses[idx], J[idx])
+    bad = Engine(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max, specialize=False)
+    path = special.code_object(bad.lib, bad.desc, compile=False, role="fault")
+    assert path is not None, "the fault-injection object is built by __graft_entry__.build()"
+    bad._ck(bad.lib.mgs_model_attach_special(bad._model, path.encode()), "mgs_model_attach_special")
+    L = bad.lib
+    prev = L.mgs_rollout_queue(-1)
+    try:
+        L.mgs_rollout_queue(8)
+        with pytest.raises(EngineError, match="rotation"):
+            sliced_rollout(plan, bad, lambda c: bad, env.ncon_max, env.ncon_max, 1, yield_every=7)
+        # device path: the sentinel marks the lost candidates
+        n = len(q)
+        plan_all = plan_for(env, poses, J)
+        sched = abi.make_schedule(plan_all.nsteps, plan_all.check_every, plan_all.check_at_end, plan_all.ctrl,
+                                  plan_all.obj_qposadr)
+        sched.yield_every = 7
+        y0, s0 = bad.queue_stats()
+        got = _device_run(bad, plan_all, q, mp, n, sched, torch.device("cuda", 0))
+        y1, s1 = bad.queue_stats()
+        assert s1 > s0 and (got["fail"] == abi.MGS["MGS_FAIL_YIELDED"]).any()
+        with pytest.raises(EngineError, match="lost"):
+            check_no_lost_candidates(got["fail"], s1 - s0)
+        # rotation off: the same engine (rings reset) gives the oracle-checked outputs
+        r = bad.rollout(plan, resumable=True)
+        _assert_same(r, env.engine.rollout(plan), "after the fault")
+    finally:
+        L.mgs_rollout_queue(prev)
+        bad.close()

@@ -31,18 +31,21 @@ class FakeEngine:
                    stats=np.zeros((n, NS), np.int32), resume=np.zeros((n, 4)))
         for k, i in enumerate(ids):
             t0, sc = (int(resume_from[k, 0]), int(resume_from[k, 1])) if resume_from is not None else (0, 0)
-            flags, label, fs = 0, True, -1
+            # a paused record keeps its flags (without the pause); an
+            # escalation's record starts afresh (the C-ABI's resume semantics)
+            rf = int(resume_from[k, 2]) if resume_from is not None else 0
+            flags, label, fs = (rf & ~PAUSED) if rf & PAUSED else 0, True, -1
             t = t0
             while t < H:
                 if pause_step > 0 and t >= pause_step:
-                    out["resume"][k] = (t, sc, 0, 0)
                     flags |= PAUSED
+                    out["resume"][k] = (t, sc, flags, 0)
                     label, fs = False, -4
                     break
                 if self.need[i, t] > self.cap:
                     flags |= CAP
                     if not capped_continue:
-                        out["resume"][k] = (t, sc, 0, 0)
+                        out["resume"][k] = (t, sc, flags, 0)
                         label, fs = False, -3
                         break
                 sc += int(min(self.need[i, t], self.cap))
@@ -109,3 +112,17 @@ def test_escalation_stops_at_max_ncon():
     assert res["overflow"] >= 1 and res["stats"][5, 2] & CAP
     assert res["label"][5] and res["fail_step"][5] == -1
     assert max(c["cap"] for c in log) == 40
+
+
+@pytest.mark.parametrize("slices", [2, 3, 7])
+def test_capped_slices_keep_capacity_flags(slices):
+    """the last escalation stage from the first launch (cap >=
+    max_ncon, capped_continue) with slices: a capped candidate that pauses keeps
+    FLAG_CAPACITY through the relaunch, so res['overflow'] equals one launch's"""
+    need, fail_at, plan = _case(4)
+    one = sliced_rollout(plan, FakeEngine(need, fail_at, 10, []), None, 10, 10, 1)
+    assert one["overflow"] > 0
+    res = sliced_rollout(plan, FakeEngine(need, fail_at, 10, []), None, 10, 10, slices)
+    assert res["overflow"] == one["overflow"]
+    for k in ("label", "fail_step", "obj_qpos", "stats"):
+        assert np.array_equal(res[k], one[k]), k

@@ -25,8 +25,19 @@ PROF = os.path.join(ROOT, "profiles")
 
 
 def rows(path, kernels=("mgs_special_rollout", "mgs_rollout_kernel")):
+    """the main rollout launches' rows (the escalation objects' *_esc kernels excluded)"""
     with open(path) as f:
-        return [r for r in csv.DictReader(f) if any(k in r["Kernel_Name"] for k in kernels)]
+        return [r for r in csv.DictReader(f)
+                if any(k in r["Kernel_Name"] for k in kernels) and "_esc" not in r["Kernel_Name"]]
+
+
+def _commit():
+    import subprocess
+    try:
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=30).stdout.strip() or None
+    except (OSError, subprocess.SubprocessError):
+        return None
 
 
 def main(d, tag="r03"):
@@ -37,7 +48,9 @@ def main(d, tag="r03"):
                      "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate --fused 0` (tools/gpu.sh pmc, "
                      f"{tag}); "
                      "per rollout dispatch",
-           "kernel": "mgs_special_rollout (code object specialised to the headline model)"}
+           "kernel": "mgs_special_rollout (code object specialised to the headline model)",
+           "measured": {"tag": tag, "commit": _commit(),
+                        "date": __import__("time").strftime("%Y-%m-%d", __import__("time").gmtime())}}
     sums = {}
     for name in ("fetch", "write", "sq", "valu", "lane"):
         p = os.path.join(d, f"pmc_{name}", "pmc_counter_collection.csv")
