@@ -1010,13 +1010,16 @@ int mgs_model_attach_special(mgs_model* m, const char* path) {
   int rc = check();
   hipFunction_t fc = nullptr, fr = nullptr;
   // main-role objects name their kernels mgs_special_*, escalation-role ones
-  // mgs_special_*_esc (mgs_special.hip)
-  if (rc == MGS_OK && !((hipModuleGetFunction(&fc, mod, "mgs_special_collision") == hipSuccess &&
-                         hipModuleGetFunction(&fr, mod, "mgs_special_rollout") == hipSuccess) ||
-                        (hipModuleGetFunction(&fc, mod, "mgs_special_collision_esc") == hipSuccess &&
-                         hipModuleGetFunction(&fr, mod, "mgs_special_rollout_esc") == hipSuccess))) {
+  // mgs_special_*_esc (mgs_special.hip).  The lookup of the naming an object
+  // does not use fails by design: its error is cleared here, or the next
+  // launch's hipGetLastError would report it
+  if (rc == MGS_OK) {
+    bool found = (hipModuleGetFunction(&fc, mod, "mgs_special_collision") == hipSuccess &&
+                  hipModuleGetFunction(&fr, mod, "mgs_special_rollout") == hipSuccess) ||
+                 (hipModuleGetFunction(&fc, mod, "mgs_special_collision_esc") == hipSuccess &&
+                  hipModuleGetFunction(&fr, mod, "mgs_special_rollout_esc") == hipSuccess);
     (void)hipGetLastError();
-    rc = fail(MGS_EINVAL, "code object %s lacks the specialised kernels", path);
+    if (!found) rc = fail(MGS_EINVAL, "code object %s lacks the specialised kernels", path);
   }
   if (rc != MGS_OK) {
     hipModuleUnload(mod);

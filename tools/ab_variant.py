@@ -3,7 +3,7 @@
 copied to a scratch tree, optionally edited, compiled for the headline model at
 a given contact capacity.
 
-  python tools/ab_variant.py NAME [--ncon N] [--noinline] [-DFLAG ...]
+  python tools/ab_variant.py NAME [--ncon N] [--noinline] [--src DIR] [-DFLAG ...]
 
 --noinline compiles every DEVI helper as a real call (register analysis and the
 two-waves-per-SIMD experiment); -D flags go to hipcc (e.g.
@@ -29,11 +29,13 @@ def main():
     from mgs.util.geo.transforms import SE3Pose
     args = sys.argv[1:]
     name = args.pop(0)
-    ncon, noinline, extra = 20, False, []
+    ncon, noinline, extra, srcdir = 20, False, [], None
     while args:
         a = args.pop(0)
         if a == "--ncon":
             ncon = int(args.pop(0))
+        elif a == "--src":
+            srcdir = args.pop(0)      # kernel sources from a scratch directory (experiments)
         elif a == "--noinline":
             noinline = True
         else:
@@ -52,7 +54,7 @@ def main():
         os.makedirs(os.path.join(td, "include"))
         shutil.copy(abi.HEADER, os.path.join(td, "include"))
         for f in os.listdir(special.CSRC):
-            shutil.copy(os.path.join(special.CSRC, f), src)
+            shutil.copy(os.path.join(srcdir or special.CSRC, f), src)
         k = os.path.join(src, "mgs_kernels.hip")
         if noinline:
             s = open(k).read()
