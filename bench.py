@@ -271,6 +271,8 @@ def main():
     ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight: pipelines (engine + HIP stream) the steps rotate over")
     ap.add_argument("--ncon-max", type=int, default=20, help="per-candidate contact capacity of the main kernel")
+    ap.add_argument("--nefc-max", type=int, default=None,
+                    help="per-candidate constraint-row capacity of the main kernel (default: auto_capacity)")
     ap.add_argument("--esc-grid", type=int, default=1, help="workgroups of the escalation list re-run")
     ap.add_argument("--esc-side", type=int, default=1, help="1: escalation re-runs on a side stream per pipeline")
     ap.add_argument("--fused", type=int, default=1,
@@ -338,7 +340,7 @@ def main():
 
     grip = GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz"))
     obj = get_object("003_cracker_box")
-    env = GravitylessObjectGrasping(grip, obj, device=local, ncon_max=args.ncon_max)
+    env = GravitylessObjectGrasping(grip, obj, device=local, ncon_max=args.ncon_max, nefc_max=args.nefc_max)
     if args.solver:
         env.model.options["solver"] = args.solver
     h = HORIZONS[args.horizon]

@@ -3,7 +3,7 @@
 copied to a scratch tree, optionally edited, compiled for the headline model at
 a given contact capacity.
 
-  python tools/ab_variant.py NAME [--ncon N] [--noinline] [--src DIR] [-DFLAG ...]
+  python tools/ab_variant.py NAME [--ncon N] [--nefc N] [--noinline] [--src DIR] [-DFLAG ...]
 
 --noinline compiles every DEVI helper as a real call (register analysis and the
 two-waves-per-SIMD experiment); -D flags go to hipcc (e.g.
@@ -29,11 +29,13 @@ def main():
     from mgs.util.geo.transforms import SE3Pose
     args = sys.argv[1:]
     name = args.pop(0)
-    ncon, noinline, extra, srcdir = 20, False, [], None
+    ncon, noinline, extra, srcdir, nefc = 20, False, [], None, None
     while args:
         a = args.pop(0)
         if a == "--ncon":
             ncon = int(args.pop(0))
+        elif a == "--nefc":
+            nefc = int(args.pop(0))
         elif a == "--src":
             srcdir = args.pop(0)      # kernel sources from a scratch directory (experiments)
         elif a == "--noinline":
@@ -41,7 +43,7 @@ def main():
         else:
             extra.append(a)
     env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
-                                    get_object("003_cracker_box"), ncon_max=ncon)
+                                    get_object("003_cracker_box"), ncon_max=ncon, nefc_max=nefc)
     fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
     lib = library_for(env.model.nv, int(fields["nefc_max"]))
     header, flags, _ = special.plan(lib, abi.make_desc(fields))
