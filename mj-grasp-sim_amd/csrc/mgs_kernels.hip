@@ -112,10 +112,30 @@ struct Dat {
 #endif
 #endif
 
-DEVI int lane_id() { return (int)__lane_id(); }
+// the lane index through an opaque move at every use: index arithmetic and
+// lane masks derived from it are recomputed where they are used instead of
+// being hoisted out of the step loop and held (in VGPRs, AGPRs and SGPR
+// spill lanes) for the whole rollout (round 5: the headline rollout 430 ->
+// 328 registers with this alone; profiles/r05c_ab.txt)
+DEVI int lane_id() {
+  int l = (int)__lane_id();
+  asm volatile("" : "+v"(l));
+  return l;
+}
 // values that are uniform across the wave but come from LDS: move to SGPRs so
 // control flow on them is scalar
 DEVI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// wave-wide shuffle from lane src (0..63): HIP's __shfl(x, src) with width 64
+// (ds_bpermute at byte address 4 src), without its lane-index term, so no
+// per-lane address is derived from the lane index and held across the step loop
+DEVI int shfl(int x, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, x); }
+DEVI double shfl(double x, int src) {
+  const int a = src << 2;
+  const int lo = __builtin_amdgcn_ds_bpermute(a, __double2loint(x));
+  const int hi = __builtin_amdgcn_ds_bpermute(a, __double2hiint(x));
+  return __hiloint2double(hi, lo);
+}
 
 // Diagnostic stage timers (built only with -DMGS_PROFILE; never in the product build)
 #ifdef MGS_PROFILE
@@ -616,7 +636,7 @@ DEVI void crb(const Mdl& md, Dat& d) {
         d.M[i * nv + j] = v;
         d.M[j * nv + i] = v;
       }
-      int jn = __shfl(dp_lane, j >= 0 ? j : 0);
+      int jn = shfl(dp_lane, j >= 0 ? j : 0);
       j = j >= 0 ? jn : -1;
     }
   } else {
@@ -1156,7 +1176,7 @@ DEVI void support_pair2(const PairCtx2& c, const double* dir, double* out1, doub
     w[q] = 16 * q + (tr ? __ffs(tr) - 1 : 0);
   }
   const int src = row == 0 ? w[0] : (row == 1 ? w[1] : (row == 2 ? w[2] : w[3]));
-  double v[3] = {__shfl(a.vx, src), __shfl(a.vy, src), __shfl(a.vz, src)};
+  double v[3] = {shfl(a.vx, src), shfl(a.vy, src), shfl(a.vz, src)};
   double t[3], wv[3];
   mulmv3(t, c.R, v);
   add3(wv, c.x, t);
@@ -1164,8 +1184,8 @@ DEVI void support_pair2(const PairCtx2& c, const double* dir, double* out1, doub
   const int s1 = lane & 32, s2 = s1 + 16;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    out1[k] = __shfl(wv[k], s1);
-    out2[k] = __shfl(wv[k], s2);
+    out1[k] = shfl(wv[k], s1);
+    out2[k] = shfl(wv[k], s2);
   }
 }
 
@@ -1629,7 +1649,7 @@ DEVI int clip_poly_wave(const P2* P, int np, P2* Q, int nq, P2* buf) {
   if (nq <= 2) {
     int r = 0;
     if (lane == 0) r = clip_poly(P, np, Q, nq, buf);
-    r = __shfl(r, 0);
+    r = shfl(r, 0);
     wsync();
     return r;
   }
@@ -1898,8 +1918,8 @@ DEVI void collide_manifold(const Mdl& md, Dat& d, const PairCtx& pc, int pair, i
       if (nr < 0) nr = refB ? hull2d(fb, nb, refpoly) : hull2d(fa, na, refpoly);
       if (ni < 0) ni = refB ? hull2d(fa, na, inc) : hull2d(fb, nb, inc);
     }
-    nr = __shfl(nr, 0);
-    ni = __shfl(ni, 0);
+    nr = shfl(nr, 0);
+    ni = shfl(ni, 0);
   }
   wsync();
   PT(48);
@@ -2060,11 +2080,11 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
   int vv[15];
 #pragma unroll
   for (int q = 0; q < 15; q++) {
-    sv[q] = __shfl(s, q);
-    lx[q] = __shfl(L[0], q);
-    ly[q] = __shfl(L[1], q);
-    lz[q] = __shfl(L[2], q);
-    vv[q] = __shfl(valid, q);
+    sv[q] = shfl(s, q);
+    lx[q] = shfl(L[0], q);
+    ly[q] = shfl(L[1], q);
+    lz[q] = shfl(L[2], q);
+    vv[q] = shfl(valid, q);
   }
   if (lane == 0) {
     double best = -INFINITY;
@@ -2253,15 +2273,15 @@ DEVI unsigned long long obb_separated_wave(const Dat& d, unsigned long long am, 
     unsigned long long m = am;      // this group's pair: the grp-th lowest bit
     for (int t = 0; t < grp; t++) m &= m - 1ull;
     int b = m ? __ffsll((long long)m) - 1 : 0;
-    int G1 = __shfl(g1, b), G2 = __shfl(g2, b);
+    int G1 = shfl(g1, b), G2 = shfl(g2, b);
     double Db[3], h1b[3], h2b[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-      Db[i] = __shfl(D[i], b);
-      h1b[i] = __shfl(h1[i], b);
-      h2b[i] = __shfl(h2[i], b);
+      Db[i] = shfl(D[i], b);
+      h1b[i] = shfl(h1[i], b);
+      h2b[i] = shfl(h2[i], b);
     }
-    double mb = __shfl(margin, b);
+    double mb = shfl(margin, b);
     int s = 0;
     if (m && q < 15) s = obb_axis_separated(q, d.geom_xmat + 9 * G1, d.geom_xmat + 9 * G2, Db, h1b, h2b, mb);
     unsigned long long sm = __ballot(s);
@@ -2700,7 +2720,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       int q = q0 + lane;
       int e = q / nv, col = q - e * nv;
       int es = e < nkeep ? e : nkeep - 1;
-      int r = __shfl(re, es), ty = __shfl(typ, es);
+      int r = shfl(re, es), ty = shfl(typ, es);
       if (q < nkeep * nv && ty >= 0) {
         const double* data = ed + 11 * e;
         if (ty == MGS_EQ_JOINT) {
@@ -2956,7 +2976,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       int q = q0 + lane;
       int c = q / nv, col = q - c * nv;
       int cs = c < nkeep ? c : nkeep - 1;
-      int r = __shfl(rc, cs), dim = __shfl(cdim, cs);
+      int r = shfl(rc, cs), dim = shfl(cdim, cs);
       if (q < nkeep * nv) {
         int b1 = gbody[d.con_g1[c]], b2 = gbody[d.con_g2[c]];
         const double* pt = d.con_pos + 3 * c;

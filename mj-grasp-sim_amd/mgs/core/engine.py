@@ -231,10 +231,13 @@ class Engine:
         if not self.lib.mgs_supports_nv(cm.nv):
             specialize = True
         if specialize and os.environ.get("MGS_SPECIAL_OBJECT"):
-            # A/B experiments (tools/ab_special.sh): an explicit object, used by
-            # the engines whose model it was made for (the attach checks that)
-            if self.lib.mgs_model_attach_special(self._model, os.environ["MGS_SPECIAL_OBJECT"].encode()) == 0:
-                specialize = False
+            # A/B experiments (tools/ab_bench.sh): explicit objects (':'-separated),
+            # each used by the engines whose model and capacity it was made for
+            # (the attach checks that)
+            for obj in os.environ["MGS_SPECIAL_OBJECT"].split(":"):
+                if obj and self.lib.mgs_model_attach_special(self._model, obj.encode()) == 0:
+                    specialize = False
+                    break
         if specialize:
             from mgs.core import special
             path = special.code_object(self.lib, self.desc, compile=specialize is True, role=role)

@@ -52,6 +52,7 @@ _JOINT_DEFAULTS = dict(type="hinge", axis="0 0 1", pos="0 0 0", range="0 0",
 _EQ_DEFAULTS = dict(solref="0.02 1", solimp="0.9 0.95 0.001 0.5 2", active="true")
 
 PAIR_CONVEX, PAIR_BOXBOX = 0, 1   # pair_kind: narrowphase used for the pair (mgs_gpu.h MGS_PAIR_*)
+GAIN_PID = 16                      # actuator_gaintype of a mujoco.pid plugin actuator (mgs_gpu.h MGS_GAIN_PID)
 CYL_SIDES = 16   # cylinder collision geoms: 32-vertex prisms (a cap fits one contact feature, K_MAXF)
 _JNT_TYPES = {"free": 0, "ball": 1, "slide": 2, "hinge": 3}
 
@@ -303,6 +304,7 @@ class _Body:
     joints: List[dict] = field(default_factory=list)
     geoms: List[dict] = field(default_factory=list)
     childclass: Optional[str] = None
+    gravcomp: float = 0.0
 
 
 class MJCFError(ValueError):
@@ -324,6 +326,7 @@ class Compiler:
         self.tendons: List[dict] = []
         self.equalities: List[dict] = []
         self.actuators: List[dict] = []
+        self.plugin_instances: Dict[str, dict] = {}   # <extension> instances: plugin, config
         root = ET.fromstring(xml)
         root = self._expand_includes(root)
         self._parse(root)
@@ -367,6 +370,15 @@ class Compiler:
                 self._parse_option(el)
             elif el.tag == "default":
                 self._parse_default(el, "main", top=True)
+            elif el.tag == "extension":
+                # <plugin plugin="..."><instance name="..."><config key= value=/>
+                for pl in el:
+                    if pl.tag != "plugin":
+                        continue
+                    for inst in pl:
+                        if inst.tag == "instance":
+                            cfg = {c.get("key"): c.get("value") for c in inst if c.tag == "config"}
+                            self.plugin_instances[inst.get("name")] = dict(plugin=pl.get("plugin"), config=cfg)
         for el in root:
             if el.tag == "asset":
                 for a in el:
@@ -551,7 +563,8 @@ class Compiler:
                 cc = ch.get("childclass", childclass)
                 b = _Body(ch.get("name", f"body{len(self.bodies)}"), parent,
                           _f(ch.get("pos", "0 0 0"), 3), self._orientation(ch.attrib),
-                          mocap=ch.get("mocap", "false") == "true", childclass=cc)
+                          mocap=ch.get("mocap", "false") == "true", childclass=cc,
+                          gravcomp=float(ch.get("gravcomp", "0")))
                 bid = len(self.bodies)
                 self.bodies.append(b)
                 for sub in ch:
@@ -948,13 +961,33 @@ class Compiler:
             elif tag == "motor":
                 gainprm[0] = 1.0
                 gt, bt = 0, 0
+            elif tag == "plugin":
+                # MuJoCo's mujoco.pid actuator plugin: gains and limits from its
+                # <extension> instance, its state (integral, previous setpoint)
+                # in the actuator's act slots
+                inst = self.plugin_instances.get(a.get("instance", ""))
+                plug = a.get("plugin") or (inst or {}).get("plugin")
+                if inst is None or plug != "mujoco.pid":
+                    raise MJCFError(f"actuator plugin {plug!r} not supported (mujoco.pid instances only)")
+                cfg = inst["config"]
+                pid = np.array([float(cfg.get("kp", "0")), float(cfg.get("ki", "0")), float(cfg.get("kd", "0")),
+                                float(cfg.get("imax", "-1")), float(cfg.get("slewmax", "-1"))])
+                if a.get("dyntype", "none") != "none":
+                    raise MJCFError("mujoco.pid with a dyntype is not supported")
+                nst = int(pid[1] != 0.0) + int(pid[4] >= 0.0)
+                if int(a.get("actdim", str(nst))) != nst:
+                    raise MJCFError(f"mujoco.pid actdim {a.get('actdim')} does not match its state ({nst})")
+                gt, bt = GAIN_PID, 0
             else:
                 raise MJCFError(f"actuator {tag} not supported")
             cr = _f(a.get("ctrlrange", "0 0"), 2)
             fr = _f(a.get("forcerange", "0 0"), 2)
             cl = a.get("ctrllimited", "auto")
             fl = a.get("forcelimited", "auto")
-            acts.append(dict(trn=trn, tid=tid, gt=gt, bt=bt, gainprm=gainprm, biasprm=biasprm,
+            if gt != GAIN_PID:
+                pid = np.zeros(5)
+                nst = 0
+            acts.append(dict(trn=trn, tid=tid, gt=gt, bt=bt, gainprm=gainprm, biasprm=biasprm, pid=pid, actnum=nst,
                              ctrlrange=cr, forcerange=fr,
                              ctrllimited=int(("ctrlrange" in a) if cl == "auto" else cl == "true"),
                              forcelimited=int(("forcerange" in a) if fl == "auto" else fl == "true"),
@@ -1053,6 +1086,19 @@ class Compiler:
         cm.actuator_ctrlrange = np.array([a["ctrlrange"] for a in acts]).reshape(-1, 2)
         cm.actuator_forcerange = np.array([a["forcerange"] for a in acts]).reshape(-1, 2)
         cm.actuator_gear = np.array([a["gear"] for a in acts], np.float64)
+        # actuator state (mujoco.pid: integral, previous setpoint), mjData.act
+        cm.actuator_actnum = np.array([a["actnum"] for a in acts], np.int32)
+        cm.actuator_actadr = np.where(cm.actuator_actnum > 0,
+                                      np.concatenate([[0], np.cumsum(cm.actuator_actnum)[:-1]]) if acts else 0,
+                                      -1).astype(np.int32)
+        cm.nact = int(cm.actuator_actnum.sum()) if acts else 0
+        cm.actuator_pidprm = np.array([a["pid"] for a in acts], np.float64).reshape(-1, 5)
+        # gravity compensation (body gravcomp): supported where it is no force
+        # (zero gravity, the gravityless env); elsewhere refused
+        cm.body_gravcomp = np.array([b.gravcomp for b in self.bodies], np.float64)
+        if np.any(cm.body_gravcomp != 0.0) and np.any(np.asarray(opt["gravity"], np.float64) != 0.0):
+            raise MJCFError("body gravcomp under nonzero gravity is not supported (the engine supports "
+                            "gravity compensation where gravity is zero)")
         cm.body_xpos0 = xpos
         cm.body_xquat0 = xquat
         cm.body_invweight0, cm.dof_invweight0, cm.meaninertia = _invweight0(cm)

@@ -68,6 +68,8 @@ def main():
         cmd = [special._hipcc(), *flags, *extra, f'-DMGS_SPECIAL="{hp}"', os.path.join(src, "mgs_special.hip"),
                "-o", path]
         r = subprocess.run(cmd, capture_output=True, text=True)
+        if os.environ.get("AB_REMARKS"):
+            print("\n".join(x for x in r.stderr.splitlines() if "remark" in x))
         if r.returncode:
             print(r.stderr[-3000:])
             return 1
