@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 20
+#define MGS_ABI_VERSION 21
 #define MGS_NSTATS 6
 
 /* error codes */
@@ -71,6 +71,8 @@ extern "C" {
 #define MGS_TRN_TENDON 3
 #define MGS_GAIN_FIXED 0
 #define MGS_GAIN_AFFINE 1
+#define MGS_GAIN_PID 16            /* MuJoCo's mujoco.pid actuator plugin (ABI 21): force from the
+                                      actuator_pidprm gains and the actuator's act state, see below */
 #define MGS_BIAS_NONE 0
 #define MGS_BIAS_AFFINE 1
 
@@ -123,6 +125,9 @@ typedef struct mgs_model_desc {
   int32_t nwrap;
   int32_t nu;
   int32_t nmocap;
+  int32_t nact;       /* actuator state (mjData.act) entries: 2 per mujoco.pid actuator (ABI 21) */
+  int32_t maxcondim;  /* largest contact dimension of the admissible pairs: 1, 3, 4 or 6 (condim 6:
+                         torsional and rolling friction; runs through a specialised code object) */
   int32_t ncon_max;   /* contact capacity per candidate (set by host) */
   int32_t nefc_max;   /* constraint-row capacity per candidate (set by host) */
   int32_t maxhullvert;
@@ -163,6 +168,8 @@ typedef struct mgs_model_desc {
   int32_t d_body_iquat;     /* 4 */
   int32_t d_body_mass;      /* 1 */
   int32_t d_body_inertia;   /* 3 */
+  int32_t d_body_gravcomp;  /* 1: gravity compensation (ABI 21): the body's weight times this,
+                               cancelled through a force at its centre of mass (passive force) */
   int32_t d_body_invweight0; /* 2: translational, rotational (MuJoCo mj_setConst) */
   int32_t d_dof_invweight0;  /* nv (indexed by dof) */
   /* joints */
@@ -247,6 +254,19 @@ typedef struct mgs_model_desc {
   int32_t d_actuator_ctrlrange; /* 2 */
   int32_t d_actuator_forcerange;/* 2 */
   int32_t d_actuator_gear;      /* 1 */
+  int32_t i_actuator_actadr;    /* first act entry of the actuator, -1 if it has none */
+  int32_t d_act0;               /* nact: the act state every candidate starts from (mj_resetData: 0;
+                                   ClutterTableEnv: the scene state's, clutter_table.py:290-291) */
+  int32_t d_actuator_pidprm;    /* 5: kp, ki, kd, imax, slewmax of a MGS_GAIN_PID actuator (imax,
+                                   slewmax < 0: not set).  Restated from MuJoCo's mujoco.pid plugin
+                                   semantics (parity unpinned: its source is not here): setpoint =
+                                   ctrl clamped to ctrlrange, then, with slewmax, to within
+                                   slewmax * dt of the previous setpoint (act entry 2); error =
+                                   setpoint - actuator length; force = kp error + kd (setpoint rate -
+                                   actuator velocity) + ki integral, clamped to forcerange, where the
+                                   integral (act entry 1) advances by error * dt, clamped so that
+                                   |ki integral| <= imax.  The act entries advance with the step
+                                   (mj_advance: act += dt * act_dot). */
   /* buffer lengths (elements) */
   int32_t isize;
   int32_t dsize;
@@ -298,14 +318,16 @@ typedef struct mgs_rollout_out {
   double* obj_qpos;        /* n * 7: object free-joint qpos when the candidate stopped (may be NULL) */
   int32_t* stats;          /* n * MGS_NSTATS: max ncon, max nefc, overflow flags, total solver
                               iterations, sum of ncon and sum of nefc over executed steps (may be NULL) */
-  double* resume;          /* n * (nq + 2 nv + MGS_RESUME_EXTRA), may be NULL.  When set, a candidate
+  double* resume;          /* n * (nq + 2 nv + nact + MGS_RESUME_EXTRA), may be NULL.  When set, a candidate
                               that exceeds the contact / row capacity stops at that step (fail_step
                               -3) and its record holds the state entering it (qpos, qvel,
                               qacc_warmstart, time) and the schedule position / partial stats, from
                               which mgs_rollout_resume continues it with more capacity */
 } mgs_rollout_out;
 #define MGS_RESUME_EXTRA 10        /* time, phase, step in phase, global step, max ncon, max nefc,
-                                      sum ncon, sum nefc, solver iterations, flags */
+                                      sum ncon, sum nefc, solver iterations, flags.  A record is
+                                      qpos (nq), qvel (nv), qacc_warmstart (nv), act (nact), then
+                                      these (ABI 21: act) */
 
 typedef struct mgs_model mgs_model;
 typedef struct mgs_batch mgs_batch;
@@ -490,9 +512,9 @@ int mgs_antipodal_contacts(int device, const double* tri, int ntri, int n, const
  * is_stable / settle, clutter_table.py:157-222): the rollout loop of `sched`
  * with its contact checks ignored (a free simulation never stops early),
  * starting from qpos_init (n * nq) and, when vstate_init is not NULL,
- * per-state qvel and qacc_warmstart (n * 2nv: qvel then warmstart; NULL = the
- * model's qvel0 / qacc_ws0).  state_out receives n * (nq + 2nv): final qpos,
- * qvel, qacc_warmstart.  stats (may be NULL): n * MGS_NSTATS as in
+ * per-state qvel, qacc_warmstart and act (n * (2nv + nact): qvel, warmstart,
+ * act; NULL = the model's qvel0 / qacc_ws0 and act 0).  state_out receives
+ * n * (nq + 2nv + nact): final qpos, qvel, qacc_warmstart, act.  stats (may be NULL): n * MGS_NSTATS as in
  * mgs_rollout_out; stats[i * MGS_NSTATS + 2] != 0 means state i exceeded the
  * contact / row capacity at some step and should be re-run wider.  Host
  * pointers (mgs_simulate) or device pointers on a stream (mgs_simulate_device,

@@ -38,6 +38,9 @@ int fail(int code, const char* fmt, const char* what = "") {
     if (_e != hipSuccess) return fail(MGS_EHIP, "HIP error: %s", hipGetErrorString(_e)); \
   } while (0)
 
+// the contact dimension the kernels for this model are built for (MGS_MAXDIM)
+int layout_maxdim(const mgs_model_desc& m) { return m.maxcondim > 4 ? 6 : 4; }
+
 // LDS carve-up of one candidate's working set (doubles, then int counters and
 // index arrays).  U is time-multiplexed: collision scratch, then composite
 // inertias / RNE temporaries, then constraint rows (G) + solver scratch, then
@@ -50,6 +53,7 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   int sizes[L_COUNT];
   sizes[L_qpos] = nq; sizes[L_qvel] = nv; sizes[L_qacc_ws] = nv; sizes[L_ctrl] = nu;
   sizes[L_mocap_pos] = 3 * m.nmocap + 3; sizes[L_mocap_quat] = 4 * m.nmocap + 4; sizes[L_time] = 1;
+  sizes[L_act] = m.nact; sizes[L_act_dot] = m.nact;
   sizes[L_xpos] = 3 * nb; sizes[L_xquat] = 4 * nb; sizes[L_xmat] = 9 * nb; sizes[L_subtree_com] = 3 * nb;
   sizes[L_cinert] = 10 * nb; sizes[L_cdof] = 6 * nv;
   sizes[L_M] = nv * nv; sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_sD] = nv; sizes[L_isD] = nv;
@@ -57,7 +61,10 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   sizes[L_qfrc_smooth] = nv; sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv;
   sizes[L_act_force] = nu; sizes[L_act_moment] = nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
   sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = 5 * nc;
-  sizes[L_con_blk] = BLKSTRIDE * nc;
+  // contact blocks (and Newton cone Hessians): maxdim^2 per contact, maxdim 6
+  // for models with condim-6 pairs (their code objects: -DMGS_MAXDIM=6)
+  const int maxdim = layout_maxdim(m);
+  sizes[L_con_blk] = maxdim * maxdim * nc;
   sizes[L_efc_R] = ne; sizes[L_efc_b] = ne; sizes[L_cert] = K_CERT * CERT_W;
   // U: per-stage sub-layouts, each packed from offset 0 (see the kernel's Lay comment)
   int us[U_COUNT];
@@ -76,7 +83,9 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   us[U_scratch] = (2 * ne > nv ? 2 * ne : nv);
   // {vel, pos, margin} (make_constraints) | Newton Hessian, which may run on into
   // the scratch slot (scratch is idle while the Hessian is live)
+  // (the Hessian's weight table, (maxdim + 1) ne, runs on into scratch too)
   int xreg = 3 * ne;
+  if (xreg + us[U_scratch] < (maxdim + 1) * ne) xreg = (maxdim + 1) * ne - us[U_scratch];
   if (xreg + us[U_scratch] < nv * nv) xreg = nv * nv - us[U_scratch];
   us[U_jar] = ne; us[U_jv] = ne; us[U_f] = ne; us[U_Dr] = ne; us[U_isR] = ne;
   us[U_nw] = nv; us[U_nw0] = nv; us[U_ng] = nv; us[U_ndir] = nv;
@@ -184,7 +193,7 @@ struct mgs_batch {
   int32_t *d_fail, *d_stats;
   double* d_G;      // MGS_G_GLOBAL: per-candidate constraint rows (HBM)
   size_t g_elems;
-  double* d_resume; // resume records (n * (nq + 2 nv + MGS_RESUME_EXTRA)), allocated on first use
+  double* d_resume; // resume records (n * (nq + 2 nv + nact + MGS_RESUME_EXTRA)), allocated on first use
   uint32_t* d_queue;                // work-queue headers (MGS_QHDR words: next index, exits, rotation
   int qslot;                        // ring head / tail, ring address), one per launch in a ring of
                                     // MGS_QUEUE_RING (launches in flight on other streams keep their
@@ -213,10 +222,28 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
   if (desc->nmocap > 1) return fail(MGS_EINVAL, "at most one mocap body%s");
   if (desc->nefc_max > 64 * MGS_RPL) return fail(MGS_EINVAL, "nefc_max exceeds this library's rows (mgs_max_rows)%s");
   if (desc->nv > 64) return fail(MGS_EINVAL, "nv must be <= 64 (lanes over dofs)%s");
+  if (desc->maxcondim != 1 && desc->maxcondim != 3 && desc->maxcondim != 4 && desc->maxcondim != 6)
+    return fail(MGS_EINVAL, "maxcondim must be 1, 3, 4 or 6%s");
   for (int p = 0; p < desc->npair; p++) {
     int cd = ibuf[desc->i_pair_condim + p];
-    if (cd != 1 && cd != 3 && cd != 4) return fail(MGS_EINVAL, "condim must be 1, 3 or 4%s");
+    if (cd != 1 && cd != 3 && cd != 4 && cd != 6) return fail(MGS_EINVAL, "condim must be 1, 3, 4 or 6%s");
+    if (cd > desc->maxcondim) return fail(MGS_EINVAL, "a pair's condim exceeds maxcondim%s");
   }
+  if (desc->nact < 0 || desc->nact > 4 * 32) return fail(MGS_EINVAL, "bad nact%s");
+  for (int u = 0, used = 0; u < desc->nu; u++) {
+    const int adr = ibuf[desc->i_actuator_actadr + u];
+    int need = 0;
+    if (ibuf[desc->i_actuator_gaintype + u] == MGS_GAIN_PID) {
+      const double* pp = dbuf + desc->d_actuator_pidprm + 5 * u;
+      need = (pp[4] >= 0.0) + (pp[1] != 0.0);
+    }
+    if (need == 0 ? adr != -1 : adr != used)
+      return fail(MGS_EINVAL, "actuator_actadr: a mujoco.pid actuator's act entries are its slew and integral "
+                              "states, packed in actuator order%s");
+    used += need;
+    if (u == desc->nu - 1 && used != desc->nact) return fail(MGS_EINVAL, "nact differs from the actuators' act entries%s");
+  }
+  if (desc->nu == 0 && desc->nact != 0) return fail(MGS_EINVAL, "nact without actuators%s");
   HIPCHK(hipSetDevice(device));
   mgs_model* m = new mgs_model();
   m->desc = *desc;
@@ -522,6 +549,9 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
   } else {
     const KernelSet* k = kernels_for(md.m.nv);
     if (!k) return fail(MGS_EINVAL, "no kernel for this nv in this library and no specialised code object attached%s");
+    if (layout_maxdim(md.m) > MGS_MAXDIM)
+      return fail(MGS_EINVAL, "condim-6 contacts run through the model's specialised code object only "
+                              "(mgs.core.special); none is attached%s");
     k->rollout(dim3(nwg), b->m->lds_bytes, st, a);
   }
   HIPCHK(hipGetLastError());
@@ -620,9 +650,9 @@ int mgs_simulate(mgs_batch* b, const mgs_schedule* sched, int n, const double* q
   int np = sched->nphase;
   HIPCHK(hipSetDevice(b->m->device));
   double *dv = nullptr, *ds = nullptr;
-  size_t nst = (size_t)n * (d.nq + 2 * d.nv);
+  size_t nst = (size_t)n * (d.nq + 2 * d.nv + d.nact);
   if (hipMalloc(&ds, nst * sizeof(double)) != hipSuccess) return fail(MGS_ENOMEM, "state buffer allocation failed%s");
-  if (vstate_init && hipMalloc(&dv, (size_t)n * 2 * d.nv * sizeof(double)) != hipSuccess) {
+  if (vstate_init && hipMalloc(&dv, (size_t)n * (2 * d.nv + d.nact) * sizeof(double)) != hipSuccess) {
     hipFree(ds);
     return fail(MGS_ENOMEM, "state buffer allocation failed%s");
   }
@@ -631,7 +661,7 @@ int mgs_simulate(mgs_batch* b, const mgs_schedule* sched, int n, const double* q
       hipMemcpy(b->d_mquat, mocap_quat, sizeof(double) * n * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(b->d_ps, phase_start, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(b->d_pt, phase_target, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice) != hipSuccess ||
-      (dv && hipMemcpy(dv, vstate_init, (size_t)n * 2 * d.nv * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
+      (dv && hipMemcpy(dv, vstate_init, (size_t)n * (2 * d.nv + d.nact) * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
     rc = fail(MGS_EHIP, "host to device copy failed%s");
   if (!rc) rc = mgs_simulate_device(b, sched, n, b->d_qpos, dv, b->d_mquat, b->d_ps, b->d_pt, ds, nullptr, nullptr);
   if (!rc && hipMemcpy(state_out, ds, nst * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
@@ -671,7 +701,7 @@ static int rollout_host(mgs_batch* b, const mgs_schedule* sched, int n, const do
   const mgs_model_desc& d = b->m->desc;
   int np = sched->nphase;
   HIPCHK(hipSetDevice(b->m->device));
-  const size_t rs = (size_t)d.nq + 2 * (size_t)d.nv + MGS_RESUME_EXTRA;
+  const size_t rs = (size_t)d.nq + 2 * (size_t)d.nv + (size_t)d.nact + MGS_RESUME_EXTRA;
   // resume records: one buffer serves as the output of a resumable run or the
   // input of a resumed one
   if ((out->resume || resume_in) && !b->d_resume &&
@@ -993,6 +1023,10 @@ int mgs_model_attach_special(mgs_model* m, const char* path) {
     if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_rows_per_lane") != hipSuccess || sz != sizeof(int) ||
         hipMemcpyDtoH(&rpl, p, sizeof(int)) != hipSuccess || rpl != MGS_RPL)
       return fail(MGS_EINVAL, "code object %s is of the other library flavour (rows per lane)", path);
+    int mxd = 0;
+    if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_maxdim") != hipSuccess || sz != sizeof(int) ||
+        hipMemcpyDtoH(&mxd, p, sizeof(int)) != hipSuccess || mxd != layout_maxdim(m->desc))
+      return fail(MGS_EINVAL, "code object %s was built for another contact dimension (MGS_MAXDIM)", path);
     if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_desc") != hipSuccess || sz != sizeof(dsc) ||
         hipMemcpyDtoH(&dsc, p, sizeof(dsc)) != hipSuccess || memcmp(&dsc, &m->desc, sizeof(dsc)) != 0)
       return fail(MGS_EINVAL, "code object %s was specialised for another model description", path);

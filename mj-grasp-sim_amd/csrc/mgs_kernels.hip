@@ -71,6 +71,7 @@ struct Mdl {
 // carve-up; the U region is time-multiplexed between pipeline stages)
 struct Dat {
   double *qpos, *qvel, *qacc_ws, *ctrl, *mocap_pos, *mocap_quat, *time;
+  double *act, *act_dot;   // actuator state (mujoco.pid setpoint / integral) and its rate (ABI 21)
   double *xpos, *xquat, *xmat, *xipos, *xanchor, *xaxis;
   double *subtree_com, *subtree_mass, *cinert, *cdof;
   double *geom_xpos, *geom_xmat;
@@ -97,7 +98,15 @@ struct Dat {
 #define NEFC ints[1]
 #define OVERFLOW ints[2]
 #define ITERS ints[3]
-#define BLKSTRIDE 16
+// largest contact dimension the kernels handle: 4 (frictionless, sliding,
+// torsional) in the libraries and most specialised objects; 6 (rolling too)
+// in the objects of models with condim-6 pairs (mgs/core/special.py,
+// -DMGS_MAXDIM=6).  Per-contact block storage is MGS_MAXDIM^2 doubles.
+#ifndef MGS_MAXDIM
+#define MGS_MAXDIM 4
+#endif
+static_assert(MGS_MAXDIM == 4 || MGS_MAXDIM == 6, "MGS_MAXDIM is 4 or 6");
+#define BLKSTRIDE (MGS_MAXDIM * MGS_MAXDIM)
 #ifndef MGS_RPL
 #define MGS_RPL 2   // constraint rows per lane (nefc_max <= 64 * MGS_RPL)
 #endif
@@ -795,6 +804,35 @@ DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double
   wsync();
 }
 
+// mujoco.pid actuator force (mgs_gpu.h d_actuator_pidprm; oracle pid_force):
+// setpoint = the clamped ctrl, slew-limited against the previous setpoint (act
+// entry 0 with slewmax), error = setpoint - length; force = kp error + kd
+// (setpoint rate - velocity) + ki integral (the next act entry with ki != 0).
+// The act rates for the step's advance go to act_dot (lane 0).  Restated from
+// MuJoCo's documented plugin semantics; parity unpinned (its source is not here).
+DEVI double pid_force(const Mdl& md, Dat& d, int u, double c, double len, double vel, int lane) {
+  const double* pp = DA(md, actuator_pidprm) + 5 * u;
+  const double dt = md.m.timestep;
+  int k = IA(md, actuator_actadr)[u];
+  double cdot = 0.0;
+  if (pp[4] >= 0.0) {
+    const double prev = d.act[k];
+    const double lo = prev - pp[4] * dt, hi = prev + pp[4] * dt;
+    if (c < lo) c = lo;
+    if (c > hi) c = hi;
+    cdot = (c - prev) / dt;
+    if (lane == 0) d.act_dot[k] = cdot;
+    k++;
+  }
+  const double err = c - len;
+  double f = pp[0] * err + pp[2] * (cdot - vel);
+  if (pp[1] != 0.0) {
+    f = f + pp[1] * d.act[k];
+    if (lane == 0) d.act_dot[k] = err;
+  }
+  return f;
+}
+
 // actuation (oracle actuation()), lanes over dofs: each lane builds its entry of
 // every moment row (tendon wraps in order), the actuator length / velocity are
 // the oracle's sequential sums evaluated uniformly, forces applied per dof.
@@ -836,10 +874,15 @@ DEVI void actuation(const Mdl& md, Dat& d) {
       if (c < crange[2 * u]) c = crange[2 * u];
       if (c > crange[2 * u + 1]) c = crange[2 * u + 1];
     }
-    double g = gain[3 * u];
-    if (gtype[u] == MGS_GAIN_AFFINE) g = (gain[3 * u] + gain[3 * u + 1] * len) + gain[3 * u + 2] * vel;
-    double f = g * c;
-    if (btype[u] == MGS_BIAS_AFFINE) f = f + ((bias[3 * u] + bias[3 * u + 1] * len) + bias[3 * u + 2] * vel);
+    double f;
+    if (md.m.nact > 0 && gtype[u] == MGS_GAIN_PID) {
+      f = pid_force(md, d, u, c, len, vel, lane);
+    } else {
+      double g = gain[3 * u];
+      if (gtype[u] == MGS_GAIN_AFFINE) g = (gain[3 * u] + gain[3 * u + 1] * len) + gain[3 * u + 2] * vel;
+      f = g * c;
+      if (btype[u] == MGS_BIAS_AFFINE) f = f + ((bias[3 * u] + bias[3 * u + 1] * len) + bias[3 * u + 2] * vel);
+    }
     if (flim[u]) {
       if (f < frange[2 * u]) f = frange[2 * u];
       if (f > frange[2 * u + 1]) f = frange[2 * u + 1];
@@ -860,7 +903,29 @@ DEVI void passive(const Mdl& md, Dat& d) {
     double v = 0.0;
     if (stiff[j] != 0.0 && (jtype[j] == MGS_JNT_HINGE || jtype[j] == MGS_JNT_SLIDE))
       v = -stiff[j] * (d.qpos[jq[j]] - qspring[jq[j]]);
-    d.qfrc_passive[lane] = v - damp[lane] * d.qvel[lane];
+    v = v - damp[lane] * d.qvel[lane];
+    // gravity compensation (oracle passive(): MuJoCo mj_gravcomp with the
+    // force's moment arm from cinert, bodies in order)
+    const double* g = md.m.gravity;
+    if (g[0] != 0.0 || g[1] != 0.0 || g[2] != 0.0) {
+      const double* gc = DA(md, body_gravcomp);
+      double acc = 0.0;
+      int any = 0;
+      for (int b = 1; b < md.m.nbody; b++) {
+        if (gc[b] == 0.0) continue;
+        const int32_t* mask = IA(md, body_dofmask) + 2 * b;
+        if (!((lane < 32) ? ((mask[0] >> lane) & 1) : ((mask[1] >> (lane - 32)) & 1))) continue;
+        const double* ci = d.cinert + 10 * b;
+        const double* cd = d.cdof + 6 * lane;
+        double cr[3];
+        cross3(cr, cd, ci + 6);
+        double t = ((g[0] * cd[3] + g[1] * cd[4]) + g[2] * cd[5]) * ci[9] + ((g[0] * cr[0] + g[1] * cr[1]) + g[2] * cr[2]);
+        acc = acc + (-gc[b]) * t;
+        any = 1;
+      }
+      if (any) v = v + acc;
+    }
+    d.qfrc_passive[lane] = v;
   }
 }
 
@@ -2368,7 +2433,7 @@ DEVI void collision(const Mdl& md, Dat& d) {
 //   constraints:   G, aref, {vel,pos,margin | Newton Hessian}, scratch, Newton rows
 //   integration:   qDeriv
 enum {
-  L_qpos, L_qvel, L_qacc_ws, L_ctrl, L_mocap_pos, L_mocap_quat, L_time,
+  L_qpos, L_qvel, L_qacc_ws, L_ctrl, L_mocap_pos, L_mocap_quat, L_time, L_act, L_act_dot,
   L_xpos, L_xquat, L_xmat, L_subtree_com, L_cinert, L_cdof,
   L_M, L_Dv, L_Dinv, L_sD, L_isD, L_tmp, L_tmp2,
   L_qfrc_smooth, L_qacc_smooth, L_qfrc_constraint,
@@ -2417,7 +2482,7 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
 #define LO(k) (SL ? mgs_sl_words[k] : l.o[k])
 #define LU(k) (SL ? mgs_sl_words[L_COUNT + (k)] : l.u[k])
 #define B(f) d.f = s + LO(L_##f)
-  B(qpos); B(qvel); B(qacc_ws); B(ctrl); B(mocap_pos); B(mocap_quat); B(time);
+  B(qpos); B(qvel); B(qacc_ws); B(ctrl); B(mocap_pos); B(mocap_quat); B(time); B(act); B(act_dot);
   B(xpos); B(xquat); B(xmat); B(subtree_com); B(cinert); B(cdof);
   B(M); B(Dv); B(Dinv); B(sD); B(isD); B(tmp); B(tmp2);
   B(qfrc_smooth); B(qacc_smooth); B(qfrc_constraint);
@@ -2931,7 +2996,8 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       wsync();
       if (lane == 0) {
         for (int j = 0; j < dim; j++) add_row(md, d, MGS_EFC_CONTACT, j == 0 ? d.con_dist[c] : 0.0, pmar[p], dim, c);
-        for (int j = 0; j < dim; j++) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
+        for (int j = 0; j < dim; j++)
+          if (MGS_MAXDIM < 6 || j < 5) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
       }
       wsync();
       int col = lane < nv ? lane : 0;
@@ -2944,6 +3010,12 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         if (dim >= 4) {
           double dr[3] = {cjr2[0] - cjr1[0], cjr2[1] - cjr1[1], cjr2[2] - cjr1[2]};
           J[(r + 3) * d.gs + col] = dot3(fr, dr);
+#if MGS_MAXDIM > 4
+          if (dim == 6) {
+            J[(r + 4) * d.gs + col] = dot3(fr + 3, dr);
+            J[(r + 5) * d.gs + col] = dot3(fr + 6, dr);
+          }
+#endif
         }
       }
     }
@@ -2967,7 +3039,9 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         int r = rc + j;
         d.efc_type[r] = MGS_EFC_CONTACT; d.efc_pos[r] = j == 0 ? d.con_dist[lane] : 0.0;
         d.efc_margin[r] = pmar[cp]; d.efc_dim[r] = cdim; d.efc_con[r] = lane;
-        d.con_mu[5 * lane + j] = (j < cdim - 1) ? pfr[5 * cp + j] : 0.0;
+        // (5 friction coefficients per contact: a condim-6 block's sixth row has
+        // no slot -- writing one would clobber the next contact's first)
+        if (MGS_MAXDIM < 6 || j < 5) d.con_mu[5 * lane + j] = (j < cdim - 1) ? pfr[5 * cp + j] : 0.0;
       }
     }
     int last = nkeep > 0 ? nkeep - 1 : 0;
@@ -2989,6 +3063,12 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         if (dim >= 4) {
           double dr[3] = {cjr2[0] - cjr1[0], cjr2[1] - cjr1[1], cjr2[2] - cjr1[2]};
           J[(r + 3) * d.gs + col] = dot3(fr, dr);
+#if MGS_MAXDIM > 4
+          if (dim == 6) {
+            J[(r + 4) * d.gs + col] = dot3(fr + 3, dr);
+            J[(r + 5) * d.gs + col] = dot3(fr + 6, dr);
+          }
+#endif
         }
       }
     }
@@ -3152,6 +3232,110 @@ DEVI void qcqp3(const double* A, const double* b, const double* mu, double r, do
   }
 }
 
+// n = 5 (condim-6 contacts: two sliding, one torsional, two rolling
+// dimensions): MuJoCo's general mju_QCQP restated (oracle qcqpn): the same
+// Newton iteration on the multiplier, with (A + la I) factored by Cholesky
+// (a pivot below 1e-10 counts as singular: result 0) instead of the closed-form
+// inverse.  Parity unpinned: MuJoCo's source is not here.
+template <int N>
+DEVI void qcqpn(const double* A, const double* b, const double* mu, double r, double* x) {
+  double As[N * N], bs[N], v[N], L[N * N], t[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    bs[i] = b[i] * mu[i];
+    v[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j++) As[i * N + j] = (A[i * N + j] * mu[i]) * mu[j];
+  }
+  double rr = r * r, la = 0.0;
+  int sing = 0;
+  for (int it = 0; it < 20; it++) {
+#pragma unroll
+    for (int q = 0; q < N * N; q++) L[q] = As[q];
+#pragma unroll
+    for (int i = 0; i < N; i++) L[i * N + i] = L[i * N + i] + la;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      double p = L[j * N + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) p = p - L[j * N + k] * L[j * N + k];
+      if (p < 1e-10) sing = 1;
+      p = sqrt(p < 1e-10 ? 1e-10 : p);
+      L[j * N + j] = p;
+#pragma unroll
+      for (int i = j + 1; i < N; i++) {
+        double s = L[i * N + j];
+#pragma unroll
+        for (int k = 0; k < j; k++) s = s - L[i * N + k] * L[j * N + k];
+        L[i * N + j] = s / p;
+      }
+    }
+    if (sing) {
+#pragma unroll
+      for (int i = 0; i < N; i++) v[i] = 0.0;
+      break;
+    }
+    // v = -(L L')^-1 bs
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      double s = bs[i];
+#pragma unroll
+      for (int k = 0; k < i; k++) s = s - L[i * N + k] * t[k];
+      t[i] = s / L[i * N + i];
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; i--) {
+      double s = t[i];
+#pragma unroll
+      for (int k = i + 1; k < N; k++) s = s - L[k * N + i] * v[k];
+      v[i] = s / L[i * N + i];
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] = -v[i];
+    double val = -rr;
+    {
+      double vv = 0.0;
+#pragma unroll
+      for (int i = 0; i < N; i++) vv = vv + v[i] * v[i];
+      val = vv - rr;
+    }
+    if (val < 1e-10) break;
+    // deriv = -2 v' (A + la I)^-1 v
+    double pv[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      double s = v[i];
+#pragma unroll
+      for (int k = 0; k < i; k++) s = s - L[i * N + k] * t[k];
+      t[i] = s / L[i * N + i];
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; i--) {
+      double s = t[i];
+#pragma unroll
+      for (int k = i + 1; k < N; k++) s = s - L[k * N + i] * pv[k];
+      pv[i] = s / L[i * N + i];
+    }
+    double vp = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; i++) vp = vp + v[i] * pv[i];
+    double deriv = -2.0 * vp;
+    double delta = -val / deriv;
+    if (delta < 1e-10) break;
+    la = la + delta;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = v[i] * mu[i];
+  if (!sing && la != 0.0) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; i++) s = s + (x[i] * x[i]) / (mu[i] * mu[i]);
+    s = sqrt((r * r) / (s > K_MINVAL ? s : K_MINVAL));
+#pragma unroll
+    for (int i = 0; i < N; i++) x[i] = x[i] * s;
+  }
+}
+
 // forces live in registers: lane l holds f[l + 64 h] in F.v[h], h < MGS_RPL
 // (rows per lane: 2 in the main library, 4 in the wide one for clutter piles)
 struct Frc {
@@ -3242,15 +3426,16 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
         for (int j = 0; j < DIM - 1; j++) s = s - Ab[(1 + i) * DIM + 1 + j] * old[1 + j];
         bq[i] = s;
       }
-      if (DIM == 3) {
+      if constexpr (DIM == 3) {
         qcqp2(Ab[4], Ab[5], Ab[8], bq[0], bq[1], mu, fn, &nw[1], &nw[2]);
       } else {
-        double Ac[9];
+        double Ac[(DIM - 1) * (DIM - 1)];
 #pragma unroll
-        for (int i = 0; i < 3; i++)
+        for (int i = 0; i < DIM - 1; i++)
 #pragma unroll
-          for (int j = 0; j < 3; j++) Ac[i * 3 + j] = Ab[(1 + i) * DIM + 1 + j];
-        qcqp3(Ac, bq, mu, fn, nw + 1);
+          for (int j = 0; j < DIM - 1; j++) Ac[i * (DIM - 1) + j] = Ab[(1 + i) * DIM + 1 + j];
+        if constexpr (DIM == 4) qcqp3(Ac, bq, mu, fn, nw + 1);
+        else qcqpn<DIM - 1>(Ac, bq, mu, fn, nw + 1);
       }
     }
     double del[DIM];
@@ -3281,15 +3466,16 @@ DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u,
     }
     double fnorm = old[0];
     if (!(fnorm < 1e-15)) {
-      if (DIM == 3) {
+      if constexpr (DIM == 3) {
         qcqp2(Ab[4], Ab[5], Ab[8], bq[0], bq[1], mu, fnorm, &nw[1], &nw[2]);
       } else {
-        double Ac[9];
+        double Ac[(DIM - 1) * (DIM - 1)];
 #pragma unroll
-        for (int i = 0; i < 3; i++)
+        for (int i = 0; i < DIM - 1; i++)
 #pragma unroll
-          for (int j = 0; j < 3; j++) Ac[i * 3 + j] = Ab[(1 + i) * DIM + 1 + j];
-        qcqp3(Ac, bq, mu, fnorm, nw + 1);
+          for (int j = 0; j < DIM - 1; j++) Ac[i * (DIM - 1) + j] = Ab[(1 + i) * DIM + 1 + j];
+        if constexpr (DIM == 4) qcqp3(Ac, bq, mu, fnorm, nw + 1);
+        else qcqpn<DIM - 1>(Ac, bq, mu, fnorm, nw + 1);
       }
     } else {
 #pragma unroll
@@ -3429,6 +3615,11 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
       } else if (dim == 3) {
         improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 0);
         r += 3;
+#if MGS_MAXDIM > 4
+      } else if (dim == 6) {
+        improvement = improvement - pgs_contact<6>(d, r, nv, P, lane, u, F, 0);
+        r += 6;
+#endif
       } else {
         improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 0);
         r += 4;
@@ -3479,9 +3670,9 @@ DEVI int next_visited(const unsigned long long (&vis)[N], int r) {
   }
   return out;
 }
-DEVI void load_block_rows(const Dat& d, int r, int dim, int nv, int lane, double (&g)[4]) {
+DEVI void load_block_rows(const Dat& d, int r, int dim, int nv, int lane, double (&g)[MGS_MAXDIM]) {
 #pragma unroll
-  for (int i = 0; i < 4; i++) g[i] = (i < dim && lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
+  for (int i = 0; i < MGS_MAXDIM; i++) g[i] = (i < dim && lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
 }
 
 DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
@@ -3498,7 +3689,7 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
     if (r < ne) {
       t = d.efc_type[r];
       dim = d.efc_dim[r];
-      v = t == MGS_EFC_FRICTION || (t == MGS_EFC_CONTACT && (dim == 3 || dim == 4) && efc_lead(d, r));
+      v = t == MGS_EFC_FRICTION || (t == MGS_EFC_CONTACT && dim > 1 && efc_lead(d, r));
     }
     tk[h] = t;
     dk[h] = dim;
@@ -3527,7 +3718,7 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
     }
     int r = next_visited(vis, -1);
     int t = 0, dim = 0;
-    double gc[4];
+    double gc[MGS_MAXDIM];
     if (r >= 0) {
       t = sel_i(tk, r);
       dim = t == MGS_EFC_FRICTION ? 1 : sel_i(dk, r);
@@ -3536,7 +3727,9 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
     while (r >= 0) {
       const int rn = next_visited(vis, r);
       int tn = 0, dimn = 0;
-      double gn[4] = {0.0, 0.0, 0.0, 0.0};
+      double gn[MGS_MAXDIM];
+#pragma unroll
+      for (int i = 0; i < MGS_MAXDIM; i++) gn[i] = 0.0;
       if (rn >= 0) {
         tn = sel_i(tk, rn);
         dimn = tn == MGS_EFC_FRICTION ? 1 : sel_i(dk, rn);
@@ -3560,6 +3753,10 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
         }
       } else if (dim == 3) {
         improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1, gc);
+#if MGS_MAXDIM > 4
+      } else if (dim == 6) {
+        improvement = improvement - pgs_contact<6>(d, r, nv, P, lane, u, F, 1, gc);
+#endif
       } else {
         improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1, gc);
       }
@@ -3567,7 +3764,7 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
       t = tn;
       dim = dimn;
 #pragma unroll
-      for (int i = 0; i < 4; i++) gc[i] = gn[i];
+      for (int i = 0; i < MGS_MAXDIM; i++) gc[i] = gn[i];
     }
     if (improvement * scale < md.m.noslip_tolerance) break;
   }
@@ -3590,7 +3787,7 @@ DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u)
     if (r < ne) {
       t = d.efc_type[r];
       dim = d.efc_dim[r];
-      v = t == MGS_EFC_FRICTION || (t == MGS_EFC_CONTACT && (dim == 3 || dim == 4) && efc_lead(d, r));
+      v = t == MGS_EFC_FRICTION || (t == MGS_EFC_CONTACT && dim > 1 && efc_lead(d, r));
     }
     tk[h] = t;
     dk[h] = dim;
@@ -3637,6 +3834,10 @@ DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u)
           }
         } else if (dim == 3) {
           improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1);
+#if MGS_MAXDIM > 4
+        } else if (dim == 6) {
+          improvement = improvement - pgs_contact<6>(d, r, nv, P, lane, u, F, 1);
+#endif
         } else {
           improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1);
         }
@@ -3741,26 +3942,26 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
   }
   // mup = mu0 / sqrt(impratio), k1 = 1 / (1 + mup^2): per-block constants of the
   // solve (oracle efc_mup, efc_k1), held in registers by the caller
-  double z[4], y[4], isr[4];
+  double z[MGS_MAXDIM], y[MGS_MAXDIM], isr[MGS_MAXDIM];
 #pragma unroll
-  for (int a = 0; a < 4; a++) {
+  for (int a = 0; a < MGS_MAXDIM; a++) {
     isr[a] = (a < dim) ? d.efc_isR[r + a] : 0.0;
     z[a] = (a < dim) ? -jr[a] * isr[a] : 0.0;
   }
   double t2 = 0.0;
 #pragma unroll
-  for (int a = 1; a < 4; a++)
+  for (int a = 1; a < MGS_MAXDIM; a++)
     if (a < dim) t2 = t2 + z[a] * z[a];
   double tn = sqrt(t2);
   double yn = 0.0, itn = 0.0, sc = 0.0;
   if (tn <= mup * z[0]) {
     st = ST_QUAD;
 #pragma unroll
-    for (int a = 0; a < 4; a++) y[a] = z[a];
+    for (int a = 0; a < MGS_MAXDIM; a++) y[a] = z[a];
   } else if (mup * tn <= -z[0]) {
     st = ST_OFF;
 #pragma unroll
-    for (int a = 0; a < 4; a++) y[a] = 0.0;
+    for (int a = 0; a < MGS_MAXDIM; a++) y[a] = 0.0;
   } else {
     st = ST_CONE;
     yn = (z[0] + mup * tn) * k1;
@@ -3768,11 +3969,11 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
     sc = (mup * yn) * itn;
     y[0] = yn;
 #pragma unroll
-    for (int a = 1; a < 4; a++) y[a] = sc * z[a];
+    for (int a = 1; a < MGS_MAXDIM; a++) y[a] = sc * z[a];
   }
   double c = 0.0;
 #pragma unroll
-  for (int a = 0; a < 4; a++) {
+  for (int a = 0; a < MGS_MAXDIM; a++) {
     if (a < dim) {
       f[a] = y[a] * isr[a];
       c = c + y[a] * y[a];
@@ -3782,22 +3983,22 @@ DEVI double row_eval(const Mdl& md, const Dat& d, int r, int t, int dim, const d
     cq[0] = k1;
     cq[1] = sc;
 #pragma unroll
-    for (int a = 1; a < 4; a++) cq[1 + a] = z[a] * itn;
+    for (int a = 1; a < MGS_MAXDIM; a++) cq[1 + a] = z[a] * itn;
   }
   if (want_hb && st == ST_CONE) {
     double k2 = sc;
-    double v[4], e[4];
+    double v[MGS_MAXDIM], e[MGS_MAXDIM];
     v[0] = 1.0;
     e[0] = 0.0;
 #pragma unroll
-    for (int a = 1; a < 4; a++) { e[a] = z[a] * itn; v[a] = mup * e[a]; }
+    for (int a = 1; a < MGS_MAXDIM; a++) { e[a] = z[a] * itn; v[a] = mup * e[a]; }
 #pragma unroll
-    for (int a = 0; a < 4; a++)
+    for (int a = 0; a < MGS_MAXDIM; a++)
 #pragma unroll
-      for (int b = 0; b < 4; b++) {
+      for (int b = 0; b < MGS_MAXDIM; b++) {
         double Pm = (k1 * v[a]) * v[b];
         if (a >= 1 && b >= 1) Pm = Pm + k2 * ((a == b ? 1.0 : 0.0) - e[a] * e[b]);
-        hb[a * 4 + b] = (isr[a] * isr[b]) * Pm;
+        hb[a * MGS_MAXDIM + b] = (isr[a] * isr[b]) * Pm;
       }
   }
   return 0.5 * c;
@@ -3847,21 +4048,21 @@ DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const dou
     if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
       int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
-      double jr[4], f[4], hb[16];
+      double jr[MGS_MAXDIM], f[MGS_MAXDIM], hb[BLKSTRIDE];
       int st = ST_OFF;
 #pragma unroll
-      for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
+      for (int a = 0; a < MGS_MAXDIM; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
       cr[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true, mupR[h], k1R[h]);
 #pragma unroll
-      for (int a = 0; a < 4; a++)
+      for (int a = 0; a < MGS_MAXDIM; a++)
         if (a < dim) { d.efc_f[r + a] = f[a]; d.efc_state[r + a] = st; }
       if (st == ST_CONE) {
-        double* o = d.con_hb + 16 * d.efc_con[r];
+        double* o = d.con_hb + BLKSTRIDE * d.efc_con[r];
 #pragma unroll
-        for (int a = 0; a < 4; a++)
+        for (int a = 0; a < MGS_MAXDIM; a++)
 #pragma unroll
-          for (int b = 0; b < 4; b++)
-            if (a < dim && b < dim) o[a * dim + b] = hb[a * 4 + b];
+          for (int b = 0; b < MGS_MAXDIM; b++)
+            if (a < dim && b < dim) o[a * dim + b] = hb[a * MGS_MAXDIM + b];
       }
     }
   }
@@ -3913,25 +4114,25 @@ DEVI void newton_eval_pair(const Mdl& md, Dat& d, const double* wa, const double
     if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
       int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
-      double jr[4], f[4], hb[16];
+      double jr[MGS_MAXDIM], f[MGS_MAXDIM], hb[BLKSTRIDE];
       int st = ST_OFF;
 #pragma unroll
-      for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? jar0[r + a] : 0.0;
+      for (int a = 0; a < MGS_MAXDIM; a++) jr[a] = (a < dim) ? jar0[r + a] : 0.0;
       cr0[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true, mupR[h], k1R[h]);
       st = ST_OFF;
 #pragma unroll
-      for (int a = 0; a < 4; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
+      for (int a = 0; a < MGS_MAXDIM; a++) jr[a] = (a < dim) ? d.efc_jar[r + a] : 0.0;
       cr1[h] = row_eval(md, d, r, t, dim, jr, f, st, hb, true, mupR[h], k1R[h]);
 #pragma unroll
-      for (int a = 0; a < 4; a++)
+      for (int a = 0; a < MGS_MAXDIM; a++)
         if (a < dim) { d.efc_f[r + a] = f[a]; d.efc_state[r + a] = st; }
       if (st == ST_CONE) {
-        double* o = d.con_hb + 16 * d.efc_con[r];
+        double* o = d.con_hb + BLKSTRIDE * d.efc_con[r];
 #pragma unroll
-        for (int a = 0; a < 4; a++)
+        for (int a = 0; a < MGS_MAXDIM; a++)
 #pragma unroll
-          for (int b = 0; b < 4; b++)
-            if (a < dim && b < dim) o[a * dim + b] = hb[a * 4 + b];
+          for (int b = 0; b < MGS_MAXDIM; b++)
+            if (a < dim && b < dim) o[a * dim + b] = hb[a * MGS_MAXDIM + b];
       }
     }
   }
@@ -3988,10 +4189,10 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
     if (r < ne && efc_lead(d, r)) {
       int t = d.efc_type[r];
       int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
-      double jr[4], jv[4], f[4], hb[16], cq[5];
+      double jr[MGS_MAXDIM], jv[MGS_MAXDIM], f[MGS_MAXDIM], hb[BLKSTRIDE], cq[MGS_MAXDIM + 1];
       int st = ST_OFF;
 #pragma unroll
-      for (int a = 0; a < 4; a++) {
+      for (int a = 0; a < MGS_MAXDIM; a++) {
         jv[a] = (a < dim) ? d.efc_jv[r + a] : 0.0;
         jr[a] = (a < dim) ? d.efc_jar[r + a] + alpha * jv[a] : 0.0;
       }
@@ -4002,21 +4203,21 @@ DEVI void ls_eval(const Mdl& md, const Dat& d, int ne, double alpha, double A1, 
         if (st == ST_QUAD) s2 = (jv[0] * d.efc_Dr[r]) * jv[0];
       } else {
 #pragma unroll
-        for (int a = 0; a < 4; a++)
+        for (int a = 0; a < MGS_MAXDIM; a++)
           if (a < dim) s1 = s1 - f[a] * jv[a];
         if (st == ST_QUAD) {
 #pragma unroll
-          for (int a = 0; a < 4; a++)
+          for (int a = 0; a < MGS_MAXDIM; a++)
             if (a < dim) s2 = s2 + (jv[a] * d.efc_Dr[r + a]) * jv[a];
         } else if (st == ST_CONE) {
           // jv' hb jv in closed form (oracle ls_eval)
           double mup = mupR[h];
-          double u[4];
+          double u[MGS_MAXDIM];
 #pragma unroll
-          for (int a = 0; a < 4; a++) u[a] = (a < dim) ? jv[a] * d.efc_isR[r + a] : 0.0;
+          for (int a = 0; a < MGS_MAXDIM; a++) u[a] = (a < dim) ? jv[a] * d.efc_isR[r + a] : 0.0;
           double vu = u[0], eu = 0.0, uu = 0.0;
 #pragma unroll
-          for (int a = 1; a < 4; a++) {
+          for (int a = 1; a < MGS_MAXDIM; a++) {
             if (a < dim) {
               vu = vu + (mup * cq[1 + a]) * u[a];
               eu = eu + cq[1 + a] * u[a];
@@ -4043,31 +4244,33 @@ template <int NV>
 DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
   constexpr int NT = (NV + 15) / 16;
   int lane = lane_id();
-  // weight table: wt[4r..4r+3] = w_a, wi[r] = lead * 8 + nd (exact in f64)
+  // weight table: wt[M r .. M r + M - 1] = w_a (M = MGS_MAXDIM), wi[r] = lead * 8 + nd (exact in f64)
   double* wt = d.nH;
-  double* wi = d.nH + 4 * md.m.nefc_max;
+  double* wi = d.nH + MGS_MAXDIM * md.m.nefc_max;
   for (int r = lane; r < ne; r += WAVE) {
     int t = d.efc_type[r];
     int st = d.efc_state[r];
-    double w0 = 0.0, w1 = 0.0, w2 = 0.0, w3 = 0.0;
+    double wv[MGS_MAXDIM];
+#pragma unroll
+    for (int a = 0; a < MGS_MAXDIM; a++) wv[a] = 0.0;
     int lead = r, nd = 0;
     if (st == ST_QUAD) {
-      w0 = d.efc_Dr[r];
+      wv[0] = d.efc_Dr[r];
       nd = 1;
     } else if (st == ST_CONE && t == MGS_EFC_CONTACT) {
       int c = d.efc_con[r], dim = d.efc_dim[r];
       int bp = 0;
-      for (int q = 1; q < 4; q++)
+      for (int q = 1; q < MGS_MAXDIM; q++)
         if (r - q >= 0 && bp == q - 1 && d.efc_type[r - q] == MGS_EFC_CONTACT && d.efc_con[r - q] == c) bp = q;
-      const double* hb = d.con_hb + 16 * c + bp;
+      const double* hb = d.con_hb + BLKSTRIDE * c + bp;
       lead = r - bp;
       nd = dim;
-      w0 = hb[0];
-      w1 = (dim > 1) ? hb[dim] : 0.0;
-      w2 = (dim > 2) ? hb[2 * dim] : 0.0;
-      w3 = (dim > 3) ? hb[3 * dim] : 0.0;
+      wv[0] = hb[0];
+#pragma unroll
+      for (int a = 1; a < MGS_MAXDIM; a++) wv[a] = (dim > a) ? hb[a * dim] : 0.0;
     }
-    wt[4 * r] = w0; wt[4 * r + 1] = w1; wt[4 * r + 2] = w2; wt[4 * r + 3] = w3;
+#pragma unroll
+    for (int a = 0; a < MGS_MAXDIM; a++) wt[MGS_MAXDIM * r + a] = wv[a];
     wi[r] = (double)(lead * 8 + nd);
   }
   wsync();
@@ -4088,8 +4291,10 @@ DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
       double v = Gr[c < NV ? c : 0];
       gv[t] = (valid && c < NV) ? v : 0.0;
     }
-    const double* wr = wt + 4 * rr;
-    double w[4] = {wr[0], wr[1], wr[2], wr[3]};
+    const double* wr = wt + MGS_MAXDIM * rr;
+    double w[MGS_MAXDIM];
+#pragma unroll
+    for (int a = 0; a < MGS_MAXDIM; a++) w[a] = wr[a];
     int info = (int)wi[rr];
     int lead = info >> 3, nd = valid ? (info & 7) : 0;
     bool multi = __ballot(nd > 1) != 0ull;
@@ -4103,7 +4308,7 @@ DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
         int cc = c < NV ? c : 0;
         double xs = 0.0;
 #pragma unroll
-        for (int a = 0; a < 4; a++) {
+        for (int a = 0; a < MGS_MAXDIM; a++) {
           int aa = a < nd ? a : 0;
           double tv = xs + d.G[(lead + aa) * GS + cc] * w[a];
           xs = (a < nd) ? tv : xs;
@@ -4144,7 +4349,7 @@ DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
 // the expressions are row_eval()'s and ls_eval()'s (oracle ls_eval), per kind.
 struct LsRow {
   int kind, dim;   // kind: 0 none, 1 equality, 2 limit / frictionless contact, 3 friction, 4 cone block
-  double jar[4], jv[4], isr[4], Dr[4];
+  double jar[MGS_MAXDIM], jv[MGS_MAXDIM], isr[MGS_MAXDIM], Dr[MGS_MAXDIM];
   double mup, k1, lim;
 };
 DEVI void ls_row_load(const Mdl& md, const Dat& d, int r, int ne, double mup, double k1, LsRow& L) {
@@ -4154,14 +4359,14 @@ DEVI void ls_row_load(const Mdl& md, const Dat& d, int r, int ne, double mup, do
   L.k1 = k1;
   L.lim = 0.0;
 #pragma unroll
-  for (int a = 0; a < 4; a++) { L.jar[a] = 0.0; L.jv[a] = 0.0; L.isr[a] = 0.0; L.Dr[a] = 0.0; }
+  for (int a = 0; a < MGS_MAXDIM; a++) { L.jar[a] = 0.0; L.jv[a] = 0.0; L.isr[a] = 0.0; L.Dr[a] = 0.0; }
   if (r < ne && efc_lead(d, r)) {
     int t = d.efc_type[r];
     int dim = (t == MGS_EFC_CONTACT) ? d.efc_dim[r] : 1;
     L.dim = dim;
     L.kind = (t == MGS_EFC_EQUALITY) ? 1 : (t == MGS_EFC_FRICTION) ? 3 : (dim == 1) ? 2 : 4;
 #pragma unroll
-    for (int a = 0; a < 4; a++) {
+    for (int a = 0; a < MGS_MAXDIM; a++) {
       if (a < dim) {
         L.jar[a] = d.efc_jar[r + a];
         L.jv[a] = d.efc_jv[r + a];
@@ -4193,15 +4398,15 @@ DEVI void ls_row(const LsRow& L, double alpha, double& s1o, double& s2o) {
   } else if (L.kind == 4) {
     int dim = L.dim;
     double mup = L.mup;
-    double z[4], y[4];
+    double z[MGS_MAXDIM], y[MGS_MAXDIM];
 #pragma unroll
-    for (int a = 0; a < 4; a++) {
+    for (int a = 0; a < MGS_MAXDIM; a++) {
       double jr = (a < dim) ? L.jar[a] + alpha * L.jv[a] : 0.0;
       z[a] = (a < dim) ? -jr * L.isr[a] : 0.0;
     }
     double t2 = 0.0;
 #pragma unroll
-    for (int a = 1; a < 4; a++)
+    for (int a = 1; a < MGS_MAXDIM; a++)
       if (a < dim) t2 = t2 + z[a] * z[a];
     double tn = sqrt(t2);
     int st;
@@ -4209,11 +4414,11 @@ DEVI void ls_row(const LsRow& L, double alpha, double& s1o, double& s2o) {
     if (tn <= mup * z[0]) {
       st = ST_QUAD;
 #pragma unroll
-      for (int a = 0; a < 4; a++) y[a] = z[a];
+      for (int a = 0; a < MGS_MAXDIM; a++) y[a] = z[a];
     } else if (mup * tn <= -z[0]) {
       st = ST_OFF;
 #pragma unroll
-      for (int a = 0; a < 4; a++) y[a] = 0.0;
+      for (int a = 0; a < MGS_MAXDIM; a++) y[a] = 0.0;
     } else {
       st = ST_CONE;
       yn = (z[0] + mup * tn) * L.k1;
@@ -4221,22 +4426,22 @@ DEVI void ls_row(const LsRow& L, double alpha, double& s1o, double& s2o) {
       sc = (mup * yn) * itn;
       y[0] = yn;
 #pragma unroll
-      for (int a = 1; a < 4; a++) y[a] = sc * z[a];
+      for (int a = 1; a < MGS_MAXDIM; a++) y[a] = sc * z[a];
     }
 #pragma unroll
-    for (int a = 0; a < 4; a++)
+    for (int a = 0; a < MGS_MAXDIM; a++)
       if (a < dim) s1 = s1 - (y[a] * L.isr[a]) * L.jv[a];
     if (st == ST_QUAD) {
 #pragma unroll
-      for (int a = 0; a < 4; a++)
+      for (int a = 0; a < MGS_MAXDIM; a++)
         if (a < dim) s2 = s2 + (L.jv[a] * L.Dr[a]) * L.jv[a];
     } else if (st == ST_CONE) {
-      double u[4];
+      double u[MGS_MAXDIM];
 #pragma unroll
-      for (int a = 0; a < 4; a++) u[a] = (a < dim) ? L.jv[a] * L.isr[a] : 0.0;
+      for (int a = 0; a < MGS_MAXDIM; a++) u[a] = (a < dim) ? L.jv[a] * L.isr[a] : 0.0;
       double vu = u[0], eu = 0.0, uu = 0.0;
 #pragma unroll
-      for (int a = 1; a < 4; a++) {
+      for (int a = 1; a < MGS_MAXDIM; a++) {
         if (a < dim) {
           double e = z[a] * itn;
           vu = vu + (mup * e) * u[a];
@@ -4586,6 +4791,30 @@ DEVI void integrate(const Mdl& md, Dat& d) {
     }
     if (lane == 0) d.time[0] = d.time[0] + dt;
   }
+  // actuator state (mj_advance: act += dt act_dot; a mujoco.pid integral then
+  // clamped to |ki integral| <= imax), lanes over actuators
+  if (md.m.nact > 0) {
+    const int32_t *gtype = IA(md, actuator_gaintype), *aadr = IA(md, actuator_actadr);
+    const double* pid = DA(md, actuator_pidprm);
+    for (int u = lane; u < md.m.nu; u += WAVE) {
+      if (gtype[u] != MGS_GAIN_PID) continue;
+      const double* pp = pid + 5 * u;
+      int k = aadr[u];
+      if (pp[4] >= 0.0) {
+        d.act[k] = d.act[k] + dt * d.act_dot[k];
+        k++;
+      }
+      if (pp[1] != 0.0) {
+        double v = d.act[k] + dt * d.act_dot[k];
+        if (pp[3] >= 0.0) {
+          const double lim = pp[3] / pp[1];
+          if (v < -lim) v = -lim;
+          if (v > lim) v = lim;
+        }
+        d.act[k] = v;
+      }
+    }
+  }
   wsync();
 }
 
@@ -4618,6 +4847,10 @@ DEVI void reset(const Mdl& md, Dat& d, const double* qpos_init, const double* mp
   const double* w0 = vstate ? vstate + nv : DA(md, qacc_ws0);
   for (int k = lane; k < md.m.nq; k += WAVE) d.qpos[k] = qpos_init[k];
   for (int k = lane; k < nv; k += WAVE) { d.qvel[k] = v0[k]; d.qacc_ws[k] = w0[k]; }
+  for (int k = lane; k < md.m.nact; k += WAVE) {
+    d.act[k] = vstate ? vstate[2 * nv + k] : DA(md, act0)[k];
+    d.act_dot[k] = 0.0;
+  }
   if (lane == 0) {
     for (int u = 0; u < (md.m.nu > 0 ? md.m.nu : 1); u++) d.ctrl[u] = 0.0;
     for (int k = 0; k < 3; k++) d.mocap_pos[k] = mpos ? mpos[k] : 0.0;
@@ -4673,8 +4906,9 @@ DEVI void save_record(const Mdl& md, Dat& d, double* rec, int p, int t, int gste
   const int lane = lane_id(), nq = md.m.nq, nvr = md.m.nv;
   for (int k = lane; k < nq; k += WAVE) rec[k] = d.qpos[k];
   for (int k = lane; k < nvr; k += WAVE) { rec[nq + k] = d.qvel[k]; rec[nq + nvr + k] = d.qacc_ws[k]; }
+  for (int k = lane; k < md.m.nact; k += WAVE) rec[nq + 2 * nvr + k] = d.act[k];
   if (lane == 0) {
-    double* tail = rec + nq + 2 * nvr;
+    double* tail = rec + nq + 2 * nvr + md.m.nact;
     tail[0] = d.time[0];
     tail[1] = p; tail[2] = t; tail[3] = gstep;
     tail[4] = maxcon; tail[5] = maxefc; tail[6] = sumcon; tail[7] = sumefc;
@@ -4835,9 +5069,9 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
   const double* ps = phase_start + (size_t)i * np * 3;
   const double* pt = phase_target + (size_t)i * np * 3;
   reset(md, d, qpos_init + (size_t)i * md.m.nq, ps, mocap_quat + 4 * i,
-        vstate_init ? vstate_init + (size_t)i * 2 * md.m.nv : nullptr);
+        vstate_init ? vstate_init + (size_t)i * (2 * md.m.nv + md.m.nact) : nullptr);
   int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
-  const int nq = md.m.nq, nvr = md.m.nv, RS = nq + 2 * nvr + MGS_RESUME_EXTRA;
+  const int nq = md.m.nq, nvr = md.m.nv, RS = nq + 2 * nvr + md.m.nact + MGS_RESUME_EXTRA;
   int p0 = 0, t0 = 0;
   if (resume_in) {
     // continue a capacity-capped run from its last step before the overflow
@@ -4845,7 +5079,8 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
     const double* rec = resume_in + (size_t)i * RS;
     for (int k = lane; k < nq; k += WAVE) d.qpos[k] = rec[k];
     for (int k = lane; k < nvr; k += WAVE) { d.qvel[k] = rec[nq + k]; d.qacc_ws[k] = rec[nq + nvr + k]; }
-    const double* tail = rec + nq + 2 * nvr;
+    for (int k = lane; k < md.m.nact; k += WAVE) d.act[k] = rec[nq + 2 * nvr + k];
+    const double* tail = rec + nq + 2 * nvr + md.m.nact;
     if (lane == 0) {
       d.time[0] = tail[0];
       d.ITERS = (int)tail[8];
@@ -5002,9 +5237,10 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
   if (obj_qpos && lane < 7) obj_qpos[7 * i + lane] = sc.obj_qposadr >= 0 ? d.qpos[sc.obj_qposadr + lane] : 0.0;
   if (state_out) {
     int nq = md.m.nq, nv = md.m.nv;
-    double* so = state_out + (size_t)i * (nq + 2 * nv);
+    double* so = state_out + (size_t)i * (nq + 2 * nv + md.m.nact);
     for (int k = lane; k < nq; k += WAVE) so[k] = d.qpos[k];
     for (int k = lane; k < nv; k += WAVE) { so[nq + k] = d.qvel[k]; so[nq + nv + k] = d.qacc_ws[k]; }
+    for (int k = lane; k < md.m.nact; k += WAVE) so[nq + 2 * nv + k] = d.act[k];
   }
   PROF_FLUSH
 }

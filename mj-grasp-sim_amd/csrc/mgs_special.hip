@@ -44,6 +44,7 @@ extern "C" {
 // not be visible to hipModuleGetGlobal)
 __device__ int mgs_special_abi = MGS_ABI_VERSION;
 __device__ int mgs_special_rows_per_lane = MGS_RPL;
+__device__ int mgs_special_maxdim = MGS_MAXDIM;
 __device__ mgs_model_desc mgs_special_desc = mgs_sl_desc;
 __device__ int mgs_special_words[L_COUNT + U_COUNT + 4] = MGS_SL_WORDS_INIT;
 

@@ -228,7 +228,8 @@ class Engine:
         self._cap = 0
         if specialize is None:
             specialize = {"1": True, "0": False}.get(os.environ.get("MGS_SPECIALIZE", "cached"), "cached")
-        if not self.lib.mgs_supports_nv(cm.nv):
+        if not self.lib.mgs_supports_nv(cm.nv) or int(fields["maxcondim"]) > 4:
+            # (condim-6 contacts run only in a code object built for them)
             specialize = True
         if specialize and os.environ.get("MGS_SPECIAL_OBJECT"):
             # A/B experiments (tools/ab_bench.sh): explicit objects (':'-separated),
@@ -295,7 +296,7 @@ class Engine:
 
     def resume_width(self):
         """doubles per resume record (mgs_rollout_out.resume)"""
-        return self.cm.nq + 2 * self.cm.nv + abi.MGS["MGS_RESUME_EXTRA"]
+        return self.cm.nq + 2 * self.cm.nv + int(self.cm.nact) + abi.MGS["MGS_RESUME_EXTRA"]
 
     def rollout(self, plan, resumable=False, resume_from=None, pause_step=0, capped_continue=False, yield_every=0):
         """mgs_rollout.  resumable: candidates overflowing the capacity stop at
@@ -354,12 +355,13 @@ class Engine:
         return res
 
     def simulate(self, plan, vstate=None, vclip=0.0):
-        """Free simulation (mgs_simulate): final qpos, qvel, qacc_warmstart and stats
-        of every state.  vstate (n, 2nv): initial qvel | qacc_warmstart per state
-        (None: the model's qvel0 / qacc_ws0); vclip > 0 clips qvel after each step."""
+        """Free simulation (mgs_simulate): final qpos, qvel, qacc_warmstart, act
+        (actuator state) and stats of every state.  vstate (n, 2nv + nact):
+        initial qvel | qacc_warmstart | act per state (None: the model's qvel0 /
+        qacc_ws0, act 0); vclip > 0 clips qvel after each step."""
         n = len(plan.qpos_init)
-        nq, nv = self.cm.nq, self.cm.nv
-        out = np.zeros((n, nq + 2 * nv))
+        nq, nv, na = self.cm.nq, self.cm.nv, int(self.cm.nact)
+        out = np.zeros((n, nq + 2 * nv + na))
         stats = np.zeros((n, abi.MGS["MGS_NSTATS"]), np.int32)
         if n:
             npz = [0] * len(plan.nsteps)
@@ -371,13 +373,14 @@ class Engine:
             vs = None
             if vstate is not None:
                 vs = np.ascontiguousarray(vstate, np.float64)
-                if vs.shape != (n, 2 * nv):
-                    raise ValueError(f"vstate has shape {vs.shape}, expected {(n, 2 * nv)}")
+                if vs.shape != (n, 2 * nv + na):
+                    raise ValueError(f"vstate has shape {vs.shape}, expected {(n, 2 * nv + na)}")
             self._ck(self.lib.mgs_simulate(self.batch(n), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
                                          None if vs is None else ptr(vs, ctypes.c_double), ptr(mq, ctypes.c_double),
                                          ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double),
                                          ptr(out, ctypes.c_double), ptr(stats, ctypes.c_int32)), "mgs_simulate")
-        return dict(qpos=out[:, :nq], qvel=out[:, nq:nq + nv], qacc_warmstart=out[:, nq + nv:], stats=stats)
+        return dict(qpos=out[:, :nq], qvel=out[:, nq:nq + nv], qacc_warmstart=out[:, nq + nv:nq + 2 * nv],
+                    act=out[:, nq + 2 * nv:], stats=stats)
 
     def collision_free_device(self, n, d_qpos, d_mpos, d_mquat, d_out, predicate="any", stream=None):
         """Asynchronous launch on device pointers (ints) with inputs resident in HBM."""

@@ -1093,12 +1093,9 @@ class Compiler:
                                       -1).astype(np.int32)
         cm.nact = int(cm.actuator_actnum.sum()) if acts else 0
         cm.actuator_pidprm = np.array([a["pid"] for a in acts], np.float64).reshape(-1, 5)
-        # gravity compensation (body gravcomp): supported where it is no force
-        # (zero gravity, the gravityless env); elsewhere refused
+        # gravity compensation (body gravcomp, MuJoCo mj_gravcomp): a passive
+        # force -gravity * mass * gravcomp at the body's centre of mass
         cm.body_gravcomp = np.array([b.gravcomp for b in self.bodies], np.float64)
-        if np.any(cm.body_gravcomp != 0.0) and np.any(np.asarray(opt["gravity"], np.float64) != 0.0):
-            raise MJCFError("body gravcomp under nonzero gravity is not supported (the engine supports "
-                            "gravity compensation where gravity is zero)")
         cm.body_xpos0 = xpos
         cm.body_xquat0 = xquat
         cm.body_invweight0, cm.dof_invweight0, cm.meaninertia = _invweight0(cm)
@@ -1244,7 +1241,7 @@ class CompiledModel:
         put_i("body_childnum", [len(k) for k in kids])
         put_i("body_child", [c for k in kids for c in k] or [0])
         for n in ["body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia",
-                  "body_invweight0", "dof_invweight0"]:
+                  "body_gravcomp", "body_invweight0", "dof_invweight0"]:
             put_d(n, getattr(self, n))
         for n in ["jnt_type", "jnt_qposadr", "jnt_dofadr", "jnt_bodyid", "jnt_limited"]:
             put_i(n, getattr(self, n))
@@ -1291,6 +1288,12 @@ class CompiledModel:
         for n in ["actuator_gainprm", "actuator_biasprm", "actuator_ctrlrange", "actuator_forcerange",
                   "actuator_gear"]:
             put_d(n, getattr(self, n))
+        put_i("actuator_actadr", self.actuator_actadr)
+        put_d("actuator_pidprm", self.actuator_pidprm)
+        # initial actuator state shared by every candidate (mj_resetData: zeros;
+        # ClutterTableEnv: the scene's env_state)
+        put_d("act0", getattr(self, "act0", None) if getattr(self, "act0", None) is not None
+              else np.zeros(int(self.nact)))
         ib = np.concatenate(ibuf) if ibuf else np.zeros(0, np.int32)
         db = np.concatenate(dbuf) if dbuf else np.zeros(0, np.float64)
         neqrow = sum({0: 3, 1: 6, 2: 1}[int(t)] for t in self.eq_type)
@@ -1307,7 +1310,7 @@ class CompiledModel:
             ngeom=len(self.geom_bodyid), nhull=len(self.hull_vertnum),
             nhullvert=len(self.hull_vert), npair=len(self.pair_geom1), neq=len(self.eq_type),
             ntendon=len(self.tendon_adr), nwrap=len(self.wrap_dofid), nu=self.nu, nmocap=self.nmocap,
-            ncon_max=ncon_max, nefc_max=nefc_max,
+            nact=int(self.nact), maxcondim=maxdim, ncon_max=ncon_max, nefc_max=nefc_max,
             maxhullvert=int(self.hull_vertnum.max()) if len(self.hull_vertnum) else 0,
             iterations=int(o["iterations"]), noslip_iterations=int(o["noslip_iterations"]),
             cone=1, integrator=2, solver={"PGS": 0, "CG": 2, "Newton": 2}[o.get("solver", "Newton")],

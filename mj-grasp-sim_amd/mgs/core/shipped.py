@@ -5,6 +5,8 @@ compiles ahead of time (mgs/core/special.py), and the pile scenes they use.
     capacity-escalation engine (twice the contacts);
   * C3 (tools/bench_configs.py): Panda x every shipped YCB object;
   * C4: Allegro x the GSO-format mug;
+  * the DEXEE hand x a YCB can (condim-6 contacts: its object is built with
+    -DMGS_MAXDIM=6);
   * C5: the Shadow Hand over the settled 5-object pile (scene state
     tests/golden/clutter_scene_shadow.npz when present, else the pile as
     built);
@@ -25,6 +27,21 @@ import numpy as np
 PILE_OBJECTS = ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange", "061_foam_brick"]
 SPREAD_PILES = [("Robotiq2f85Gripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can"]),
                 ("PandaGripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange"])]
+
+# the dexee x YCB configuration (condim-6 fingertips, mujoco.pid actuators;
+# tests/test_dexee.py)
+DEXEE_OBJECT = "005_tomato_soup_can"
+
+# gravity compensation under gravity (the dexee's gravcomp="1" bodies in a
+# clutter scene): a jointed free body, every body's gravcomp set to {gc}
+# (tests/test_dexee.py::test_gravcomp_gpu_parity)
+GRAVCOMP_XML = """
+<mujoco><option gravity="0 0 -9.81" cone="elliptic" integrator="implicitfast" timestep="0.002"/>
+<worldbody><body name="a" pos="0 0 1" gravcomp="{gc}"><freejoint name="fj"/>
+  <geom type="box" size="0.05 0.05 0.05" mass="2" contype="0" conaffinity="0"/>
+  <body name="b" pos="0.2 0 0" gravcomp="{gc}"><joint name="h" axis="0 1 0"/>
+    <geom type="sphere" size="0.03" pos="0.1 0 0" mass="1" contype="0" conaffinity="0"/></body>
+</body></worldbody></mujoco>"""
 
 _ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..", ".."))
 C5_SCENE = os.path.join(_ROOT, "tests", "golden", "clutter_scene_shadow.npz")
@@ -67,7 +84,8 @@ def shipped_engines() -> List[Tuple[object, int, object, str]]:
     out = []
     for grip, objs in (("Robotiq2f85Gripper", ["003_cracker_box"]),
                        ("PandaGripper", ObjectYCB.all_object_ids()),
-                       ("AllegroGripper", ["Synthetic_Mug_Body"])):
+                       ("AllegroGripper", ["Synthetic_Mug_Body"]),
+                       ("DexeeGripper", [DEXEE_OBJECT])):
         for o in objs:
             env = GravitylessObjectGrasping(get_gripper({"name": grip}), get_object(o))
             out.append((env.model, env.ncon_max, env.nefc_max, "main"))
@@ -84,4 +102,6 @@ def shipped_engines() -> List[Tuple[object, int, object, str]]:
     scenes = [env] + [spread_pile(g, objs) for g, objs in SPREAD_PILES]
     for env in scenes:
         out.append((env.model_for(env.get_state()), env.ncon_max, env._nefc_max, "main"))
+    from mgs.core.mjcf import compile_xml
+    out.append((compile_xml(GRAVCOMP_XML.format(gc=0.5)), 4, None, "main"))
     return out

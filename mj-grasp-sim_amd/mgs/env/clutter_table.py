@@ -121,6 +121,7 @@ class ClutterTableEnv:
         self.nbody = probe.nbody
         self.neq = len(probe.eq_type)
         self.nu = probe.nu
+        self.na = int(probe.nact)                # actuator state (the gripper's mujoco.pid actuators)
         self._state = self._initial_state(probe)
         self._model_key = None
         self._model = None
@@ -140,7 +141,8 @@ class ClutterTableEnv:
 
     # -- state vector (mjSTATE_INTEGRATION of the reference model) ------------
     def _sizes(self):
-        return [("time", 1), ("qpos", self.ref_nq), ("qvel", self.ref_nv), ("qacc_warmstart", self.ref_nv),
+        return [("time", 1), ("qpos", self.ref_nq), ("qvel", self.ref_nv), ("act", self.na),
+                ("qacc_warmstart", self.ref_nv),
                 ("ctrl", self.nu), ("qfrc_applied", self.ref_nv), ("xfrc_applied", 6 * self.nbody),
                 ("eq_active", self.neq), ("mocap_pos", 3), ("mocap_quat", 4)]
 
@@ -166,7 +168,7 @@ class ClutterTableEnv:
         qpos = np.concatenate([cm.qpos0[:gq], CAMERA_QPOS0, cm.qpos0[gq:]])
         mp = cm.body_pos[cm.body_names.index("mocap")]
         mq = cm.body_quat[cm.body_names.index("mocap")]
-        return self.join_state(dict(time=[0.0], qpos=qpos, qvel=np.zeros(self.ref_nv),
+        return self.join_state(dict(time=[0.0], qpos=qpos, qvel=np.zeros(self.ref_nv), act=np.zeros(self.na),
                                     qacc_warmstart=np.zeros(self.ref_nv), ctrl=np.zeros(self.nu),
                                     qfrc_applied=np.zeros(self.ref_nv), xfrc_applied=np.zeros(6 * self.nbody),
                                     eq_active=np.ones(self.neq), mocap_pos=mp, mocap_quat=mq))
@@ -226,6 +228,7 @@ class ClutterTableEnv:
         cm = self._model
         cm.qvel0 = self._reduce(parts["qvel"], "v")
         cm.qacc_ws0 = self._reduce(parts["qacc_warmstart"], "v")
+        cm.act0 = np.array(parts["act"], np.float64)
         return cm
 
     @property
@@ -236,7 +239,7 @@ class ClutterTableEnv:
         from mgs.core.engine import Engine
         cm = self.model_for(state)
         nc = self.ncon_max if ncon_max is None else ncon_max
-        key = (nc, cm.qvel0.tobytes(), cm.qacc_ws0.tobytes())
+        key = (nc, cm.qvel0.tobytes(), cm.qacc_ws0.tobytes(), cm.act0.tobytes())
         if key not in self._engines:
             self._engines = {k: v for k, v in self._engines.items() if k[1:] == key[1:]}
             # escalation capacities re-run few candidates: specialised only if cached
@@ -413,11 +416,11 @@ class ClutterTableEnv:
     def free_plan(self, states, nsteps: int):
         """RolloutPlan of a free simulation of integration states (rows of
         `states`): ctrl and mocap held at the first state's, plus the per-state
-        initial (qvel | qacc_warmstart) in the compiled model's layout."""
+        initial (qvel | qacc_warmstart | act) in the compiled model's layout."""
         parts = [self.split_state(s) for s in states]
         q = np.stack([self._reduce(p["qpos"], "q") for p in parts])
-        vs = np.stack([np.concatenate([self._reduce(p["qvel"], "v"), self._reduce(p["qacc_warmstart"], "v")])
-                       for p in parts])
+        vs = np.stack([np.concatenate([self._reduce(p["qvel"], "v"), self._reduce(p["qacc_warmstart"], "v"),
+                                       p["act"]]) for p in parts])
         mp = np.ascontiguousarray(np.stack([p["mocap_pos"] for p in parts])[:, None, :])
         mq = np.ascontiguousarray(np.stack([p["mocap_quat"] for p in parts]))
         plan = RolloutPlan(nsteps=[int(nsteps)], check_every=[0], check_at_end=[0],
@@ -438,7 +441,8 @@ class ClutterTableEnv:
             p = dict(self.split_state(out[i]))
             p = dict(p, time=t[i:i + 1], qpos=self._expand(p["qpos"], res["qpos"][i], "q"),
                      qvel=self._expand(p["qvel"], res["qvel"][i], "v"),
-                     qacc_warmstart=self._expand(p["qacc_warmstart"], res["qacc_warmstart"][i], "v"))
+                     qacc_warmstart=self._expand(p["qacc_warmstart"], res["qacc_warmstart"][i], "v"),
+                     act=res["act"][i] if "act" in res else p["act"])
             out[i] = self.join_state(p)
         return out
 

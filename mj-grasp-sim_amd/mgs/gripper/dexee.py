@@ -63,7 +63,7 @@ _MASS = {"base": 0.51, "finger_base": 0.89937782, "knuckle": 0.13077995, "proxim
 _HARD = 'condim="4" friction="1 0.001 2e-05" solref="-7000 -167"'
 _SOFT = 'condim="6" friction="1 0.005 0.0001" solref="-2500 -100"'
 # knuckle body orientation: euler="-1.0472 0 0" (radians)
-_KNUCKLE_QUAT = f"{np.cos(-1.0472 / 2)!r} {np.sin(-1.0472 / 2)!r} 0 0"
+_KNUCKLE_QUAT = f"{float(np.cos(-1.0472 / 2))!r} {float(np.sin(-1.0472 / 2))!r} 0 0"
 
 
 class GripperDexee(MjShakableOpenCloseGripper):

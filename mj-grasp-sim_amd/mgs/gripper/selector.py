@@ -3,6 +3,7 @@ import numpy as np
 
 from mgs.gripper.base import MjShakableOpenCloseGripper
 from mgs.gripper.allegro import GripperAllegro
+from mgs.gripper.dexee import GripperDexee
 from mgs.gripper.panda import GripperPanda
 from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
 from mgs.gripper.shadow import GripperShadowRight
@@ -10,7 +11,7 @@ from mgs.util.geo.transforms import SE3Pose
 
 _GRIPPERS = {"Robotiq2f85Gripper": GripperRobotiq2f85, "PandaGripper": GripperPanda,
              "AllegroGripper": GripperAllegro,
-             "ShadowHand": GripperShadowRight}
+             "ShadowHand": GripperShadowRight, "DexeeGripper": GripperDexee}
 
 
 def get_gripper(cfg, default_pose=None) -> MjShakableOpenCloseGripper:

@@ -66,6 +66,7 @@ typedef struct {
   int nq, nv, nb, ng, nu, ncon_max, nefc_max;
   /* state */
   double *qpos, *qvel, *qacc_ws, *ctrl, *mocap_pos, *mocap_quat;
+  double *act, *act_dot;   /* actuator state (mujoco.pid) and its rate */
   double time;
   /* kinematics */
   double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis;
@@ -255,6 +256,7 @@ static Dat* dat_alloc(const Mdl* md) {
   size_t tot = 0;
 #define TAKE(ptr, n) do { d->ptr = p; if (p) p += (n); tot += (size_t)(n); } while (0)
   TAKE(qpos, nq); TAKE(qvel, nv); TAKE(qacc_ws, nv); TAKE(ctrl, nu);
+  TAKE(act, m->nact > 0 ? m->nact : 1); TAKE(act_dot, m->nact > 0 ? m->nact : 1);
   TAKE(mocap_pos, 3 * m->nmocap + 3); TAKE(mocap_quat, 4 * m->nmocap + 4);
   TAKE(xpos, 3 * nb); TAKE(xquat, 4 * nb); TAKE(xmat, 9 * nb); TAKE(xipos, 3 * nb); TAKE(ximat, 9 * nb);
   TAKE(xanchor, 3 * nj); TAKE(xaxis, 3 * nj);
@@ -525,6 +527,37 @@ static void ldl_solve(int n, const double* L, const double* Dinv, const double* 
   }
 }
 
+/* MuJoCo's mujoco.pid actuator plugin, restated from its documented
+ * semantics (parity unpinned: the plugin's source is not in the reference or
+ * this image).  pidprm = kp, ki, kd, imax, slewmax (imax / slewmax < 0: not
+ * set).  Setpoint: the clamped ctrl, held within slewmax dt of the previous
+ * setpoint (act entry 0 when slewmax is set); error = setpoint - length;
+ * force = kp error + kd (setpoint rate - velocity) + ki integral (the next act
+ * entry when ki != 0).  act_dot: the setpoint rate and the error, advanced by
+ * integrate() (mj_advance) with the integral clamped to |ki integral| <= imax. */
+static double pid_force(const Mdl* md, Dat* d, int u, double c, double len, double vel) {
+  const double* pp = DA(md, actuator_pidprm) + 5 * u;
+  const double dt = md->m->timestep;
+  int k = IA(md, actuator_actadr)[u];
+  double cdot = 0.0;
+  if (pp[4] >= 0.0) {
+    const double prev = d->act[k];
+    const double lo = prev - pp[4] * dt, hi = prev + pp[4] * dt;
+    if (c < lo) c = lo;
+    if (c > hi) c = hi;
+    cdot = (c - prev) / dt;
+    d->act_dot[k] = cdot;
+    k++;
+  }
+  const double err = c - len;
+  double f = pp[0] * err + pp[2] * (cdot - vel);
+  if (pp[1] != 0.0) {
+    f = f + pp[1] * d->act[k];
+    d->act_dot[k] = err;
+  }
+  return f;
+}
+
 /* tendon length/moment, actuator length/moment/velocity/force, qfrc_actuator */
 static void actuation(const Mdl* md, Dat* d) {
   const mgs_model_desc* m = md->m;
@@ -566,10 +599,15 @@ static void actuation(const Mdl* md, Dat* d) {
       if (c < crange[2 * u]) c = crange[2 * u];
       if (c > crange[2 * u + 1]) c = crange[2 * u + 1];
     }
-    double g = gain[3 * u];
-    if (gtype[u] == MGS_GAIN_AFFINE) g = (gain[3 * u] + gain[3 * u + 1] * len) + gain[3 * u + 2] * vel;
-    double f = g * c;
-    if (btype[u] == MGS_BIAS_AFFINE) f = f + ((bias[3 * u] + bias[3 * u + 1] * len) + bias[3 * u + 2] * vel);
+    double f;
+    if (gtype[u] == MGS_GAIN_PID) {
+      f = pid_force(md, d, u, c, len, vel);
+    } else {
+      double g = gain[3 * u];
+      if (gtype[u] == MGS_GAIN_AFFINE) g = (gain[3 * u] + gain[3 * u + 1] * len) + gain[3 * u + 2] * vel;
+      f = g * c;
+      if (btype[u] == MGS_BIAS_AFFINE) f = f + ((bias[3 * u] + bias[3 * u + 1] * len) + bias[3 * u + 2] * vel);
+    }
     if (flim[u]) {
       if (f < frange[2 * u]) f = frange[2 * u];
       if (f > frange[2 * u + 1]) f = frange[2 * u + 1];
@@ -591,6 +629,33 @@ static void passive(const Mdl* md, Dat* d) {
       d->qfrc_passive[jd[j]] = -stiff[j] * (d->qpos[jq[j]] - qspring[jq[j]]);
   }
   for (int k = 0; k < m->nv; k++) d->qfrc_passive[k] = d->qfrc_passive[k] - damp[k] * d->qvel[k];
+  /* gravity compensation (MuJoCo mj_gravcomp: mj_applyFT of -gravity mass
+   * gravcomp at xipos, added to qfrc_passive; parity unpinned -- only the
+   * dexee's bodies carry gravcomp and no reference vector covers it).  With h
+   * = mass (xipos - subtree_com) = cinert[6..8], a dof's Jacobian column
+   * dotted with the force is -gravcomp ((g . cdof_lin) mass + g . (cdof_ang x h)),
+   * summed over bodies in order. */
+  const double* g = m->gravity;
+  if (g[0] != 0.0 || g[1] != 0.0 || g[2] != 0.0) {
+    const double* gc = DA(md, body_gravcomp);
+    const int32_t *last = IA(md, body_lastdof), *dpar = IA(md, dof_parentid);
+    double acc[128] = {0};
+    int any[128] = {0};
+    for (int b = 1; b < m->nbody; b++) {
+      if (gc[b] == 0.0) continue;
+      const double* ci = d->cinert + 10 * b;
+      for (int k = last[b]; k >= 0; k = dpar[k]) {
+        const double* cd = d->cdof + 6 * k;
+        double cr[3];
+        cross3(cr, cd, ci + 6);
+        double t = ((g[0] * cd[3] + g[1] * cd[4]) + g[2] * cd[5]) * ci[9] + ((g[0] * cr[0] + g[1] * cr[1]) + g[2] * cr[2]);
+        acc[k] = acc[k] + (-gc[b]) * t;
+        any[k] = 1;
+      }
+    }
+    for (int k = 0; k < m->nv; k++)
+      if (any[k]) d->qfrc_passive[k] = d->qfrc_passive[k] + acc[k];
+  }
 }
 
 /* mj_comVel + mj_rne (no acceleration term) -> qfrc_bias */
@@ -1877,9 +1942,83 @@ static void qcqp3(const double* A, const double* b, const double* mu, double r, 
   }
 }
 
+/* n = 5 (condim-6 contacts): MuJoCo's general mju_QCQP restated (parity
+ * unpinned: its source is not here).  The same Newton iteration on the
+ * multiplier with (A + la I) factored by Cholesky; a pivot below 1e-10 counts
+ * as singular (result 0).  The kernel's qcqpn<N> has this arithmetic. */
+static void qcqpn(int n, const double* A, const double* b, const double* mu, double r, double* x) {
+  double As[25], bs[5], v[5], L[25], t[5], pv[5];
+  for (int i = 0; i < n; i++) {
+    bs[i] = b[i] * mu[i];
+    v[i] = 0.0;
+    for (int j = 0; j < n; j++) As[i * n + j] = (A[i * n + j] * mu[i]) * mu[j];
+  }
+  double rr = r * r, la = 0.0;
+  int sing = 0;
+  for (int it = 0; it < 20; it++) {
+    for (int q = 0; q < n * n; q++) L[q] = As[q];
+    for (int i = 0; i < n; i++) L[i * n + i] = L[i * n + i] + la;
+    for (int j = 0; j < n; j++) {
+      double p = L[j * n + j];
+      for (int k = 0; k < j; k++) p = p - L[j * n + k] * L[j * n + k];
+      if (p < 1e-10) sing = 1;
+      p = sqrt(p < 1e-10 ? 1e-10 : p);
+      L[j * n + j] = p;
+      for (int i = j + 1; i < n; i++) {
+        double s = L[i * n + j];
+        for (int k = 0; k < j; k++) s = s - L[i * n + k] * L[j * n + k];
+        L[i * n + j] = s / p;
+      }
+    }
+    if (sing) {
+      for (int i = 0; i < n; i++) v[i] = 0.0;
+      break;
+    }
+    for (int i = 0; i < n; i++) {
+      double s = bs[i];
+      for (int k = 0; k < i; k++) s = s - L[i * n + k] * t[k];
+      t[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+      double s = t[i];
+      for (int k = i + 1; k < n; k++) s = s - L[k * n + i] * v[k];
+      v[i] = s / L[i * n + i];
+    }
+    for (int i = 0; i < n; i++) v[i] = -v[i];
+    double vv = 0.0;
+    for (int i = 0; i < n; i++) vv = vv + v[i] * v[i];
+    double val = vv - rr;
+    if (val < 1e-10) break;
+    for (int i = 0; i < n; i++) {
+      double s = v[i];
+      for (int k = 0; k < i; k++) s = s - L[i * n + k] * t[k];
+      t[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+      double s = t[i];
+      for (int k = i + 1; k < n; k++) s = s - L[k * n + i] * pv[k];
+      pv[i] = s / L[i * n + i];
+    }
+    double vp = 0.0;
+    for (int i = 0; i < n; i++) vp = vp + v[i] * pv[i];
+    double deriv = -2.0 * vp;
+    double delta = -val / deriv;
+    if (delta < 1e-10) break;
+    la = la + delta;
+  }
+  for (int i = 0; i < n; i++) x[i] = v[i] * mu[i];
+  if (!sing && la != 0.0) {
+    double s = 0.0;
+    for (int i = 0; i < n; i++) s = s + (x[i] * x[i]) / (mu[i] * mu[i]);
+    s = sqrt((r * r) / (s > O_MINVAL ? s : O_MINVAL));
+    for (int i = 0; i < n; i++) x[i] = x[i] * s;
+  }
+}
+
 static void qcqp(int n, const double* A, const double* b, const double* mu, double r, double* x) {
   if (n == 2) qcqp2(A, b, mu, r, x);
-  else qcqp3(A, b, mu, r, x);
+  else if (n == 3) qcqp3(A, b, mu, r, x);
+  else qcqpn(n, A, b, mu, r, x);
 }
 
 /* MuJoCo's costChange (engine_solver.c): the change of the dual cost
@@ -2376,7 +2515,7 @@ static void solve_newton(const Mdl* md, Dat* d) {
        bit-exactly on MI355X, tools/probes/mfma_f64_check.py). */
     for (int r = 0; r < ne; r++) {
       int t = d->efc_type[r], st = d->efc_state[r];
-      double wv[4] = {0.0, 0.0, 0.0, 0.0};
+      double wv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
       int lead = r, nd = 0;
       if (st == ST_QUAD) {
         wv[0] = d->efc_Dr[r];
@@ -2384,7 +2523,7 @@ static void solve_newton(const Mdl* md, Dat* d) {
       } else if (st == ST_CONE && t == MGS_EFC_CONTACT) {
         lead = r;
         while (lead > 0 && d->efc_type[lead - 1] == MGS_EFC_CONTACT && d->efc_con[lead - 1] == d->efc_con[r] &&
-               r - lead < 3)
+               r - lead < 5)
           lead--;
         int dim = d->efc_dim[r], bp = r - lead;
         const double* hb = d->efc_hb + 36 * lead;
@@ -2540,6 +2679,28 @@ static void integrate(const Mdl* md, Dat* d) {
   }
   for (int k = 0; k < nv; k++) d->qacc_ws[k] = d->qacc[k];
   d->time = d->time + dt;
+  /* actuator state (mj_advance: act += dt act_dot), a mujoco.pid integral then
+   * clamped to |ki integral| <= imax */
+  const int32_t* aadr = IA(md, actuator_actadr);
+  const double* pid = DA(md, actuator_pidprm);
+  for (int u = 0; u < m->nu && m->nact > 0; u++) {
+    if (gtype[u] != MGS_GAIN_PID) continue;
+    const double* pp = pid + 5 * u;
+    int k = aadr[u];
+    if (pp[4] >= 0.0) {
+      d->act[k] = d->act[k] + dt * d->act_dot[k];
+      k++;
+    }
+    if (pp[1] != 0.0) {
+      double v = d->act[k] + dt * d->act_dot[k];
+      if (pp[3] >= 0.0) {
+        const double lim = pp[3] / pp[1];
+        if (v < -lim) v = -lim;
+        if (v > lim) v = lim;
+      }
+      d->act[k] = v;
+    }
+  }
 }
 
 static void step(const Mdl* md, Dat* d) {
@@ -2591,6 +2752,7 @@ static void reset(const Mdl* md, Dat* d, const double* qpos_init, const double* 
   memcpy(d->qvel, DA(md, qvel0), sizeof(double) * m->nv);
   memcpy(d->qacc_ws, DA(md, qacc_ws0), sizeof(double) * m->nv);
   memset(d->ctrl, 0, sizeof(double) * (m->nu > 0 ? m->nu : 1));
+  for (int k = 0; k < m->nact; k++) { d->act[k] = DA(md, act0)[k]; d->act_dot[k] = 0.0; }
   for (int k = 0; k < 3; k++) d->mocap_pos[k] = mpos ? mpos[k] : 0.0;
   for (int k = 0; k < 4; k++) d->mocap_quat[k] = mquat[k];
   d->time = 0.0;
@@ -2632,7 +2794,7 @@ static void rollout_batch(const mgs_model_desc* desc, const int32_t* I, const do
   Mdl md = {desc, I, D};
   int np = sc->nphase;
   int obj_qposadr = sc->obj_qposadr;
-  int nq = desc->nq, nv = desc->nv;
+  int nq = desc->nq, nv = desc->nv, na = desc->nact;
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
   {
     Dat* d = dat_alloc(&md);
@@ -2642,8 +2804,10 @@ static void rollout_batch(const mgs_model_desc* desc, const int32_t* I, const do
       const double* pt = phase_target + (size_t)i * np * 3;
       reset(&md, d, qpos_init + (size_t)i * nq, ps, mocap_quat + 4 * i);
       if (vstate_init) {
-        memcpy(d->qvel, vstate_init + (size_t)i * 2 * nv, sizeof(double) * nv);
-        memcpy(d->qacc_ws, vstate_init + (size_t)i * 2 * nv + nv, sizeof(double) * nv);
+        const double* vs = vstate_init + (size_t)i * (2 * nv + na);
+        memcpy(d->qvel, vs, sizeof(double) * nv);
+        memcpy(d->qacc_ws, vs + nv, sizeof(double) * nv);
+        if (na > 0) memcpy(d->act, vs + 2 * nv, sizeof(double) * na);
       }
       int ok = 1, gstep = 0, fstep = -1, maxcon = 0, maxefc = 0, sumcon = 0, sumefc = 0;
       for (int p = 0; p < np && ok; p++) {
@@ -2685,10 +2849,11 @@ static void rollout_batch(const mgs_model_desc* desc, const int32_t* I, const do
         st[0] = maxcon; st[1] = maxefc; st[2] = d->overflow; st[3] = d->iters; st[4] = sumcon; st[5] = sumefc;
       }
       if (state_out) {
-        double* so = state_out + (size_t)i * (nq + 2 * nv);
+        double* so = state_out + (size_t)i * (nq + 2 * nv + na);
         memcpy(so, d->qpos, sizeof(double) * nq);
         memcpy(so + nq, d->qvel, sizeof(double) * nv);
         memcpy(so + nq + nv, d->qacc_ws, sizeof(double) * nv);
+        if (na > 0) memcpy(so + nq + 2 * nv, d->act, sizeof(double) * na);
       }
     }
     dat_free(d);
@@ -2704,8 +2869,8 @@ int oracle_rollout(const mgs_model_desc* desc, const int32_t* I, const double* D
   return 0;
 }
 
-/* mgs_simulate restated: the rollout loop from per-state (qpos, qvel, warmstart),
- * final state out (n * (nq + 2nv)) */
+/* mgs_simulate restated: the rollout loop from per-state (qpos, qvel,
+ * warmstart, act), final state out (n * (nq + 2nv + nact)) */
 int oracle_simulate_batch(const mgs_model_desc* desc, const int32_t* I, const double* D,
                           const mgs_schedule* sc, int n, const double* qpos_init, const double* vstate_init,
                           const double* mocap_quat, const double* phase_start, const double* phase_target,

@@ -91,24 +91,29 @@ class OracleModel:
         return dict(label=label.astype(bool), fail_step=fail, obj_qpos=objq, stats=stats)
 
     def simulate_batch(self, plan, vstate=None, vclip=0.0, nthreads=1):
-        """mgs_simulate restated: final qpos, qvel, qacc_warmstart and stats of every state."""
+        """mgs_simulate restated: final qpos, qvel, qacc_warmstart, act and stats of
+        every state; vstate (n, 2nv + nact): initial qvel | warmstart | act."""
         n = len(plan.qpos_init)
         cm = self.cm
         sched = abi.make_schedule(plan.nsteps, plan.check_every, plan.check_at_end, plan.ctrl, plan.obj_qposadr,
                                   check_offset=getattr(plan, "check_offset", None), vclip=vclip)
-        out = np.zeros((n, cm.nq + 2 * cm.nv))
+        na = int(cm.nact)
+        out = np.zeros((n, cm.nq + 2 * cm.nv + na))
         stats = np.zeros((n, abi.MGS["MGS_NSTATS"]), np.int32)
         q = np.ascontiguousarray(plan.qpos_init, np.float64)
         mq = np.ascontiguousarray(plan.mocap_quat, np.float64)
         ps = np.ascontiguousarray(plan.phase_start, np.float64)
         pt = np.ascontiguousarray(plan.phase_target, np.float64)
         vs = None if vstate is None else np.ascontiguousarray(vstate, np.float64)
+        if vs is not None and vs.shape != (n, 2 * cm.nv + na):
+            raise ValueError(f"vstate has shape {vs.shape}, expected {(n, 2 * cm.nv + na)}")
         lib().oracle_simulate_batch(*self._args(), ctypes.byref(sched), n, ptr(q, ctypes.c_double),
                                     None if vs is None else ptr(vs, ctypes.c_double), ptr(mq, ctypes.c_double),
                                     ptr(ps, ctypes.c_double), ptr(pt, ctypes.c_double), ptr(out, ctypes.c_double),
                                     ptr(stats, ctypes.c_int32), nthreads)
         nq, nv = cm.nq, cm.nv
-        return dict(qpos=out[:, :nq], qvel=out[:, nq:nq + nv], qacc_warmstart=out[:, nq + nv:], stats=stats)
+        return dict(qpos=out[:, :nq], qvel=out[:, nq:nq + nv], qacc_warmstart=out[:, nq + nv:nq + 2 * nv],
+                    act=out[:, nq + 2 * nv:], stats=stats)
 
     def trace(self, qpos, mocap_pos, mocap_quat, ctrl, nsteps):
         nq = self.cm.nq
