@@ -489,6 +489,16 @@ int mgs_rollout_grid(mgs_batch* batch, int n);
  * rotation (grown, with a device synchronisation, when a launch's n exceeds
  * it), whatever the batch capacity. */
 int mgs_queue_stats(mgs_batch* batch, uint64_t* out);
+/* Execution spans of the batch's work-queue rollout launches (round 5), from
+ * the device's 100 MHz real-time counter: the workgroup that takes candidate 0
+ * records the start, the last workgroup to leave records the end, in the
+ * launch's queue header.  Writes up to cap spans (ms) of the launches completed
+ * since the previous call, in queue-slot order (the slots cycle through 64
+ * headers, so call at least every 64 launches), sets *count, and clears the
+ * spans it returned.  Synchronises the device.  (bench.py: the per-launch
+ * duration of the roofline line, the kernel-trace duration without a
+ * profiler.) */
+int mgs_queue_spans(mgs_batch* batch, double* out_ms, int cap, int* count);
 /* Rollout launch mode for this process; returns the previous one and leaves it
  * unchanged if mode < 0.  0: one workgroup per candidate; 1 (default): the work
  * queue on the resident grid; k >= 2: the queue on at most k workgroups (tests

@@ -581,6 +581,28 @@ int mgs_queue_stats(mgs_batch* b, uint64_t* out) {
   return MGS_OK;
 }
 
+int mgs_queue_spans(mgs_batch* b, double* out_ms, int cap, int* count) {
+  if (!b || !out_ms || !count || cap < 0) return fail(MGS_EINVAL, "mgs_queue_spans: bad argument%s");
+  HIPCHK(hipSetDevice(b->m->device));
+  uint32_t h[MGS_QHDR * MGS_QUEUE_RING];
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(h, b->d_queue, sizeof(h), hipMemcpyDeviceToHost));
+  int k = 0;
+  for (int i = 0; i < MGS_QUEUE_RING; i++) {
+    // oldest first: the slot after the last one handed out
+    const int s = (b->qslot + i) % MGS_QUEUE_RING;
+    uint64_t t0, t1;
+    memcpy(&t0, h + MGS_QHDR * s + 8, sizeof(t0));
+    memcpy(&t1, h + MGS_QHDR * s + 10, sizeof(t1));
+    if (t0 == 0 || t1 <= t0) continue;
+    if (k < cap) out_ms[k++] = (double)(t1 - t0) * 1e-5;   // 100 MHz ticks
+    HIPCHK(hipMemset(b->d_queue + MGS_QHDR * s + 8, 0, 4 * sizeof(uint32_t)));
+  }
+  HIPCHK(hipDeviceSynchronize());
+  *count = k;
+  return MGS_OK;
+}
+
 int mgs_overflow_list_device(int n, const int32_t* d_stats, int flag_mask, int32_t* d_count, int32_t* d_list,
                              void* stream) {
   if (n < 0 || !d_stats || !d_count || !d_list) return fail(MGS_EINVAL, "mgs_overflow_list_device: bad argument%s");

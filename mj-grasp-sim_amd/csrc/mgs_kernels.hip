@@ -4940,8 +4940,10 @@ DEVI void save_record(const Mdl& md, Dat& d, double* rec, int p, int t, int gste
 // overwrites them), and the host entries compare word 7 after every launch
 // and fail with MGS_EQUEUE when it grew.  The ring holds MGS_QRING_F(n)
 // words for the launch's n (the host sizes the rings for the largest n it
-// launched, so a ring slot index never leaves its allocation).
-#define MGS_QHDR 8
+// launched, so a ring slot index never leaves its allocation).  [8..9] /
+// [10..11]: the launch's start / end on the 100 MHz real-time counter (the
+// workgroup that takes candidate 0 / the last one to leave; mgs_queue_spans).
+#define MGS_QHDR 12
 #define MGS_QRING_F(n) (2u * (uint32_t)(n))
 #ifndef MGS_SPIN_MAX
 #define MGS_SPIN_MAX (1u << 22)
@@ -5294,6 +5296,9 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
         const uint32_t u = __builtin_amdgcn_readfirstlane(t);
         if (u < (uint32_t)n) s = (int)u;
         else fresh = 0;
+        if (u == 0 && lane_id() == 0)
+          __hip_atomic_store((unsigned long long*)(queue + 8), (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (s < 0 && yq) {
         s = ring_pop(yq, n);
@@ -5306,6 +5311,8 @@ DEVI void rollout_entry(double* smem, const Mdl& mdarg, const int32_t* __restric
     }
     if (lane_id() == 0 &&
         __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store((unsigned long long*)(queue + 10), (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(queue + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(queue + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -60,6 +60,7 @@ def load_library(wide: bool = False):
     L.mgs_rollout_resume.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
                                      P(abi.RolloutOut)]
     L.mgs_queue_stats.argtypes = [vp, P(ctypes.c_uint64)]
+    L.mgs_queue_spans.argtypes = [vp, P(c_d), ctypes.c_int, P(ctypes.c_int)]
     L.mgs_last_kernel_ms.argtypes = [vp]
     L.mgs_last_kernel_ms.restype = ctypes.c_double
     L.mgs_last_collision_ms.argtypes = [vp]
@@ -439,6 +440,15 @@ class Engine:
         out = (ctypes.c_uint64 * 2)()
         self._ck(self.lib.mgs_queue_stats(self.batch(1), out), "mgs_queue_stats")
         return int(out[0]), int(out[1])
+
+    def queue_spans(self):
+        """execution spans (ms, device real-time counter) of this engine's
+        work-queue rollout launches completed since the previous call, oldest
+        first (mgs_queue_spans; synchronises the device)"""
+        out = (ctypes.c_double * 64)()
+        cnt = ctypes.c_int()
+        self._ck(self.lib.mgs_queue_spans(self.batch(1), out, 64, ctypes.byref(cnt)), "mgs_queue_spans")
+        return [float(out[i]) for i in range(cnt.value)]
 
     def last_collision_ms(self):
         return self.lib.mgs_last_collision_ms(self._batch)

@@ -787,3 +787,25 @@ def test_lost_rotation_candidate_raises(env, candidates):
     finally:
         L.mgs_rollout_queue(prev)
         bad.close()
+
+
+@pytest.mark.gpu
+def test_queue_spans_device_clock(env, candidates):
+    """mgs_queue_spans: a work-queue rollout launch leaves its execution span
+    on the device's real-time counter (bench.py's launch_ms); the call
+    returns each completed launch once, then clears it"""
+    from conftest import plan_for
+    eng = env.engine
+    eng.queue_spans()
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(eng.collision_free(q, mp, mq))[0]
+    prev = eng.lib.mgs_rollout_queue(16)       # the queue on 16 workgroups: a real work queue
+    try:
+        r = eng.rollout(plan_for(env, poses[idx], J[idx]))
+    finally:
+        eng.lib.mgs_rollout_queue(prev)
+    s = eng.queue_spans()
+    assert len(s) == 1
+    assert 0.0 < s[0] <= r["kernel_ms"] * 1.05 + 0.05     # inside the HIP events around the launch
+    assert eng.queue_spans() == []
