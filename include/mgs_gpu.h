@@ -254,6 +254,9 @@ typedef struct mgs_model_desc {
   int32_t d_actuator_ctrlrange; /* 2 */
   int32_t d_actuator_forcerange;/* 2 */
   int32_t d_actuator_gear;      /* 1 */
+  int32_t d_actuator_moment;    /* nu x nv: the actuator moment rows (joint: gear at the joint's dof;
+                                   fixed tendon: 0 + sum of wrap coef x gear in wrap order), constant
+                                   for these transmissions (round 5: the wide build reads them here) */
   int32_t i_actuator_actadr;    /* first act entry of the actuator, -1 if it has none */
   int32_t d_act0;               /* nact: the act state every candidate starts from (mj_resetData: 0;
                                    ClutterTableEnv: the scene state's, clutter_table.py:290-291) */

@@ -56,10 +56,11 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   sizes[L_act] = m.nact; sizes[L_act_dot] = m.nact;
   sizes[L_xpos] = 3 * nb; sizes[L_xquat] = 4 * nb; sizes[L_xmat] = 9 * nb; sizes[L_subtree_com] = 3 * nb;
   sizes[L_cinert] = 10 * nb; sizes[L_cdof] = 6 * nv;
-  sizes[L_M] = nv * nv; sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_sD] = nv; sizes[L_isD] = nv;
+  sizes[L_M] = TRI_SIZE(nv); sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_sD] = nv; sizes[L_isD] = nv;
   sizes[L_tmp] = nv; sizes[L_tmp2] = nv;
   sizes[L_qfrc_smooth] = nv; sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv;
-  sizes[L_act_force] = nu; sizes[L_act_moment] = nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
+  // (the wide build reads the actuator moment rows from the model)
+  sizes[L_act_force] = nu; sizes[L_act_moment] = MGS_PACKED ? 0 : nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
   sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = 5 * nc;
   // contact blocks (and Newton cone Hessians): maxdim^2 per contact, maxdim 6
   // for models with condim-6 pairs (their code objects: -DMGS_MAXDIM=6)
@@ -86,7 +87,7 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   // (the Hessian's weight table, (maxdim + 1) ne, runs on into scratch too)
   int xreg = 3 * ne;
   if (xreg + us[U_scratch] < (maxdim + 1) * ne) xreg = (maxdim + 1) * ne - us[U_scratch];
-  if (xreg + us[U_scratch] < nv * nv) xreg = nv * nv - us[U_scratch];
+  if (xreg + us[U_scratch] < TRI_SIZE(nv)) xreg = TRI_SIZE(nv) - us[U_scratch];
   us[U_jar] = ne; us[U_jv] = ne; us[U_f] = ne; us[U_Dr] = ne; us[U_isR] = ne;
   us[U_nw] = nv; us[U_nw0] = nv; us[U_ng] = nv; us[U_ndir] = nv;
   int U = 0, off;
@@ -107,9 +108,9 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   l.u[U_vel] = off; l.u[U_pos] = off + ne; l.u[U_margin] = off + 2 * ne; l.u[U_nH] = off; off += xreg;
   for (int k = U_scratch; k <= U_ndir; k++) { l.u[k] = off; off += us[k]; }
   if (off > U) U = off;
-  // integration
+  // integration: M - dt qDeriv is formed in place in M (the qDeriv view is
+  // not stored)
   l.u[U_qDeriv] = 0;
-  if (nv * nv > U) U = nv * nv;
   sizes[L_U] = U;
   sizes[L_ints] = (16 + 3 * nc + 4 * ne + 1) / 2;
   off = 0;

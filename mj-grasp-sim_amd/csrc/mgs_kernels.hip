@@ -121,6 +121,28 @@ static_assert(MGS_MAXDIM == 4 || MGS_MAXDIM == 6, "MGS_MAXDIM is 4 or 6");
 #endif
 #endif
 
+// Packed storage of the mass matrix / its LDL factor and of the Newton
+// Hessian (symmetric; only the lower triangle is ever read): row i of the
+// lower triangle at i (i + 1) / 2 instead of i nv.  The wide build (clutter
+// piles, nv up to 58, whose row loops read M and H from LDS anyway) packs
+// them: 2 x 1653 doubles less at nv 58 (round 5, two pile workgroups per CU);
+// the main build keeps the square layout its register-row factor loads.
+#ifndef MGS_PACKED
+#ifdef MGS_WIDE
+#define MGS_PACKED 1
+#else
+#define MGS_PACKED 0
+#endif
+#endif
+#if MGS_PACKED
+#define TRI(i, k, n) ((((i) * ((i) + 1)) >> 1) + (k))
+#define TRI_SIZE(n) (((n) * ((n) + 1)) >> 1)
+#else
+#define TRI(i, k, n) ((i) * (n) + (k))
+#define TRI_SIZE(n) ((n) * (n))
+#endif
+static_assert(!(MGS_PACKED && MGS_REG_ROWS), "packed M / H needs the LDS row factor (MGS_REG_ROWS 0)");
+
 // the lane index through an opaque move at every use: index arithmetic and
 // lane masks derived from it are recomputed where they are used instead of
 // being hoisted out of the step loop and held (in VGPRs, AGPRs and SGPR
@@ -627,7 +649,7 @@ DEVI void crb(const Mdl& md, Dat& d) {
   for (int k = lane; k < 10 * nb; k += WAVE) d.crb[k] = d.cinert[k];
   wsync();
   accumulate_up<10>(md, d.crb, 0);
-  for (int k = lane; k < nv * nv; k += WAVE) d.M[k] = 0.0;
+  for (int k = lane; k < TRI_SIZE(nv); k += WAVE) d.M[k] = 0.0;
   wsync();
   if (nv <= WAVE) {
     // lane i walks dof i's ancestors; the walk reads a lane-resident copy of
@@ -637,13 +659,15 @@ DEVI void crb(const Mdl& md, Dat& d) {
     int i = lane < nv ? lane : 0;
     double buf[6];
     mul_inert_vec(buf, d.crb + 10 * dbody[i], d.cdof + 6 * i);
-    if (lane < nv) d.M[i * nv + i] = dot6(d.cdof + 6 * i, buf) + arm[i];
+    if (lane < nv) d.M[TRI(i, i, nv)] = dot6(d.cdof + 6 * i, buf) + arm[i];
     int j = dp_lane;
     while (__ballot(j >= 0)) {
       if (j >= 0) {
         double v = dot6(d.cdof + 6 * j, buf);
-        d.M[i * nv + j] = v;
+        d.M[TRI(i, j, nv)] = v;
+#if !MGS_PACKED
         d.M[j * nv + i] = v;
+#endif
       }
       int jn = shfl(dp_lane, j >= 0 ? j : 0);
       j = j >= 0 ? jn : -1;
@@ -652,12 +676,14 @@ DEVI void crb(const Mdl& md, Dat& d) {
     for (int i = lane; i < nv; i += WAVE) {
       double buf[6];
       mul_inert_vec(buf, d.crb + 10 * dbody[i], d.cdof + 6 * i);
-      d.M[i * nv + i] = dot6(d.cdof + 6 * i, buf) + arm[i];
+      d.M[TRI(i, i, nv)] = dot6(d.cdof + 6 * i, buf) + arm[i];
       int j = dpar[i];
       while (j >= 0) {
         double v = dot6(d.cdof + 6 * j, buf);
-        d.M[i * nv + j] = v;
+        d.M[TRI(i, j, nv)] = v;
+#if !MGS_PACKED
         d.M[j * nv + i] = v;
+#endif
         j = dpar[j];
       }
     }
@@ -708,35 +734,46 @@ DEVI void ldl_factor_lds(double* A, double* Dv, double* Dinv) {
   const int lane = lane_id();
   const int li = lane < NV ? lane : 0;
   for (int c = 0; c < NV; c++) {
-    double s = A[li * NV + c];
+    double s = A[TRI(li, c, NV)];
     // four products' operands loaded ahead of their FMAs (the LDS latency is
     // paid once per four terms instead of once per term); the FMA chain and
-    // its ascending-k order are unchanged
+    // its ascending-k order are unchanged.  V_ck = l_ck d_k: parked in the
+    // dead upper triangle (square layout), or formed again from l_ck and
+    // Dv[k] (packed layout: the same product of the same operands)
+#if MGS_PACKED
+#define LDL_V(k) (A[TRI(c, (k), NV)] * Dv[k])
+#else
+#define LDL_V(k) A[(k) * NV + c]
+#endif
     int k = 0;
     // eight at a time first (one LDS latency per eight terms), then four
     for (; k + 8 <= c; k += 8) {
       double a[8], b[8];
 #pragma unroll
-      for (int q = 0; q < 8; q++) { a[q] = A[li * NV + k + q]; b[q] = A[(k + q) * NV + c]; }
+      for (int q = 0; q < 8; q++) { a[q] = A[TRI(li, k + q, NV)]; b[q] = LDL_V(k + q); }
 #pragma unroll
       for (int q = 0; q < 8; q++) s = __builtin_fma(-a[q], b[q], s);
     }
     for (; k + 4 <= c; k += 4) {
-      const double a0 = A[li * NV + k], a1 = A[li * NV + k + 1], a2 = A[li * NV + k + 2], a3 = A[li * NV + k + 3];
-      const double b0 = A[k * NV + c], b1 = A[(k + 1) * NV + c], b2 = A[(k + 2) * NV + c], b3 = A[(k + 3) * NV + c];
+      const double a0 = A[TRI(li, k, NV)], a1 = A[TRI(li, k + 1, NV)], a2 = A[TRI(li, k + 2, NV)],
+                   a3 = A[TRI(li, k + 3, NV)];
+      const double b0 = LDL_V(k), b1 = LDL_V(k + 1), b2 = LDL_V(k + 2), b3 = LDL_V(k + 3);
       s = __builtin_fma(-a0, b0, s);
       s = __builtin_fma(-a1, b1, s);
       s = __builtin_fma(-a2, b2, s);
       s = __builtin_fma(-a3, b3, s);
     }
-    for (; k < c; k++) s = __builtin_fma(-A[li * NV + k], A[k * NV + c], s);
+    for (; k < c; k++) s = __builtin_fma(-A[TRI(li, k, NV)], LDL_V(k), s);
+#undef LDL_V
     double dc = readlane_d(s, c);
     double inv = 1.0 / dc;
     if (lane == 0) { Dv[c] = dc; Dinv[c] = inv; }
     if (lane > c && lane < NV) {
       double l = s * inv;
-      A[li * NV + c] = l;
+      A[TRI(li, c, NV)] = l;
+#if !MGS_PACKED
       A[c * NV + li] = l * dc;
+#endif
     }
     wsync();
   }
@@ -782,8 +819,8 @@ DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double
 #define LS_LR(k) Lr[k]
 #define LS_LC(k) Lc[k]
 #else
-#define LS_LR(k) L[li * NV + (k)]
-#define LS_LC(k) L[(k) * NV + li]
+#define LS_LR(k) L[TRI(li, (k), NV)]
+#define LS_LC(k) L[TRI((k), li, NV)]
 #endif
   double acc = b[li];
 #pragma unroll
@@ -850,6 +887,23 @@ DEVI void actuation(const Mdl& md, Dat& d) {
   const int32_t *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
   double qfa = 0.0;
   for (int u = 0; u < md.m.nu; u++) {
+#if MGS_PACKED
+    // the wide build reads the moment rows from the model (joint and fixed-
+    // tendon transmissions: constant; mgs_model_desc.d_actuator_moment, the
+    // same sums formed on the host) instead of keeping nu x nv of them in LDS
+    const double* mom = DA(md, actuator_moment) + u * nv;
+    double m = lane < nv ? mom[lane] : 0.0, len;
+    if (trntype[u] == MGS_TRN_JOINT) {
+      len = d.qpos[jq[trnid[u]]] * gear[u];
+    } else {
+      int t = trnid[u];
+      double tl = 0.0;
+      for (int w = tadr[t]; w < tadr[t] + tnum[t]; w++) tl = tl + wcoef[w] * d.qpos[wq[w]];
+      len = tl * gear[u];
+    }
+    (void)jd;
+    (void)wdof;
+#else
     double* mom = d.act_moment + u * nv;
     double m = 0.0, len;
     if (trntype[u] == MGS_TRN_JOINT) {
@@ -867,6 +921,7 @@ DEVI void actuation(const Mdl& md, Dat& d) {
     }
     if (lane < nv) mom[lane] = m;
     wsync();
+#endif
     double vel = 0.0;
     for (int k = 0; k < nv; k++) vel = vel + mom[k] * d.qvel[k];
     double c = d.ctrl[u];
@@ -3101,7 +3156,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     for (int i = 0; i < NV; i++) {
       double s = g[i];
 #pragma unroll
-      for (int k = 0; k < i; k++) s = __builtin_fma(-d.M[i * NV + k], g[k], s);
+      for (int k = 0; k < i; k++) s = __builtin_fma(-d.M[TRI(i, k, NV)], g[k], s);
       g[i] = s;
     }
 #pragma unroll
@@ -3541,7 +3596,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   if (lane == 0) {
     for (int i = 0; i < nv; i++) {
       double s = d.qacc_ws[i];
-      for (int k = i + 1; k < nv; k++) s = s + d.M[k * nv + i] * d.qacc_ws[k];
+      for (int k = i + 1; k < nv; k++) s = s + d.M[TRI(k, i, nv)] * d.qacc_ws[k];
       d.tmp[i] = s * d.sD[i];
     }
   }
@@ -3871,8 +3926,8 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u_main, double u) {
 #define FS_LR(k) Lr[k]
 #define FS_LC(k) Lc[k]
 #else
-#define FS_LR(k) d.M[li * NV + (k)]
-#define FS_LC(k) d.M[(k) * NV + li]
+#define FS_LR(k) d.M[TRI(li, (k), NV)]
+#define FS_LC(k) d.M[TRI((k), li, NV)]
 #endif
   double z = u_main * d.isD[li];
 #pragma unroll
@@ -4336,7 +4391,7 @@ DEVI void hessian_mfma(const Mdl& md, Dat& d, int ne) {
 #pragma unroll
       for (int g = 0; g < 4; g++) {
         int j = rg + 4 * g + 16 * tj;
-        if (i < NV && j <= i) d.nH[i * NV + j] = (i == j ? 1.0 : 0.0) + acc[q][g];
+        if (i < NV && j <= i) d.nH[TRI(i, j, NV)] = (i == j ? 1.0 : 0.0) + acc[q][g];
       }
       q++;
     }
@@ -4503,7 +4558,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     double s = d.qacc_smooth[li], s2 = d.qacc_ws[li];
 #pragma unroll
     for (int k = 1; k < NV; k++) {
-      double l = d.M[k * NV + li];
+      double l = d.M[TRI(k, li, NV)];
       if (k > lane) {
         s = __builtin_fma(l, d.qacc_smooth[k], s);
         s2 = __builtin_fma(l, d.qacc_ws[k], s2);
@@ -4664,7 +4719,7 @@ DEVI double* m_copy_slot(const Mdl& md, const Dat& d) {
   return nullptr;
 #else
   const int nv = md.m.nv;
-  const int tail0 = md.m.nefc_max * GS - nv * NV;
+  const int tail0 = md.m.nefc_max * GS - TRI_SIZE(NV);
   const int dyn_end = 6 * (3 * md.m.nbody + nv) + 3 * nv;
   return tail0 >= dyn_end ? d.G + tail0 : nullptr;
 #endif
@@ -4673,7 +4728,7 @@ template <int NV>
 DEVI void save_M(const Mdl& md, Dat& d) {
   double* mc = m_copy_slot<NV>(md, d);
   if (!mc) return;
-  for (int k = lane_id(); k < md.m.nv * NV; k += WAVE) mc[k] = d.M[k];
+  for (int k = lane_id(); k < TRI_SIZE(NV); k += WAVE) mc[k] = d.M[k];
   wsync();
 }
 
@@ -4724,7 +4779,7 @@ DEVI void integrate(const Mdl& md, Dat& d) {
   {
     const double* mc = m_copy_slot<NV>(md, d);
     if (mc && uni(d.NEFC) * GS <= (int)(mc - d.G)) {
-      for (int k = lane; k < nv * NV; k += WAVE) d.M[k] = mc[k];
+      for (int k = lane; k < TRI_SIZE(NV); k += WAVE) d.M[k] = mc[k];
       wsync();
     } else {
       crb(md, d);
@@ -4750,14 +4805,19 @@ DEVI void integrate(const Mdl& md, Dat& d) {
       if (btype[u] == MGS_BIAS_AFFINE) dv = dv + bias[3 * u + 2];
       if (gtype[u] == MGS_GAIN_AFFINE) dv = dv + gain[3 * u + 2] * d.ctrl[u];
       if (dv == 0.0) continue;
+#if MGS_PACKED
+      const double* mom = DA(md, actuator_moment) + u * nv;
+#else
       const double* mom = d.act_moment + u * nv;
+#endif
       double mi = mom[lane];
       if (mi == 0.0) continue;
 #pragma unroll
       for (int j = 0; j < NV; j++) q[j] = q[j] + mi * (mom[j] * dv);
     }
 #pragma unroll
-    for (int j = 0; j < NV; j++) d.M[lane * NV + j] = d.M[lane * NV + j] - dt * q[j];
+    for (int j = 0; j < NV; j++)
+      if (!MGS_PACKED || j <= lane) d.M[TRI(lane, j, NV)] = d.M[TRI(lane, j, NV)] - dt * q[j];
   }
   wsync();
   PT(20);

@@ -1194,6 +1194,22 @@ class CompiledModel:
             jid = -1
         return int(self.jnt_qposadr[jid])
 
+    def actuator_moment(self):
+        """(nu, nv) actuator moment rows, constant for joint and fixed-tendon
+        transmissions: the kernels' / oracle's actuation() sums (joint: gear at
+        the joint's dof; tendon: 0 + wrap coef x gear over the wraps in order)"""
+        mom = np.zeros((self.nu, self.nv))
+        for u in range(self.nu):
+            g = float(self.actuator_gear[u])
+            t = int(self.actuator_trnid[u])
+            if int(self.actuator_trntype[u]) == 0:
+                mom[u, int(self.jnt_dofadr[t])] = g
+            else:
+                for w in range(int(self.tendon_adr[t]), int(self.tendon_adr[t]) + int(self.tendon_num[t])):
+                    k = int(self.wrap_dofid[w])
+                    mom[u, k] = float(mom[u, k]) + float(self.wrap_coef[w]) * g
+        return mom
+
     def body_dofmask(self):
         """(nbody, 2) int32 bit masks of the dofs on each body's chain to the root."""
         m = np.zeros((self.nbody, 2), np.uint32)
@@ -1288,6 +1304,7 @@ class CompiledModel:
         for n in ["actuator_gainprm", "actuator_biasprm", "actuator_ctrlrange", "actuator_forcerange",
                   "actuator_gear"]:
             put_d(n, getattr(self, n))
+        put_d("actuator_moment", self.actuator_moment())
         put_i("actuator_actadr", self.actuator_actadr)
         put_d("actuator_pidprm", self.actuator_pidprm)
         # initial actuator state shared by every candidate (mj_resetData: zeros;

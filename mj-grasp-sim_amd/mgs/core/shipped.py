@@ -101,7 +101,8 @@ def shipped_engines() -> List[Tuple[object, int, object, str]]:
         env.set_state(np.load(C5_SCENE)["state"])
     scenes = [env] + [spread_pile(g, objs) for g, objs in SPREAD_PILES]
     for env in scenes:
-        out.append((env.model_for(env.get_state()), env.ncon_max, env._nefc_max, "main"))
+        cm = env.model_for(env.get_state())
+        out.append((cm, env.ncon_max, env.rows_for(cm, env.ncon_max), "main"))
     from mgs.core.mjcf import compile_xml
     out.append((compile_xml(GRAVCOMP_XML.format(gc=0.5)), 4, None, "main"))
     return out

@@ -99,7 +99,7 @@ def _frozen_object_xml(xml_bytes: bytes, qpos7) -> bytes:
 
 class ClutterTableEnv:
     def __init__(self, gripper, objects: list, scene_randomization=True, device: int = 0,
-                 ncon_max: int = 96, nefc_max: Optional[int] = None):
+                 ncon_max: int = 64, nefc_max: Optional[int] = None):
         self.gripper = gripper
         self.objects = list(objects)
         self.object_names = [o.name for o in self.objects]
@@ -243,10 +243,26 @@ class ClutterTableEnv:
         if key not in self._engines:
             self._engines = {k: v for k, v in self._engines.items() if k[1:] == key[1:]}
             # escalation capacities re-run few candidates: specialised only if cached
-            self._engines[key] = Engine(cm, device=self.device, ncon_max=nc, nefc_max=self._nefc_max,
+            self._engines[key] = Engine(cm, device=self.device, ncon_max=nc, nefc_max=self.rows_for(cm, nc),
                                         specialize=None if nc == self.ncon_max else "cached",
                                         role="main" if nc == self.ncon_max else "escalation")
         return self._engines[key]
+
+    def rows_for(self, cm, nc):
+        """constraint rows of the engine at nc contacts: the env's nefc_max if
+        one was given; at the main capacity the rows that keep the most pile
+        candidates per CU (auto_capacity: two per CU at 64 contacts and about
+        190 rows, DESIGN §3b), whose overflow the escalation continues wider;
+        an escalation capacity's engine the library's worst case (None)"""
+        from mgs.core.engine import auto_capacity
+        if self._nefc_max is not None:
+            return self._nefc_max
+        if nc != self.ncon_max:
+            return None
+        key = (nc, cm.nv, len(cm.pair_condim), len(cm.eq_type))
+        if getattr(self, "_rows_key", None) != key:
+            self._rows_key, self._rows = key, auto_capacity(cm, nc)[1]
+        return self._rows
 
     # -- reference helpers ---------------------------------------------------
     def get_joint_idxs(self, joint_list: List[str]) -> List[int]:

@@ -49,6 +49,14 @@ def oracle_model(env):
     return O.OracleModel(env.model, ncon_max=env.ncon_max, nefc_max=env.nefc_max)
 
 
+def full_capacity_oracle(env, state):
+    """the oracle at a clutter env's last escalation capacity (128 contacts,
+    256 rows: sliced_rollout's max_ncon and the wide library's rows), which a
+    run escalated from the env's main capacity equals bit for bit"""
+    from oracle import oracle as O
+    return O.OracleModel(env.model_for(state), ncon_max=128, nefc_max=256)
+
+
 def plan_for(env, poses, joints, horizon="h200"):
     from mgs.env.gravityless_object_grasping import HORIZONS
     h = HORIZONS[horizon]

@@ -118,7 +118,9 @@ def test_clutter_gpu_parity(cenv, ccand):
     for k in ("label", "fail_step", "stats"):
         assert np.array_equal(rg[k], ro[k]), k
     lab = cenv.grasp_stable_mask(poses[idx], J[idx], st, nstep_lift=600, close_steps=600, enough_stable=3)
-    assert lab.sum() == min(3, int(ro["label"].sum()))
+    from conftest import full_capacity_oracle
+    rf = full_capacity_oracle(cenv, st).rollout(plan, nthreads=8)     # the env escalates past its capacity
+    assert lab.sum() == min(3, int(rf["label"].sum()))
 
 
 def test_scene_file_roundtrip(cenv, tmp_path):

@@ -94,26 +94,27 @@ def test_shadow_pile_gpu_parity(senv, scand):
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(rg[k], ro[k]), k
     lab = senv.grasp_stable_mask(poses[idx], J[idx], st, nstep_lift=200, close_steps=200, enough_stable=2)
-    assert lab.sum() == min(2, int(ro["label"].sum()))
+    from conftest import full_capacity_oracle
+    rf = full_capacity_oracle(senv, st).rollout(plan, nthreads=8)     # the env escalates past its capacity
+    assert lab.sum() == min(2, int(rf["label"].sum()))
 
 
 @pytest.mark.gpu
 def test_shadow_pile_reference_schedule_parity(senv, scand):
     """C5 at the reference's own schedule: close 3000 + lift 3000 steps
-    (clutter_table.py:277,307) on two pile candidates, bit-exact against the
-    oracle"""
+    (clutter_table.py:277,307) on two pile candidates through the env's own
+    rollout (main capacity, escalation past it), bit-exact against the oracle
+    at the escalation's full capacity"""
     _init_torch()
-    from oracle import oracle as O
+    from conftest import full_capacity_oracle
     poses, J = scand
     st = senv.get_state()
-    eng = senv.engine_for_state(st)
-    om = O.OracleModel(senv.model_for(st), ncon_max=senv.ncon_max, nefc_max=eng.desc.nefc_max)
     idx = np.nonzero(senv.grasp_collision_mask(poses, J))[0][:2]
     plan = senv.stable_plan(poses[idx], J[idx], st)
     assert plan.nsteps == [3000, 3000]
-    rg, ro = eng.rollout(plan), om.rollout(plan, nthreads=2)
-    assert (rg["stats"][:, 2] == 0).all()
-    for k in ("label", "fail_step", "obj_qpos", "stats"):
+    rg, ro = senv.rollout(plan, st), full_capacity_oracle(senv, st).rollout(plan, nthreads=2)
+    assert rg["overflow"] == 0 and (ro["stats"][:, 2] == 0).all()
+    for k in ("label", "fail_step", "obj_qpos"):
         assert np.array_equal(rg[k], ro[k]), k
 
 
@@ -133,9 +134,8 @@ def test_shadow_pile_capacity_escalation(senv, scand):
     assert (first["stats"][:, 2] != 0).any()
     res = small.rollout(plan, st)
     assert res["overflow"] == 0
-    big = senv.engine_for_state(st)
-    om = O.OracleModel(senv.model_for(st), ncon_max=senv.ncon_max, nefc_max=big.desc.nefc_max)
-    ro = om.rollout(plan, nthreads=8)
+    from conftest import full_capacity_oracle
+    ro = full_capacity_oracle(senv, st).rollout(plan, nthreads=8)
     for k in ("label", "fail_step", "obj_qpos"):
         assert np.array_equal(res[k], ro[k]), k
 

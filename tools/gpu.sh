@@ -22,6 +22,7 @@
 #   heavy     stage timers over the 64 heaviest rollouts of the headline batch
 #   configs   tools/bench_configs.py (C3, C4, C5)
 #   c5big     C5 at 3000 + 3000 steps on 10 240 candidates, rotation on / off
+#   c5cpu     the same (rotation on) with a same-run 16-thread CPU baseline
 #   c5ab:a,b  C5 (600 + 600) on the listed mgs/_lib/ab objects (MGS_SPECIAL_OBJECT)
 #   py:<file> python3 <file> (a probe script under tools/)
 # Outputs: gpurun_out/<tag>/
@@ -158,6 +159,12 @@ for step in "$@"; do
           > $O/c5big_y$y.jsonl 2> $O/c5big_y$y.err || fail c5big $O/c5big_y$y.err
         cut -c1-400 $O/c5big_y$y.jsonl
       done ;;
+    c5cpu)
+      # C5 at the reference's schedule on 10 240 candidates with a same-run CPU
+      # baseline (the C oracle, 16 threads, 400 evenly spaced candidates)
+      timeout -k 10 900 python3 tools/bench_configs.py c5 --c5-per-object 2048 --c5-steps 3000 --c5-cpu-sample 400 \
+        > $O/c5cpu.jsonl 2> $O/c5cpu.err || fail c5cpu $O/c5cpu.err
+      cut -c1-600 $O/c5cpu.jsonl ;;
     c5ab:*)
       # C5 (600 + 600, 1280 candidates: one round of 48 rollouts, i.e. their latency) on
       # each listed object of mgs/_lib/ab (MGS_SPECIAL_OBJECT), interleaved twice

@@ -39,7 +39,7 @@ if "--compile-only" in sys.argv:
     from mgs.core import abi
     from mgs.core.engine import default_rows, library_for
     cm = env.model_for(st)
-    ne = env._nefc_max or default_rows(cm, int(cm.pack(ncon_max=env.ncon_max)[0]["nefc_max"]))
+    ne = env.rows_for(cm, env.ncon_max) or default_rows(cm, int(cm.pack(ncon_max=env.ncon_max)[0]["nefc_max"]))
     fields, _, _ = cm.pack(ncon_max=env.ncon_max, nefc_max=ne)
     print(special.code_object(library_for(cm.nv, int(fields["nefc_max"])), abi.make_desc(fields), profile=True))
     sys.exit(0)
