@@ -379,7 +379,7 @@ def main():
     class Pipe:
         def __init__(self, s):
             self.eng = env.engine if s == 0 else Engine(env.model, device=local, ncon_max=env.ncon_max,
-                                                          nefc_max=env.nefc_max)
+                                                          nefc_max=env.nefc_max, g_rows_hbm="auto")
             self.stream = torch.cuda.current_stream(dev) if s == 0 else torch.cuda.Stream(dev)
             self.free = torch.zeros(N, dtype=torch.uint8, device=dev)
             self.label = torch.zeros(N, dtype=torch.uint8, device=dev)

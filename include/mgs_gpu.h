@@ -128,6 +128,10 @@ typedef struct mgs_model_desc {
   int32_t nact;       /* actuator state (mjData.act) entries: 2 per mujoco.pid actuator (ABI 21) */
   int32_t maxcondim;  /* largest contact dimension of the admissible pairs: 1, 3, 4 or 6 (condim 6:
                          torsional and rolling friction; runs through a specialised code object) */
+  int32_t g_rows_hbm; /* 1: the whitened constraint rows G of each candidate live in a batch-owned
+                         HBM buffer instead of LDS (always so in the wide library; in the main
+                         library an option of the specialised code objects, which are then built
+                         with -DMGS_G_GLOBAL; the library kernels refuse it) */
   int32_t ncon_max;   /* contact capacity per candidate (set by host) */
   int32_t nefc_max;   /* constraint-row capacity per candidate (set by host) */
   int32_t maxhullvert;

@@ -38,6 +38,22 @@ int fail(int code, const char* fmt, const char* what = "") {
     if (_e != hipSuccess) return fail(MGS_EHIP, "HIP error: %s", hipGetErrorString(_e)); \
   } while (0)
 
+// whether a model's G rows live in HBM
+#ifdef MGS_G_GLOBAL
+bool g_in_hbm(const mgs_model_desc&) { return true; }
+#else
+bool g_in_hbm(const mgs_model_desc& m) { return m.g_rows_hbm != 0; }
+#endif
+
+// main-library objects with G in HBM also pack M / the Newton Hessian and read
+// the contacts' friction from the model (-DMGS_PACKED=1 -DMGS_MU_MODEL=1,
+// mgs/core/special.py), so that six headline candidates fit a CU
+int m_square_size(const mgs_model_desc& m) {
+  const int nv = m.nv;
+  return (MGS_PACKED || m.g_rows_hbm) ? nv * (nv + 1) / 2 : nv * nv;
+}
+bool mu_from_model(const mgs_model_desc& m) { return !MGS_PACKED && m.g_rows_hbm; }
+
 // the contact dimension the kernels for this model are built for (MGS_MAXDIM)
 int layout_maxdim(const mgs_model_desc& m) { return m.maxcondim > 4 ? 6 : 4; }
 
@@ -56,12 +72,12 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   sizes[L_act] = m.nact; sizes[L_act_dot] = m.nact;
   sizes[L_xpos] = 3 * nb; sizes[L_xquat] = 4 * nb; sizes[L_xmat] = 9 * nb; sizes[L_subtree_com] = 3 * nb;
   sizes[L_cinert] = 10 * nb; sizes[L_cdof] = 6 * nv;
-  sizes[L_M] = TRI_SIZE(nv); sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_sD] = nv; sizes[L_isD] = nv;
+  sizes[L_M] = m_square_size(m); sizes[L_Dv] = nv; sizes[L_Dinv] = nv; sizes[L_sD] = nv; sizes[L_isD] = nv;
   sizes[L_tmp] = nv; sizes[L_tmp2] = nv;
   sizes[L_qfrc_smooth] = nv; sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv;
   // (the wide build reads the actuator moment rows from the model)
   sizes[L_act_force] = nu; sizes[L_act_moment] = MGS_PACKED ? 0 : nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
-  sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = 5 * nc;
+  sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = mu_from_model(m) ? 0 : 5 * nc;
   // contact blocks (and Newton cone Hessians): maxdim^2 per contact, maxdim 6
   // for models with condim-6 pairs (their code objects: -DMGS_MAXDIM=6)
   const int maxdim = layout_maxdim(m);
@@ -75,11 +91,9 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   us[U_comacc] = 4 * nb;
   us[U_cvel] = 6 * nb; us[U_cacc] = 6 * nb; us[U_cfrc] = 6 * nb; us[U_cdof_dot] = 6 * nv;
   us[U_qfrc_bias] = nv; us[U_qfrc_passive] = nv; us[U_qfrc_actuator] = nv;
-#ifdef MGS_G_GLOBAL
-  us[U_G] = 0;               // G in HBM (batch buffer), see bind()
-#else
-  us[U_G] = ne * (nv + MGS_GPAD);   // row stride: GS in the kernel
-#endif
+  // G in HBM (batch buffer, see bind()): the wide library always, the main
+  // library's specialised objects on request (mgs_model_desc.g_rows_hbm)
+  us[U_G] = g_in_hbm(m) ? 0 : ne * (nv + MGS_GPAD);   // row stride: GS in the kernel
   us[U_aref] = ne;
   us[U_scratch] = (2 * ne > nv ? 2 * ne : nv);
   // {vel, pos, margin} (make_constraints) | Newton Hessian, which may run on into
@@ -87,7 +101,7 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   // (the Hessian's weight table, (maxdim + 1) ne, runs on into scratch too)
   int xreg = 3 * ne;
   if (xreg + us[U_scratch] < (maxdim + 1) * ne) xreg = (maxdim + 1) * ne - us[U_scratch];
-  if (xreg + us[U_scratch] < TRI_SIZE(nv)) xreg = TRI_SIZE(nv) - us[U_scratch];
+  if (xreg + us[U_scratch] < m_square_size(m)) xreg = m_square_size(m) - us[U_scratch];
   us[U_jar] = ne; us[U_jv] = ne; us[U_f] = ne; us[U_Dr] = ne; us[U_isR] = ne;
   us[U_nw] = nv; us[U_nw0] = nv; us[U_ng] = nv; us[U_ndir] = nv;
   int U = 0, off;
@@ -336,17 +350,18 @@ void mgs_batch_close(mgs_batch* b) {
 static int launch_layout(mgs_batch* b, int n, Lay* lay) {
   *lay = b->m->lay;
   lay->gmem = nullptr;
-#ifdef MGS_G_GLOBAL
-  size_t need = (size_t)n * (size_t)b->m->desc.nefc_max * (size_t)b->m->desc.nv;
-  if (need > b->g_elems) {
-    if (b->d_G) HIPCHK(hipFree(b->d_G));
-    b->d_G = nullptr;
-    b->g_elems = 0;
-    if (hipMalloc(&b->d_G, need * sizeof(double)) != hipSuccess) return fail(MGS_ENOMEM, "G buffer allocation failed%s");
-    b->g_elems = need;
+  if (g_in_hbm(b->m->desc)) {
+    size_t need = (size_t)n * (size_t)b->m->desc.nefc_max * (size_t)b->m->desc.nv;
+    if (need > b->g_elems) {
+      if (b->d_G) HIPCHK(hipFree(b->d_G));
+      b->d_G = nullptr;
+      b->g_elems = 0;
+      if (hipMalloc(&b->d_G, need * sizeof(double)) != hipSuccess)
+        return fail(MGS_ENOMEM, "G buffer allocation failed%s");
+      b->g_elems = need;
+    }
+    lay->gmem = b->d_G;
   }
-  lay->gmem = b->d_G;
-#endif
   return MGS_OK;
 }
 
@@ -553,6 +568,10 @@ static int launch_rollout(mgs_batch* b, const mgs_schedule* sched, int n, const 
     if (layout_maxdim(md.m) > MGS_MAXDIM)
       return fail(MGS_EINVAL, "condim-6 contacts run through the model's specialised code object only "
                               "(mgs.core.special); none is attached%s");
+#ifndef MGS_G_GLOBAL
+    if (md.m.g_rows_hbm)
+      return fail(MGS_EINVAL, "g_rows_hbm: G rows in HBM need the model's specialised code object%s");
+#endif
     k->rollout(dim3(nwg), b->m->lds_bytes, st, a);
   }
   HIPCHK(hipGetLastError());

@@ -141,7 +141,14 @@ static_assert(MGS_MAXDIM == 4 || MGS_MAXDIM == 6, "MGS_MAXDIM is 4 or 6");
 #define TRI(i, k, n) ((i) * (n) + (k))
 #define TRI_SIZE(n) ((n) * (n))
 #endif
-static_assert(!(MGS_PACKED && MGS_REG_ROWS), "packed M / H needs the LDS row factor (MGS_REG_ROWS 0)");
+// (the register-row factor and solves load row i's lower entries by TRI too;
+// the upper ones they load are never used, and TRI keeps them in bounds)
+// the friction coefficients of a contact: its pair's row of the model instead
+// of a per-contact copy in LDS (main-library objects with G in HBM, round 5:
+// the same values -- the copy's one extra slot, mu[dim - 1] = 0, is never read)
+#ifndef MGS_MU_MODEL
+#define MGS_MU_MODEL 0
+#endif
 
 // the lane index through an opaque move at every use: index arithmetic and
 // lane masks derived from it are recomputed where they are used instead of
@@ -785,7 +792,7 @@ DEVI void store_lower(double* A, const double (&r)[NV]) {
   if (lane < NV) {
 #pragma unroll
     for (int k = 0; k < NV; k++)
-      if (k < lane) A[lane * NV + k] = r[k];
+      if (k < lane) A[TRI(lane, k, NV)] = r[k];
   }
   wsync();
 }
@@ -796,7 +803,7 @@ DEVI void ldl_factor(double* A, double* Dv, double* Dinv) {
   int li = lane < NV ? lane : 0;
   double r[NV];
 #pragma unroll
-  for (int k = 0; k < NV; k++) r[k] = A[li * NV + k];
+  for (int k = 0; k < NV; k++) r[k] = A[TRI(li, k, NV)];
   ldl_factor_regs<NV>(r, Dv, Dinv);
   store_lower<NV>(A, r);
 #else
@@ -815,7 +822,7 @@ DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double
 #if MGS_REG_ROWS
   double Lr[NV], Lc[NV];
 #pragma unroll
-  for (int k = 0; k < NV; k++) { Lr[k] = L[li * NV + k]; Lc[k] = L[k * NV + li]; }
+  for (int k = 0; k < NV; k++) { Lr[k] = L[TRI(li, k, NV)]; Lc[k] = L[TRI(k, li, NV)]; }
 #define LS_LR(k) Lr[k]
 #define LS_LC(k) Lc[k]
 #else
@@ -2595,6 +2602,16 @@ DEVI int efc_lead(const Dat& d, int r) {
          d.efc_con[r - 1] != d.efc_con[r];
 }
 
+// contact c's friction coefficients (see MGS_MU_MODEL)
+DEVI const double* con_mu_of(const Mdl& md, const Dat& d, int c) {
+#if MGS_MU_MODEL
+  return DA(md, pair_friction) + 5 * d.con_pair[c];
+#else
+  (void)md;
+  return d.con_mu + 5 * c;
+#endif
+}
+
 // frictionloss of a FRICTION row (its efc_con is the dof), 0 otherwise
 DEVI double row_floss(const Mdl& md, const Dat& d, int r) {
   return d.efc_type[r] == MGS_EFC_FRICTION ? DA(md, dof_frictionloss)[d.efc_con[r]] : 0.0;
@@ -3052,7 +3069,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
       if (lane == 0) {
         for (int j = 0; j < dim; j++) add_row(md, d, MGS_EFC_CONTACT, j == 0 ? d.con_dist[c] : 0.0, pmar[p], dim, c);
         for (int j = 0; j < dim; j++)
-          if (MGS_MAXDIM < 6 || j < 5) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
+          if (!MGS_MU_MODEL && (MGS_MAXDIM < 6 || j < 5)) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
       }
       wsync();
       int col = lane < nv ? lane : 0;
@@ -3096,7 +3113,8 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         d.efc_margin[r] = pmar[cp]; d.efc_dim[r] = cdim; d.efc_con[r] = lane;
         // (5 friction coefficients per contact: a condim-6 block's sixth row has
         // no slot -- writing one would clobber the next contact's first)
-        if (MGS_MAXDIM < 6 || j < 5) d.con_mu[5 * lane + j] = (j < cdim - 1) ? pfr[5 * cp + j] : 0.0;
+        if (!MGS_MU_MODEL && (MGS_MAXDIM < 6 || j < 5))
+          d.con_mu[5 * lane + j] = (j < cdim - 1) ? pfr[5 * cp + j] : 0.0;
       }
     }
     int last = nkeep > 0 ? nkeep - 1 : 0;
@@ -3180,7 +3198,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     } else if (efc_lead(d, r)) {
       int p = d.con_pair[id];
       row_params(md, d, r, d.efc_dim[r], DA(md, pair_solref) + 2 * p, DA(md, pair_solimp) + 5 * p,
-                 d.con_mu + 5 * id, 1, d.efc_pos[r]);
+                 con_mu_of(md, d, id), 1, d.efc_pos[r]);
     }
   }
   wsync();
@@ -3437,12 +3455,12 @@ DEVI double cost_change(const double* A, const double* delta, const double* res)
 
 // one PGS update of the contact block starting at row r with DIM rows
 template <int DIM>
-DEVI double pgs_contact(const Dat& d, int r, int nv, int P, int lane, double& u, Frc& F, int noslip,
+DEVI double pgs_contact(const Mdl& md, const Dat& d, int r, int nv, int P, int lane, double& u, Frc& F, int noslip,
                         const double* gpre = nullptr) {
   double g[DIM], res[DIM], old[DIM], nw[DIM];
   const int c = uni(d.efc_con[r]);
   const double* blk = d.con_blk + BLKSTRIDE * c;
-  const double* mu = d.con_mu + 5 * c;
+  const double* mu = con_mu_of(md, d, c);
 #pragma unroll
   for (int i = 0; i < DIM; i++) {
     // gpre: the block's G rows loaded ahead by the caller (lanes over dofs)
@@ -3578,7 +3596,7 @@ DEVI void project_block_lds(const Mdl& md, const Dat& d, int r, double* f) {
     int dim = d.efc_dim[r];
     if (f[0] < 0.0) { for (int j = 0; j < dim; j++) f[j] = 0.0; return; }
     if (dim == 1) return;
-    const double* mu = d.con_mu + 5 * d.efc_con[r];
+    const double* mu = con_mu_of(md, d, d.efc_con[r]);
     double s = 0.0;
     for (int j = 1; j < dim; j++) { double q = f[j] / mu[j - 1]; s = s + q * q; }
     double nt = sqrt(s);
@@ -3668,15 +3686,15 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
         }
         r += 1;
       } else if (dim == 3) {
-        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 0);
+        improvement = improvement - pgs_contact<3>(md, d, r, nv, P, lane, u, F, 0);
         r += 3;
 #if MGS_MAXDIM > 4
       } else if (dim == 6) {
-        improvement = improvement - pgs_contact<6>(d, r, nv, P, lane, u, F, 0);
+        improvement = improvement - pgs_contact<6>(md, d, r, nv, P, lane, u, F, 0);
         r += 6;
 #endif
       } else {
-        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 0);
+        improvement = improvement - pgs_contact<4>(md, d, r, nv, P, lane, u, F, 0);
         r += 4;
       }
     }
@@ -3807,13 +3825,13 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
           setf(F, r, fnew[0], lane);
         }
       } else if (dim == 3) {
-        improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1, gc);
+        improvement = improvement - pgs_contact<3>(md, d, r, nv, P, lane, u, F, 1, gc);
 #if MGS_MAXDIM > 4
       } else if (dim == 6) {
-        improvement = improvement - pgs_contact<6>(d, r, nv, P, lane, u, F, 1, gc);
+        improvement = improvement - pgs_contact<6>(md, d, r, nv, P, lane, u, F, 1, gc);
 #endif
       } else {
-        improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1, gc);
+        improvement = improvement - pgs_contact<4>(md, d, r, nv, P, lane, u, F, 1, gc);
       }
       r = rn;
       t = tn;
@@ -3888,13 +3906,13 @@ DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u)
             setf(F, r, fnew[0], lane);
           }
         } else if (dim == 3) {
-          improvement = improvement - pgs_contact<3>(d, r, nv, P, lane, u, F, 1);
+          improvement = improvement - pgs_contact<3>(md, d, r, nv, P, lane, u, F, 1);
 #if MGS_MAXDIM > 4
         } else if (dim == 6) {
-          improvement = improvement - pgs_contact<6>(d, r, nv, P, lane, u, F, 1);
+          improvement = improvement - pgs_contact<6>(md, d, r, nv, P, lane, u, F, 1);
 #endif
         } else {
-          improvement = improvement - pgs_contact<4>(d, r, nv, P, lane, u, F, 1);
+          improvement = improvement - pgs_contact<4>(md, d, r, nv, P, lane, u, F, 1);
         }
       }
     }
@@ -3922,7 +3940,7 @@ DEVI void finalize_solution(const Mdl& md, Dat& d, double u_main, double u) {
 #if MGS_REG_ROWS
   double Lr[NV], Lc[NV];
 #pragma unroll
-  for (int k = 0; k < NV; k++) { Lr[k] = d.M[li * NV + k]; Lc[k] = d.M[k * NV + li]; }
+  for (int k = 0; k < NV; k++) { Lr[k] = d.M[TRI(li, k, NV)]; Lc[k] = d.M[TRI(k, li, NV)]; }
 #define FS_LR(k) Lr[k]
 #define FS_LC(k) Lc[k]
 #else
@@ -4547,7 +4565,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     k1R[h] = 0.0;
     int r = lane + h * WAVE;
     if (r < ne && d.efc_type[r] == MGS_EFC_CONTACT && d.efc_dim[r] > 1) {
-      double mup = d.con_mu[5 * d.efc_con[r]] / sqrt(md.m.impratio);
+      double mup = con_mu_of(md, d, d.efc_con[r])[0] / sqrt(md.m.impratio);
       mupR[h] = mup;
       k1R[h] = 1.0 / (1.0 + mup * mup);
     }

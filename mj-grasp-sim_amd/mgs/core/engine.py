@@ -204,18 +204,39 @@ def check_no_lost_candidates(fail_step, expired_spins=0):
 class Engine:
     """One compiled model resident on one GPU plus a reusable batch."""
 
-    def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None, specialize=None, role="main"):
+    def __init__(self, cm, device: int = 0, ncon_max: int = 16, nefc_max=None, specialize=None, role="main",
+                 g_rows_hbm=None):
         """specialize: True = attach the model-specialised code object, compiling
         it if it is not cached; "cached" = attach it only if cached; False = the
         library's runtime-layout kernels.  Default (None): MGS_SPECIALIZE from the
         environment ("1" / "cached" / "0"), else "cached".  A dof count the
         library has no kernel for always specialises (compiling if needed).
         role: the object's role (mgs.core.special.ROLE_FLAGS): "escalation" for
-        the capacity escalation's engines (kernel symbols *_esc in traces)."""
+        the capacity escalation's engines (kernel symbols *_esc in traces).
+        g_rows_hbm: keep the constraint rows G in HBM instead of LDS (a main-
+        flavour model then runs a specialised object with at most 256
+        registers, packed M and the friction read from the model: six headline
+        candidates per CU instead of four, +26 % on the driver's command, round
+        5).  True / False; "auto" (the envs' primary engines): when that object
+        is cached; None: MGS_G_HBM from the environment ("1" / "0"), else
+        False.  MGS_G_HBM also overrides "auto"."""
         if nefc_max is None:
             nefc_max = default_rows(cm, int(cm.pack(ncon_max=ncon_max)[0]["nefc_max"]))
         fields, self._ib, self._db = cm.pack(ncon_max=ncon_max, nefc_max=nefc_max)
         self.lib = library_for(cm.nv, int(fields["nefc_max"]))
+        env_g = os.environ.get("MGS_G_HBM")
+        if g_rows_hbm is None or (g_rows_hbm == "auto" and env_g is not None):
+            g_rows_hbm = env_g == "1"
+        if g_rows_hbm and self.lib.mgs_rows_per_lane() != 4:
+            # main flavour with the G rows in HBM: a specialised object only;
+            # "auto" takes it when its object is cached (the shipped engines'
+            # are prebuilt), else keeps G in LDS
+            g_fields = dict(fields, g_rows_hbm=1)
+            from mgs.core import special
+            if g_rows_hbm is True or special.code_object(self.lib, abi.make_desc(g_fields), compile=False,
+                                                         role=role) is not None:
+                fields = g_fields
+                specialize = True
         if self.lib.mgs_device_count() <= device:
             raise EngineError("no HIP device visible for the MI355X engine")
         self.desc = abi.make_desc(fields)

@@ -245,7 +245,8 @@ class ClutterTableEnv:
             # escalation capacities re-run few candidates: specialised only if cached
             self._engines[key] = Engine(cm, device=self.device, ncon_max=nc, nefc_max=self.rows_for(cm, nc),
                                         specialize=None if nc == self.ncon_max else "cached",
-                                        role="main" if nc == self.ncon_max else "escalation")
+                                        role="main" if nc == self.ncon_max else "escalation",
+                                        g_rows_hbm="auto" if nc == self.ncon_max else None)
         return self._engines[key]
 
     def rows_for(self, cm, nc):

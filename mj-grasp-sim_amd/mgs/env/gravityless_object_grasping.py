@@ -144,7 +144,8 @@ class GravitylessObjectGrasping:
     def engine(self):
         if self._engine is None:
             from mgs.core.engine import Engine
-            self._engine = Engine(self.model, device=self.device, ncon_max=self.ncon_max, nefc_max=self.nefc_max)
+            self._engine = Engine(self.model, device=self.device, ncon_max=self.ncon_max, nefc_max=self.nefc_max,
+                                  g_rows_hbm="auto")
         return self._engine
 
     def engine_for(self, ncon_max: int):

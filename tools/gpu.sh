@@ -23,6 +23,7 @@
 #   configs   tools/bench_configs.py (C3, C4, C5)
 #   c5big     C5 at 3000 + 3000 steps on 10 240 candidates, rotation on / off
 #   c5cpu     the same (rotation on) with a same-run 16-thread CPU baseline
+#   ghbm      G rows in HBM (MGS_G_HBM=1) vs LDS (=0: library kernels), driver's command x 2
 #   c5ab:a,b  C5 (600 + 600) on the listed mgs/_lib/ab objects (MGS_SPECIAL_OBJECT)
 #   py:<file> python3 <file> (a probe script under tools/)
 # Outputs: gpurun_out/<tag>/
@@ -159,6 +160,14 @@ for step in "$@"; do
           > $O/c5big_y$y.jsonl 2> $O/c5big_y$y.err || fail c5big $O/c5big_y$y.err
         cut -c1-400 $O/c5big_y$y.jsonl
       done ;;
+    ghbm)
+      # G rows in HBM (mgs_model_desc.g_rows_hbm: five headline workgroups per CU,
+      # <= 256 registers) against G in LDS on the driver's command, interleaved
+      for r in 1 2; do for g in 0 1; do
+        MGS_G_HBM=$g timeout -k 10 300 python3 $DRIVER --cpu-budget 0 --e2e-steps 0 > $O/ghbm$g.$r.json \
+          2> $O/ghbm$g.$r.err || fail ghbm $O/ghbm$g.$r.err
+        summ $O/ghbm$g.$r.json
+      done; done ;;
     c5cpu)
       # C5 at the reference's schedule on 10 240 candidates with a same-run CPU
       # baseline (the C oracle, 16 threads, 400 evenly spaced candidates)
