@@ -53,6 +53,15 @@ int m_square_size(const mgs_model_desc& m) {
   return (MGS_PACKED || m.g_rows_hbm) ? nv * (nv + 1) / 2 : nv * nv;
 }
 bool mu_from_model(const mgs_model_desc& m) { return !MGS_PACKED && m.g_rows_hbm; }
+// ... and keep certificates, contact frames and contact blocks in the HBM
+// slice (-DMGS_HBM_EXTRA=1): seven headline candidates per CU
+bool hbm_extra(const mgs_model_desc& m) { return !MGS_PACKED && m.g_rows_hbm; }
+int layout_maxdim(const mgs_model_desc& m);
+size_t hbm_slice_doubles(const mgs_model_desc& m) {
+  const int md = layout_maxdim(m);
+  return (size_t)m.nefc_max * m.nv +
+         (hbm_extra(m) ? (size_t)(K_CERT * CERT_W + 9 * m.ncon_max + md * md * m.ncon_max) : 0);
+}
 
 // the contact dimension the kernels for this model are built for (MGS_MAXDIM)
 int layout_maxdim(const mgs_model_desc& m) { return m.maxcondim > 4 ? 6 : 4; }
@@ -77,16 +86,16 @@ Lay make_layout(const mgs_model_desc& m, size_t* bytes) {
   sizes[L_qfrc_smooth] = nv; sizes[L_qacc_smooth] = nv; sizes[L_qfrc_constraint] = nv;
   // (the wide build reads the actuator moment rows from the model)
   sizes[L_act_force] = nu; sizes[L_act_moment] = MGS_PACKED ? 0 : nu * nv; sizes[L_act_length] = nu; sizes[L_act_vel] = nu;
-  sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = mu_from_model(m) ? 0 : 5 * nc;
+  sizes[L_con_pos] = 3 * nc; sizes[L_con_frame] = hbm_extra(m) ? 0 : 9 * nc; sizes[L_con_dist] = nc; sizes[L_con_mu] = mu_from_model(m) ? 0 : 5 * nc;
   // contact blocks (and Newton cone Hessians): maxdim^2 per contact, maxdim 6
   // for models with condim-6 pairs (their code objects: -DMGS_MAXDIM=6)
   const int maxdim = layout_maxdim(m);
-  sizes[L_con_blk] = maxdim * maxdim * nc;
-  sizes[L_efc_R] = ne; sizes[L_efc_b] = ne; sizes[L_cert] = K_CERT * CERT_W;
+  sizes[L_con_blk] = hbm_extra(m) ? 0 : maxdim * maxdim * nc;
+  sizes[L_efc_R] = ne; sizes[L_efc_b] = ne; sizes[L_cert] = hbm_extra(m) ? 0 : K_CERT * CERT_W;
   // U: per-stage sub-layouts, each packed from offset 0 (see the kernel's Lay comment)
   int us[U_COUNT];
   for (int k = 0; k < U_COUNT; k++) us[k] = 0;
-  us[U_poly] = 6 * K_MAXPOLY * 3; us[U_pdep] = K_MAXPOLY; us[U_geom_xpos] = 3 * ng; us[U_geom_xmat] = 9 * ng;
+  us[U_poly] = K_POLY_POINTS * 3; us[U_pdep] = K_MAXPOLY; us[U_geom_xpos] = 3 * ng; us[U_geom_xmat] = 9 * ng;
   us[U_xipos] = 3 * nb; us[U_xanchor] = 3 * nj; us[U_xaxis] = 3 * nj; us[U_subtree_mass] = nb;
   us[U_comacc] = 4 * nb;
   us[U_cvel] = 6 * nb; us[U_cacc] = 6 * nb; us[U_cfrc] = 6 * nb; us[U_cdof_dot] = 6 * nv;
@@ -351,7 +360,7 @@ static int launch_layout(mgs_batch* b, int n, Lay* lay) {
   *lay = b->m->lay;
   lay->gmem = nullptr;
   if (g_in_hbm(b->m->desc)) {
-    size_t need = (size_t)n * (size_t)b->m->desc.nefc_max * (size_t)b->m->desc.nv;
+    size_t need = (size_t)n * hbm_slice_doubles(b->m->desc);
     if (need > b->g_elems) {
       if (b->d_G) HIPCHK(hipFree(b->d_G));
       b->d_G = nullptr;

@@ -28,6 +28,7 @@
 #define K_MINVAL 1e-15
 #define K_MAXF 16
 #define K_MAXPOLY 40
+#define K_POLY_POINTS (4 * K_MAXF + 3 * K_MAXPOLY)   // collide_manifold's polygon scratch
 #define K_MPR_MAXIT 64
 #define K_FEAT_EPS 1e-5
 #define K_BB_MERGE 1e-6     // box-box: merge distance of manifold points, x face half size (oracle BB_MERGE)
@@ -2012,12 +2013,16 @@ DEVI void collide_manifold(const Mdl& md, Dat& d, const PairCtx& pc, int pair, i
   int lane = lane_id();
   double t1[3], t2[3];
   make_frame(n, t1, t2);
-  P2* fa = d.poly;                 // K_MAXPOLY each
-  P2* fb = d.poly + K_MAXPOLY;
-  P2* buf = d.poly + 2 * K_MAXPOLY;
-  P2* refpoly = d.poly + 3 * K_MAXPOLY;
-  P2* inc = d.poly + 4 * K_MAXPOLY;
-  P2* pts = d.poly + 5 * K_MAXPOLY;
+  // the polygon scratch (K_POLY_POINTS points): each buffer sized for what
+  // reaches it -- features <= K_MAXF points, the reference hull <= 2 K_MAXF
+  // (the monotone chain's stack), the clipped polygon and its kept points
+  // <= K_MAXPOLY (the clip's cap)
+  P2* fa = d.poly;
+  P2* fb = fa + K_MAXF;
+  P2* refpoly = fb + K_MAXF;
+  P2* inc = refpoly + 2 * K_MAXF;
+  P2* buf = inc + K_MAXPOLY;
+  P2* pts = buf + K_MAXPOLY;
   double* dep = d.pdep;
   double s1, s2;
   // first pass: only the extremes are used (the oracle's first feature() pass
@@ -2510,6 +2515,15 @@ enum {
   U_G, U_aref, U_vel, U_pos, U_margin, U_nH, U_scratch, U_jar, U_jv, U_f, U_Dr, U_isR, U_nw, U_nw0, U_ng,
   U_ndir, U_qDeriv, U_COUNT
 };
+// doubles of one candidate's HBM slice (G rows, and with MGS_HBM_EXTRA the
+// certificates, contact frames and contact blocks); mgs_capi.hip's hbm_slice
+// allocates the same
+#ifndef MGS_HBM_EXTRA
+#define MGS_HBM_EXTRA 0
+#endif
+DEVI size_t hbm_slice(int ne, int nv, int nc) {
+  return (size_t)ne * nv + (MGS_HBM_EXTRA ? (size_t)(K_CERT * CERT_W + 9 * nc + BLKSTRIDE * nc) : 0);
+}
 struct Lay {
   int o[L_COUNT];
   int u[U_COUNT];   // offsets relative to o[L_U]
@@ -2561,8 +2575,23 @@ DEVI void bind(Dat& d, double* s, const Lay& l) {
   BU(qfrc_bias, U_qfrc_bias); BU(qfrc_passive, U_qfrc_passive); BU(qfrc_actuator, U_qfrc_actuator);
 #ifdef MGS_G_GLOBAL
   // wide library (clutter piles): G = D^-1/2 L^-1 J' is too large for LDS at
-  // nefc_max 256 x nv 58; it lives in this candidate's HBM slice (L2-cached)
-  d.G = l.gmem + (size_t)blockIdx.x * (size_t)l.nefc_max * (size_t)l.nv;
+  // nefc_max 256 x nv 58; it lives in this candidate's HBM slice (L2-cached).
+  // Main-library objects with G in HBM (MGS_HBM_EXTRA) keep the separation
+  // certificates, the contact frames and the contact blocks there too.
+  {
+    const int sl_nc = SL ? mgs_sl_words[L_COUNT + U_COUNT] : l.ncon_max;
+    const int sl_ne = SL ? mgs_sl_words[L_COUNT + U_COUNT + 1] : l.nefc_max;
+    const int sl_nv = SL ? mgs_sl_words[L_COUNT + U_COUNT + 2] : l.nv;
+    d.G = l.gmem + (size_t)blockIdx.x * hbm_slice(sl_ne, sl_nv, sl_nc);
+#if MGS_HBM_EXTRA
+    double* x = d.G + (size_t)sl_ne * sl_nv;
+    d.cert = x;
+    x += K_CERT * CERT_W;
+    d.con_frame = x;
+    x += 9 * sl_nc;
+    d.con_blk = x;
+#endif
+  }
 #else
   BU(G, U_G);
 #endif
