@@ -3,7 +3,8 @@
 copied to a scratch tree, optionally edited, compiled for the headline model at
 a given contact capacity.
 
-  python tools/ab_variant.py NAME [--ncon N] [--nefc N] [--noinline] [--src DIR] [-DFLAG ...]
+  python tools/ab_variant.py NAME [--ncon N] [--nefc N] [--noinline] [--ghbm] [--drop FLAG] [--src DIR]
+                             [-DFLAG ...]
 
 --noinline compiles every DEVI helper as a real call (register analysis and the
 two-waves-per-SIMD experiment); -D flags go to hipcc (e.g.
@@ -29,7 +30,7 @@ def main():
     from mgs.util.geo.transforms import SE3Pose
     args = sys.argv[1:]
     name = args.pop(0)
-    ncon, noinline, extra, srcdir, nefc = 20, False, [], None, None
+    ncon, noinline, extra, srcdir, nefc, ghbm, drop = 20, False, [], None, None, False, []
     while args:
         a = args.pop(0)
         if a == "--ncon":
@@ -40,13 +41,22 @@ def main():
             srcdir = args.pop(0)      # kernel sources from a scratch directory (experiments)
         elif a == "--noinline":
             noinline = True
+        elif a == "--ghbm":
+            ghbm = True               # the G-rows-in-HBM object (mgs_model_desc.g_rows_hbm)
+        elif a == "--drop":
+            drop.append(args.pop(0))  # a planned flag to leave out (e.g. -disable-machine-licm)
         else:
             extra.append(a)
     env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
                                     get_object("003_cracker_box"), ncon_max=ncon, nefc_max=nefc)
     fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
     lib = library_for(env.model.nv, int(fields["nefc_max"]))
+    if ghbm:
+        fields["g_rows_hbm"] = 1
     header, flags, _ = special.plan(lib, abi.make_desc(fields))
+    for f in drop:
+        i = flags.index(f)
+        flags = flags[:i - 1] + flags[i + 1:] if i > 0 and flags[i - 1] == "-mllvm" else flags[:i] + flags[i + 1:]
     out_dir = os.path.join(special.CACHE, "..", "ab")
     os.makedirs(out_dir, exist_ok=True)
     path = os.path.abspath(os.path.join(out_dir, name + ".hsaco"))
