@@ -63,8 +63,10 @@ def main():
         from mgs.core import abi
         from mgs.core.engine import library_for
         fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
-        print(special.code_object(library_for(env.model.nv, int(fields["nefc_max"])), abi.make_desc(fields),
-                                  profile=True))
+        lib = library_for(env.model.nv, int(fields["nefc_max"]))
+        if "--lds-rows" not in sys.argv and lib.mgs_rows_per_lane() != 4:
+            fields["g_rows_hbm"] = 1      # as env.engine (Engine(g_rows_hbm="auto")) runs it
+        print(special.code_object(lib, abi.make_desc(fields), profile=True))
         return
     N = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64
     heavy = "--heavy" in sys.argv
