@@ -42,8 +42,11 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 21
+#define MGS_ABI_VERSION 22
 #define MGS_NSTATS 6
+/* largest dof count: 64 for the libraries' kernels (one dof per lane), 128
+   for model-specialised code objects (two dofs per lane, ABI 22) */
+#define MGS_MAX_NV 128
 
 /* error codes */
 #define MGS_OK 0
@@ -160,7 +163,7 @@ typedef struct mgs_model_desc {
   int32_t i_body_dofnum;
   int32_t i_body_dofadr;
   int32_t i_body_lastdof;   /* last dof in the body's kinematic chain, -1 if none */
-  int32_t i_body_dofmask;   /* 2: bit d set if dof d moves the body (dofs 0-31, 32-63) */
+  int32_t i_body_dofmask;   /* 2 (4 when nv > 64): bit d set if dof d moves the body (dofs 0-31, 32-63, ...) */
   int32_t i_body_depth;     /* tree depth (world 0); entry [nbody] = max depth */
   int32_t i_body_childadr;  /* first entry of the body's children in body_child */
   int32_t i_body_childnum;  /* number of children */

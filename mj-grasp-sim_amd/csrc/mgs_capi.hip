@@ -245,7 +245,11 @@ int mgs_model_create(const mgs_model_desc* desc, const int32_t* ibuf, const doub
   if (desc->nu > 32) return fail(MGS_EINVAL, "at most 32 actuators%s");
   if (desc->nmocap > 1) return fail(MGS_EINVAL, "at most one mocap body%s");
   if (desc->nefc_max > 64 * MGS_RPL) return fail(MGS_EINVAL, "nefc_max exceeds this library's rows (mgs_max_rows)%s");
-  if (desc->nv > 64) return fail(MGS_EINVAL, "nv must be <= 64 (lanes over dofs)%s");
+  // more than 64 dofs: the model's specialised code object runs it (two dofs
+  // per lane); the library's kernels refuse it at launch (no instantiation)
+  if (desc->nv > MGS_MAX_NV) return fail(MGS_EINVAL, "nv must be <= 128 (two dofs per lane)%s");
+  if (desc->nbody > 64) return fail(MGS_EINVAL, "at most 64 bodies (lanes over bodies)%s");
+  if (desc->njnt > 64) return fail(MGS_EINVAL, "at most 64 joints (lanes over joints)%s");
   if (desc->maxcondim != 1 && desc->maxcondim != 3 && desc->maxcondim != 4 && desc->maxcondim != 6)
     return fail(MGS_EINVAL, "maxcondim must be 1, 3, 4 or 6%s");
   for (int p = 0; p < desc->npair; p++) {
@@ -1078,6 +1082,10 @@ int mgs_model_attach_special(mgs_model* m, const char* path) {
     if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_maxdim") != hipSuccess || sz != sizeof(int) ||
         hipMemcpyDtoH(&mxd, p, sizeof(int)) != hipSuccess || mxd != layout_maxdim(m->desc))
       return fail(MGS_EINVAL, "code object %s was built for another contact dimension (MGS_MAXDIM)", path);
+    int mxnv = 0;
+    if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_max_nv") != hipSuccess || sz != sizeof(int) ||
+        hipMemcpyDtoH(&mxnv, p, sizeof(int)) != hipSuccess || mxnv < m->desc.nv)
+      return fail(MGS_EINVAL, "code object %s holds fewer dofs per lane than the model needs (MGS_DPL)", path);
     if (hipModuleGetGlobal(&p, &sz, mod, "mgs_special_desc") != hipSuccess || sz != sizeof(dsc) ||
         hipMemcpyDtoH(&dsc, p, sizeof(dsc)) != hipSuccess || memcmp(&dsc, &m->desc, sizeof(dsc)) != 0)
       return fail(MGS_EINVAL, "code object %s was specialised for another model description", path);

@@ -389,6 +389,74 @@ DEVI int next_pow2(int n) {
   return P;
 }
 
+// Dofs per lane.  Lanes over dofs is the unit of the dynamics, the solves and
+// the solver sweeps: lane l owns dof l (MGS_DPL 1, every library build and
+// every model of at most 64 dofs) or dofs l and l + 64 (MGS_DPL 2: the
+// specialised objects of models with 65-128 dofs, clutter piles of 7-10
+// objects).  A dof-indexed value held in registers is a DofV; with MGS_DPL 1
+// every helper below is the single-slot expression it replaces.
+#ifndef MGS_DPL
+#define MGS_DPL 1
+#endif
+static_assert(MGS_DPL == 1 || MGS_DPL == 2, "MGS_DPL is 1 or 2");
+static_assert(MGS_DPL == 1 || (MGS_PACKED && !MGS_REG_ROWS), "two dofs per lane: the wide flavour (MGS_WIDE)");
+#define MGS_MAXNV (WAVE * MGS_DPL)
+struct DofV {
+  double v[MGS_DPL];
+};
+DEVI DofV dof_zero() {
+  DofV x;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) x.v[h] = 0.0;
+  return x;
+}
+// p[dof] on the dof's lane, 0 past nv
+DEVI DofV dof_load(const double* p, int nv, int lane) {
+  DofV x;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) x.v[h] = (lane + h * WAVE < nv) ? p[lane + h * WAVE] : 0.0;
+  return x;
+}
+DEVI DofV dof_mul(const DofV& a, const DofV& b) {
+  DofV x;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) x.v[h] = a.v[h] * b.v[h];
+  return x;
+}
+// the oracle's tree_dot over the dof leaves (P = next_pow2(nv)): a tree over
+// 128 leaves is the tree over dofs 0-63 plus the tree over dofs 64-127 (its
+// last level adds leaf 64 to leaf 0)
+DEVI double dof_tree(const DofV& x, int P) {
+  if (MGS_DPL == 1 || P <= WAVE) return tree_sum(x.v[0], P);
+  return tree_sum(x.v[0], WAVE) + tree_sum(x.v[MGS_DPL - 1], WAVE);
+}
+// u += g delta on the lanes' dofs below nv (the others keep their value)
+DEVI void dof_axpy(DofV& u, const DofV& g, double delta, int nv, int lane) {
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    double s = u.v[h] + g.v[h] * delta;
+    if (lane + h * WAVE < nv) u.v[h] = s;
+  }
+}
+// `DOF_SLOTS(i, nv) stmt;`: stmt for each dof i < nv of this lane (lane, lane + 64)
+#define DOF_SLOTS(i, nv) \
+  _Pragma("unroll") for (int _h = 0, i = lane + 0; _h < MGS_DPL; _h++, i += WAVE) if (i < (nv))
+// dof k's value, uniform (k uniform)
+DEVI double dof_readlane(const DofV& x, int k) {
+  if (MGS_DPL == 1) return readlane_d(x.v[0], k);
+  return readlane_d((k >> 6) ? x.v[MGS_DPL - 1] : x.v[0], k & (WAVE - 1));
+}
+// dof col moves body b: the model's body_dofmask, bit col of the body's words
+// (2 words per body, 4 for models of more than 64 dofs; mgs_gpu.h)
+DEVI int dof_moves(const Mdl& md, int b, int col) {
+  if (MGS_DPL == 1) {
+    const int32_t* mask = IA(md, body_dofmask) + 2 * b;
+    return (col < 32) ? ((mask[0] >> col) & 1) : ((mask[1] >> (col - 32)) & 1);
+  }
+  const int32_t* mask = IA(md, body_dofmask) + (md.m.nv > 64 ? 4 : 2) * b;
+  return (mask[col >> 5] >> (col & 31)) & 1;
+}
+
 // ---------------------------------------------------------------------------
 // Tree-level parallel forward kinematics (oracle kinematics()): lane b owns
 // body b; bodies of one tree depth are independent given their parents, so the
@@ -740,48 +808,58 @@ DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
 template <int NV>
 DEVI void ldl_factor_lds(double* A, double* Dv, double* Dinv) {
   const int lane = lane_id();
-  const int li = lane < NV ? lane : 0;
   for (int c = 0; c < NV; c++) {
-    double s = A[TRI(li, c, NV)];
-    // four products' operands loaded ahead of their FMAs (the LDS latency is
-    // paid once per four terms instead of once per term); the FMA chain and
-    // its ascending-k order are unchanged.  V_ck = l_ck d_k: parked in the
-    // dead upper triangle (square layout), or formed again from l_ck and
-    // Dv[k] (packed layout: the same product of the same operands)
+    DofV sv;
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++) {
+      // row lane + 64 h (MGS_DPL 2: each lane factors its two rows in turn)
+      const int li = lane + h * WAVE < NV ? lane + h * WAVE : 0;
+      double s = A[TRI(li, c, NV)];
+      // four products' operands loaded ahead of their FMAs (the LDS latency is
+      // paid once per four terms instead of once per term); the FMA chain and
+      // its ascending-k order are unchanged.  V_ck = l_ck d_k: parked in the
+      // dead upper triangle (square layout), or formed again from l_ck and
+      // Dv[k] (packed layout: the same product of the same operands)
 #if MGS_PACKED
 #define LDL_V(k) (A[TRI(c, (k), NV)] * Dv[k])
 #else
 #define LDL_V(k) A[(k) * NV + c]
 #endif
-    int k = 0;
-    // eight at a time first (one LDS latency per eight terms), then four
-    for (; k + 8 <= c; k += 8) {
-      double a[8], b[8];
+      int k = 0;
+      // eight at a time first (one LDS latency per eight terms), then four
+      for (; k + 8 <= c; k += 8) {
+        double a[8], b[8];
 #pragma unroll
-      for (int q = 0; q < 8; q++) { a[q] = A[TRI(li, k + q, NV)]; b[q] = LDL_V(k + q); }
+        for (int q = 0; q < 8; q++) { a[q] = A[TRI(li, k + q, NV)]; b[q] = LDL_V(k + q); }
 #pragma unroll
-      for (int q = 0; q < 8; q++) s = __builtin_fma(-a[q], b[q], s);
-    }
-    for (; k + 4 <= c; k += 4) {
-      const double a0 = A[TRI(li, k, NV)], a1 = A[TRI(li, k + 1, NV)], a2 = A[TRI(li, k + 2, NV)],
-                   a3 = A[TRI(li, k + 3, NV)];
-      const double b0 = LDL_V(k), b1 = LDL_V(k + 1), b2 = LDL_V(k + 2), b3 = LDL_V(k + 3);
-      s = __builtin_fma(-a0, b0, s);
-      s = __builtin_fma(-a1, b1, s);
-      s = __builtin_fma(-a2, b2, s);
-      s = __builtin_fma(-a3, b3, s);
-    }
-    for (; k < c; k++) s = __builtin_fma(-A[TRI(li, k, NV)], LDL_V(k), s);
+        for (int q = 0; q < 8; q++) s = __builtin_fma(-a[q], b[q], s);
+      }
+      for (; k + 4 <= c; k += 4) {
+        const double a0 = A[TRI(li, k, NV)], a1 = A[TRI(li, k + 1, NV)], a2 = A[TRI(li, k + 2, NV)],
+                     a3 = A[TRI(li, k + 3, NV)];
+        const double b0 = LDL_V(k), b1 = LDL_V(k + 1), b2 = LDL_V(k + 2), b3 = LDL_V(k + 3);
+        s = __builtin_fma(-a0, b0, s);
+        s = __builtin_fma(-a1, b1, s);
+        s = __builtin_fma(-a2, b2, s);
+        s = __builtin_fma(-a3, b3, s);
+      }
+      for (; k < c; k++) s = __builtin_fma(-A[TRI(li, k, NV)], LDL_V(k), s);
 #undef LDL_V
-    double dc = readlane_d(s, c);
+      sv.v[h] = s;
+    }
+    double dc = dof_readlane(sv, c);
     double inv = 1.0 / dc;
     if (lane == 0) { Dv[c] = dc; Dinv[c] = inv; }
-    if (lane > c && lane < NV) {
-      double l = s * inv;
-      A[TRI(li, c, NV)] = l;
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++) {
+      const int i = lane + h * WAVE;
+      if (i > c && i < NV) {
+        double l = sv.v[h] * inv;
+        A[TRI(i, c, NV)] = l;
 #if !MGS_PACKED
-      A[c * NV + li] = l * dc;
+        A[c * NV + i] = l * dc;
 #endif
+      }
     }
     wsync();
   }
@@ -819,33 +897,46 @@ DEVI void ldl_factor(double* A, double* Dv, double* Dinv) {
 template <int NV>
 DEVI void ldl_solve(const double* L, const double* Dinv, const double* b, double* x) {
   int lane = lane_id();
-  int li = lane < NV ? lane : 0;
+  // lane's row in slot h (rows past NV: row 0, never stored)
+#define LS_ROW(h) (lane + (h) * WAVE < NV ? lane + (h) * WAVE : 0)
 #if MGS_REG_ROWS
+  static_assert(MGS_DPL == 1, "register rows hold one dof per lane");
+  int li = LS_ROW(0);
   double Lr[NV], Lc[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) { Lr[k] = L[TRI(li, k, NV)]; Lc[k] = L[TRI(k, li, NV)]; }
-#define LS_LR(k) Lr[k]
-#define LS_LC(k) Lc[k]
+#define LS_LR(h, k) Lr[k]
+#define LS_LC(h, k) Lc[k]
 #else
-#define LS_LR(k) L[TRI(li, (k), NV)]
-#define LS_LC(k) L[TRI((k), li, NV)]
+#define LS_LR(h, k) L[TRI(LS_ROW(h), (k), NV)]
+#define LS_LC(h, k) L[TRI((k), LS_ROW(h), NV)]
 #endif
-  double acc = b[li];
+  DofV acc;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) acc.v[h] = b[LS_ROW(h)];
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    double yk = readlane_d(acc, k);
-    if (lane > k) acc = __builtin_fma(-LS_LR(k), yk, acc);
+    double yk = dof_readlane(acc, k);
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      if (lane + h * WAVE > k) acc.v[h] = __builtin_fma(-LS_LR(h, k), yk, acc.v[h]);
   }
-  acc = acc * Dinv[li];
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) acc.v[h] = acc.v[h] * Dinv[LS_ROW(h)];
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
-    double xk = readlane_d(acc, k);
-    if (lane < k) acc = __builtin_fma(-LS_LC(k), xk, acc);
+    double xk = dof_readlane(acc, k);
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      if (lane + h * WAVE < k) acc.v[h] = __builtin_fma(-LS_LC(h, k), xk, acc.v[h]);
   }
 #undef LS_LR
 #undef LS_LC
+#undef LS_ROW
   wsync();
-  if (lane < NV) x[lane] = acc;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++)
+    if (lane + h * WAVE < NV) x[lane + h * WAVE] = acc.v[h];
   wsync();
 }
 
@@ -893,14 +984,15 @@ DEVI void actuation(const Mdl& md, Dat& d) {
   const int32_t *wdof = IA(md, wrap_dofid), *wq = IA(md, wrap_qposadr);
   const double* wcoef = DA(md, wrap_coef);
   const int32_t *jq = IA(md, jnt_qposadr), *jd = IA(md, jnt_dofadr);
-  double qfa = 0.0;
+  DofV qfa = dof_zero();
   for (int u = 0; u < md.m.nu; u++) {
 #if MGS_PACKED
     // the wide build reads the moment rows from the model (joint and fixed-
     // tendon transmissions: constant; mgs_model_desc.d_actuator_moment, the
     // same sums formed on the host) instead of keeping nu x nv of them in LDS
     const double* mom = DA(md, actuator_moment) + u * nv;
-    double m = lane < nv ? mom[lane] : 0.0, len;
+    DofV m = dof_load(mom, nv, lane);
+    double len;
     if (trntype[u] == MGS_TRN_JOINT) {
       len = d.qpos[jq[trnid[u]]] * gear[u];
     } else {
@@ -912,22 +1004,24 @@ DEVI void actuation(const Mdl& md, Dat& d) {
     (void)jd;
     (void)wdof;
 #else
+    static_assert(MGS_DPL == 1, "two dofs per lane read the moment rows from the model (MGS_PACKED)");
     double* mom = d.act_moment + u * nv;
-    double m = 0.0, len;
+    DofV m = dof_zero();
+    double len;
     if (trntype[u] == MGS_TRN_JOINT) {
       int j = trnid[u];
       len = d.qpos[jq[j]] * gear[u];
-      if (lane == jd[j]) m = gear[u];
+      if (lane == jd[j]) m.v[0] = gear[u];
     } else {
       int t = trnid[u];
       double tl = 0.0;
       for (int w = tadr[t]; w < tadr[t] + tnum[t]; w++) {
         tl = tl + wcoef[w] * d.qpos[wq[w]];
-        if (lane == wdof[w]) m = m + wcoef[w] * gear[u];
+        if (lane == wdof[w]) m.v[0] = m.v[0] + wcoef[w] * gear[u];
       }
       len = tl * gear[u];
     }
-    if (lane < nv) mom[lane] = m;
+    if (lane < nv) mom[lane] = m.v[0];
     wsync();
 #endif
     double vel = 0.0;
@@ -951,22 +1045,28 @@ DEVI void actuation(const Mdl& md, Dat& d) {
       if (f > frange[2 * u + 1]) f = frange[2 * u + 1];
     }
     if (lane == 0) { d.act_length[u] = len; d.act_vel[u] = vel; d.act_force[u] = f; }
-    qfa = qfa + m * f;
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++) qfa.v[h] = qfa.v[h] + m.v[h] * f;
   }
-  if (lane < nv) d.qfrc_actuator[lane] = qfa;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++)
+    if (lane + h * WAVE < nv) d.qfrc_actuator[lane + h * WAVE] = qfa.v[h];
 }
 
 // passive forces (oracle passive()), one dof per lane
 DEVI void passive(const Mdl& md, Dat& d) {
   const int32_t *jtype = IA(md, jnt_type), *jq = IA(md, jnt_qposadr), *djnt = IA(md, dof_jntid);
   const double *stiff = DA(md, jnt_stiffness), *qspring = DA(md, qpos_spring), *damp = DA(md, dof_damping);
-  int lane = lane_id();
-  if (lane < md.m.nv) {
-    int j = djnt[lane];
+  const int lane = lane_id();
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;   // this slot's dof
+    if (i >= md.m.nv) continue;
+    int j = djnt[i];
     double v = 0.0;
     if (stiff[j] != 0.0 && (jtype[j] == MGS_JNT_HINGE || jtype[j] == MGS_JNT_SLIDE))
       v = -stiff[j] * (d.qpos[jq[j]] - qspring[jq[j]]);
-    v = v - damp[lane] * d.qvel[lane];
+    v = v - damp[i] * d.qvel[i];
     // gravity compensation (oracle passive(): MuJoCo mj_gravcomp with the
     // force's moment arm from cinert, bodies in order)
     const double* g = md.m.gravity;
@@ -976,10 +1076,9 @@ DEVI void passive(const Mdl& md, Dat& d) {
       int any = 0;
       for (int b = 1; b < md.m.nbody; b++) {
         if (gc[b] == 0.0) continue;
-        const int32_t* mask = IA(md, body_dofmask) + 2 * b;
-        if (!((lane < 32) ? ((mask[0] >> lane) & 1) : ((mask[1] >> (lane - 32)) & 1))) continue;
+        if (!dof_moves(md, b, i)) continue;
         const double* ci = d.cinert + 10 * b;
-        const double* cd = d.cdof + 6 * lane;
+        const double* cd = d.cdof + 6 * i;
         double cr[3];
         cross3(cr, cd, ci + 6);
         double t = ((g[0] * cd[3] + g[1] * cd[4]) + g[2] * cd[5]) * ci[9] + ((g[0] * cr[0] + g[1] * cr[1]) + g[2] * cr[2]);
@@ -988,7 +1087,7 @@ DEVI void passive(const Mdl& md, Dat& d) {
       }
       if (any) v = v + acc;
     }
-    d.qfrc_passive[lane] = v;
+    d.qfrc_passive[i] = v;
   }
 }
 
@@ -1033,7 +1132,11 @@ DEVI void rne(const Mdl& md, Dat& d) {
     wsync();
   }
   accumulate_up<6>(md, d.cfrc, 0);
-  if (lane < md.m.nv) d.qfrc_bias[lane] = dot6(d.cdof + 6 * lane, d.cfrc + 6 * dbody[lane]);
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;
+    if (i < md.m.nv) d.qfrc_bias[i] = dot6(d.cdof + 6 * i, d.cfrc + 6 * dbody[i]);
+  }
   wsync();
 }
 
@@ -2671,9 +2774,7 @@ DEVI void jac_point(const Mdl& md, const Dat& d, int b, const double* pt, double
 // column `col` of the point Jacobian of body b at pt (oracle jac_point(), one
 // dof per lane): zero unless dof col moves the body (model body_dofmask).
 DEVI void jac_col(const Mdl& md, const Dat& d, int b, const double* pt, int col, double* jp, double* jr) {
-  const int32_t* mask = IA(md, body_dofmask) + 2 * b;
-  int in = (col < 32) ? ((mask[0] >> col) & 1) : ((mask[1] >> (col - 32)) & 1);
-  if (in) {
+  if (dof_moves(md, b, col)) {
     const double* cd = d.cdof + 6 * col;
     const double* c = d.subtree_com + 3 * IA(md, body_rootid)[b];
     double off[3], cr[3];
@@ -2960,12 +3061,16 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
         for (int k = 0; k < 3; k++) add_row(md, d, MGS_EFC_EQUALITY, p1[k] - p2[k], 0.0, 1, e);
       wsync();
       int r0 = d.NEFC - 3;
-      double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
-      int col = lane < nv ? lane : 0;
-      jac_col(md, d, b1, p1, col, cjp1, cjr1);
-      jac_col(md, d, b2, p2, col, cjp2, cjr2);
-      if (lane < nv)
-        for (int k = 0; k < 3; k++) J[(r0 + k) * d.gs + lane] = cjp1[k] - cjp2[k];
+      double cjp1[MGS_DPL][3], cjr1[MGS_DPL][3], cjp2[MGS_DPL][3], cjr2[MGS_DPL][3];
+#pragma unroll
+      for (int h = 0; h < MGS_DPL; h++) {
+        const int i = lane + h * WAVE;
+        int col = i < nv ? i : 0;
+        jac_col(md, d, b1, p1, col, cjp1[h], cjr1[h]);
+        jac_col(md, d, b2, p2, col, cjp2[h], cjr2[h]);
+        if (i < nv)
+          for (int k = 0; k < 3; k++) J[(r0 + k) * d.gs + i] = cjp1[h][k] - cjp2[h][k];
+      }
       if (et[e] == MGS_EQ_WELD) {
         double q1r[4], q2c[4], qe[4];
         quatmul(q1r, d.xquat + 4 * b1, data + 3);
@@ -2978,12 +3083,16 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
           for (int k = 0; k < 3; k++) add_row(md, d, MGS_EFC_EQUALITY, qe[1 + k] * ts, 0.0, 1, e);
         wsync();
         int rr = d.NEFC - 3;
-        if (lane < nv) {
-          double ax[4] = {0.0, cjr1[0] - cjr2[0], cjr1[1] - cjr2[1], cjr1[2] - cjr2[2]};
-          double t1q[4], t2q[4];
-          quatmul(t1q, q2c, ax);
-          quatmul(t2q, t1q, q1r);
-          for (int k = 0; k < 3; k++) J[(rr + k) * d.gs + lane] = (0.5 * t2q[1 + k]) * ts;
+#pragma unroll
+        for (int h = 0; h < MGS_DPL; h++) {
+          const int i = lane + h * WAVE;
+          if (i < nv) {
+            double ax[4] = {0.0, cjr1[h][0] - cjr2[h][0], cjr1[h][1] - cjr2[h][1], cjr1[h][2] - cjr2[h][2]};
+            double t1q[4], t2q[4];
+            quatmul(t1q, q2c, ax);
+            quatmul(t2q, t1q, q1r);
+            for (int k = 0; k < 3; k++) J[(rr + k) * d.gs + i] = (0.5 * t2q[1 + k]) * ts;
+          }
         }
       }
       wsync();
@@ -3023,14 +3132,21 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
   {
     int ne0 = uni(d.NEFC);
     const double* floss = DA(md, dof_frictionloss);
-    int hasf = (lane < nv) && floss[lane] > 0.0;
-    unsigned long long mf = __ballot(hasf);
     unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
-    int nf = __popcll(mf);
-    int rf = ne0 + __popcll(mf & lt);
-    if (hasf && rf < md.m.nefc_max) {
-      d.efc_type[rf] = MGS_EFC_FRICTION; d.efc_pos[rf] = 0.0; d.efc_margin[rf] = 0.0;
-      d.efc_dim[rf] = 1; d.efc_con[rf] = lane;
+    // friction rows in dof order: slot h's rows follow the lower slots' rows
+    int hasf[MGS_DPL], rf[MGS_DPL];
+    int nf = 0;
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++) {
+      const int i = lane + h * WAVE;
+      hasf[h] = (i < nv) && floss[i] > 0.0;
+      unsigned long long mf = __ballot(hasf[h]);
+      rf[h] = ne0 + nf + __popcll(mf & lt);
+      nf += __popcll(mf);
+      if (hasf[h] && rf[h] < md.m.nefc_max) {
+        d.efc_type[rf[h]] = MGS_EFC_FRICTION; d.efc_pos[rf[h]] = 0.0; d.efc_margin[rf[h]] = 0.0;
+        d.efc_dim[rf[h]] = 1; d.efc_con[rf[h]] = i;
+      }
     }
     int ne1 = ne0 + nf;
     if (ne1 > md.m.nefc_max) ne1 = md.m.nefc_max;
@@ -3062,7 +3178,9 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
     // J rows [ne0, ne2): zeros, then the unit entries
     for (int e = lane; e < (ne2 - ne0) * GS; e += WAVE) J[ne0 * GS + e] = 0.0;
     wsync();
-    if (hasf && rf < md.m.nefc_max) J[rf * GS + lane] = 1.0;
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      if (hasf[h] && rf[h] < md.m.nefc_max) J[rf[h] * GS + lane + h * WAVE] = 1.0;
     if (lo && rl < md.m.nefc_max) J[rl * GS + jd[lane]] = 1.0;
     if (hi && rh < md.m.nefc_max) J[rh * GS + jd[lane]] = -1.0;
     if (lane == 0) {
@@ -3101,11 +3219,14 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
           if (!MGS_MU_MODEL && (MGS_MAXDIM < 6 || j < 5)) d.con_mu[5 * c + j] = (j < dim - 1) ? pfr[5 * p + j] : 0.0;
       }
       wsync();
-      int col = lane < nv ? lane : 0;
+#pragma unroll
+      for (int h = 0; h < MGS_DPL; h++) {
+      const int i = lane + h * WAVE;
+      int col = i < nv ? i : 0;
       double cjp1[3], cjr1[3], cjp2[3], cjr2[3];
       jac_col(md, d, b1, pt, col, cjp1, cjr1);
       jac_col(md, d, b2, pt, col, cjp2, cjr2);
-      if (lane < nv) {
+      if (i < nv) {
         double dp[3] = {cjp2[0] - cjp1[0], cjp2[1] - cjp1[1], cjp2[2] - cjp1[2]};
         for (int j = 0; j < dim && j < 3; j++) J[(r + j) * d.gs + col] = dot3(fr + 3 * j, dp);
         if (dim >= 4) {
@@ -3118,6 +3239,7 @@ DEVI void make_constraints(const Mdl& md, Dat& d) {
           }
 #endif
         }
+      }
       }
     }
   } else {
@@ -3484,20 +3606,21 @@ DEVI double cost_change(const double* A, const double* delta, const double* res)
 
 // one PGS update of the contact block starting at row r with DIM rows
 template <int DIM>
-DEVI double pgs_contact(const Mdl& md, const Dat& d, int r, int nv, int P, int lane, double& u, Frc& F, int noslip,
-                        const double* gpre = nullptr) {
-  double g[DIM], res[DIM], old[DIM], nw[DIM];
+DEVI double pgs_contact(const Mdl& md, const Dat& d, int r, int nv, int P, int lane, DofV& u, Frc& F, int noslip,
+                        const DofV* gpre = nullptr) {
+  DofV g[DIM];
+  double res[DIM], old[DIM], nw[DIM];
   const int c = uni(d.efc_con[r]);
   const double* blk = d.con_blk + BLKSTRIDE * c;
   const double* mu = con_mu_of(md, d, c);
 #pragma unroll
   for (int i = 0; i < DIM; i++) {
     // gpre: the block's G rows loaded ahead by the caller (lanes over dofs)
-    g[i] = gpre ? gpre[i] : ((lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0);
+    g[i] = gpre ? gpre[i] : dof_load(d.G + (r + i) * d.gs, nv, lane);
     old[i] = getf(F, r + i);
     // noslip never reads the normal row's residual: its reduction is skipped
     if (noslip && i == 0) { res[i] = 0.0; continue; }
-    double jw = tree_sum(g[i] * u, P);
+    double jw = dof_tree(dof_mul(g[i], u), P);
     res[i] = noslip ? (jw + d.efc_b[r + i]) : ((jw + d.efc_R[r + i] * old[i]) + d.efc_b[r + i]);
   }
   PT(42);
@@ -3549,10 +3672,13 @@ DEVI double pgs_contact(const Mdl& md, const Dat& d, int r, int nv, int P, int l
       for (int i = 0; i < DIM; i++) { nw[i] = old[i]; del[i] = 0.0; }
       dc = 0.0;
     }
-    double s = u;
 #pragma unroll
-    for (int i = 0; i < DIM; i++) s = s + g[i] * del[i];
-    if (lane < nv) u = s;
+    for (int h = 0; h < MGS_DPL; h++) {
+      double s = u.v[h];
+#pragma unroll
+      for (int i = 0; i < DIM; i++) s = s + g[i].v[h] * del[i];
+      if (lane + h * WAVE < nv) u.v[h] = s;
+    }
 #pragma unroll
     for (int i = 0; i < DIM; i++) setf(F, r + i, nw[i], lane);
   } else {
@@ -3593,10 +3719,13 @@ DEVI double pgs_contact(const Mdl& md, const Dat& d, int r, int nv, int P, int l
       for (int i = 0; i < NF; i++) { nw[1 + i] = old[1 + i]; del[i] = 0.0; }
       dc = 0.0;
     }
-    double s = u;
 #pragma unroll
-    for (int i = 0; i < NF; i++) s = s + g[1 + i] * del[i];
-    if (lane < nv) u = s;
+    for (int h = 0; h < MGS_DPL; h++) {
+      double s = u.v[h];
+#pragma unroll
+      for (int i = 0; i < NF; i++) s = s + g[1 + i].v[h] * del[i];
+      if (lane + h * WAVE < nv) u.v[h] = s;
+    }
 #pragma unroll
     for (int i = 0; i < NF; i++) setf(F, r + 1 + i, nw[1 + i], lane);
   }
@@ -3636,7 +3765,7 @@ DEVI void project_block_lds(const Mdl& md, const Dat& d, int r, double* f) {
   }
 }
 
-DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, DofV& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   // warmstart: hws = D^1/2 L^T qacc_ws (lane 0), f_r by lanes over rows, block projection
@@ -3667,12 +3796,16 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   }
   wsync();
   // u = G^T f (lane k), then dual cost terms (lanes over rows), summed in row order
-  u = 0.0;
-  if (lane < nv) {
-    double s = 0.0;
-    for (int r = 0; r < ne; r++) s = s + d.G[r * d.gs + lane] * fl[r];
-    u = s;
-    d.tmp2[lane] = s;
+  u = dof_zero();
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;
+    if (i < nv) {
+      double s = 0.0;
+      for (int r = 0; r < ne; r++) s = s + d.G[r * d.gs + i] * fl[r];
+      u.v[h] = s;
+      d.tmp2[i] = s;
+    }
   }
   wsync();
   for (int r = lane; r < ne; r += WAVE) {
@@ -3688,7 +3821,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
   if (!(cw < 0.0)) {
 #pragma unroll
     for (int h = 0; h < MGS_RPL; h++) F.v[h] = 0.0;
-    u = 0.0;
+    u = dof_zero();
   }
   int it;
   for (it = 0; it < md.m.iterations && ne > 0; it++) {
@@ -3697,8 +3830,8 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
       int t = uni(d.efc_type[r]);
       int dim = uni(d.efc_dim[r]);
       if (t != MGS_EFC_CONTACT || dim == 1) {
-        double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
-        double jw = tree_sum(g * u, P);
+        DofV g = dof_load(d.G + r * d.gs, nv, lane);
+        double jw = dof_tree(dof_mul(g, u), P);
         double fo = getf(F, r);
         double res = (jw + d.efc_R[r] * fo) + d.efc_b[r];
         double AR = row_sqnorm(d, r, nv) + d.efc_R[r];
@@ -3709,8 +3842,7 @@ DEVI void solve_pgs(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
         if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
         improvement = improvement - ch;
         if (delta != 0.0) {
-          double s = u + g * delta;
-          if (lane < nv) u = s;
+          dof_axpy(u, g, delta, nv, lane);
           setf(F, r, fnew[0], lane);
         }
         r += 1;
@@ -3772,12 +3904,15 @@ DEVI int next_visited(const unsigned long long (&vis)[N], int r) {
   }
   return out;
 }
-DEVI void load_block_rows(const Dat& d, int r, int dim, int nv, int lane, double (&g)[MGS_MAXDIM]) {
+DEVI void load_block_rows(const Dat& d, int r, int dim, int nv, int lane, DofV (&g)[MGS_MAXDIM]) {
 #pragma unroll
-  for (int i = 0; i < MGS_MAXDIM; i++) g[i] = (i < dim && lane < nv) ? d.G[(r + i) * d.gs + lane] : 0.0;
+  for (int i = 0; i < MGS_MAXDIM; i++)
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      g[i].v[h] = (i < dim && lane + h * WAVE < nv) ? d.G[(r + i) * d.gs + lane + h * WAVE] : 0.0;
 }
 
-DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, DofV& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   if (md.m.noslip_iterations <= 0 || ne <= 0) return;
@@ -3820,7 +3955,7 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
     }
     int r = next_visited(vis, -1);
     int t = 0, dim = 0;
-    double gc[MGS_MAXDIM];
+    DofV gc[MGS_MAXDIM];
     if (r >= 0) {
       t = sel_i(tk, r);
       dim = t == MGS_EFC_FRICTION ? 1 : sel_i(dk, r);
@@ -3829,17 +3964,17 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
     while (r >= 0) {
       const int rn = next_visited(vis, r);
       int tn = 0, dimn = 0;
-      double gn[MGS_MAXDIM];
+      DofV gn[MGS_MAXDIM];
 #pragma unroll
-      for (int i = 0; i < MGS_MAXDIM; i++) gn[i] = 0.0;
+      for (int i = 0; i < MGS_MAXDIM; i++) gn[i] = dof_zero();
       if (rn >= 0) {
         tn = sel_i(tk, rn);
         dimn = tn == MGS_EFC_FRICTION ? 1 : sel_i(dk, rn);
         load_block_rows(d, rn, dimn, nv, lane, gn);
       }
       if (t == MGS_EFC_FRICTION) {
-        double g = gc[0];
-        double res = tree_sum(g * u, P) + d.efc_b[r];
+        const DofV g = gc[0];
+        double res = dof_tree(dof_mul(g, u), P) + d.efc_b[r];
         double fo = getf(F, r);
         double Arr = sel_d(Ak, r);
         double fnew[1] = {fo - res * (1.0 / Arr)};
@@ -3849,8 +3984,7 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
         if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
         improvement = improvement - ch;
         if (delta != 0.0) {
-          double s = u + g * delta;
-          if (lane < nv) u = s;
+          dof_axpy(u, g, delta, nv, lane);
           setf(F, r, fnew[0], lane);
         }
       } else if (dim == 3) {
@@ -3876,7 +4010,7 @@ DEVI void noslip_prefetch(const Mdl& md, Dat& d, double scale, Frc& F, double& u
 // in place; G in HBM (wide build): noslip_prefetch (C5 pile rollout 2148 ->
 // 2058 ms, profiles/r04m_noslip_ab.txt; the main build measured 1 % slower
 // with it)
-DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, DofV& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   if (md.m.noslip_iterations <= 0 || ne <= 0) return;
@@ -3919,8 +4053,8 @@ DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u)
         const int r = l + h * WAVE;
         const int t = __builtin_amdgcn_readlane(tk[h], l), dim = __builtin_amdgcn_readlane(dk[h], l);
         if (t == MGS_EFC_FRICTION) {
-          double g = (lane < nv) ? d.G[r * d.gs + lane] : 0.0;
-          double res = tree_sum(g * u, P) + d.efc_b[r];
+          DofV g = dof_load(d.G + r * d.gs, nv, lane);
+          double res = dof_tree(dof_mul(g, u), P) + d.efc_b[r];
           double fo = getf(F, r);
           double Arr = row_sqnorm(d, r, nv);
           double fnew[1] = {fo - res * (1.0 / Arr)};
@@ -3930,8 +4064,7 @@ DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u)
           if (ch > 1e-10) { delta = 0.0; ch = 0.0; }
           improvement = improvement - ch;
           if (delta != 0.0) {
-            double s = u + g * delta;
-            if (lane < nv) u = s;
+            dof_axpy(u, g, delta, nv, lane);
             setf(F, r, fnew[0], lane);
           }
         } else if (dim == 3) {
@@ -3949,7 +4082,7 @@ DEVI void noslip_inplace(const Mdl& md, Dat& d, double scale, Frc& F, double& u)
   }
 }
 
-DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, DofV& u) {
 #ifdef MGS_G_GLOBAL
   noslip_prefetch(md, d, scale, F, u);
 #else
@@ -3963,37 +4096,54 @@ DEVI void noslip(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
 // u_main: the main solver's u (MuJoCo saves qacc_warmstart before noslip;
 // qacc feeds only the warmstart, implicitfast integrates qfrc_constraint)
 template <int NV>
-DEVI void finalize_solution(const Mdl& md, Dat& d, double u_main, double u) {
+DEVI void finalize_solution(const Mdl& md, Dat& d, const DofV& u_main, const DofV& u) {
   int lane = lane_id();
-  int li = lane < NV ? lane : 0;
+#define FS_ROW(h) (lane + (h) * WAVE < NV ? lane + (h) * WAVE : 0)
 #if MGS_REG_ROWS
+  static_assert(MGS_DPL == 1, "register rows hold one dof per lane");
+  int li = FS_ROW(0);
   double Lr[NV], Lc[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) { Lr[k] = d.M[TRI(li, k, NV)]; Lc[k] = d.M[TRI(k, li, NV)]; }
-#define FS_LR(k) Lr[k]
-#define FS_LC(k) Lc[k]
+#define FS_LR(h, k) Lr[k]
+#define FS_LC(h, k) Lc[k]
 #else
-#define FS_LR(k) d.M[TRI(li, (k), NV)]
-#define FS_LC(k) d.M[TRI((k), li, NV)]
+#define FS_LR(h, k) d.M[TRI(FS_ROW(h), (k), NV)]
+#define FS_LC(h, k) d.M[TRI((k), FS_ROW(h), NV)]
 #endif
-  double z = u_main * d.isD[li];
+  DofV z;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) z.v[h] = u_main.v[h] * d.isD[FS_ROW(h)];
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
-    double zk = readlane_d(z, k);
-    if (lane < k) z = __builtin_fma(-FS_LC(k), zk, z);
+    double zk = dof_readlane(z, k);
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      if (lane + h * WAVE < k) z.v[h] = __builtin_fma(-FS_LC(h, k), zk, z.v[h]);
   }
-  double t = u * d.sD[li];
-  double q = t;
+  DofV t, q;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    t.v[h] = u.v[h] * d.sD[FS_ROW(h)];
+    q.v[h] = t.v[h];
+  }
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    double tk = readlane_d(t, k);
-    if (lane > k) q = __builtin_fma(FS_LR(k), tk, q);
+    double tk = dof_readlane(t, k);
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      if (lane + h * WAVE > k) q.v[h] = __builtin_fma(FS_LR(h, k), tk, q.v[h]);
   }
 #undef FS_LR
 #undef FS_LC
-  if (lane < NV) {
-    d.qfrc_constraint[lane] = q;
-    d.qacc_ws[lane] = d.qacc_smooth[lane] + z;   // qacc, kept as next step's warmstart
+#undef FS_ROW
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;
+    if (i < NV) {
+      d.qfrc_constraint[i] = q.v[h];
+      d.qacc_ws[i] = d.qacc_smooth[i] + z.v[h];   // qacc, kept as next step's warmstart
+    }
   }
   wsync();
 }
@@ -4125,8 +4275,10 @@ template <int NV>
 DEVI double newton_eval(const Mdl& md, Dat& d, const double* w, int P, const double* mupR, const double* k1R) {
   int ne = uni(d.NEFC), lane = lane_id();
   PCNT(37, 1);
-  double q = (lane < NV) ? w[lane] - d.nw0[lane] : 0.0;
-  double gauss = 0.5 * tree_sum(q * q, P);
+  DofV q;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) q.v[h] = (lane + h * WAVE < NV) ? w[lane + h * WAVE] - d.nw0[lane + h * WAVE] : 0.0;
+  double gauss = 0.5 * dof_tree(dof_mul(q, q), P);
 #if MGS_REG_ROWS
   double wr[NV];
 #pragma unroll
@@ -4182,10 +4334,15 @@ DEVI void newton_eval_pair(const Mdl& md, Dat& d, const double* wa, const double
                            const double* k1R, double& c0, double& c1) {
   int ne = uni(d.NEFC), lane = lane_id();
   PCNT(37, 2);
-  double qa = (lane < NV) ? wa[lane] - d.nw0[lane] : 0.0;
-  double qb = (lane < NV) ? wb[lane] - d.nw0[lane] : 0.0;
-  double gauss0 = 0.5 * tree_sum(qa * qa, P);
-  double gauss1 = 0.5 * tree_sum(qb * qb, P);
+  DofV qa, qb;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;
+    qa.v[h] = (i < NV) ? wa[i] - d.nw0[i] : 0.0;
+    qb.v[h] = (i < NV) ? wb[i] - d.nw0[i] : 0.0;
+  }
+  double gauss0 = 0.5 * dof_tree(dof_mul(qa, qa), P);
+  double gauss1 = 0.5 * dof_tree(dof_mul(qb, qb), P);
   double* jar0 = d.scratch;   // idle until the first Newton Hessian
 #if MGS_REG_ROWS
   double ra[NV], rb[NV];
@@ -4247,7 +4404,10 @@ DEVI void newton_eval_pair(const Mdl& md, Dat& d, const double* wa, const double
 template <int NV>
 DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
   int ne = uni(d.NEFC), lane = lane_id();
-  if (lane < NV) {
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;   // this slot's dof
+    if (i >= NV) continue;
     double s = 0.0;
     int r = 0;
 #ifdef MGS_G_GLOBAL
@@ -4256,23 +4416,23 @@ DEVI void newton_grad(const Mdl& md, Dat& d, const double* w) {
     for (; r + 16 <= ne; r += 16) {
       double g[16], f[16];
 #pragma unroll
-      for (int q = 0; q < 16; q++) { g[q] = d.G[(r + q) * GS + lane]; f[q] = d.efc_f[r + q]; }
+      for (int q = 0; q < 16; q++) { g[q] = d.G[(r + q) * GS + i]; f[q] = d.efc_f[r + q]; }
 #pragma unroll
       for (int q = 0; q < 16; q++) s = __builtin_fma(g[q], f[q], s);
     }
 #endif
     // rows in order, four loads in flight per step
     for (; r + 4 <= ne; r += 4) {
-      double g0 = d.G[r * GS + lane], g1 = d.G[(r + 1) * GS + lane], g2 = d.G[(r + 2) * GS + lane],
-             g3 = d.G[(r + 3) * GS + lane];
+      double g0 = d.G[r * GS + i], g1 = d.G[(r + 1) * GS + i], g2 = d.G[(r + 2) * GS + i],
+             g3 = d.G[(r + 3) * GS + i];
       double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
       s = __builtin_fma(g0, f0, s);
       s = __builtin_fma(g1, f1, s);
       s = __builtin_fma(g2, f2, s);
       s = __builtin_fma(g3, f3, s);
     }
-    for (; r < ne; r++) s = __builtin_fma(d.G[r * GS + lane], d.efc_f[r], s);
-    d.ng[lane] = (w[lane] - d.nw0[lane]) - s;
+    for (; r < ne; r++) s = __builtin_fma(d.G[r * GS + i], d.efc_f[r], s);
+    d.ng[i] = (w[i] - d.nw0[i]) - s;
   }
   wsync();
 }
@@ -4578,7 +4738,7 @@ DEVI void ls_eval_fast(const Mdl& md, const Dat& d, int ne, const LsRow& L, doub
 }
 
 template <int NV>
-DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
+DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, DofV& u) {
   int nv = md.m.nv, ne = uni(d.NEFC), lane = lane_id();
   int P = next_pow2(nv);
   for (int r = lane; r < ne; r += WAVE) {
@@ -4600,20 +4760,22 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     }
   }
   // w0 = W(qacc_smooth), w = W(qacc_ws)   (lane i: s_i = a_i + sum_{k>i} L_ki a_k)
-  {
-    int li = lane < NV ? lane : 0;
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;
+    int li = i < NV ? i : 0;
     double s = d.qacc_smooth[li], s2 = d.qacc_ws[li];
 #pragma unroll
     for (int k = 1; k < NV; k++) {
       double l = d.M[TRI(k, li, NV)];
-      if (k > lane) {
+      if (k > i) {
         s = __builtin_fma(l, d.qacc_smooth[k], s);
         s2 = __builtin_fma(l, d.qacc_ws[k], s2);
       }
     }
-    if (lane < NV) {
-      d.nw0[lane] = s * d.sD[lane];
-      d.nw[lane] = s2 * d.sD[lane];
+    if (i < NV) {
+      d.nw0[i] = s * d.sD[i];
+      d.nw[i] = s2 * d.sD[i];
     }
   }
   wsync();
@@ -4626,12 +4788,12 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     if (cws < c0) {
       C = cws;
     } else {
-      if (lane < nv) d.nw[lane] = d.nw0[lane];
+      DOF_SLOTS(k, nv) d.nw[k] = d.nw0[k];
       wsync();
       C = newton_eval<NV>(md, d, d.nw, P, mupR, k1R);
     }
   } else {
-    if (lane < nv) d.nw[lane] = d.nw0[lane];
+    DOF_SLOTS(k, nv) d.nw[k] = d.nw0[k];
     wsync();
   }
   newton_grad<NV>(md, d, d.nw);
@@ -4654,7 +4816,7 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     }
     PT(13);
     ldl_solve<NV>(d.nH, d.tmp2, d.ng, d.ndir);
-    if (lane < nv) d.ndir[lane] = -d.ndir[lane];
+    DOF_SLOTS(k, nv) d.ndir[k] = -d.ndir[k];
     wsync();
     {
 #if MGS_REG_ROWS
@@ -4674,10 +4836,12 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     }
     wsync();
     PT(14);
-    double dl = (lane < nv) ? d.ndir[lane] : 0.0;
-    double q = (lane < nv) ? d.nw[lane] - d.nw0[lane] : 0.0;
-    double A1 = tree_sum(q * dl, P);
-    double A2 = tree_sum(dl * dl, P);
+    DofV dl = dof_load(d.ndir, nv, lane), q;
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      q.v[h] = (lane + h * WAVE < nv) ? d.nw[lane + h * WAVE] - d.nw0[lane + h * WAVE] : 0.0;
+    double A1 = dof_tree(dof_mul(q, dl), P);
+    double A2 = dof_tree(dof_mul(dl, dl), P);
     double p0, q0, alpha = 0.0;
     LsRow LR;
     ls_row_load(md, d, lane, ne, mupR[0], k1R[0], LR);
@@ -4699,35 +4863,40 @@ DEVI void solve_newton(const Mdl& md, Dat& d, double scale, Frc& F, double& u) {
     }
     PT(15);
     if (!(alpha > 0.0)) { it++; break; }
-    if (lane < nv) d.nw[lane] = d.nw[lane] + alpha * dl;
+#pragma unroll
+    for (int h = 0; h < MGS_DPL; h++)
+      if (lane + h * WAVE < nv) d.nw[lane + h * WAVE] = d.nw[lane + h * WAVE] + alpha * dl.v[h];
     wsync();
     double Cn = newton_eval<NV>(md, d, d.nw, P, mupR, k1R);
     newton_grad<NV>(md, d, d.nw);
     double improvement = scale * (C - Cn);
     C = Cn;
-    double gl = (lane < nv) ? d.ng[lane] : 0.0;
-    double gn = scale * sqrt(tree_sum(gl * gl, P));
+    DofV gl = dof_load(d.ng, nv, lane);
+    double gn = scale * sqrt(dof_tree(dof_mul(gl, gl), P));
     PT(16);
     if (improvement < md.m.tolerance || gn < md.m.tolerance) { it++; break; }
   }
   if (lane == 0) d.ITERS += it;
   // forces to registers, u = G^T f
   load_frc(F, d.efc_f, ne, lane);
-  u = 0.0;
-  if (lane < NV) {
+  u = dof_zero();
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;
+    if (i >= NV) continue;
     double s = 0.0;
     int r = 0;
     for (; r + 4 <= ne; r += 4) {
-      double g0 = d.G[r * GS + lane], g1 = d.G[(r + 1) * GS + lane], g2 = d.G[(r + 2) * GS + lane],
-             g3 = d.G[(r + 3) * GS + lane];
+      double g0 = d.G[r * GS + i], g1 = d.G[(r + 1) * GS + i], g2 = d.G[(r + 2) * GS + i],
+             g3 = d.G[(r + 3) * GS + i];
       double f0 = d.efc_f[r], f1 = d.efc_f[r + 1], f2 = d.efc_f[r + 2], f3 = d.efc_f[r + 3];
       s = __builtin_fma(g0, f0, s);
       s = __builtin_fma(g1, f1, s);
       s = __builtin_fma(g2, f2, s);
       s = __builtin_fma(g3, f3, s);
     }
-    for (; r < ne; r++) s = __builtin_fma(d.G[r * GS + lane], d.efc_f[r], s);
-    u = s;
+    for (; r < ne; r++) s = __builtin_fma(d.G[r * GS + i], d.efc_f[r], s);
+    u.v[h] = s;
   }
 }
 
@@ -4738,7 +4907,7 @@ DEVI void solve(const Mdl& md, Dat& d) {
   // mean diagonal of M at qpos0 (mj_setConst), a model constant
   double scale = 1.0 / (md.m.meaninertia * (double)(nv > 1 ? nv : 1));
   Frc F;
-  double u;
+  DofV u;
   if (md.m.solver == 0) {
     contact_blocks(md, d);
     solve_pgs(md, d, scale, F, u);
@@ -4747,7 +4916,7 @@ DEVI void solve(const Mdl& md, Dat& d) {
     if (md.m.noslip_iterations > 0) contact_blocks(md, d);   // overwrites the cone Hessians
   }
   PT(16);
-  double u_main = u;
+  const DofV u_main = u;
   noslip(md, d, scale, F, u);
   PT(17);
   finalize_solution<NV>(md, d, u_main, u);
@@ -4799,7 +4968,11 @@ DEVI void forward_rows(const Mdl& md, Dat& d) {
   actuation(md, d);
   passive(md, d);
   rne(md, d);
-  if (lane < nv) d.qfrc_smooth[lane] = (d.qfrc_passive[lane] - d.qfrc_bias[lane]) + d.qfrc_actuator[lane];
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;
+    if (i < nv) d.qfrc_smooth[i] = (d.qfrc_passive[i] - d.qfrc_bias[i]) + d.qfrc_actuator[i];
+  }
   wsync();
   ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
   make_constraints<NV>(md, d);
@@ -4835,8 +5008,12 @@ DEVI void integrate(const Mdl& md, Dat& d) {
   PT(19);
   // M - dt * qDeriv, lane i forms row i of qDeriv (-damping on the diagonal,
   // then each active affine actuator's mom_i (mom_j dv) in actuator order) and
-  // applies it straight to M (the oracle's element expressions)
-  if (lane < nv) {
+  // applies it straight to M (the oracle's element expressions); with two
+  // dofs per lane, row lane then row lane + 64
+#pragma unroll
+  for (int h = 0; h < MGS_DPL; h++) {
+    const int i = lane + h * WAVE;   // this slot's row
+    if (i >= nv) continue;
     const double* damp = DA(md, dof_damping);
     const int32_t *gtype = IA(md, actuator_gaintype), *btype = IA(md, actuator_biastype);
     const int32_t* flim = IA(md, actuator_forcelimited);
@@ -4844,7 +5021,7 @@ DEVI void integrate(const Mdl& md, Dat& d) {
     const double* frange = DA(md, actuator_forcerange);
     double q[NV];
 #pragma unroll
-    for (int j = 0; j < NV; j++) q[j] = (j == lane) ? -damp[lane] : 0.0;
+    for (int j = 0; j < NV; j++) q[j] = (j == i) ? -damp[i] : 0.0;
     for (int u = 0; u < md.m.nu; u++) {
       double f = d.act_force[u];
       if (flim[u] && (f <= frange[2 * u] || f >= frange[2 * u + 1])) continue;
@@ -4857,14 +5034,14 @@ DEVI void integrate(const Mdl& md, Dat& d) {
 #else
       const double* mom = d.act_moment + u * nv;
 #endif
-      double mi = mom[lane];
+      double mi = mom[i];
       if (mi == 0.0) continue;
 #pragma unroll
       for (int j = 0; j < NV; j++) q[j] = q[j] + mi * (mom[j] * dv);
     }
 #pragma unroll
     for (int j = 0; j < NV; j++)
-      if (!MGS_PACKED || j <= lane) d.M[TRI(lane, j, NV)] = d.M[TRI(lane, j, NV)] - dt * q[j];
+      if (!MGS_PACKED || j <= i) d.M[TRI(i, j, NV)] = d.M[TRI(i, j, NV)] - dt * q[j];
   }
   wsync();
   PT(20);
@@ -5266,7 +5443,11 @@ DEVI void rollout_one(const Mdl& md, double* smem, const Lay& lay, const mgs_sch
       wsync(); PT(34);
       rne(md, d);
       PT(35);
-      if (lane < md.m.nv) d.qfrc_smooth[lane] = (d.qfrc_passive[lane] - d.qfrc_bias[lane]) + d.qfrc_actuator[lane];
+#pragma unroll
+      for (int h = 0; h < MGS_DPL; h++) {
+        const int i = lane + h * WAVE;
+        if (i < md.m.nv) d.qfrc_smooth[i] = (d.qfrc_passive[i] - d.qfrc_bias[i]) + d.qfrc_actuator[i];
+      }
       wsync();
       ldl_solve<NV>(d.M, d.Dinv, d.qfrc_smooth, d.qacc_smooth);
       PT(8);

@@ -10,7 +10,8 @@
 // The kernels are the rollout / collision kernels of mgs_kernels.hip
 // instantiated at the model's dof count with SL = 1 (every LDS view and every
 // model size / table offset a compile-time constant).  Any dof count up to 64
-// can be specialised, so models the library has no instantiation for (clutter
+// can be specialised, and up to 128 with two dofs per lane (-DMGS_DPL=2, the
+// wide flavour), so models the library has no instantiation for (clutter
 // piles of any size, other grippers) run through these objects.
 #include <hip/hip_runtime.h>
 
@@ -45,6 +46,8 @@ extern "C" {
 __device__ int mgs_special_abi = MGS_ABI_VERSION;
 __device__ int mgs_special_rows_per_lane = MGS_RPL;
 __device__ int mgs_special_maxdim = MGS_MAXDIM;
+__device__ int mgs_special_max_nv = MGS_MAXNV;   // 64, or 128 with two dofs per lane (-DMGS_DPL=2)
+static_assert(MGS_SL_NV <= MGS_MAXNV, "a model of more than 64 dofs is specialised with -DMGS_DPL=2");
 __device__ mgs_model_desc mgs_special_desc = mgs_sl_desc;
 __device__ int mgs_special_words[L_COUNT + U_COUNT + 4] = MGS_SL_WORDS_INIT;
 

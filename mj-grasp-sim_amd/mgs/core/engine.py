@@ -100,6 +100,10 @@ def load_library(wide: bool = False):
 # chip) serves dof counts up to this; larger ones use the wide flavour (4 rows
 # per lane, G in HBM), instantiated or specialised (mgs.core.special)
 MAIN_NV_MAX = 34
+# largest dof count: 64 with one dof per lane (the libraries' kernels and most
+# specialised objects), 128 with two (specialised objects of the wide flavour,
+# mgs.core.special; clutter piles of 7-10 objects)
+MAX_NV = 128
 
 
 def library_for(nv: int, nefc_max: int):
@@ -107,8 +111,8 @@ def library_for(nv: int, nefc_max: int):
     when it has a kernel for nv, or nv is small enough for its flavour, and the
     rows fit; else the wide one.  A dof count without an instantiation in the
     chosen library runs through a specialised code object."""
-    if nv < 1 or nv > 64:
-        raise EngineError(f"nv={nv}: the kernels hold 1 to 64 dofs (lanes over dofs)")
+    if nv < 1 or nv > MAX_NV:
+        raise EngineError(f"nv={nv}: the kernels hold 1 to {MAX_NV} dofs (lanes over dofs, two per lane past 64)")
     L = load_library()
     if nefc_max <= L.mgs_max_rows() and (L.mgs_supports_nv(nv) or nv <= MAIN_NV_MAX):
         return L

@@ -1211,8 +1211,9 @@ class CompiledModel:
         return mom
 
     def body_dofmask(self):
-        """(nbody, 2) int32 bit masks of the dofs on each body's chain to the root."""
-        m = np.zeros((self.nbody, 2), np.uint32)
+        """(nbody, W) int32 bit masks of the dofs on each body's chain to the root:
+        W = 2 words (dofs 0-63), 4 for models of more than 64 dofs (mgs_gpu.h)"""
+        m = np.zeros((self.nbody, 4 if self.nv > 64 else 2), np.uint32)
         for b in range(self.nbody):
             d = int(self.body_lastdof[b])
             while d >= 0:

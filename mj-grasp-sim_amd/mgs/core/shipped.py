@@ -11,7 +11,9 @@ compiles ahead of time (mgs/core/special.py), and the pile scenes they use.
     tests/golden/clutter_scene_shadow.npz when present, else the pile as
     built);
   * the spread piles of 3 and 4 objects the GPU tests run (nv 32, a dof count
-    no library instantiates).
+    no library instantiates);
+  * the Shadow Hand over spread piles of 7 and 10 objects (nv 70 and 88: two
+    dofs per lane, -DMGS_DPL=2).
 
 Nothing here imports the test tree or pytest.
 """
@@ -27,6 +29,13 @@ import numpy as np
 PILE_OBJECTS = ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange", "061_foam_brick"]
 SPREAD_PILES = [("Robotiq2f85Gripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can"]),
                 ("PandaGripper", ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange"])]
+
+# piles past 64 dofs (tests/test_pile_wide.py): the Shadow Hand over 7 and 10
+# objects drawn with repetition, as the reference draws its pile sizes
+# (mgs/obj/selector.py:124-130)
+WIDE_PILE_OBJECTS = ["010_potted_meat_can", "061_foam_brick", "005_tomato_soup_can", "017_orange", "061_foam_brick",
+                     "010_potted_meat_can", "017_orange", "005_tomato_soup_can", "061_foam_brick", "017_orange"]
+WIDE_PILES = [("ShadowHand", WIDE_PILE_OBJECTS[:7]), ("ShadowHand", WIDE_PILE_OBJECTS[:10])]
 
 # the dexee x YCB configuration (condim-6 fingertips, mujoco.pid actuators;
 # tests/test_dexee.py)
@@ -99,7 +108,7 @@ def shipped_engines() -> List[Tuple[object, int, object, str]]:
     env = pile_env("ShadowHand")
     if os.path.isfile(C5_SCENE):
         env.set_state(np.load(C5_SCENE)["state"])
-    scenes = [env] + [spread_pile(g, objs) for g, objs in SPREAD_PILES]
+    scenes = [env] + [spread_pile(g, objs) for g, objs in SPREAD_PILES + WIDE_PILES]
     for env in scenes:
         cm = env.model_for(env.get_state())
         out.append((cm, env.ncon_max, env.rows_for(cm, env.ncon_max), "main"))

@@ -128,16 +128,17 @@ class ClutterTableEnv:
         self._engines = {}
 
     def _check_kernel(self, nv):
-        """the kernels hold up to 64 dofs (lanes over dofs): dof counts the
-        libraries instantiate run directly, any other through a model-specialised
-        code object (mgs.core.special, compiled on first use); fail here, with
-        the largest pile, rather than at the first simulation"""
-        if nv > 64:
+        """the kernels hold up to 128 dofs (lanes over dofs: one per lane up to
+        64, two per lane beyond, in a model-specialised code object compiled on
+        first use, mgs.core.special); fail here, with the largest pile, rather
+        than at the first simulation"""
+        from mgs.core.engine import MAX_NV
+        if nv > MAX_NV:
             g = self._gripper_nv
             raise ValueError(
                 f"no GPU kernel for this scene: {len(self.objects) - len(self.removed)} free objects with this "
-                f"gripper give nv={nv}; the kernels hold at most 64 dofs, i.e. piles of at most {(64 - g) // 6} "
-                f"free objects for this gripper")
+                f"gripper give nv={nv}; the kernels hold at most {MAX_NV} dofs, i.e. piles of at most "
+                f"{(MAX_NV - g) // 6} free objects for this gripper")
 
     # -- state vector (mjSTATE_INTEGRATION of the reference model) ------------
     def _sizes(self):

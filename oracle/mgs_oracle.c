@@ -2487,7 +2487,8 @@ static void solve_newton(const Mdl* md, Dat* d) {
     r += dim;
   }
   /* whitened smooth and warmstart accelerations: W(a)_i = sD_i (a_i + sum_{k>i} L_ki a_k) */
-  double w0[64], w[64], g[64], dir[64], H[64 * 64], HL[64 * 64], HDinv[64], HDv[64];
+  double w0[MGS_MAX_NV], w[MGS_MAX_NV], g[MGS_MAX_NV], dir[MGS_MAX_NV], HDinv[MGS_MAX_NV], HDv[MGS_MAX_NV];
+  static __thread double H[MGS_MAX_NV * MGS_MAX_NV], HL[MGS_MAX_NV * MGS_MAX_NV];   /* 2 x 128 KB: per thread, off the stack */
   for (int i = 0; i < nv; i++) {
     double s = d->qacc_smooth[i], s2 = d->qacc_ws[i];
     for (int k = i + 1; k < nv; k++) s = fma(d->L[k * nv + i], d->qacc_smooth[k], s);
@@ -2552,7 +2553,7 @@ static void solve_newton(const Mdl* md, Dat* d) {
       for (int k = 0; k < nv; k++) s = fma(Gr[k], dir[k], s);
       d->efc_jv[r] = s;
     }
-    double q[64];
+    double q[MGS_MAX_NV];
     for (int k = 0; k < nv; k++) q[k] = w[k] - w0[k];
     double A1 = tree_dot(q, dir, nv);
     double A2 = tree_dot(dir, dir, nv);

@@ -165,19 +165,19 @@ def test_eval_grasps_cli(cenv, ccand, tmp_path, monkeypatch):
 
 
 def test_oversized_pile_fails_clearly():
-    """the kernels hold at most 64 dofs (any count up to that runs, through a
-    specialised code object where the libraries have no instantiation); a pile
-    beyond it is refused when the env is built, with the largest pile size in
-    the message (not at the first simulation)"""
+    """the kernels hold at most 128 dofs (any count up to that runs, through a
+    specialised code object where the libraries have no instantiation, two
+    dofs per lane past 64); a pile beyond it is refused when the env is built,
+    with the largest pile size in the message (not at the first simulation)"""
     from mgs.env.clutter_table import ClutterTableEnv
     from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
     from mgs.obj.selector import get_object
     from mgs.util.geo.transforms import SE3Pose
     grip = GripperRobotiq2f85(SE3Pose(np.array([5.0, 5.0, 1.0]), np.array([1.0, 0, 0, 0]), "wxyz"))
-    objs = [get_object("003_cracker_box") for _ in range(9)]
+    objs = [get_object("003_cracker_box") for _ in range(20)]
     for i, o in enumerate(objs):
         o.name = f"o{i}"
-    with pytest.raises(ValueError, match="piles of at most 8 free objects"):
+    with pytest.raises(ValueError, match="piles of at most 19 free objects"):
         ClutterTableEnv(grip, objs)
 
 

@@ -243,7 +243,7 @@ def test_gen_scene_cli(tmp_path, monkeypatch):
 def test_gen_scene_refuses_oversized_pile_before_any_compile(monkeypatch):
     """the reference draws pile sizes at random (mgs/obj/selector.py:124-130;
     num_objects overrides it, cli/config/gen_scene.yaml:10); the kernels hold
-    at most 64 dofs, so gen_scene refuses a Shadow pile of 7 with the limit in
+    at most 128 dofs, so gen_scene refuses a Shadow pile of 17 with the limit in
     the message, from the model sizes alone: no code object is compiled and
     nothing is simulated"""
     from mgs.cli import gen_scene
@@ -253,6 +253,6 @@ def test_gen_scene_refuses_oversized_pile_before_any_compile(monkeypatch):
     def no_compile(*a, **k):
         raise AssertionError("a code object was compiled")
     monkeypatch.setattr(special, "compile_object", no_compile)
-    cfg = compose("gen_scene", ["num_objects=7", "gripper=shadow"])
-    with pytest.raises(ValueError, match=r"nv=\d+; the kernels hold at most 64 dofs, i.e. piles of at most \d free"):
+    cfg = compose("gen_scene", ["num_objects=17", "gripper=shadow"])
+    with pytest.raises(ValueError, match=r"nv=\d+; the kernels hold at most 128 dofs, i.e. piles of at most 16 free"):
         gen_scene.gen_stable_scene(cfg, rng=0)
