@@ -111,11 +111,15 @@ static_assert(MGS_MAXDIM == 4 || MGS_MAXDIM == 6, "MGS_MAXDIM is 4 or 6");
 #ifndef MGS_RPL
 #define MGS_RPL 2   // constraint rows per lane (nefc_max <= 64 * MGS_RPL)
 #endif
-// NV-long operand rows of the triangular solves / G products held in registers
-// (main build) or read from LDS at each use (wide build: nv up to 58 would
-// spill them to scratch).  Same values either way.
+// NV-long operand rows of the factor, the triangular solves and the G
+// products held in registers, or read from LDS at each use.  Registers in
+// every build of one dof per lane: the wide flavour's pile objects (nv 38-58,
+// one wave per SIMD) hold them in 424 VGPRs without spilling, and the C5 pile
+// rollout runs 6 % faster for it (round 5, profiles/r05w_c5_register_rows_ab.txt);
+// with two dofs per lane (MGS_DPL 2) each lane has two rows: LDS.  Same values
+// either way.
 #ifndef MGS_REG_ROWS
-#ifdef MGS_WIDE
+#if defined(MGS_DPL) && MGS_DPL > 1
 #define MGS_REG_ROWS 0
 #else
 #define MGS_REG_ROWS 1
@@ -799,8 +803,8 @@ DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
     }
   }
 }
-// The same factor without register rows (wide build, nv 38-58, where NV-long
-// register rows spill): left-looking, lane i keeps row i in LDS; column c of
+// The same factor without register rows (two dofs per lane, nv 65-128):
+// left-looking, lane i keeps row i in LDS; column c of
 // every row takes sum_{k<c} l_ik (l_ck d_k) in ascending k -- the products and
 // order of the right-looking loop above, so the factor is bit-identical.  The
 // l_ck d_k are parked in the (dead) upper triangle, V[c][k] at A[k][c].  The

@@ -1,6 +1,8 @@
 """Build the headline engine's specialised code object from the working tree's
 kernel sources into mj-grasp-sim_amd/mgs/_lib/ab/<name>.hsaco (A/B experiments,
-tools/ab_special.sh).  Usage: python tools/ab_build.py name [-DFLAG ...]"""
+tools/ab_special.sh).  Usage: python tools/ab_build.py name [-DFLAG ...]
+(name starting with "c5": the C5 pile engine's object instead, for the
+c5ab:<names> step of tools/gpu.sh)"""
 import os
 import sys
 
@@ -16,10 +18,18 @@ def main():
     from mgs.gripper.robotiq2f85 import GripperRobotiq2f85
     from mgs.obj.selector import get_object
     from mgs.util.geo.transforms import SE3Pose
-    env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
-                                    get_object("003_cracker_box"))
-    fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
-    lib = library_for(env.model.nv, int(fields["nefc_max"]))
+    if sys.argv[1].startswith("c5"):
+        from mgs.core.shipped import C5_SCENE, pile_env
+        env = pile_env("ShadowHand")
+        env.set_state(np.load(C5_SCENE)["state"])
+        cm = env.model_for(env.get_state())
+        fields, _, _ = cm.pack(ncon_max=env.ncon_max, nefc_max=env.rows_for(cm, env.ncon_max))
+        lib = library_for(cm.nv, int(fields["nefc_max"]))
+    else:
+        env = GravitylessObjectGrasping(GripperRobotiq2f85(SE3Pose(np.zeros(3), np.array([1.0, 0, 0, 0]), "wxyz")),
+                                        get_object("003_cracker_box"))
+        fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
+        lib = library_for(env.model.nv, int(fields["nefc_max"]))
     header, flags, _ = special.plan(lib, abi.make_desc(fields))
     out = os.path.join(special.CACHE, "..", "ab")
     os.makedirs(out, exist_ok=True)
