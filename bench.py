@@ -551,6 +551,10 @@ def main():
     if args.e2e_yield is not None:
         env.YIELD_EVERY = args.e2e_yield
     if args.e2e_steps > 0:
+        # the env's engines are created once per env (as a CLI run creates them
+        # once): one untimed call builds the small-call engine
+        # (GravitylessObjectGrasping.engine_for_rollouts) before the timed ones
+        e2e_api(env, poses, J, h, 1)
         m2, l2, t2 = e2e_api(env, poses, J, h, args.e2e_steps)
         large = None
         if args.e2e_large > 1:
@@ -571,7 +575,9 @@ def main():
                "what": "env.grasp_collision_mask + grasp_stability_evaluation_from_joints on host arrays "
                        "(filter_to_stable.py:39-50 call pattern): host SE3 processing, schedule, PCIe "
                        "copies and the host round trip between mask and rollout included; per rank, "
-                       "median over batches"}
+                       "median over batches after one untimed call",
+               "rollout_engine": ("G rows in LDS" if env.engine_for_rollouts(int(free.sum())) is not env.engine
+                                  else "G rows in HBM" if int(env.engine.desc.g_rows_hbm) else "G rows in LDS")}
     shard_check = None
     if world > 1 and args.shard_check:
         # the global candidate set is the concatenation of the

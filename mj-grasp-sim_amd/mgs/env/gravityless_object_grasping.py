@@ -171,11 +171,44 @@ class GravitylessObjectGrasping:
     # the horizon is its own launch (pause_step); the default is one launch
     SLICES = 1
 
+    # A call of a few rollouts (the stability call of filter_to_stable: the
+    # collision-free part of one candidate file) is one round of them, i.e. its
+    # heaviest rollout's latency.  The G-rows-in-LDS object (four per CU) steps
+    # faster than the eight-per-CU one that holds the throughput: it finishes
+    # calls of up to about 1.5 x its resident grid sooner (1173 rollouts: 58.2
+    # vs 61.6 ms; 2048: 68.1 vs 63.9; profiles/r05l_latency_engine.txt).
+    # Same results bit for bit (both objects are the oracle's arithmetic).
+    LATENCY_ROUNDS = 1.5
+
+    @property
+    def latency_engine(self):
+        """the main capacity's G-rows-in-LDS engine when the main engine keeps
+        its rows in HBM and that object is cached, else None"""
+        main = self.engine
+        # (keyed by the main engine: a copied env with a rebuilt engine builds its own)
+        if getattr(self, "_latency_for", None) is not main:
+            self._latency_for, self._latency_engine = main, None
+            if int(main.desc.g_rows_hbm):
+                from mgs.core.engine import Engine
+                e = Engine(self.model, device=self.device, ncon_max=self.ncon_max, nefc_max=self.nefc_max,
+                           g_rows_hbm=False, specialize="cached")
+                self._latency_engine = e if e.specialized() else None
+        return self._latency_engine
+
+    def engine_for_rollouts(self, n: int):
+        """the engine a rollout call of n candidates runs on (LATENCY_ROUNDS)"""
+        le = self.latency_engine
+        if le is not None and 0 < n <= self.LATENCY_ROUNDS * le.rollout_grid(n):
+            return le
+        return self.engine
+
     def rollout(self, plan: "RolloutPlan", max_ncon: int = 40, slices: Optional[int] = None,
                 yield_every: Optional[int] = None):
         """engine.rollout with capacity escalation, in-launch rotation and
-        optional time slices by relaunch (sliced_rollout below)."""
-        return sliced_rollout(plan, self.engine, self.engine_for, self.ncon_max, max_ncon,
+        optional time slices by relaunch (sliced_rollout below), on the engine
+        that finishes a call of this size first (engine_for_rollouts)."""
+        return sliced_rollout(plan, self.engine_for_rollouts(len(plan.qpos_init)), self.engine_for, self.ncon_max,
+                              max_ncon,
                               self.SLICES if slices is None else slices,
                               yield_every=self.YIELD_EVERY if yield_every is None else yield_every)
 

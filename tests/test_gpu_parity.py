@@ -809,3 +809,26 @@ def test_queue_spans_device_clock(env, candidates):
     assert len(s) == 1
     assert 0.0 < s[0] <= r["kernel_ms"] * 1.05 + 0.05     # inside the HIP events around the launch
     assert eng.queue_spans() == []
+
+
+@pytest.mark.gpu
+def test_small_rollout_calls_take_the_latency_engine(env, candidates):
+    """a rollout call of at most LATENCY_ROUNDS x the G-rows-in-LDS engine's
+    resident grid runs on that engine (shorter steps: one round of rollouts
+    ends sooner), a larger one on the eight-per-CU main engine; both give the
+    oracle's results bit for bit, so the env's answer does not depend on the
+    choice"""
+    from conftest import plan_for
+    from mgs.env.gravityless_object_grasping import sliced_rollout
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    idx = np.nonzero(env.engine.collision_free(q, mp, mq))[0][:48]
+    plan = plan_for(env, poses[idx], J[idx])
+    le = env.latency_engine
+    assert int(env.engine.desc.g_rows_hbm) and le is not None and not int(le.desc.g_rows_hbm)
+    assert env.engine_for_rollouts(len(idx)) is le
+    big = int(env.LATENCY_ROUNDS * le.rollout_grid(4096)) + 1
+    assert env.engine_for_rollouts(big) is env.engine
+    r_small = env.rollout(plan)
+    r_main = sliced_rollout(plan, env.engine, env.engine_for, env.ncon_max, 40, 1, yield_every=env.YIELD_EVERY)
+    _assert_same(r_small, r_main, "latency engine vs main engine")
