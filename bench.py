@@ -257,7 +257,7 @@ def main():
                     help="N > 1: skip rank 0's single-GPU re-evaluation of every rank's block")
     ap.add_argument("--e2e-large", type=int, default=8,
                     help="also time the drop-in API on the batch repeated this many times in one call (0 = skip)")
-    ap.add_argument("--e2e-steps", type=int, default=2,
+    ap.add_argument("--e2e-steps", type=int, default=5,
                     help="batches timed through the drop-in env API on host arrays (0 = skip)")
     ap.add_argument("--e2e-slices", type=int, default=None,
                     help="time slices by relaunch of the env API's rollout calls (default: the env's SLICES)")

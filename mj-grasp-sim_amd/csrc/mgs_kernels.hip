@@ -781,6 +781,13 @@ DEVI void crb(const Mdl& md, Dat& d) {
 // NV: the model's dof count as a compile-time constant (kernels are
 // instantiated per supported nv, see MGS_NV_LIST in mgs_capi.hip), so the
 // register rows and their loops are fully static.
+// column broadcasts of the register factor through LDS (1) or v_readlane (0);
+// default (-1): LDS up to 32 dofs, where it measured faster (the headline
+// +1.2 %, profiles/r05b_ldl_broadcast_ab.txt), v_readlane above (at nv 58
+// the LDS form's loads are hoisted into 9 k VGPR spills: C5 -20 %)
+#ifndef MGS_LDL_LDS_BCAST
+#define MGS_LDL_LDS_BCAST -1
+#endif
 template <int NV>
 DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
   // right-looking: after pivot j is scaled, every later column c takes its
@@ -796,10 +803,22 @@ DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
     if (lane > j) r[j] = r[j] * inv;
     if (lane == 0) { Dv[j] = dj; Dinv[j] = inv; }
     double v = r[j] * dj;   // lane c: l_cj d_j
+    if constexpr (MGS_LDL_LDS_BCAST > 0 || (MGS_LDL_LDS_BCAST < 0 && NV <= 32)) {
+      // the column's l_cj d_j to every lane through LDS: lane c parks it in
+      // Dv[c], a slot column c itself writes later (the wave's LDS operations
+      // complete in order), and every lane reads them at uniform addresses --
+      // no SGPR per broadcast (the readlane form spills them)
+      if (lane > j && lane < NV) Dv[lane] = v;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
-    for (int c = j + 1; c < NV; c++) {
-      double w = readlane_d(v, c);
-      r[c] = __builtin_fma(-r[j], w, r[c]);
+      for (int c = j + 1; c < NV; c++) r[c] = __builtin_fma(-r[j], Dv[c], r[c]);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    } else {
+#pragma unroll
+      for (int c = j + 1; c < NV; c++) {
+        double w = readlane_d(v, c);
+        r[c] = __builtin_fma(-r[j], w, r[c]);
+      }
     }
   }
 }
