@@ -177,7 +177,7 @@ class GravitylessObjectGrasping:
     # faster than the eight-per-CU one that holds the throughput: it finishes
     # calls of up to about 1.25-1.5 x its resident grid sooner (1173 rollouts:
     # 58.4 vs 59.5 ms; 1536: 61.2 vs 59.9; 2048: 68.7 vs 61.7;
-    # profiles/r05l_latency_engine.txt, r05c2).  Same results bit for bit
+    # profiles/r05lat_latency_engine.txt).  Same results bit for bit
     # (both objects are the oracle's arithmetic).
     LATENCY_ROUNDS = 1.25
 
