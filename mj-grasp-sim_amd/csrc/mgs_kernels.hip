@@ -782,9 +782,11 @@ DEVI void crb(const Mdl& md, Dat& d) {
 // instantiated per supported nv, see MGS_NV_LIST in mgs_capi.hip), so the
 // register rows and their loops are fully static.
 // column broadcasts of the register factor through LDS (1) or v_readlane (0);
-// default (-1): LDS up to 32 dofs, where it measured faster (the headline
-// +1.2 %, profiles/r05b_ldl_broadcast_ab.txt), v_readlane above (at nv 58
-// the LDS form's loads are hoisted into 9 k VGPR spills: C5 -20 %)
+// default (-1): LDS up to 20 dofs, where it measured faster (the headline
+// +1.2 %, profiles/r05b_ldl_broadcast_ab.txt), v_readlane above: the LDS
+// form's unrolled loads are hoisted into registers, and past 20 dofs that
+// spills (nv 28 under the 256-register cap: 94 -> 1305 VGPR spills, C4 -21 %;
+// nv 58: 9 k, C5 -20 %)
 #ifndef MGS_LDL_LDS_BCAST
 #define MGS_LDL_LDS_BCAST -1
 #endif
@@ -803,7 +805,7 @@ DEVI void ldl_factor_regs(double (&r)[NV], double* Dv, double* Dinv) {
     if (lane > j) r[j] = r[j] * inv;
     if (lane == 0) { Dv[j] = dj; Dinv[j] = inv; }
     double v = r[j] * dj;   // lane c: l_cj d_j
-    if constexpr (MGS_LDL_LDS_BCAST > 0 || (MGS_LDL_LDS_BCAST < 0 && NV <= 32)) {
+    if constexpr (MGS_LDL_LDS_BCAST > 0 || (MGS_LDL_LDS_BCAST < 0 && NV <= 20)) {
       // the column's l_cj d_j to every lane through LDS: lane c parks it in
       // Dv[c], a slot column c itself writes later (the wave's LDS operations
       // complete in order), and every lane reads them at uniform addresses --
