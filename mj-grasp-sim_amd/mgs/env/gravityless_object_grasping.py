@@ -194,12 +194,15 @@ class GravitylessObjectGrasping:
                 e = Engine(self.model, device=self.device, ncon_max=self.ncon_max, nefc_max=self.nefc_max,
                            g_rows_hbm=False, specialize="cached")
                 self._latency_engine = e if e.specialized() else None
+                # its resident grid, once (a launch larger than the grid runs the
+                # work queue, whose grid is the device's resident capacity)
+                self._latency_grid = e.rollout_grid(4096) if self._latency_engine else 0
         return self._latency_engine
 
     def engine_for_rollouts(self, n: int):
         """the engine a rollout call of n candidates runs on (LATENCY_ROUNDS)"""
         le = self.latency_engine
-        if le is not None and 0 < n <= self.LATENCY_ROUNDS * le.rollout_grid(n):
+        if le is not None and 0 < n <= self.LATENCY_ROUNDS * self._latency_grid:
             return le
         return self.engine
 
