@@ -527,7 +527,13 @@ def main():
     # the timed main launches' execution spans on the device clock (first
     # candidate taken -> last workgroup out, mgs_queue_spans): what a kernel
     # trace reports as their durations, without a profiler attached
-    spans = [x for p in pipes for x in p.eng.queue_spans()]
+    spans, spans_lost = [], 0
+    for p in pipes:
+        spans += p.eng.queue_spans()
+        spans_lost += p.eng.spans_overwritten
+    if spans_lost:
+        print(f"bench: {spans_lost} timed launch span(s) overwritten before they were read (more than 64 "
+              "launches per pipeline); launch_ms averages the rest", file=sys.stderr)
     t = torch.tensor([dt], dtype=torch.float64, device="cpu" if shared else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -661,7 +667,7 @@ def main():
                      "algorithmic_bytes_per_launch": alg,
                      "launch_ms": launch_ms,
                      "launch_ms_device_span": span_avg,
-                     "launch_spans_measured": len(spans),
+                     "launch_spans_measured": len(spans), "launch_spans_overwritten": spans_lost,
                      "launch_ms_hip_events": roll_avg,
                      "launches_in_flight": len(pipes),
                      "achieved_device": achieved_device,

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MGS_ABI_VERSION 22
+#define MGS_ABI_VERSION 23
 #define MGS_NSTATS 6
 /* largest dof count: 64 for the libraries' kernels (one dof per lane), 128
    for model-specialised code objects (two dofs per lane, ABI 22) */
@@ -102,9 +102,27 @@ extern "C" {
  * lost -- never in a correct run; callers of the device entries treat it as an error. */
 #define MGS_FAIL_YIELDED (-5)
 
-/* narrowphase of a geom pair (pair_kind) */
-#define MGS_PAIR_CONVEX 0          /* general convex path: MPR + feature clipping (mjc_Convex role) */
+/* narrowphase of a geom pair (pair_kind).  With ccd_mode 0 only the first two
+ * occur; with ccd_mode 1 / 2 the pairs follow MuJoCo 3.2.2's collision table
+ * (engine_collision_driver.c mjCOLLISIONFUNC; geom1 has the smaller MuJoCo geom
+ * type, as mj_collideGeoms orders them; ABI 23) */
+#define MGS_PAIR_CONVEX 0          /* mjc_Convex: MPR (ccd_mode 0: + feature clipping; 1: + multiccd) */
 #define MGS_PAIR_BOXBOX 1          /* box-box separating-axis collider (mjc_BoxBox role) */
+#define MGS_PAIR_CONVEX_SMOOTH 2   /* mjc_Convex with a sphere in the pair: one MPR contact (no multiccd) */
+#define MGS_PAIR_SPHERE_SPHERE 3   /* mjc_SphereSphere  (1 contact) */
+#define MGS_PAIR_SPHERE_CAPSULE 4  /* mjc_SphereCapsule (1) */
+#define MGS_PAIR_CAPSULE_CAPSULE 5 /* mjc_CapsuleCapsule (1; 2 for parallel axes) */
+#define MGS_PAIR_SPHERE_BOX 6      /* mjc_SphereBox (1) */
+#define MGS_PAIR_CAPSULE_BOX 7     /* mjc_CapsuleBox (1 or 2) */
+#define MGS_PAIR_SPHERE_CYLINDER 8 /* mjc_SphereCylinder (1) */
+
+/* ccd_mode: how convex pairs make contacts */
+#define MGS_CCD_R5 0               /* round 5's contract: MPR + face clipping (<= 4 points), rounded geoms
+                                      as hull (+) ball (kept for the contact-set study) */
+#define MGS_CCD_MULTI 1            /* MuJoCo 3.2.2 restated: libccd's MPR penetration (point-triangle
+                                      depth, tetrahedron barycentre position) + multiccd (4 perturbed
+                                      MPRs, <= 5 contacts); analytic primitive colliders */
+#define MGS_CCD_SINGLE 2           /* the same without the multiccd flag: one MPR contact per pair */
 
 /* predicate for the collision pre-filter */
 #define MGS_PRED_ANY_CONTACT 0     /* data.ncon != 0            (gravityless :306-307) */
@@ -129,6 +147,7 @@ typedef struct mgs_model_desc {
   int32_t nu;
   int32_t nmocap;
   int32_t nact;       /* actuator state (mjData.act) entries: 2 per mujoco.pid actuator (ABI 21) */
+  int32_t npid;       /* mujoco.pid actuators (MGS_GAIN_PID), with or without act entries (ABI 23) */
   int32_t maxcondim;  /* largest contact dimension of the admissible pairs: 1, 3, 4 or 6 (condim 6:
                          torsional and rolling friction; runs through a specialised code object) */
   int32_t g_rows_hbm; /* 1: the whitened constraint rows G of each candidate live in a batch-owned
@@ -145,6 +164,8 @@ typedef struct mgs_model_desc {
   int32_t integrator; /* 2 = implicitfast (the only integrator supported) */
   int32_t solver;     /* MuJoCo mjtSolver numbering: 0 = PGS, 2 = Newton (MuJoCo's default) */
   int32_t ls_iterations;
+  int32_t ccd_mode;       /* MGS_CCD_*: the collision table and the convex pairs' contacts (ABI 23) */
+  int32_t ccd_iterations; /* MuJoCo opt.ccd_iterations (50): MPR penetration refinement cap */
   double ls_tolerance;
   double timestep;
   double impratio;
@@ -220,6 +241,8 @@ typedef struct mgs_model_desc {
                                18).  A cylinder's supports and contact features are the exact
                                ones; its hull, a 16-sided prism inscribed in it (rim vertices
                                on the true circle), serves the broadphase and the cap polygon */
+  int32_t d_geom_size;      /* 3: MuJoCo geom_size (sphere r; capsule r, half-length; box half sizes;
+                               cylinder r, half-height): the analytic colliders (ABI 23) */
   /* convex hulls */
   int32_t i_hull_vertadr;
   int32_t i_hull_vertnum;
@@ -230,8 +253,7 @@ typedef struct mgs_model_desc {
   int32_t i_pair_geom1;
   int32_t i_pair_geom2;
   int32_t i_pair_condim;
-  int32_t i_pair_kind;      /* MGS_PAIR_CONVEX (MPR + feature clipping) or MGS_PAIR_BOXBOX
-                               (separating-axis box collider; MuJoCo's mjc_BoxBox role) */
+  int32_t i_pair_kind;      /* MGS_PAIR_*: the pair's collider (see above) */
   int32_t d_pair_friction;  /* 5 */
   int32_t d_pair_solref;    /* 2 */
   int32_t d_pair_solimp;    /* 5 */
@@ -488,6 +510,10 @@ int mgs_mask_rollout_device(mgs_batch* batch, const mgs_schedule* sched, int n, 
  * that grid (n if n is smaller, or in mode 0 of mgs_rollout_queue: one
  * workgroup per candidate); needs the device. */
 int mgs_rollout_grid(mgs_batch* batch, int n);
+/* The rollout workgroups the device holds at once for this model (occupancy
+ * at its LDS size x CUs; -1 if unknown), the grid of a work-queue launch in
+ * mode 1, without opening a batch (ABI 23). */
+int mgs_model_resident(mgs_model* model);
 /* In-launch rotation counters of a batch (ABI 19), cumulative over its
  * launches: out[0] yields (a candidate handed its slot to a waiting one),
  * out[1] expired ring spins (0 unless the rotation protocol is broken; see
@@ -505,10 +531,11 @@ int mgs_queue_stats(mgs_batch* batch, uint64_t* out);
  * launch's queue header.  Writes up to cap spans (ms) of the launches completed
  * since the previous call, in queue-slot order (the slots cycle through 64
  * headers, so call at least every 64 launches), sets *count, and clears the
- * spans it returned.  Synchronises the device.  (bench.py: the per-launch
+ * spans it returned.  *overwritten (may be NULL; ABI 23): the launches since
+ * the previous call whose spans were lost to that cycling (0 if none).  Synchronises the device.  (bench.py: the per-launch
  * duration of the roofline line, the kernel-trace duration without a
  * profiler.) */
-int mgs_queue_spans(mgs_batch* batch, double* out_ms, int cap, int* count);
+int mgs_queue_spans(mgs_batch* batch, double* out_ms, int cap, int* count, int* overwritten);
 /* Rollout launch mode for this process; returns the previous one and leaves it
  * unchanged if mode < 0.  0: one workgroup per candidate; 1 (default): the work
  * queue on the resident grid; k >= 2: the queue on at most k workgroups (tests

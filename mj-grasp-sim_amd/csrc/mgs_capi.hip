@@ -226,6 +226,7 @@ struct mgs_batch {
   int ring_n;                       // allocated on the first launch with yield_every > 0 and grown
                                     // when a launch's n exceeds ring_n (the kernel indexes a ring by
                                     // its launch's n, which may exceed the batch capacity: ADVICE r4)
+  int qslot_drained;                // qslot at the last mgs_queue_spans (spans older than 64 launches are lost)
   uint64_t spins_seen;              // expired ring spins already reported (mgs_queue_stats word 7)
   hipEvent_t e0, e1, e2, e3;
   double last_ms;
@@ -415,6 +416,12 @@ static int resident_workgroups(mgs_model* m) {
   return m->resident;
 }
 
+int mgs_model_resident(mgs_model* model) {
+  if (!model) return fail(MGS_EINVAL, "mgs_model_resident: null model%s");
+  HIPCHK(hipSetDevice(model->device));
+  return resident_workgroups(model);
+}
+
 static Mdl device_model(const mgs_model* m) {
   Mdl md;
   md.m = m->desc;
@@ -515,6 +522,24 @@ static int expired_spins(mgs_batch* b, uint64_t* out) {
 // candidate possibly lost, a ring slot possibly written after its launch
 // ended) fails the call with MGS_EQUEUE and resets every ring and ring
 // head / tail, so the next launch starts from a clean protocol state
+// before a synchronous rotating launch: expired spins left by earlier launches
+// (the device entries', which their callers audit) are acknowledged here and
+// the rings they may have left dirty are reset, so the check after this launch
+// counts only its own
+static int sync_rotation(mgs_batch* b) {
+  if (!b->d_rings) return MGS_OK;
+  uint64_t e = 0;
+  int rc = expired_spins(b, &e);
+  if (rc) return rc;
+  if (e == b->spins_seen) return MGS_OK;
+  b->spins_seen = e;
+  HIPCHK(hipMemset(b->d_rings, 0, sizeof(uint32_t) * MGS_QRING_F(b->ring_n) * MGS_QUEUE_RING));
+  for (int k = 0; k < MGS_QUEUE_RING; k++)
+    HIPCHK(hipMemset(b->d_queue + MGS_QHDR * k + 2, 0, 2 * sizeof(uint32_t)));
+  HIPCHK(hipDeviceSynchronize());
+  return MGS_OK;
+}
+
 static int check_rotation(mgs_batch* b) {
   if (!b->d_rings) return MGS_OK;
   uint64_t e = 0;
@@ -614,8 +639,13 @@ int mgs_queue_stats(mgs_batch* b, uint64_t* out) {
   return MGS_OK;
 }
 
-int mgs_queue_spans(mgs_batch* b, double* out_ms, int cap, int* count) {
+int mgs_queue_spans(mgs_batch* b, double* out_ms, int cap, int* count, int* overwritten) {
   if (!b || !out_ms || !count || cap < 0) return fail(MGS_EINVAL, "mgs_queue_spans: bad argument%s");
+  // launches since the previous call beyond the ring's 64 headers: their spans
+  // were overwritten before they could be read
+  const int since = b->qslot - b->qslot_drained;
+  if (overwritten) *overwritten = since > MGS_QUEUE_RING ? since - MGS_QUEUE_RING : 0;
+  b->qslot_drained = b->qslot;
   HIPCHK(hipSetDevice(b->m->device));
   uint32_t h[MGS_QHDR * MGS_QUEUE_RING];
   HIPCHK(hipDeviceSynchronize());
@@ -767,7 +797,9 @@ static int rollout_host(mgs_batch* b, const mgs_schedule* sched, int n, const do
   HIPCHK(hipMemcpy(b->d_ps, phase_start, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b->d_pt, phase_target, sizeof(double) * n * 3 * np, hipMemcpyHostToDevice));
   if (resume_in) HIPCHK(hipMemcpy(b->d_resume, resume_in, sizeof(double) * rs * n, hipMemcpyHostToDevice));
-  int rc = launch_rollout(b, sched, n, b->d_qpos, b->d_mquat, b->d_ps, b->d_pt, nullptr, b->d_label, b->d_fail,
+  int rc;
+  if (sched->yield_every > 0 && (rc = sync_rotation(b))) return rc;
+  rc = launch_rollout(b, sched, n, b->d_qpos, b->d_mquat, b->d_ps, b->d_pt, nullptr, b->d_label, b->d_fail,
                           b->d_objq, b->d_stats, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                           out->resume ? b->d_resume : nullptr, resume_in ? b->d_resume : nullptr);
   if (rc) return rc;

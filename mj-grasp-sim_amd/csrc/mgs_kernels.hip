@@ -1057,7 +1057,7 @@ DEVI void actuation(const Mdl& md, Dat& d) {
       if (c > crange[2 * u + 1]) c = crange[2 * u + 1];
     }
     double f;
-    if (md.m.nact > 0 && gtype[u] == MGS_GAIN_PID) {
+    if (md.m.npid > 0 && gtype[u] == MGS_GAIN_PID) {
       f = pid_force(md, d, u, c, len, vel, lane);
     } else {
       double g = gain[3 * u];
@@ -2480,6 +2480,633 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
   wsync();
 }
 
+// ---------------------------------------------------------------------------
+// MuJoCo 3.2.2's collision table (ccd_mode 1 / 2, ABI 23): the oracle's
+// collide_convex_mj / collide_prim, same expressions in the same order.
+// Convex pairs: libccd's ccdMPRPenetration (libccd's ccdIsZero / ccdEq tests,
+// the depth as the distance from the origin to the final portal triangle, the
+// position as the tetrahedron barycentre of the origin); with multiccd four more
+// MPRs with the geoms turned by -+1e-3 rad about the first contact's tangents.
+// Primitive pairs: the analytic colliders.  Parity vs MuJoCo unpinned
+// (DESIGN.md §2); GPU == oracle bit for bit.
+#define CCD_EPS 2.2204460492503131e-16
+#define MCCD_RELTOL 1e-3
+#define MCCD_C 0.9999998750000026       // cos(5e-4): half the perturbation angle
+#define MCCD_S 4.999999791666669e-04    // sin(5e-4)
+#define CCD_MAXLOOP 64
+#define MGS_CB_NCAND 49
+
+DEVI int ccd_iszero(double x) { return fabs(x) < CCD_EPS; }
+DEVI int ccd_eq(double a, double b) {
+  double ab = fabs(a - b);
+  if (ab < CCD_EPS) return 1;
+  double fa = fabs(a), fb = fabs(b);
+  return fb > fa ? (ab < CCD_EPS * fb) : (ab < CCD_EPS * fa);
+}
+DEVI int ccd_vzero(const double* a) { return ccd_eq(a[0], 0.0) && ccd_eq(a[1], 0.0) && ccd_eq(a[2], 0.0); }
+DEVI void ccd_normalize(double* v) {
+  double k = 1.0 / sqrt(dot3(v, v));
+  v[0] = v[0] * k; v[1] = v[1] * k; v[2] = v[2] * k;
+}
+DEVI void mulmm3(double* r, const double* a, const double* b) {
+  double t[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) t[3 * i + j] = (a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j];
+#pragma unroll
+  for (int k = 0; k < 9; k++) r[k] = t[k];
+}
+DEVI int ccd_reach_tol(const SupPt& p1, const SupPt& p2, const SupPt& p3, const SupPt& p4, const double* n,
+                       double tol) {
+  double dv4 = dot3(p4.v, n);
+  double t1 = dv4 - dot3(p1.v, n);
+  double t2 = dv4 - dot3(p2.v, n);
+  double t3 = dv4 - dot3(p3.v, n);
+  double mn = t1 < t2 ? t1 : t2;
+  mn = mn < t3 ? mn : t3;
+  return ccd_eq(mn, tol) || mn < tol;
+}
+DEVI void ccd_portal_dir(double* n, const SupPt& p1, const SupPt& p2, const SupPt& p3) {
+  double e1[3], e2[3];
+  sub3(e1, p2.v, p1.v);
+  sub3(e2, p3.v, p1.v);
+  cross3(n, e1, e2);
+  ccd_normalize(n);
+}
+DEVI double ccd_seg_dist2(const double* x0, const double* b, double* w) {
+  double dd[3], a[3] = {x0[0], x0[1], x0[2]};
+  sub3(dd, b, x0);
+  double t = -dot3(a, dd);
+  t = t / dot3(dd, dd);
+  if (t < 0.0 || ccd_iszero(t)) {
+    w[0] = x0[0]; w[1] = x0[1]; w[2] = x0[2];
+  } else if (t > 1.0 || ccd_eq(t, 1.0)) {
+    w[0] = b[0]; w[1] = b[1]; w[2] = b[2];
+  } else {
+    w[0] = dd[0] * t + x0[0]; w[1] = dd[1] * t + x0[1]; w[2] = dd[2] * t + x0[2];
+  }
+  return dot3(w, w);
+}
+DEVI double ccd_tri_dist2(const double* x0, const double* B, const double* C, double* w) {
+  double d1[3], d2[3];
+  sub3(d1, B, x0);
+  sub3(d2, C, x0);
+  const double* a = x0;
+  double v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  double dt = ww * v - r * r, s, t;
+  if (ccd_iszero(dt)) {
+    s = -1.0; t = -1.0;
+  } else {
+    s = (q * r - ww * p) / dt;
+    t = (-s * r - q) / ww;
+  }
+  if ((ccd_iszero(s) || s > 0.0) && (ccd_eq(s, 1.0) || s < 1.0) && (ccd_iszero(t) || t > 0.0) &&
+      (ccd_eq(t, 1.0) || t < 1.0) && (ccd_eq(t + s, 1.0) || t + s < 1.0)) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) w[k] = (x0[k] + d1[k] * s) + d2[k] * t;
+    return dot3(w, w);
+  }
+  double w2[3];
+  double dist = ccd_seg_dist2(x0, B, w);
+  double d2b = ccd_seg_dist2(x0, C, w2);
+  if (d2b < dist) { dist = d2b; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  d2b = ccd_seg_dist2(B, C, w2);
+  if (d2b < dist) { dist = d2b; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  return dist;
+}
+DEVI void ccd_find_pos(const SupPt& p0, const SupPt& p1, const SupPt& p2, const SupPt& p3, double* pos) {
+  double dir[3], c[3], b0, b1, b2, b3;
+  ccd_portal_dir(dir, p1, p2, p3);
+  cross3(c, p1.v, p2.v); b0 = dot3(c, p3.v);
+  cross3(c, p3.v, p2.v); b1 = dot3(c, p0.v);
+  cross3(c, p0.v, p1.v); b2 = dot3(c, p3.v);
+  cross3(c, p2.v, p1.v); b3 = dot3(c, p0.v);
+  double sum = ((b0 + b1) + b2) + b3;
+  if (ccd_iszero(sum) || sum < 0.0) {
+    b0 = 0.0;
+    cross3(c, p2.v, p3.v); b1 = dot3(c, dir);
+    cross3(c, p3.v, p1.v); b2 = dot3(c, dir);
+    cross3(c, p1.v, p2.v); b3 = dot3(c, dir);
+    sum = (b1 + b2) + b3;
+  }
+  double inv = 1.0 / sum;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    double a1 = (((0.0 + p0.a[k] * b0) + p1.a[k] * b1) + p2.a[k] * b2) + p3.a[k] * b3;
+    double a2 = (((0.0 + p0.b[k] * b0) + p1.b[k] * b1) + p2.b[k] * b2) + p3.b[k] * b3;
+    pos[k] = (a1 * inv + a2 * inv) * 0.5;
+  }
+}
+
+// oracle ccd_mpr (Ctx: PairCtx, or PairCtx2 for two pairs on the two halves;
+// g1 / g2 the half's geoms, whose centres are their geom_xpos); dir is the
+// caller's array as in mpr_penetration (the certificate's direction on a miss)
+#define CCD_CERT(P) do { *cm = -dot3((P).v, dir); } while (0)
+template <class Ctx>
+DEVI int ccd_mpr(const Mdl& md, const Dat& d, const Ctx& pc, int g1, int g2, double* n, double* depth, double* pos,
+                 double* dir, double* cm) {
+  *cm = -1.0;
+  const double tol = md.m.mpr_tolerance;
+  const int maxit = md.m.ccd_iterations;
+  SupPt p0, p1, p2, p3, p4;
+  double dt;
+#pragma unroll
+  for (int k = 0; k < 3; k++) { p0.a[k] = d.geom_xpos[3 * g1 + k]; p0.b[k] = d.geom_xpos[3 * g2 + k]; }
+  sub3(p0.v, p0.a, p0.b);
+  if (ccd_vzero(p0.v)) p0.v[0] = p0.v[0] + CCD_EPS * 10.0;
+  dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
+  ccd_normalize(dir);
+  mink_support(pc, dir, &p1);
+  dt = dot3(p1.v, dir);
+  if (ccd_iszero(dt) || dt < 0.0) { CCD_CERT(p1); return 0; }
+  cross3(dir, p0.v, p1.v);
+  if (ccd_iszero(dot3(dir, dir))) {
+    if (ccd_vzero(p1.v)) return 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { n[k] = p1.v[k]; pos[k] = (p1.a[k] + p1.b[k]) * 0.5; }
+    *depth = sqrt(dot3(n, n));
+    ccd_normalize(n);
+    return 1;
+  }
+  ccd_normalize(dir);
+  mink_support(pc, dir, &p2);
+  dt = dot3(p2.v, dir);
+  if (ccd_iszero(dt) || dt < 0.0) { CCD_CERT(p2); return 0; }
+  {
+    double e1[3], e2[3];
+    sub3(e1, p1.v, p0.v);
+    sub3(e2, p2.v, p0.v);
+    cross3(dir, e1, e2);
+    ccd_normalize(dir);
+  }
+  if (dot3(dir, p0.v) > 0.0) {
+    SupPt tmp = p1; p1 = p2; p2 = tmp;
+    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+  }
+  int it;
+  for (it = 0; it < CCD_MAXLOOP; it++) {
+    mink_support(pc, dir, &p3);
+    dt = dot3(p3.v, dir);
+    if (ccd_iszero(dt) || dt < 0.0) { CCD_CERT(p3); return 0; }
+    double c[3];
+    int cont = 0;
+    cross3(c, p1.v, p3.v);
+    dt = dot3(c, p0.v);
+    if (dt < 0.0 && !ccd_iszero(dt)) { p2 = p3; cont = 1; }
+    if (!cont) {
+      cross3(c, p3.v, p2.v);
+      dt = dot3(c, p0.v);
+      if (dt < 0.0 && !ccd_iszero(dt)) { p1 = p3; cont = 1; }
+    }
+    if (!cont) break;
+    double e1[3], e2[3];
+    sub3(e1, p1.v, p0.v);
+    sub3(e2, p2.v, p0.v);
+    cross3(dir, e1, e2);
+    ccd_normalize(dir);
+  }
+  if (it == CCD_MAXLOOP) return 0;
+  for (it = 0; it < CCD_MAXLOOP; it++) {
+    ccd_portal_dir(dir, p1, p2, p3);
+    dt = dot3(dir, p1.v);
+    if (ccd_iszero(dt) || dt > 0.0) break;
+    mink_support(pc, dir, &p4);
+    dt = dot3(p4.v, dir);
+    if (!(ccd_iszero(dt) || dt > 0.0)) { CCD_CERT(p4); return 0; }
+    if (ccd_reach_tol(p1, p2, p3, p4, dir, tol)) return 0;
+    PORTAL_EXPAND(p0, p1, p2, p3, p4);
+  }
+  if (it == CCD_MAXLOOP) return 0;
+  for (it = 0;; it++) {
+    ccd_portal_dir(dir, p1, p2, p3);
+    mink_support(pc, dir, &p4);
+    if (ccd_reach_tol(p1, p2, p3, p4, dir, tol) || it > maxit) {
+      double w[3];
+      double dep = sqrt(ccd_tri_dist2(p1.v, p2.v, p3.v, w));
+      if (ccd_iszero(dep)) return 0;
+      n[0] = w[0]; n[1] = w[1]; n[2] = w[2];
+      ccd_normalize(n);
+      *depth = dep;
+      ccd_find_pos(p0, p1, p2, p3, pos);
+      return 1;
+    }
+    PORTAL_EXPAND(p0, p1, p2, p3, p4);
+  }
+}
+#undef CCD_CERT
+
+// multiccd (oracle collide_convex_mj after its first contact): the pair's
+// first contact (n, pos) is in; four more MPRs with geom 1 turned by -+angle
+// and geom 2 by the opposite angle about the frame's tangents, each new
+// contact farther than MCCD_RELTOL x the smaller bounding radius from the
+// pair's contacts so far added (all lanes; lane 0 writes)
+DEVI void multiccd(const Mdl& md, Dat& d, const PairCtx& pc, int pair, int g1, int g2, const double* n,
+                   const double* pos) {
+  double t1[3], t2[3];
+  make_frame(n, t1, t2);
+  double cpx[5], cpy[5], cpz[5];
+  cpx[0] = pos[0]; cpy[0] = pos[1]; cpz[0] = pos[2];
+  int nc = 1;
+  const double* rb = DA(md, geom_rbound);
+  const double* rr = DA(md, geom_radius);
+  double rb1 = rb[g1] + rr[g1], rb2 = rb[g2] + rr[g2];
+  double tolr = MCCD_RELTOL * (rb1 < rb2 ? rb1 : rb2);
+  const int ncmax = md.m.ncon_max;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int ax = q >> 1, sg = q & 1;
+    double axis[3] = {ax ? t2[0] : t1[0], ax ? t2[1] : t1[1], ax ? t2[2] : t1[2]};
+    double s = sg ? MCCD_S : -MCCD_S;
+    double q1[4] = {MCCD_C, axis[0] * s, axis[1] * s, axis[2] * s};
+    double q2[4] = {MCCD_C, -(axis[0] * s), -(axis[1] * s), -(axis[2] * s)};
+    double M1[9], M2[9];
+    quat2mat(M1, q1);
+    quat2mat(M2, q2);
+    PairCtx pp = pc;
+    mulmm3(pp.R1, M1, pc.R1);
+    mulmm3(pp.R2, M2, pc.R2);
+    double nn[3], dd, ppos[3], dir[3], cmx;
+    if (!ccd_mpr(md, d, pp, g1, g2, nn, &dd, ppos, dir, &cmx)) continue;
+    int isnew = 1;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      if (k < nc) {
+        double dx[3] = {ppos[0] - cpx[k], ppos[1] - cpy[k], ppos[2] - cpz[k]};
+        if (sqrt(dot3(dx, dx)) < tolr) isnew = 0;
+      }
+    }
+    if (!isnew) continue;
+#pragma unroll
+    for (int k = 1; k < 5; k++)
+      if (k == nc) { cpx[k] = ppos[0]; cpy[k] = ppos[1]; cpz[k] = ppos[2]; }
+    nc++;
+    double u1[3], u2[3];
+    make_frame(nn, u1, u2);
+    if (lane_id() == 0) add_contact(d, ncmax, pair, g1, g2, ppos, nn, u1, u2, -dd);
+  }
+  wsync();
+}
+
+// one convex pair (ccd_mode 1 / 2): MPR, certificate, first contact, multiccd
+DEVI void collide_pair_mj(const Mdl& md, Dat& d, int pair, int multi) {
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  double n[3], depth, pos[3], cd[3], cm;
+  PairCtx pc;
+  pair_ctx(md, d, g1, g2, pc);
+  int hit = ccd_mpr(md, d, pc, g1, g2, n, &depth, pos, cd, &cm);
+  cert_update(md, d, pair, g1, g2, hit, cd, cm);
+  PCNT(26, 1);
+  PCNT(27, hit);
+  if (!hit) return;
+  double t1[3], t2[3];
+  make_frame(n, t1, t2);
+  if (lane_id() == 0) add_contact(d, md.m.ncon_max, pair, g1, g2, pos, n, t1, t2, -depth);
+  wsync();
+  if (multi) multiccd(md, d, pc, pair, g1, g2, n, pos);
+  PT(41);
+}
+
+// two convex pairs with small hulls (ccd_mode 1 / 2): both first MPRs at once
+// on the two halves, then per pair in order certificate, contact and multiccd
+DEVI void collide_pair2_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
+  const int lane = lane_id();
+  const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
+  const int gA1 = p1[pairA], gA2 = p2[pairA], gB1 = p1[pairB], gB2 = p2[pairB];
+  PairCtx2 q;
+  pair_ctx2(md, d, gA1, gA2, gB1, gB2, q);
+  const int g1 = lane < 32 ? gA1 : gB1, g2 = lane < 32 ? gA2 : gB2;
+  double n[3], depth, pos[3], cd[3], cm;
+  int hit = ccd_mpr(md, d, q, g1, g2, n, &depth, pos, cd, &cm);
+  PT(4);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int src = 32 * k, pair = k ? pairB : pairA, G1 = k ? gB1 : gA1, G2 = k ? gB2 : gA2;
+    const int hk = __builtin_amdgcn_readlane(hit, src);
+    double nk[3], pk[3], ck[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      nk[i] = readlane_d(n[i], src);
+      pk[i] = readlane_d(pos[i], src);
+      ck[i] = readlane_d(cd[i], src);
+    }
+    cert_update(md, d, pair, G1, G2, hk, ck, readlane_d(cm, src));
+    PCNT(26, 1);
+    PCNT(27, hk);
+    if (hk) {
+      double t1[3], t2[3];
+      make_frame(nk, t1, t2);
+      if (lane == 0) add_contact(d, md.m.ncon_max, pair, G1, G2, pk, nk, t1, t2, -readlane_d(depth, src));
+      wsync();
+      if (md.m.ccd_mode == MGS_CCD_MULTI && IA(md, pair_kind)[pair] == MGS_PAIR_CONVEX) {
+        PairCtx pc;
+        pair_ctx(md, d, G1, G2, pc);
+        multiccd(md, d, pc, pair, G1, G2, nk, pk);
+      }
+    }
+  }
+}
+
+// analytic primitive colliders (oracle collide_prim): every lane computes the
+// same values (the capsule-box candidates: one per lane), lane 0 adds them
+DEVI double kdist3(const double* a, const double* b) {
+  double dx[3];
+  sub3(dx, a, b);
+  return sqrt(dot3(dx, dx));
+}
+DEVI int raw_sphere_sphere(const double* p1, const double* z1, double r1, const double* p2, const double* z2,
+                           double r2, double margin, double* pos, double* n, double* dist) {
+  double dd = (kdist3(p1, p2) - r1) - r2;
+  if (dd > margin) return 0;
+  sub3(n, p2, p1);
+  if (normalize3(n) < K_MINVAL) {
+    cross3(n, z1, z2);
+    normalize3(n);
+  }
+  double s = r1 + 0.5 * dd;
+#pragma unroll
+  for (int k = 0; k < 3; k++) pos[k] = p1[k] + n[k] * s;
+  *dist = dd;
+  return 1;
+}
+DEVI int raw_sphere_box(const double* c, double r, const double* x, const double* R, const double* s, double margin,
+                        double* pos, double* n, double* dist) {
+  double t[3], cl[3], q[3], df[3], nl[3], pl[3];
+  sub3(t, c, x);
+  mulmtv3(cl, R, t);
+#pragma unroll
+  for (int k = 0; k < 3; k++) q[k] = cl[k] < -s[k] ? -s[k] : (cl[k] > s[k] ? s[k] : cl[k]);
+  sub3(df, q, cl);
+  double dc = sqrt(dot3(df, df));
+  if (dc - r > margin) return 0;
+  double dd;
+  if (dc > K_MINVAL) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) nl[k] = df[k] / dc;
+    dd = dc - r;
+  } else {
+    int kk = 0;
+    double a = s[0] - fabs(cl[0]);
+    double a1 = s[1] - fabs(cl[1]);
+    if (a1 < a) { a = a1; kk = 1; }
+    double a2 = s[2] - fabs(cl[2]);
+    if (a2 < a) { a = a2; kk = 2; }
+    double sgn = (kk == 0 ? cl[0] : (kk == 1 ? cl[1] : cl[2])) >= 0.0 ? -1.0 : 1.0;
+    nl[0] = kk == 0 ? sgn : 0.0;
+    nl[1] = kk == 1 ? sgn : 0.0;
+    nl[2] = kk == 2 ? sgn : 0.0;
+    dd = -(a + r);
+  }
+  double h = r + 0.5 * dd;
+#pragma unroll
+  for (int k = 0; k < 3; k++) pl[k] = cl[k] + nl[k] * h;
+  mulmv3(n, R, nl);
+  mulmv3(t, R, pl);
+  add3(pos, x, t);
+  *dist = dd;
+  return 1;
+}
+DEVI double box_phi(const double* p, const double* s) {
+  double o0 = fabs(p[0]) - s[0], o1 = fabs(p[1]) - s[1], o2 = fabs(p[2]) - s[2];
+  if (o0 > 0.0 || o1 > 0.0 || o2 > 0.0) {
+    double a = o0 > 0.0 ? o0 : 0.0, b = o1 > 0.0 ? o1 : 0.0, c = o2 > 0.0 ? o2 : 0.0;
+    return sqrt((a * a + b * b) + c * c);
+  }
+  double m = o0 > o1 ? o0 : o1;
+  return m > o2 ? m : o2;
+}
+// oracle capbox_cand: candidate k of the segment parameter (0 if it does not exist)
+DEVI int capbox_cand(int k, const double* c, const double* a, const double* s, double* tout) {
+  double t;
+  if (k < 2) { *tout = k ? 1.0 : -1.0; return 1; }
+  if (k < 8) {
+    int i = (k - 2) >> 1;
+    double sg = ((k - 2) & 1) ? 1.0 : -1.0;
+    double ai = i == 0 ? a[0] : (i == 1 ? a[1] : a[2]);
+    double ci = i == 0 ? c[0] : (i == 1 ? c[1] : c[2]);
+    double si = i == 0 ? s[0] : (i == 1 ? s[1] : s[2]);
+    if (fabs(ai) < K_MINVAL) return 0;
+    t = (sg * si - ci) / ai;
+  } else if (k < 34) {
+    int code = k - 8 + 1;
+    double num = 0.0, den = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      int dgt = code % 3;
+      code /= 3;
+      if (dgt != 0) {
+        double sg = dgt == 1 ? -1.0 : 1.0;
+        num = num + (c[i] - sg * s[i]) * a[i];
+        den = den + a[i] * a[i];
+      }
+    }
+    if (den < K_MINVAL) return 0;
+    t = -num / den;
+    t = t < -1.0 ? -1.0 : (t > 1.0 ? 1.0 : t);
+    *tout = t;
+    return 1;
+  } else {
+    int q = k - 34, l1 = 0, l2 = 1;
+    for (int x = 0; x < 6; x++)
+      for (int y = x + 1; y < 6; y++) {
+        if (q == 0) { l1 = x; l2 = y; }
+        q--;
+      }
+    int i = l1 >> 1, j = l2 >> 1;
+    double si = (l1 & 1) ? 1.0 : -1.0, sj = (l2 & 1) ? 1.0 : -1.0;
+    double ai = i == 0 ? a[0] : (i == 1 ? a[1] : a[2]), aj = j == 0 ? a[0] : (j == 1 ? a[1] : a[2]);
+    double ci = i == 0 ? c[0] : (i == 1 ? c[1] : c[2]), cj = j == 0 ? c[0] : (j == 1 ? c[1] : c[2]);
+    double Si = i == 0 ? s[0] : (i == 1 ? s[1] : s[2]), Sj = j == 0 ? s[0] : (j == 1 ? s[1] : s[2]);
+    double coef = si * ai - sj * aj;
+    if (fabs(coef) < K_MINVAL) return 0;
+    t = ((Si - Sj) - (si * ci - sj * cj)) / coef;
+  }
+  if (!(t >= -1.0 && t <= 1.0)) return 0;
+  *tout = t;
+  return 1;
+}
+DEVI void collide_prim(const Mdl& md, Dat& d, int pair, int kind) {
+  const int lane = lane_id();
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  double R1[9], R2[9], x1[3], x2[3], s1[3], s2[3];
+#pragma unroll
+  for (int k = 0; k < 9; k++) { R1[k] = d.geom_xmat[9 * g1 + k]; R2[k] = d.geom_xmat[9 * g2 + k]; }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    x1[k] = d.geom_xpos[3 * g1 + k]; x2[k] = d.geom_xpos[3 * g2 + k];
+    s1[k] = DA(md, geom_size)[3 * g1 + k]; s2[k] = DA(md, geom_size)[3 * g2 + k];
+  }
+  const double margin = DA(md, pair_margin)[pair];
+  double z1[3] = {R1[2], R1[5], R1[8]}, z2[3] = {R2[2], R2[5], R2[8]};
+  double pos0[3], n0[3], dist0, pos1[3] = {0.0, 0.0, 0.0}, n1[3] = {1.0, 0.0, 0.0}, dist1 = 0.0;
+  int nc = 0;
+  if (kind == MGS_PAIR_SPHERE_SPHERE) {
+    nc = raw_sphere_sphere(x1, z1, s1[0], x2, z2, s2[0], margin, pos0, n0, &dist0);
+  } else if (kind == MGS_PAIR_SPHERE_CAPSULE) {
+    double v[3], q[3];
+    sub3(v, x1, x2);
+    double xx = dot3(z2, v);
+    xx = xx < -s2[1] ? -s2[1] : (xx > s2[1] ? s2[1] : xx);
+#pragma unroll
+    for (int k = 0; k < 3; k++) q[k] = x2[k] + z2[k] * xx;
+    nc = raw_sphere_sphere(x1, z1, s1[0], q, z2, s2[0], margin, pos0, n0, &dist0);
+  } else if (kind == MGS_PAIR_CAPSULE_CAPSULE) {
+    double a1[3], a2[3], df[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { a1[k] = z1[k] * s1[1]; a2[k] = z2[k] * s2[1]; }
+    sub3(df, x1, x2);
+    double ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+    double u = -dot3(a1, df), v = dot3(a2, df);
+    double det = ma * mc - mb * mb;
+    double v1[3], v2[3];
+    if (fabs(det) >= K_MINVAL) {
+      double xa = (mc * u - mb * v) / det, xb = (ma * v - mb * u) / det;
+      if (xa > 1.0) { xa = 1.0; xb = (v - mb) / mc; }
+      else if (xa < -1.0) { xa = -1.0; xb = (v + mb) / mc; }
+      if (xb > 1.0) {
+        xb = 1.0;
+        xa = (u - mb) / ma;
+        xa = xa < -1.0 ? -1.0 : (xa > 1.0 ? 1.0 : xa);
+      } else if (xb < -1.0) {
+        xb = -1.0;
+        xa = (u + mb) / ma;
+        xa = xa < -1.0 ? -1.0 : (xa > 1.0 ? 1.0 : xa);
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) { v1[k] = x1[k] + a1[k] * xa; v2[k] = x2[k] + a2[k] * xb; }
+      nc = raw_sphere_sphere(v1, z1, s1[0], v2, z2, s2[0], margin, pos0, n0, &dist0);
+    } else {
+      for (int e = 0; e < 4 && nc < 2; e++) {
+        double sg = (e & 1) ? -1.0 : 1.0, xx;
+        if (e < 2) {
+          xx = (sg > 0.0 ? (v - mb) : (v + mb)) / mc;
+          xx = xx < -1.0 ? -1.0 : (xx > 1.0 ? 1.0 : xx);
+#pragma unroll
+          for (int k = 0; k < 3; k++) { v1[k] = x1[k] + sg * a1[k]; v2[k] = x2[k] + a2[k] * xx; }
+        } else {
+          xx = (sg > 0.0 ? (u - mb) : (u + mb)) / ma;
+          xx = xx < -1.0 ? -1.0 : (xx > 1.0 ? 1.0 : xx);
+#pragma unroll
+          for (int k = 0; k < 3; k++) { v2[k] = x2[k] + sg * a2[k]; v1[k] = x1[k] + a1[k] * xx; }
+        }
+        double pp[3], nn[3], dd;
+        if (raw_sphere_sphere(v1, z1, s1[0], v2, z2, s2[0], margin, pp, nn, &dd)) {
+          if (nc == 0) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) { pos0[k] = pp[k]; n0[k] = nn[k]; }
+            dist0 = dd;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 3; k++) { pos1[k] = pp[k]; n1[k] = nn[k]; }
+            dist1 = dd;
+          }
+          nc++;
+        }
+      }
+    }
+  } else if (kind == MGS_PAIR_SPHERE_BOX) {
+    nc = raw_sphere_box(x1, s1[0], x2, R2, s2, margin, pos0, n0, &dist0);
+  } else if (kind == MGS_PAIR_CAPSULE_BOX) {
+    double t[3], c[3], a[3], hz[3];
+    sub3(t, x1, x2);
+    mulmtv3(c, R2, t);
+#pragma unroll
+    for (int k = 0; k < 3; k++) hz[k] = z1[k] * s1[1];
+    mulmtv3(a, R2, hz);
+    // candidate k on lane k, then the first (lowest k) of the smallest phi
+    double tk = 0.0, ph = INFINITY;
+    if (lane < MGS_CB_NCAND && capbox_cand(lane, c, a, s2, &tk)) {
+      double p[3] = {c[0] + a[0] * tk, c[1] + a[1] * tk, c[2] + a[2] * tk};
+      ph = box_phi(p, s2);
+    }
+    double m = ph;
+#pragma unroll
+    for (int sel = 0; sel < 4; sel++) { double o = dpp_d(m, sel); m = o < m ? o : m; }
+    double M = readlane_d(m, 0);
+    double r1 = readlane_d(m, 16), r2 = readlane_d(m, 32), r3 = readlane_d(m, 48);
+    M = r1 < M ? r1 : M;
+    M = r2 < M ? r2 : M;
+    M = r3 < M ? r3 : M;
+    unsigned long long tied = __ballot(ph == M);
+    int wl = tied ? __ffsll((long long)tied) - 1 : 0;
+    double tb = readlane_d(tk, wl);
+    double ctr[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) ctr[k] = x1[k] + hz[k] * tb;
+    nc = raw_sphere_box(ctr, s1[0], x2, R2, s2, margin, pos0, n0, &dist0);
+    if (nc) {
+      double pe0[3], ne0[3], de0, pe1[3], ne1[3], de1, ce[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) ce[k] = x1[k] - hz[k];
+      int ok = raw_sphere_box(ce, s1[0], x2, R2, s2, margin, pe0, ne0, &de0) && ne0[0] == n0[0] &&
+               ne0[1] == n0[1] && ne0[2] == n0[2];
+      if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) ce[k] = x1[k] + hz[k];
+        ok = raw_sphere_box(ce, s1[0], x2, R2, s2, margin, pe1, ne1, &de1) && ne1[0] == n0[0] &&
+             ne1[1] == n0[1] && ne1[2] == n0[2];
+      }
+      if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) { pos0[k] = pe0[k]; n0[k] = ne0[k]; pos1[k] = pe1[k]; n1[k] = ne1[k]; }
+        dist0 = de0;
+        dist1 = de1;
+        nc = 2;
+      }
+    }
+  } else if (kind == MGS_PAIR_SPHERE_CYLINDER) {
+    double t[3], cl[3], q[3], df[3], nl[3], pl[3];
+    const double r = s1[0], cr = s2[0], ch = s2[1];
+    sub3(t, x1, x2);
+    mulmtv3(cl, R2, t);
+    double rho = sqrt(cl[0] * cl[0] + cl[1] * cl[1]);
+    if (rho > cr) { q[0] = cl[0] / rho * cr; q[1] = cl[1] / rho * cr; }
+    else { q[0] = cl[0]; q[1] = cl[1]; }
+    q[2] = cl[2] < -ch ? -ch : (cl[2] > ch ? ch : cl[2]);
+    sub3(df, q, cl);
+    double dc = sqrt(dot3(df, df)), dd;
+    if (dc - r <= margin) {
+      if (dc > K_MINVAL) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) nl[k] = df[k] / dc;
+        dd = dc - r;
+      } else {
+        double side = cr - rho, cap = ch - fabs(cl[2]), a;
+        if (side < cap && rho > K_MINVAL) {
+          nl[0] = -(cl[0] / rho); nl[1] = -(cl[1] / rho); nl[2] = 0.0;
+          a = side;
+        } else {
+          nl[0] = nl[1] = 0.0;
+          nl[2] = cl[2] >= 0.0 ? -1.0 : 1.0;
+          a = cap;
+        }
+        dd = -(a + r);
+      }
+      double h = r + 0.5 * dd;
+#pragma unroll
+      for (int k = 0; k < 3; k++) pl[k] = cl[k] + nl[k] * h;
+      mulmv3(n0, R2, nl);
+      mulmv3(t, R2, pl);
+      add3(pos0, x2, t);
+      dist0 = dd;
+      nc = 1;
+    }
+  }
+  if (lane == 0) {
+    const int ncmax = md.m.ncon_max;
+    double t1[3], t2[3];
+    if (nc > 0) {
+      make_frame(n0, t1, t2);
+      add_contact(d, ncmax, pair, g1, g2, pos0, n0, t1, t2, dist0);
+    }
+    if (nc > 1) {
+      make_frame(n1, t1, t2);
+      add_contact(d, ncmax, pair, g1, g2, pos1, n1, t1, t2, dist1);
+    }
+  }
+  wsync();
+}
+
 /* Second broadphase stage: separating-axis test between the geoms' oriented
  * bounding boxes (their local AABBs posed in the world; 15 axes).  Each convex
  * hull lies inside its box, so separated boxes cannot produce a contact and the
@@ -2593,7 +3220,10 @@ DEVI void collision(const Mdl& md, Dat& d) {
     PT(59);
     // convex pairs whose four hulls fit 16-lane rows may go two at a time
     int small2 = 0;
-    if (ov && IA(md, pair_kind)[p] != MGS_PAIR_BOXBOX) {
+    const int pk = p < npair ? IA(md, pair_kind)[p] : MGS_PAIR_BOXBOX;
+    const bool mpr_pair = md.m.ccd_mode == MGS_CCD_R5 ? pk != MGS_PAIR_BOXBOX
+                                                       : (pk == MGS_PAIR_CONVEX || pk == MGS_PAIR_CONVEX_SMOOTH);
+    if (ov && mpr_pair) {
       const int32_t *ghull = IA(md, geom_hullid), *hnum = IA(md, hull_vertnum);
       small2 = hnum[ghull[g[0]]] <= 16 && hnum[ghull[g[1]]] <= 16;
     }
@@ -2606,14 +3236,20 @@ DEVI void collision(const Mdl& md, Dat& d) {
     while (mask) {
       int b = __ffsll((long long)mask) - 1;
       mask &= mask - 1ull;
+      const int kind = IA(md, pair_kind)[c0 + b];
       if (((smallm >> b) & 1ull) && mask && ((smallm >> (__ffsll((long long)mask) - 1)) & 1ull)) {
         int b2 = __ffsll((long long)mask) - 1;
         mask &= mask - 1ull;
-        collide_pair2(md, d, c0 + b, c0 + b2);
-      } else if (IA(md, pair_kind)[c0 + b] == MGS_PAIR_BOXBOX) {
+        if (md.m.ccd_mode == MGS_CCD_R5) collide_pair2(md, d, c0 + b, c0 + b2);
+        else collide_pair2_mj(md, d, c0 + b, c0 + b2);
+      } else if (kind == MGS_PAIR_BOXBOX) {
         collide_boxbox(md, d, c0 + b);
-      } else {
+      } else if (md.m.ccd_mode == MGS_CCD_R5) {
         collide_pair(md, d, c0 + b);
+      } else if (kind == MGS_PAIR_CONVEX || kind == MGS_PAIR_CONVEX_SMOOTH) {
+        collide_pair_mj(md, d, c0 + b, kind == MGS_PAIR_CONVEX && md.m.ccd_mode == MGS_CCD_MULTI);
+      } else {
+        collide_prim(md, d, c0 + b, kind);
       }
     }
   }
@@ -5116,7 +5752,7 @@ DEVI void integrate(const Mdl& md, Dat& d) {
       if (pp[1] != 0.0) {
         double v = d.act[k] + dt * d.act_dot[k];
         if (pp[3] >= 0.0) {
-          const double lim = pp[3] / pp[1];
+          const double lim = pp[3] / fabs(pp[1]);
           if (v < -lim) v = -lim;
           if (v > lim) v = lim;
         }

@@ -60,7 +60,7 @@ def load_library(wide: bool = False):
     L.mgs_rollout_resume.argtypes = [vp, P(abi.Schedule), ctypes.c_int, P(c_d), P(c_d), P(c_d), P(c_d), P(c_d),
                                      P(abi.RolloutOut)]
     L.mgs_queue_stats.argtypes = [vp, P(ctypes.c_uint64)]
-    L.mgs_queue_spans.argtypes = [vp, P(c_d), ctypes.c_int, P(ctypes.c_int)]
+    L.mgs_queue_spans.argtypes = [vp, P(c_d), ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int)]
     L.mgs_last_kernel_ms.argtypes = [vp]
     L.mgs_last_kernel_ms.restype = ctypes.c_double
     L.mgs_last_collision_ms.argtypes = [vp]
@@ -87,6 +87,8 @@ def load_library(wide: bool = False):
     L.mgs_supports_nv.argtypes = [ctypes.c_int]
     L.mgs_supports_nv.restype = ctypes.c_int
     L.mgs_rollout_grid.argtypes = [vp, ctypes.c_int]
+    L.mgs_model_resident.argtypes = [vp]
+    L.mgs_model_resident.restype = ctypes.c_int
     L.mgs_rollout_grid.restype = ctypes.c_int
     L.mgs_rollout_queue.argtypes = [ctypes.c_int]
     L.mgs_rollout_queue.restype = ctypes.c_int
@@ -298,6 +300,18 @@ class Engine:
             self._cap = cap
         return self._batch
 
+    def queue_grid(self, n):
+        """the rollout_grid of a launch over n candidates under the process's
+        current queue mode, from the model's resident workgroup count
+        (mgs_model_resident) without opening a batch"""
+        mode = int(self.lib.mgs_rollout_queue(-1))
+        r = int(self.lib.mgs_model_resident(self._model))
+        if mode == 0 or r <= 0:
+            return n
+        if mode > 1 and r > mode:
+            r = mode
+        return r if r < n else n
+
     def rollout_grid(self, n):
         """workgroups a rollout launch over n candidates uses (mgs_rollout_grid:
         the device's resident capacity when the work queue runs, else n)"""
@@ -469,10 +483,14 @@ class Engine:
     def queue_spans(self):
         """execution spans (ms, device real-time counter) of this engine's
         work-queue rollout launches completed since the previous call, oldest
-        first (mgs_queue_spans; synchronises the device)"""
+        first (mgs_queue_spans; synchronises the device).  self.spans_overwritten:
+        the launches since the previous call whose spans the 64-slot ring had
+        already overwritten (call at least every 64 launches to keep it 0)"""
         out = (ctypes.c_double * 64)()
-        cnt = ctypes.c_int()
-        self._ck(self.lib.mgs_queue_spans(self.batch(1), out, 64, ctypes.byref(cnt)), "mgs_queue_spans")
+        cnt, lost = ctypes.c_int(), ctypes.c_int()
+        self._ck(self.lib.mgs_queue_spans(self.batch(1), out, 64, ctypes.byref(cnt), ctypes.byref(lost)),
+                 "mgs_queue_spans")
+        self.spans_overwritten = int(lost.value)
         return [float(out[i]) for i in range(cnt.value)]
 
     def last_collision_ms(self):

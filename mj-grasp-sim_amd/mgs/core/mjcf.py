@@ -52,6 +52,17 @@ _JOINT_DEFAULTS = dict(type="hinge", axis="0 0 1", pos="0 0 0", range="0 0",
 _EQ_DEFAULTS = dict(solref="0.02 1", solimp="0.9 0.95 0.001 0.5 2", active="true")
 
 PAIR_CONVEX, PAIR_BOXBOX = 0, 1   # pair_kind: narrowphase used for the pair (mgs_gpu.h MGS_PAIR_*)
+# ABI 23: MuJoCo 3.2.2's collision table restated (ccd_mode 1 / 2): MPR pairs
+# with a sphere (no multiccd), and the analytic primitive colliders
+PAIR_CONVEX_SMOOTH, PAIR_SPHERE_SPHERE, PAIR_SPHERE_CAPSULE, PAIR_CAPSULE_CAPSULE = 2, 3, 4, 5
+PAIR_SPHERE_BOX, PAIR_CAPSULE_BOX, PAIR_SPHERE_CYLINDER = 6, 7, 8
+# MuJoCo mjtGeom numbering (the collision table is indexed type1 <= type2)
+GEOM_TYPES = {"plane": 0, "hfield": 1, "sphere": 2, "capsule": 3, "ellipsoid": 4, "cylinder": 5, "box": 6,
+              "mesh": 7}
+_PRIM_KIND = {(2, 2): PAIR_SPHERE_SPHERE, (2, 3): PAIR_SPHERE_CAPSULE, (3, 3): PAIR_CAPSULE_CAPSULE,
+              (2, 6): PAIR_SPHERE_BOX, (3, 6): PAIR_CAPSULE_BOX, (2, 5): PAIR_SPHERE_CYLINDER,
+              (6, 6): PAIR_BOXBOX}
+CCD_MODES = {"r5": 0, "multiccd": 1, "single": 2}   # mgs_model_desc.ccd_mode
 GAIN_PID = 16                      # actuator_gaintype of a mujoco.pid plugin actuator (mgs_gpu.h MGS_GAIN_PID)
 CYL_SIDES = 16   # cylinder collision geoms: 32-vertex prisms (a cap fits one contact feature, K_MAXF)
 _JNT_TYPES = {"free": 0, "ball": 1, "slide": 2, "hinge": 3}
@@ -317,7 +328,8 @@ class Compiler:
         self.options = dict(timestep=0.002, impratio=1.0, tolerance=1e-8, iterations=100,
                             noslip_iterations=0, noslip_tolerance=1e-6, gravity=np.array([0, 0, -9.81]),
                             cone="pyramidal", integrator="Euler", mpr_tolerance=1e-6, solver="Newton",
-                            ls_iterations=50, ls_tolerance=0.01)
+                            ls_iterations=50, ls_tolerance=0.01, ccd_iterations=50, multiccd=False,
+                            contact_model="mujoco")
         self.compiler = dict(angle="degree", meshdir="", autolimits=True, discardvisual=False)
         self.defaults: Dict[str, dict] = {"main": {"parent": None}}
         self.meshes: Dict[str, dict] = {}
@@ -413,14 +425,21 @@ class Compiler:
         for k, v in el.attrib.items():
             if k in ("timestep", "impratio", "tolerance", "noslip_tolerance", "mpr_tolerance", "ls_tolerance"):
                 o[k] = float(v)
+            elif k == "ccd_tolerance":          # MuJoCo 3.x name of mpr_tolerance
+                o["mpr_tolerance"] = float(v)
             elif k in ("iterations", "noslip_iterations", "ls_iterations"):
                 o[k] = int(v)
+            elif k in ("ccd_iterations", "mpr_iterations"):
+                o["ccd_iterations"] = int(v)
             elif k == "gravity":
                 o[k] = _f(v, 3)
             elif k in ("cone", "integrator", "solver", "jacobian"):
                 o[k] = v
-        # <flag> children (multiccd etc.) are accepted; contact generation is
-        # always multi-contact in this engine.
+        # <flag multiccd="enable"/>: MuJoCo's multi-contact convex collisions
+        # (perturbed MPR, ccd_mode 1); other flags are accepted and ignored
+        for fl in el:
+            if fl.tag == "flag" and "multiccd" in fl.attrib:
+                o["multiccd"] = fl.get("multiccd") == "enable"
 
     def _parse_default(self, el, name, top=False):
         if top:
@@ -828,7 +847,10 @@ class Compiler:
             cyl = _f(g["size"], 3)[:2].copy() if t == "cylinder" else np.zeros(2)
             side = 0 if partition is None else int(np.sign(gid - partition))
             fr = _fv(g, "friction")
-            cgeoms.append(dict(gid=gid, body=bi, hull=hid, pos=gpos, quat=gquat, contype=ct,
+            size3 = np.zeros(3)
+            sz = _f(g["size"])
+            size3[:min(3, len(sz))] = sz[:3]
+            cgeoms.append(dict(gid=gid, body=bi, hull=hid, pos=gpos, quat=gquat, contype=ct, size=size3,
                                conaffinity=ca, condim=int(g.get("condim", "3")), friction=fr,
                                solref=_fv(g, "solref"), solimp=_fv(g, "solimp"),
                                margin=float(g.get("margin", "0")), gap=float(g.get("gap", "0")),
@@ -1050,6 +1072,14 @@ class Compiler:
         cm.geom_cyl = np.array([g["cyl"] for g in cgeoms], np.float64).reshape(-1, 2)
         cm.geom_rbound = np.array([float(np.max(np.linalg.norm(hulls[g["hull"]], axis=1)))
                                    for g in cgeoms], np.float64)
+        cm.geom_type = np.array([GEOM_TYPES[g["type"]] for g in cgeoms], np.int32)
+        # per-geom contact parameters after the default-class cascade (the pairs
+        # mix them; kept for tests of a template's classes)
+        cm.geom_condim = np.array([g["condim"] for g in cgeoms], np.int32)
+        cm.geom_friction = np.array([g["friction"] for g in cgeoms], np.float64).reshape(-1, 3)
+        cm.geom_solref = np.array([g["solref"] for g in cgeoms], np.float64).reshape(-1, 2)
+        cm.geom_priority = np.array([g["priority"] for g in cgeoms], np.int32)
+        cm.geom_size = np.array([g["size"] for g in cgeoms], np.float64).reshape(-1, 3)
         cm.hull_vertnum = np.array([len(h) for h in hulls], np.int32)
         cm.hull_vertadr = np.concatenate([[0], np.cumsum(cm.hull_vertnum)[:-1]]).astype(np.int32) if hulls else np.zeros(0, np.int32)
         cm.hull_vert = np.concatenate(hulls).reshape(-1, 3) if hulls else np.zeros((0, 3))
@@ -1228,6 +1258,43 @@ class CompiledModel:
     def geom_id(self, name):
         return self.geom_names.index(name)
 
+    def ccd_mode(self):
+        """mgs_model_desc.ccd_mode of this model: options["contact_model"] "r5"
+        (round 5's face-clipping manifold, kept for the contact-set study) -> 0;
+        else MuJoCo 3.2.2's collision table restated, with the multiccd flag
+        (<flag multiccd="enable"/>) -> 1, without -> 2"""
+        o = self.options
+        if o.get("contact_model", "mujoco") == "r5":
+            return 0
+        return 1 if o.get("multiccd", False) else 2
+
+    def pair_table(self, ccd_mode):
+        """(geom1, geom2, kind) of every admissible pair for a ccd mode.  Mode 0:
+        the compiled order (geom index) with the convex / box-box kinds.  Modes
+        1-2: MuJoCo's collision table (engine_collision_driver.c mjCOLLISIONFUNC,
+        indexed by type1 <= type2: mj_collideGeoms swaps a pair whose first geom
+        has the larger type): the analytic colliders for sphere / capsule / box /
+        cylinder pairs (engine_collision_primitive.c), mjc_BoxBox for box pairs,
+        and mjc_Convex (MPR) for the rest -- a pair with a sphere never takes
+        multiccd (mjc_Convex skips spheres and ellipsoids)."""
+        g1 = np.asarray(self.pair_geom1, np.int32).copy()
+        g2 = np.asarray(self.pair_geom2, np.int32).copy()
+        kind = np.asarray(self.pair_kind, np.int32).copy()
+        if ccd_mode == 0 or len(g1) == 0:
+            return g1, g2, kind
+        t = np.asarray(self.geom_type)
+        for p in range(len(g1)):
+            a, b = int(g1[p]), int(g2[p])
+            if t[a] > t[b]:
+                a, b = b, a
+            g1[p], g2[p] = a, b
+            ta, tb = int(t[a]), int(t[b])
+            k = _PRIM_KIND.get((ta, tb))
+            if k is None:
+                k = PAIR_CONVEX_SMOOTH if GEOM_TYPES["sphere"] in (ta, tb) else PAIR_CONVEX
+            kind[p] = k
+        return g1, g2, kind
+
     def pack(self, ncon_max=16, nefc_max=None):
         """Build (desc_fields dict, ibuf int32 array, dbuf float64 array)."""
         ibuf, dbuf = [], []
@@ -1280,6 +1347,7 @@ class CompiledModel:
             put_i(n, getattr(self, n))
         for n in ["geom_pos", "geom_quat", "geom_aabb", "geom_radius", "geom_rbound", "geom_cyl"]:
             put_d(n, getattr(self, n))
+        put_d("geom_size", self.geom_size)
         put_i("hull_vertadr", self.hull_vertadr)
         put_i("hull_vertnum", self.hull_vertnum)
         # per hull x[n], y[n], z[n] (SoA): the kernels' support scans then read
@@ -1288,8 +1356,12 @@ class CompiledModel:
                                            for a, n in zip(self.hull_vertadr, self.hull_vertnum)])
               if len(self.hull_vertnum) else self.hull_vert)
         put_d("hull_center", self.hull_center)
-        for n in ["pair_geom1", "pair_geom2", "pair_condim", "pair_kind"]:
-            put_i(n, getattr(self, n))
+        ccd_mode = self.ccd_mode()
+        g1, g2, kind = self.pair_table(ccd_mode)
+        put_i("pair_geom1", g1)
+        put_i("pair_geom2", g2)
+        put_i("pair_condim", self.pair_condim)
+        put_i("pair_kind", kind)
         for n in ["pair_friction", "pair_solref", "pair_solimp", "pair_margin"]:
             put_d(n, getattr(self, n))
         for n in ["eq_type", "eq_obj1id", "eq_obj2id"]:
@@ -1328,7 +1400,8 @@ class CompiledModel:
             ngeom=len(self.geom_bodyid), nhull=len(self.hull_vertnum),
             nhullvert=len(self.hull_vert), npair=len(self.pair_geom1), neq=len(self.eq_type),
             ntendon=len(self.tendon_adr), nwrap=len(self.wrap_dofid), nu=self.nu, nmocap=self.nmocap,
-            nact=int(self.nact), maxcondim=maxdim, ncon_max=ncon_max, nefc_max=nefc_max,
+            nact=int(self.nact), npid=int(np.sum(np.asarray(self.actuator_gaintype) == GAIN_PID)),
+            maxcondim=maxdim, ncon_max=ncon_max, nefc_max=nefc_max,
             maxhullvert=int(self.hull_vertnum.max()) if len(self.hull_vertnum) else 0,
             iterations=int(o["iterations"]), noslip_iterations=int(o["noslip_iterations"]),
             cone=1, integrator=2, solver={"PGS": 0, "CG": 2, "Newton": 2}[o.get("solver", "Newton")],
@@ -1336,6 +1409,7 @@ class CompiledModel:
             timestep=float(o["timestep"]), impratio=float(o["impratio"]),
             tolerance=float(o["tolerance"]), noslip_tolerance=float(o["noslip_tolerance"]),
             mpr_tolerance=float(o.get("mpr_tolerance", 1e-6)), meaninertia=float(self.meaninertia),
+            ccd_mode=ccd_mode, ccd_iterations=int(o.get("ccd_iterations", 50)),
             gravity=[float(x) for x in o["gravity"]], isize=len(ib), dsize=len(db))
         return fields, ib, db
 

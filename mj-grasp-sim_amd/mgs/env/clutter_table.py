@@ -390,14 +390,17 @@ class ClutterTableEnv:
     SLICES = 1
 
     def rollout(self, plan: RolloutPlan, env_state, max_ncon: int = 128, slices: Optional[int] = None,
-                yield_every: Optional[int] = None):
+                yield_every: Optional[int] = None, on_capacity: str = "raise"):
         """engine rollout with contact-capacity escalation (continued from the
         overflowing step), in-launch rotation and optional time slices by
-        relaunch, as GravitylessObjectGrasping.rollout (sliced_rollout)."""
+        relaunch, as GravitylessObjectGrasping.rollout (sliced_rollout; a
+        candidate still over max_ncon raises CapacityError unless
+        on_capacity="capped")."""
         return sliced_rollout(plan, self.engine_for_state(env_state),
                               lambda c: self.engine_for_state(env_state, ncon_max=c), self.ncon_max, max_ncon,
                               self.SLICES if slices is None else slices,
-                              yield_every=self.YIELD_EVERY if yield_every is None else yield_every)
+                              yield_every=self.YIELD_EVERY if yield_every is None else yield_every,
+                              on_capacity=on_capacity)
 
     def grasp_stable_mask(self, poses: SE3Pose, joints: np.ndarray, env_state, nstep_lift: int = 3000,
                           lift_dist: float = 0.3, enough_stable=None, *, close_steps: Optional[int] = None,

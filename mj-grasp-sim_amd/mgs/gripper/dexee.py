@@ -98,8 +98,8 @@ class GripperDexee(MjShakableOpenCloseGripper):
         return mesh_inertial_xml(vol, data["com_" + name], data["inertia_" + name], _MASS[name] / vol)
 
     def _finger(self, data, f, pos, quat):
-        def col(mesh, cls, extra=""):
-            return f'<geom type="mesh" mesh="{mesh}" {cls}{extra}/>'
+        def col(mesh, cls, extra="", name=None):
+            return f'<geom name="{f}/{name or mesh.replace("_col", "_geom_col")}" type="mesh" mesh="{mesh}" {cls}{extra}/>'
 
         def joint(k):
             j, axis, rng, _, _ = _JOINTS[k]
@@ -107,7 +107,7 @@ class GripperDexee(MjShakableOpenCloseGripper):
                     'frictionloss="0.009"/>')
         return [f'<body name="{f}/" pos="{pos}" quat="{quat}">',
                 f'<body name="{f}/finger_base" gravcomp="1">', self._inertial(data, "finger_base"),
-                col("finger_base_col", _HARD, ' quat="1 -1 0 0"'),
+                col("finger_base_col", _HARD, ' quat="1 -1 0 0"', name="base_geom_col"),
                 f'<body name="{f}/finger_knuckle" pos="0 0.015 0.17902" quat="{_KNUCKLE_QUAT}" gravcomp="1">',
                 joint(0), self._inertial(data, "knuckle"), col("knuckle_col", _HARD),
                 f'<body name="{f}/finger_proximal" pos="0 -0.03 0" gravcomp="1">',
@@ -115,7 +115,8 @@ class GripperDexee(MjShakableOpenCloseGripper):
                 f'<body name="{f}/finger_middle" pos="0 -0.05 0" gravcomp="1">',
                 joint(2), self._inertial(data, "middle"), col("middle_col", _HARD),
                 f'<body name="{f}/finger_distal" pos="0 -0.035 0" quat="0 0 -1 1" gravcomp="1">',
-                joint(3), self._inertial(data, "distal"), col("distal_col", _HARD), col("tip_col", _SOFT),
+                joint(3), self._inertial(data, "distal"), col("distal_col", _HARD),
+                col("tip_col", _SOFT, name="distal_geom_tip_col"),
                 "</body></body></body></body></body></body>"]
 
     def to_xml(self) -> Tuple[str, Dict[str, Any]]:
@@ -135,7 +136,10 @@ class GripperDexee(MjShakableOpenCloseGripper):
                 f'<body name="dexee_gripper" pos="{pos}" quat="{quat}" gravcomp="1">',
                 '<freejoint name="freejoint"/>',
                 '<body name="hand_base" gravcomp="1">', self._inertial(data, "base"),
-                f'<geom type="mesh" mesh="base_col" {_HARD}/>', f'<geom type="mesh" mesh="puck_col" {_HARD}/>',
+                # the hand base's collision geoms carry no class (dexee.py:132,135-136):
+                # MuJoCo's geom defaults, condim 3, friction 1 0.005 0.0001, solref 0.02 1
+                '<geom name="hand_base_geom_col" type="mesh" mesh="base_col"/>',
+                '<geom name="hand_base_puck_geom_col" type="mesh" mesh="puck_col"/>',
                 "</body>"]
         for f, p, q in _FINGERS:
             out += self._finger(data, f, p, q)

@@ -721,11 +721,11 @@ static void cyl_support(double* v, const double* cy, const double* dl) {
   v[2] = dl[2] > 0.0 ? cy[1] : (dl[2] < 0.0 ? -cy[1] : 0.0);
 }
 
-static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, double* out) {
+/* support of geom g posed at (R, x) along the unit world direction dir */
+static int support_pose(const Mdl* md, int g, const double* R, const double* x, const double* dir, double* out) {
   int h = IA(md, geom_hullid)[g];
   int adr = IA(md, hull_vertadr)[h], num = IA(md, hull_vertnum)[h];
   const double* V = DA(md, hull_vert) + 3 * adr;
-  const double* R = d->geom_xmat + 9 * g;
   double dl[3];
   mulmtv3(dl, R, dir);
   double best = -INFINITY;
@@ -738,11 +738,15 @@ static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, d
   const double* cy = DA(md, geom_cyl) + 2 * g;
   if (cy[0] > 0.0) cyl_support(vb, cy, dl);
   mulmv3(t, R, vb);
-  add3(out, d->geom_xpos + 3 * g, t);
+  add3(out, x, t);
   /* rounded geoms (sphere, capsule): hull (+) ball; dir is a unit vector */
   double r = DA(md, geom_radius)[g];
   if (r > 0.0) { out[0] = out[0] + r * dir[0]; out[1] = out[1] + r * dir[1]; out[2] = out[2] + r * dir[2]; }
   return bi;
+}
+
+static int support_geom(const Mdl* md, const Dat* d, int g, const double* dir, double* out) {
+  return support_pose(md, g, d->geom_xmat + 9 * g, d->geom_xpos + 3 * g, dir, out);
 }
 
 static void mink_support(const Mdl* md, const Dat* d, int g1, int g2, const double* dir, SupPt* p) {
@@ -1441,6 +1445,557 @@ static void collide_boxbox(const Mdl* md, Dat* d, int pair) {
   }
 }
 
+/* ------------------------------------------------------------------------ */
+/* MuJoCo 3.2.2's collision table restated (ccd_mode 1 / 2, ABI 23; the kernels'
+ * collide_convex_mj / collide_prim).  PARITY UNPINNED: MuJoCo's source is not
+ * vendored in the reference or installed here, and no reference fixture holds
+ * a contact; the rules below restate the published algorithms (libccd 2.x's
+ * mpr.c, which MuJoCo 3.2.2 links for mjc_Convex; engine_collision_convex.c's
+ * multiccd; engine_collision_primitive.c) as documented in DESIGN.md §2.
+ *
+ * Convex pairs (mjc_Convex): libccd's ccdMPRPenetration -- portal discovery,
+ * refinement, penetration -- with libccd's tolerance tests (ccdIsZero / ccdEq at
+ * CCD_EPS = DBL_EPSILON), the depth as the distance from the origin to the final
+ * portal triangle (ccdVec3PointTriDist2) along its witness direction, and the
+ * position as the tetrahedron barycentre of the origin (findPos).  With the
+ * multiccd flag (both envs: gravityless_object_grasping.py:40,
+ * clutter_table.py:48) and no sphere in the pair, four more MPR runs with the
+ * geoms turned about their centres -- geom 1 by +-1e-3 rad and geom 2 by the
+ * opposite angle about each tangent of the first contact's frame -- add every
+ * contact farther than 1e-3 x the smaller bounding radius from the pair's
+ * contacts so far (<= 5 per pair).  Box pairs keep collide_boxbox. */
+#define CCD_EPS 2.2204460492503131e-16   /* libccd CCD_EPS, double build (DBL_EPSILON) */
+#define MCCD_ANGLE 1e-3                  /* multiccd perturbation angle */
+#define MCCD_RELTOL 1e-3                 /* multiccd distinct-contact tolerance, x min rbound */
+/* half-angle sine / cosine of the perturbation (literals: the kernels use the same doubles) */
+#define MCCD_C 0.9999998750000026       /* cos(5e-4) */
+#define MCCD_S 4.999999791666669e-04    /* sin(5e-4) */
+#define CCD_MAXLOOP 64                   /* safety cap of libccd's unbounded discovery / refinement loops */
+static inline int ccd_iszero(double x) { return fabs(x) < CCD_EPS; }
+static inline int ccd_eq(double a, double b) {
+  double ab = fabs(a - b);
+  if (ab < CCD_EPS) return 1;
+  double fa = fabs(a), fb = fabs(b);
+  return fb > fa ? (ab < CCD_EPS * fb) : (ab < CCD_EPS * fa);
+}
+static inline int ccd_vzero(const double* a) { return ccd_eq(a[0], 0.0) && ccd_eq(a[1], 0.0) && ccd_eq(a[2], 0.0); }
+/* ccdVec3Normalize: scale by 1 / sqrt(|v|^2) */
+static inline void ccd_normalize(double* v) {
+  double k = 1.0 / sqrt(dot3(v, v));
+  v[0] = v[0] * k; v[1] = v[1] * k; v[2] = v[2] * k;
+}
+static inline void mulmm3(double* r, const double* a, const double* b) {
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = (a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j];
+  for (int k = 0; k < 9; k++) r[k] = t[k];
+}
+
+typedef struct { int g; const double* R; const double* x; } CObj;
+static void ccd_support(const Mdl* md, const CObj* o1, const CObj* o2, const double* dir, SupPt* p) {
+  g_sup_calls++;
+  double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  support_pose(md, o1->g, o1->R, o1->x, dir, p->a);
+  support_pose(md, o2->g, o2->R, o2->x, nd, p->b);
+  sub3(p->v, p->a, p->b);
+}
+/* portalReachTolerance with ccdEq */
+static int ccd_reach_tol(const SupPt* p1, const SupPt* p2, const SupPt* p3, const SupPt* p4, const double* n,
+                         double tol) {
+  double dv4 = dot3(p4->v, n);
+  double t1 = dv4 - dot3(p1->v, n);
+  double t2 = dv4 - dot3(p2->v, n);
+  double t3 = dv4 - dot3(p3->v, n);
+  double mn = t1 < t2 ? t1 : t2;
+  mn = mn < t3 ? mn : t3;
+  return ccd_eq(mn, tol) || mn < tol;
+}
+static void ccd_portal_dir(double* n, const SupPt* p1, const SupPt* p2, const SupPt* p3) {
+  double e1[3], e2[3];
+  sub3(e1, p2->v, p1->v);
+  sub3(e2, p3->v, p1->v);
+  cross3(n, e1, e2);
+  ccd_normalize(n);
+}
+/* __ccdVec3PointSegmentDist2 (P = origin) */
+static double ccd_seg_dist2(const double* x0, const double* b, double* w) {
+  double dd[3], a[3] = {x0[0], x0[1], x0[2]};
+  sub3(dd, b, x0);
+  double t = -dot3(a, dd);
+  t = t / dot3(dd, dd);
+  if (t < 0.0 || ccd_iszero(t)) {
+    w[0] = x0[0]; w[1] = x0[1]; w[2] = x0[2];
+  } else if (t > 1.0 || ccd_eq(t, 1.0)) {
+    w[0] = b[0]; w[1] = b[1]; w[2] = b[2];
+  } else {
+    w[0] = dd[0] * t + x0[0]; w[1] = dd[1] * t + x0[1]; w[2] = dd[2] * t + x0[2];
+  }
+  return dot3(w, w);
+}
+/* ccdVec3PointTriDist2 (P = origin) with its witness point */
+static double ccd_tri_dist2(const double* x0, const double* B, const double* C, double* w) {
+  double d1[3], d2[3];
+  sub3(d1, B, x0);
+  sub3(d2, C, x0);
+  const double* a = x0;
+  double v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  double dt = ww * v - r * r, s, t;
+  if (ccd_iszero(dt)) {
+    s = -1.0; t = -1.0;
+  } else {
+    s = (q * r - ww * p) / dt;
+    t = (-s * r - q) / ww;
+  }
+  if ((ccd_iszero(s) || s > 0.0) && (ccd_eq(s, 1.0) || s < 1.0) && (ccd_iszero(t) || t > 0.0) &&
+      (ccd_eq(t, 1.0) || t < 1.0) && (ccd_eq(t + s, 1.0) || t + s < 1.0)) {
+    for (int k = 0; k < 3; k++) w[k] = (x0[k] + d1[k] * s) + d2[k] * t;
+    return dot3(w, w);
+  }
+  double w2[3];
+  double dist = ccd_seg_dist2(x0, B, w);
+  double d2b = ccd_seg_dist2(x0, C, w2);
+  if (d2b < dist) { dist = d2b; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  d2b = ccd_seg_dist2(B, C, w2);
+  if (d2b < dist) { dist = d2b; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  return dist;
+}
+/* findPos: the origin's barycentric coordinates in the tetrahedron (v0..v3),
+ * or in the portal triangle when they degenerate; pos = mean of the two
+ * objects' weighted support points */
+static void ccd_find_pos(const SupPt* p0, const SupPt* p1, const SupPt* p2, const SupPt* p3, double* pos) {
+  double dir[3], c[3], b[4];
+  ccd_portal_dir(dir, p1, p2, p3);
+  cross3(c, p1->v, p2->v); b[0] = dot3(c, p3->v);
+  cross3(c, p3->v, p2->v); b[1] = dot3(c, p0->v);
+  cross3(c, p0->v, p1->v); b[2] = dot3(c, p3->v);
+  cross3(c, p2->v, p1->v); b[3] = dot3(c, p0->v);
+  double sum = ((b[0] + b[1]) + b[2]) + b[3];
+  if (ccd_iszero(sum) || sum < 0.0) {
+    b[0] = 0.0;
+    cross3(c, p2->v, p3->v); b[1] = dot3(c, dir);
+    cross3(c, p3->v, p1->v); b[2] = dot3(c, dir);
+    cross3(c, p1->v, p2->v); b[3] = dot3(c, dir);
+    sum = (b[1] + b[2]) + b[3];
+  }
+  double inv = 1.0 / sum;
+  const SupPt* P[4] = {p0, p1, p2, p3};
+  double a1[3] = {0.0, 0.0, 0.0}, a2[3] = {0.0, 0.0, 0.0};
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 3; k++) {
+      a1[k] = a1[k] + P[i]->a[k] * b[i];
+      a2[k] = a2[k] + P[i]->b[k] * b[i];
+    }
+  for (int k = 0; k < 3; k++) pos[k] = (a1[k] * inv + a2[k] * inv) * 0.5;
+}
+
+#define CCD_CERT(P) do { *cm = -dot3((P).v, dir); cd[0] = dir[0]; cd[1] = dir[1]; cd[2] = dir[2]; } while (0)
+/* ccdMPRPenetration: 1 with the unit normal n (geom 1 -> geom 2), depth > 0 and
+ * position; 0 without penetration, or when libccd's normal is undefined
+ * (touching, depth 0: mjc_CCDIteration then makes no contact).  cd / cm: the
+ * separating direction of a certified miss (as mpr_penetration). */
+static int ccd_mpr(const Mdl* md, const CObj* o1, const CObj* o2, double* n, double* depth, double* pos,
+                   double* cd, double* cm) {
+  *cm = -1.0;
+  const double tol = md->m->mpr_tolerance;
+  const int maxit = md->m->ccd_iterations;
+  SupPt p0, p1, p2, p3, p4;
+  double dir[3], dt;
+  /* findOrigin: the geom centres (mjccd_center: geom_xpos) */
+  for (int k = 0; k < 3; k++) { p0.a[k] = o1->x[k]; p0.b[k] = o2->x[k]; }
+  sub3(p0.v, p0.a, p0.b);
+  if (ccd_vzero(p0.v)) p0.v[0] = p0.v[0] + CCD_EPS * 10.0;
+  dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
+  ccd_normalize(dir);
+  ccd_support(md, o1, o2, dir, &p1);
+  dt = dot3(p1.v, dir);
+  if (ccd_iszero(dt) || dt < 0.0) { CCD_CERT(p1); return 0; }
+  cross3(dir, p0.v, p1.v);
+  if (ccd_iszero(dot3(dir, dir))) {
+    if (ccd_vzero(p1.v)) return 0;           /* touching at v1: normal undefined */
+    /* findPenetrSegment: the origin on the segment v0-v1 */
+    for (int k = 0; k < 3; k++) { n[k] = p1.v[k]; pos[k] = (p1.a[k] + p1.b[k]) * 0.5; }
+    *depth = sqrt(dot3(n, n));
+    ccd_normalize(n);
+    return 1;
+  }
+  ccd_normalize(dir);
+  ccd_support(md, o1, o2, dir, &p2);
+  dt = dot3(p2.v, dir);
+  if (ccd_iszero(dt) || dt < 0.0) { CCD_CERT(p2); return 0; }
+  {
+    double e1[3], e2[3];
+    sub3(e1, p1.v, p0.v);
+    sub3(e2, p2.v, p0.v);
+    cross3(dir, e1, e2);
+    ccd_normalize(dir);
+  }
+  if (dot3(dir, p0.v) > 0.0) {
+    SupPt tmp = p1; p1 = p2; p2 = tmp;
+    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+  }
+  int it;
+  for (it = 0; it < CCD_MAXLOOP; it++) {
+    ccd_support(md, o1, o2, dir, &p3);
+    dt = dot3(p3.v, dir);
+    if (ccd_iszero(dt) || dt < 0.0) { CCD_CERT(p3); return 0; }
+    double c[3];
+    int cont = 0;
+    cross3(c, p1.v, p3.v);
+    dt = dot3(c, p0.v);
+    if (dt < 0.0 && !ccd_iszero(dt)) { p2 = p3; cont = 1; }
+    if (!cont) {
+      cross3(c, p3.v, p2.v);
+      dt = dot3(c, p0.v);
+      if (dt < 0.0 && !ccd_iszero(dt)) { p1 = p3; cont = 1; }
+    }
+    if (!cont) break;
+    double e1[3], e2[3];
+    sub3(e1, p1.v, p0.v);
+    sub3(e2, p2.v, p0.v);
+    cross3(dir, e1, e2);
+    ccd_normalize(dir);
+  }
+  if (it == CCD_MAXLOOP) return 0;
+  /* refinePortal */
+  for (it = 0; it < CCD_MAXLOOP; it++) {
+    ccd_portal_dir(dir, &p1, &p2, &p3);
+    dt = dot3(dir, p1.v);
+    if (ccd_iszero(dt) || dt > 0.0) break;
+    ccd_support(md, o1, o2, dir, &p4);
+    dt = dot3(p4.v, dir);
+    if (!(ccd_iszero(dt) || dt > 0.0)) { CCD_CERT(p4); return 0; }
+    if (ccd_reach_tol(&p1, &p2, &p3, &p4, dir, tol)) return 0;
+    portal_expand(&p0, &p1, &p2, &p3, &p4);
+  }
+  if (it == CCD_MAXLOOP) return 0;
+  /* findPenetr */
+  for (it = 0;; it++) {
+    ccd_portal_dir(dir, &p1, &p2, &p3);
+    ccd_support(md, o1, o2, dir, &p4);
+    if (ccd_reach_tol(&p1, &p2, &p3, &p4, dir, tol) || it > maxit) {
+      double w[3];
+      double dep = sqrt(ccd_tri_dist2(p1.v, p2.v, p3.v, w));
+      if (ccd_iszero(dep)) return 0;         /* touching: normal undefined */
+      n[0] = w[0]; n[1] = w[1]; n[2] = w[2];
+      ccd_normalize(n);
+      *depth = dep;
+      ccd_find_pos(&p0, &p1, &p2, &p3, pos);
+      return 1;
+    }
+    portal_expand(&p0, &p1, &p2, &p3, &p4);
+  }
+}
+#undef CCD_CERT
+
+static inline double mccd_rbound(const Mdl* md, int g) {
+  return DA(md, geom_rbound)[g] + DA(md, geom_radius)[g];    /* MuJoCo geom_rbound */
+}
+/* mjc_Convex with multiccd (multi = 1) or one contact (multi = 0) */
+static void collide_convex_mj(const Mdl* md, Dat* d, int pair, int multi) {
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  const double *R1 = d->geom_xmat + 9 * g1, *R2 = d->geom_xmat + 9 * g2;
+  const double *x1 = d->geom_xpos + 3 * g1, *x2 = d->geom_xpos + 3 * g2;
+  CObj o1 = {g1, R1, x1}, o2 = {g2, R2, x2};
+  double n[3], depth, pos[3], cd[3] = {0.0, 0.0, 0.0}, cm;
+  int hit = ccd_mpr(md, &o1, &o2, n, &depth, pos, cd, &cm);
+  cert_update(md, d, pair, g1, g2, hit, cd, cm);
+  if (!hit) return;
+  double t1[3], t2[3];
+  make_frame(n, t1, t2);
+  add_contact(md, d, pair, g1, g2, pos, n, t1, t2, -depth);
+  if (!multi) return;
+  double cp[5][3];
+  cp[0][0] = pos[0]; cp[0][1] = pos[1]; cp[0][2] = pos[2];
+  int nc = 1;
+  double rb1 = mccd_rbound(md, g1), rb2 = mccd_rbound(md, g2);
+  double tolr = MCCD_RELTOL * (rb1 < rb2 ? rb1 : rb2);
+  for (int ax = 0; ax < 2; ax++) {
+    const double* axis = ax ? t2 : t1;
+    for (int sg = 0; sg < 2; sg++) {
+      /* geom 1 turned by -angle then +angle about the axis, geom 2 the opposite way */
+      double s = sg ? MCCD_S : -MCCD_S;
+      double q1[4] = {MCCD_C, axis[0] * s, axis[1] * s, axis[2] * s};
+      double q2[4] = {MCCD_C, -(axis[0] * s), -(axis[1] * s), -(axis[2] * s)};
+      double M1[9], M2[9], R1p[9], R2p[9];
+      quat2mat(M1, q1);
+      quat2mat(M2, q2);
+      mulmm3(R1p, M1, R1);
+      mulmm3(R2p, M2, R2);
+      CObj p1o = {g1, R1p, x1}, p2o = {g2, R2p, x2};
+      double nn[3], dd, pp[3], cdx[3], cmx;
+      if (!ccd_mpr(md, &p1o, &p2o, nn, &dd, pp, cdx, &cmx)) continue;
+      int isnew = 1;
+      for (int k = 0; k < nc; k++) {
+        double dx[3];
+        sub3(dx, pp, cp[k]);
+        if (sqrt(dot3(dx, dx)) < tolr) isnew = 0;
+      }
+      if (!isnew) continue;
+      cp[nc][0] = pp[0]; cp[nc][1] = pp[1]; cp[nc][2] = pp[2];
+      nc++;
+      double u1[3], u2[3];
+      make_frame(nn, u1, u2);
+      add_contact(md, d, pair, g1, g2, pp, nn, u1, u2, -dd);
+    }
+  }
+}
+
+/* Analytic primitive colliders (engine_collision_primitive.c restated; the
+ * normal points from geom 1 to geom 2, the position is midway between the two
+ * surfaces, dist < 0 in penetration; a pair makes contacts with dist <= margin). */
+static inline double dist3(const double* a, const double* b) {
+  double dx[3];
+  sub3(dx, a, b);
+  return sqrt(dot3(dx, dx));
+}
+/* mjraw_SphereSphere: spheres (p1, r1) and (p2, r2); z1 / z2 the geoms' z axes
+ * (the normal of concentric spheres: their cross product, else x) */
+static int raw_sphere_sphere(const double* p1, const double* z1, double r1, const double* p2, const double* z2,
+                             double r2, double margin, double* pos, double* n, double* dist) {
+  double dd = (dist3(p1, p2) - r1) - r2;
+  if (dd > margin) return 0;
+  sub3(n, p2, p1);
+  if (normalize3(n) < O_MINVAL) {
+    cross3(n, z1, z2);
+    normalize3(n);
+  }
+  double s = r1 + 0.5 * dd;
+  for (int k = 0; k < 3; k++) pos[k] = p1[k] + n[k] * s;
+  *dist = dd;
+  return 1;
+}
+/* sphere (centre c, radius r) against the box (x, R, half sizes s): the box
+ * point nearest the centre; a centre inside the box leaves through the face of
+ * least depth (first on ties) */
+static int raw_sphere_box(const double* c, double r, const double* x, const double* R, const double* s, double margin,
+                          double* pos, double* n, double* dist) {
+  double t[3], cl[3], q[3], df[3], nl[3], pl[3];
+  sub3(t, c, x);
+  mulmtv3(cl, R, t);
+  for (int k = 0; k < 3; k++) q[k] = cl[k] < -s[k] ? -s[k] : (cl[k] > s[k] ? s[k] : cl[k]);
+  sub3(df, q, cl);
+  double dc = sqrt(dot3(df, df));
+  if (dc - r > margin) return 0;
+  double dd;
+  if (dc > O_MINVAL) {
+    for (int k = 0; k < 3; k++) nl[k] = df[k] / dc;
+    dd = dc - r;
+  } else {
+    int kk = 0;
+    double a = s[0] - fabs(cl[0]);
+    for (int k = 1; k < 3; k++) {
+      double ak = s[k] - fabs(cl[k]);
+      if (ak < a) { a = ak; kk = k; }
+    }
+    nl[0] = nl[1] = nl[2] = 0.0;
+    nl[kk] = cl[kk] >= 0.0 ? -1.0 : 1.0;
+    dd = -(a + r);
+  }
+  double h = r + 0.5 * dd;
+  for (int k = 0; k < 3; k++) pl[k] = cl[k] + nl[k] * h;
+  mulmv3(n, R, nl);
+  mulmv3(t, R, pl);
+  add3(pos, x, t);
+  *dist = dd;
+  return 1;
+}
+/* signed distance of a box-frame point to the box (negative inside) */
+static double box_phi(const double* p, const double* s) {
+  double o0 = fabs(p[0]) - s[0], o1 = fabs(p[1]) - s[1], o2 = fabs(p[2]) - s[2];
+  if (o0 > 0.0 || o1 > 0.0 || o2 > 0.0) {
+    double a = o0 > 0.0 ? o0 : 0.0, b = o1 > 0.0 ? o1 : 0.0, c = o2 > 0.0 ? o2 : 0.0;
+    return sqrt((a * a + b * b) + c * c);
+  }
+  double m = o0 > o1 ? o0 : o1;
+  return m > o2 ? m : o2;
+}
+/* capsule segment parameter of candidate k (0..MGS_CB_NCAND-1) in the box frame
+ * (centre c, half axis a): the stationary points of the segment's signed
+ * distance to the box, which is convex along the segment -- the ends, the slab
+ * crossings, the minimisers of each outside active set, the equal-depth points
+ * of two face planes.  Returns 0 for a candidate that does not exist. */
+#define MGS_CB_NCAND 49
+static int capbox_cand(int k, const double* c, const double* a, const double* s, double* tout) {
+  double t;
+  if (k < 2) { *tout = k ? 1.0 : -1.0; return 1; }
+  if (k < 8) {
+    int i = (k - 2) >> 1;
+    double sg = ((k - 2) & 1) ? 1.0 : -1.0;
+    if (fabs(a[i]) < O_MINVAL) return 0;
+    t = (sg * s[i] - c[i]) / a[i];
+  } else if (k < 34) {
+    int code = k - 8 + 1;      /* 1..26: base-3 digits = per-axis side (0 in, 1 below, 2 above) */
+    double num = 0.0, den = 0.0;
+    for (int i = 0; i < 3; i++) {
+      int dgt = code % 3;
+      code /= 3;
+      if (dgt == 0) continue;
+      double sg = dgt == 1 ? -1.0 : 1.0;
+      num = num + (c[i] - sg * s[i]) * a[i];
+      den = den + a[i] * a[i];
+    }
+    if (den < O_MINVAL) return 0;
+    t = -num / den;
+    t = t < -1.0 ? -1.0 : (t > 1.0 ? 1.0 : t);
+    *tout = t;
+    return 1;
+  } else {
+    /* face lines l = 2 i + side: side(c_i + t a_i) - s_i; pairs in lexicographic order */
+    int q = k - 34, l1 = 0, l2 = 1;
+    for (int x = 0; x < 6; x++)
+      for (int y = x + 1; y < 6; y++) {
+        if (q == 0) { l1 = x; l2 = y; }
+        q--;
+      }
+    int i = l1 >> 1, j = l2 >> 1;
+    double si = (l1 & 1) ? 1.0 : -1.0, sj = (l2 & 1) ? 1.0 : -1.0;
+    double coef = si * a[i] - sj * a[j];
+    if (fabs(coef) < O_MINVAL) return 0;
+    t = ((s[i] - s[j]) - (si * c[i] - sj * c[j])) / coef;
+  }
+  if (!(t >= -1.0 && t <= 1.0)) return 0;
+  *tout = t;
+  return 1;
+}
+static void collide_prim(const Mdl* md, Dat* d, int pair, int kind) {
+  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
+  const double *R1 = d->geom_xmat + 9 * g1, *R2 = d->geom_xmat + 9 * g2;
+  const double *x1 = d->geom_xpos + 3 * g1, *x2 = d->geom_xpos + 3 * g2;
+  const double *s1 = DA(md, geom_size) + 3 * g1, *s2 = DA(md, geom_size) + 3 * g2;
+  const double margin = DA(md, pair_margin)[pair];
+  double z1[3] = {R1[2], R1[5], R1[8]}, z2[3] = {R2[2], R2[5], R2[8]};
+  double pos[2][3], n[2][3], dist[2];
+  int nc = 0;
+  if (kind == MGS_PAIR_SPHERE_SPHERE) {
+    nc = raw_sphere_sphere(x1, z1, s1[0], x2, z2, s2[0], margin, pos[0], n[0], dist);
+  } else if (kind == MGS_PAIR_SPHERE_CAPSULE) {
+    /* the capsule axis point nearest the sphere centre, then sphere-sphere */
+    double v[3], q[3];
+    sub3(v, x1, x2);
+    double xx = dot3(z2, v);
+    xx = xx < -s2[1] ? -s2[1] : (xx > s2[1] ? s2[1] : xx);
+    for (int k = 0; k < 3; k++) q[k] = x2[k] + z2[k] * xx;
+    nc = raw_sphere_sphere(x1, z1, s1[0], q, z2, s2[0], margin, pos[0], n[0], dist);
+  } else if (kind == MGS_PAIR_CAPSULE_CAPSULE) {
+    double a1[3], a2[3], df[3];
+    for (int k = 0; k < 3; k++) { a1[k] = z1[k] * s1[1]; a2[k] = z2[k] * s2[1]; }
+    sub3(df, x1, x2);
+    double ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+    double u = -dot3(a1, df), v = dot3(a2, df);
+    double det = ma * mc - mb * mb;
+    double v1[3], v2[3];
+    if (fabs(det) >= O_MINVAL) {
+      double xa = (mc * u - mb * v) / det, xb = (ma * v - mb * u) / det;
+      if (xa > 1.0) { xa = 1.0; xb = (v - mb) / mc; }
+      else if (xa < -1.0) { xa = -1.0; xb = (v + mb) / mc; }
+      if (xb > 1.0) {
+        xb = 1.0;
+        xa = (u - mb) / ma;
+        xa = xa < -1.0 ? -1.0 : (xa > 1.0 ? 1.0 : xa);
+      } else if (xb < -1.0) {
+        xb = -1.0;
+        xa = (u + mb) / ma;
+        xa = xa < -1.0 ? -1.0 : (xa > 1.0 ? 1.0 : xa);
+      }
+      for (int k = 0; k < 3; k++) { v1[k] = x1[k] + a1[k] * xa; v2[k] = x2[k] + a2[k] * xb; }
+      nc = raw_sphere_sphere(v1, z1, s1[0], v2, z2, s2[0], margin, pos[0], n[0], dist);
+    } else {
+      /* parallel axes: the ends of each against the other segment, <= 2 contacts */
+      for (int e = 0; e < 4 && nc < 2; e++) {
+        double sg = (e & 1) ? -1.0 : 1.0, xx;
+        if (e < 2) {
+          xx = (sg > 0.0 ? (v - mb) : (v + mb)) / mc;
+          xx = xx < -1.0 ? -1.0 : (xx > 1.0 ? 1.0 : xx);
+          for (int k = 0; k < 3; k++) { v1[k] = x1[k] + sg * a1[k]; v2[k] = x2[k] + a2[k] * xx; }
+        } else {
+          xx = (sg > 0.0 ? (u - mb) : (u + mb)) / ma;
+          xx = xx < -1.0 ? -1.0 : (xx > 1.0 ? 1.0 : xx);
+          for (int k = 0; k < 3; k++) { v2[k] = x2[k] + sg * a2[k]; v1[k] = x1[k] + a1[k] * xx; }
+        }
+        nc += raw_sphere_sphere(v1, z1, s1[0], v2, z2, s2[0], margin, pos[nc], n[nc], dist + nc);
+      }
+    }
+  } else if (kind == MGS_PAIR_SPHERE_BOX) {
+    nc = raw_sphere_box(x1, s1[0], x2, R2, s2, margin, pos[0], n[0], dist);
+  } else if (kind == MGS_PAIR_CAPSULE_BOX) {
+    /* the segment point deepest in / nearest to the box, then sphere-box; a
+     * capsule whose two ends both touch the same face makes one contact at
+     * each end */
+    double t[3], c[3], a[3], hz[3];
+    sub3(t, x1, x2);
+    mulmtv3(c, R2, t);
+    for (int k = 0; k < 3; k++) hz[k] = z1[k] * s1[1];
+    mulmtv3(a, R2, hz);
+    double best = INFINITY, tb = -1.0;
+    for (int k = 0; k < MGS_CB_NCAND; k++) {
+      double tk, p[3];
+      if (!capbox_cand(k, c, a, s2, &tk)) continue;
+      for (int i = 0; i < 3; i++) p[i] = c[i] + a[i] * tk;
+      double ph = box_phi(p, s2);
+      if (ph < best) { best = ph; tb = tk; }
+    }
+    double ctr[3], pe[2][3], ne[2][3], de[2];
+    for (int k = 0; k < 3; k++) ctr[k] = x1[k] + hz[k] * tb;
+    nc = raw_sphere_box(ctr, s1[0], x2, R2, s2, margin, pos[0], n[0], dist);
+    if (nc) {
+      int ok = 1;
+      for (int e = 0; e < 2 && ok; e++) {
+        double sg = e ? 1.0 : -1.0, ce[3];
+        for (int k = 0; k < 3; k++) ce[k] = x1[k] + hz[k] * sg;
+        ok = raw_sphere_box(ce, s1[0], x2, R2, s2, margin, pe[e], ne[e], de + e) &&
+             ne[e][0] == n[0][0] && ne[e][1] == n[0][1] && ne[e][2] == n[0][2];
+      }
+      if (ok) {
+        for (int e = 0; e < 2; e++) {
+          for (int k = 0; k < 3; k++) { pos[e][k] = pe[e][k]; n[e][k] = ne[e][k]; }
+          dist[e] = de[e];
+        }
+        nc = 2;
+      }
+    }
+  } else if (kind == MGS_PAIR_SPHERE_CYLINDER) {
+    double t[3], cl[3], q[3], df[3], nl[3], pl[3];
+    const double r = s1[0], cr = s2[0], ch = s2[1];
+    sub3(t, x1, x2);
+    mulmtv3(cl, R2, t);
+    double rho = sqrt(cl[0] * cl[0] + cl[1] * cl[1]);
+    if (rho > cr) { q[0] = cl[0] / rho * cr; q[1] = cl[1] / rho * cr; }
+    else { q[0] = cl[0]; q[1] = cl[1]; }
+    q[2] = cl[2] < -ch ? -ch : (cl[2] > ch ? ch : cl[2]);
+    sub3(df, q, cl);
+    double dc = sqrt(dot3(df, df)), dd;
+    if (dc - r <= margin) {
+      if (dc > O_MINVAL) {
+        for (int k = 0; k < 3; k++) nl[k] = df[k] / dc;
+        dd = dc - r;
+      } else {
+        double side = cr - rho, cap = ch - fabs(cl[2]), a;
+        if (side < cap && rho > O_MINVAL) {
+          nl[0] = -(cl[0] / rho); nl[1] = -(cl[1] / rho); nl[2] = 0.0;
+          a = side;
+        } else {
+          nl[0] = nl[1] = 0.0;
+          nl[2] = cl[2] >= 0.0 ? -1.0 : 1.0;
+          a = cap;
+        }
+        dd = -(a + r);
+      }
+      double h = r + 0.5 * dd;
+      for (int k = 0; k < 3; k++) pl[k] = cl[k] + nl[k] * h;
+      mulmv3(n[0], R2, nl);
+      mulmv3(t, R2, pl);
+      add3(pos[0], x2, t);
+      dist[0] = dd;
+      nc = 1;
+    }
+  }
+  for (int c = 0; c < nc; c++) {
+    double t1[3], t2[3];
+    make_frame(n[c], t1, t2);
+    add_contact(md, d, pair, g1, g2, pos[c], n[c], t1, t2, dist[c]);
+  }
+}
+
 #define OBB_FN static
 /* Second broadphase stage: separating-axis test between the geoms' oriented
  * bounding boxes (their local AABBs posed in the world; 15 axes).  Each convex
@@ -1513,8 +2068,12 @@ static void collision(const Mdl* md, Dat* d) {
       if (p < 256) g_pair_bp[p]++;
       int n0 = d->ncon;
       long s0 = g_sup_calls;
-      if (IA(md, pair_kind)[p] == MGS_PAIR_BOXBOX) collide_boxbox(md, d, p);
-      else collide_pair(md, d, p);
+      int kind = IA(md, pair_kind)[p];
+      if (kind == MGS_PAIR_BOXBOX) collide_boxbox(md, d, p);
+      else if (m->ccd_mode == MGS_CCD_R5) collide_pair(md, d, p);
+      else if (kind == MGS_PAIR_CONVEX || kind == MGS_PAIR_CONVEX_SMOOTH)
+        collide_convex_mj(md, d, p, kind == MGS_PAIR_CONVEX && m->ccd_mode == MGS_CCD_MULTI);
+      else collide_prim(md, d, p, kind);
       if (p < 256) g_pair_sup[p] += g_sup_calls - s0;
       if (p < 256 && d->ncon > n0) g_pair_hit[p]++;
     }
@@ -2695,7 +3254,7 @@ static void integrate(const Mdl* md, Dat* d) {
     if (pp[1] != 0.0) {
       double v = d->act[k] + dt * d->act_dot[k];
       if (pp[3] >= 0.0) {
-        const double lim = pp[3] / pp[1];
+        const double lim = pp[3] / fabs(pp[1]);
         if (v < -lim) v = -lim;
         if (v > lim) v = lim;
       }

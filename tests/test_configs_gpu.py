@@ -202,7 +202,9 @@ def test_allegro_gso_oracle(genv, gcand):
     from conftest import plan_for
     from oracle import oracle as O
     poses, J = gcand
-    om = O.OracleModel(genv.model, ncon_max=genv.ncon_max, nefc_max=genv.nefc_max)
+    # full capacity (the last stage of the env's escalation, 64 contacts / 256
+    # rows is beyond it): multiccd contacts of a hand grasp fit, nothing capped
+    om = O.OracleModel(genv.model, ncon_max=64, nefc_max=256)
     q, mp, mq, _ = genv.initial_state(poses, J)
     free = om.collision_free(q, mp, mq, nthreads=8)
     assert 16 <= free.sum() < len(free)

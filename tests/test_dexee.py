@@ -46,7 +46,8 @@ def dom(denv):
 def test_dexee_model(denv):
     cm = denv.model
     assert (cm.nv, cm.nu, cm.nact) == (24, 12, 24)          # gripper free joint + 12 finger joints + object
-    assert set(np.unique(cm.pair_condim)) == {4, 6}
+    # the hand base's two collision geoms have MuJoCo's defaults (condim 3)
+    assert set(np.unique(cm.pair_condim)) == {3, 4, 6}
     assert list(cm.actuator_actadr) == list(range(0, 24, 2))
     fields, _, _ = cm.pack(ncon_max=denv.ncon_max)
     assert fields["maxcondim"] == 6 and fields["nact"] == 24
@@ -54,6 +55,32 @@ def test_dexee_model(denv):
     assert np.allclose(cm.actuator_pidprm[0], [2.8, 4.0, 0.03, 0.1, 3.14159])
     assert denv.gripper.close_steps == 500
     assert np.array_equal(denv.gripper.close_ctrl(None), CLOSE)
+
+
+def test_dexee_collision_geom_classes(denv):
+    """every DEXEE collision geom's condim / friction / solref / priority as the
+    template's default classes give them (dexee.py:39-47): finger/collision_hard
+    on the finger links (dexee.py:154-186), finger/collision_soft on the
+    fingertip pads (:187), and no class -- MuJoCo's geom defaults -- on the hand
+    base's two geoms (:132,135-136)"""
+    cm = denv.model
+    hard = (4, [1.0, 0.001, 2e-05], [-7000.0, -167.0])
+    soft = (6, [1.0, 0.005, 0.0001], [-2500.0, -100.0])
+    default = (3, [1.0, 0.005, 0.0001], [0.02, 1.0])
+    want = {"hand_base_geom_col": default, "hand_base_puck_geom_col": default}
+    for f in ("F0", "F1", "F2"):
+        for link in ("base", "knuckle", "proximal", "middle", "distal"):
+            want[f"{f}/{link}_geom_col"] = hard
+        want[f"{f}/distal_geom_tip_col"] = soft
+    names = list(cm.geom_names)
+    for name, (condim, fr, sr) in want.items():
+        g = names.index(name)
+        assert cm.geom_condim[g] == condim, name
+        assert np.array_equal(cm.geom_friction[g], fr), name
+        assert np.array_equal(cm.geom_solref[g], sr), name
+        assert cm.geom_priority[g] == 0, name
+    # the gripper's collision geoms are exactly these (the object and the ground follow)
+    assert sum(n in want for n in names) == len(want) == 20
 
 
 PID_XML = """
@@ -248,3 +275,66 @@ def test_gravcomp_gpu_parity():
     g, o = eng.simulate(plan, vstate=vs), om.simulate_batch(plan, vstate=vs)
     for k in ("qpos", "qvel", "qacc_warmstart"):
         assert np.array_equal(g[k], o[k]), k
+
+
+PID_KPKD_XML = PID_XML.replace('<config key="ki" value="4.0"/>', '<config key="ki" value="0"/>') \
+    .replace('<config key="imax" value="0.1"/><config key="slewmax" value="3.14159"/>', '') \
+    .replace(' actdim="2"', ' actdim="0"')
+
+
+def _pid_plan(cm, ctrl, nsteps, n=1, q=None, vs=None):
+    from types import SimpleNamespace
+    z = np.zeros((n, 1, 3))
+    return SimpleNamespace(nsteps=[nsteps], check_every=[0], check_at_end=[0], ctrl=[np.array([ctrl])],
+                           obj_qposadr=-1, check_offset=None,
+                           qpos_init=np.tile(cm.qpos0, (n, 1)) if q is None else q,
+                           mocap_quat=np.tile([1.0, 0, 0, 0], (n, 1)), phase_start=z, phase_target=z)
+
+
+def test_pid_kp_kd_only_has_no_act_state():
+    """a mujoco.pid actuator with ki = 0 and no slewmax has no act entries
+    (nact 0) and is still a pid: force kp (ctrl - q) + kd (0 - v), clamped"""
+    from mgs.core.mjcf import compile_xml
+    from oracle import oracle as O
+    cm = compile_xml(PID_KPKD_XML)
+    assert (cm.nu, cm.nact) == (1, 0)
+    fields, _, _ = cm.pack()
+    assert fields["npid"] == 1 and fields["nact"] == 0
+    r = O.OracleModel(cm).simulate_batch(_pid_plan(cm, 0.8, 200))
+    # by hand: the same loop without slew / integral
+    kp, kd, dt, inertia = 2.8, 0.03, 0.002, (0.1 ** 2 + 0.02 ** 2) / 3.0
+    q = v = 0.0
+    for _ in range(200):
+        f = min(max(kp * (0.8 - q) + kd * (0.0 - v), -0.9), 0.53)
+        v = v + dt * (f / inertia)
+        q = q + dt * v
+    assert np.allclose([r["qpos"][0, 0], r["qvel"][0, 0]], [q, v], rtol=1e-9, atol=1e-12)
+
+
+def test_pid_negative_ki_clamps_by_magnitude():
+    """|ki integral| <= imax also for ki < 0 (the clamp bound is imax / |ki|)"""
+    from mgs.core.mjcf import compile_xml
+    from oracle import oracle as O
+    cm = compile_xml(PID_XML.replace('value="4.0"', 'value="-4.0"'))
+    r = O.OracleModel(cm).simulate_batch(_pid_plan(cm, 0.8, 400))
+    assert abs(r["act"][0, 1]) <= 0.1 / 4.0 + 1e-15
+    assert r["act"][0, 1] > 0.0          # the error stays positive: the integral sits at +imax / |ki|
+
+
+@pytest.mark.gpu
+def test_pid_kp_kd_only_gpu_parity():
+    """the kernel took the pid branch only for models with act
+    state; a kp / kd-only pid (nact 0) now runs it on the device too (npid)"""
+    from mgs.core.engine import Engine
+    from mgs.core.mjcf import compile_xml
+    from oracle import oracle as O
+    cm = compile_xml(PID_KPKD_XML)
+    eng, om = Engine(cm, ncon_max=4), O.OracleModel(cm, ncon_max=4)
+    rng = np.random.default_rng(5)
+    n = 8
+    q = np.tile(cm.qpos0, (n, 1)) + rng.uniform(-0.5, 0.5, (n, cm.nq))
+    plan = _pid_plan(cm, 0.8, 300, n=n, q=q)
+    g, o = eng.simulate(plan), om.simulate_batch(plan)
+    for k in ("qpos", "qvel"):
+        assert np.array_equal(g[k], o[k]), k
+    assert np.abs(g["qpos"][:, 0] - 0.8).max() < 0.5

@@ -1,28 +1,34 @@
-"""Rounded and cylinder collision geoms (sphere / capsule = hull (+) ball;
-cylinder = the exact solid: analytic support in MPR, rim polygons turned onto
-the true extreme for the contact features) in the oracle's narrowphase, pinned by analytic
-contact geometry: MuJoCo's sphere-box and capsule-box colliders
-(engine_collision_primitive.c in MuJoCo 3.2.2, not vendored) return the deepest
-point (sphere) and the two segment-end points of a capsule lying on a face, with
-the contact midway between the surfaces and depth = penetration.  Tolerances:
-single-point contacts come from MPR, converged to MuJoCo's mpr_tolerance 1e-6
-(as libccd's MPR in MuJoCo); manifold points from face clipping are exact up
+"""Collision geometry of the contact models (mgs_model_desc.ccd_mode).
+
+MuJoCo 3.2.2's collision table restated (ccd_mode 1 with the multiccd flag, 2
+without; the envs run 1): analytic sphere / capsule / box / cylinder colliders
+(engine_collision_primitive.c: midpoint contacts, depth = penetration, a
+capsule lying on a face gives a contact at each end), libccd's MPR for convex
+pairs (depth to the final portal triangle, position the tetrahedron
+barycentre of the origin -- within the contact patch, not at its deepest
+point), multiccd's perturbed extra contacts.  MuJoCo's source is not vendored:
+these pin the restated rules (parity unpinned).  Round 5's
+contract (ccd_mode 0: face clipping, rounded geoms as hull (+) ball) is kept
+for the contact-set study, its tests under contact_model="r5".  Tolerances:
+MPR converges to mpr_tolerance 1e-6; analytic and clipped values are exact up
 to rounding."""
 import numpy as np
 import pytest
 
 BASE = """
-<mujoco><option gravity="0 0 0" cone="elliptic" integrator="implicitfast"/>
+<mujoco><option gravity="0 0 0" cone="elliptic" integrator="implicitfast">{flag}</option>
 <worldbody>
   <body name="floor" pos="0 0 0"><geom name="floor" type="box" size="0.1 0.1 0.02"/></body>
   <body name="b" pos="{pos}" quat="{quat}"><freejoint name="fj"/>{geom}</body>
 </worldbody></mujoco>"""
+MULTICCD = '<flag multiccd="enable"/>'
 
 
-def contacts(geom, pos, quat="1 0 0 0"):
+def contacts(geom, pos, quat="1 0 0 0", flag="", model="mujoco"):
     from mgs.core.mjcf import compile_xml
     from oracle import oracle as O
-    cm = compile_xml(BASE.format(geom=geom, pos=pos, quat=quat))
+    cm = compile_xml(BASE.format(geom=geom, pos=pos, quat=quat, flag=flag))
+    cm.options["contact_model"] = model
     om = O.OracleModel(cm)
     n, p, fr, dist, g = om.contacts(cm.qpos0, np.zeros(3), np.array([1.0, 0, 0, 0]))
     return n, p, fr, dist
@@ -52,17 +58,35 @@ def test_capsule_upright_one_contact():
     assert np.allclose(p[0], [0, 0, 0.01975], atol=1e-6)
 
 
-def test_cylinder_standing_on_box_four_contacts():
-    # the cap face: 16 rim points on the true circle, the manifold keeps 4, depth 1 mm
-    n, p, fr, dist = contacts('<geom type="cylinder" size="0.02 0.03"/>', "0 0 0.049")
+def test_cylinder_standing_on_box_r5_four_contacts():
+    # round 5's contract: the cap face, 16 rim points on the true circle, the manifold keeps 4, depth 1 mm
+    n, p, fr, dist = contacts('<geom type="cylinder" size="0.02 0.03"/>', "0 0 0.049", model="r5")
     assert n == 4
     assert np.allclose(dist, -0.001, atol=1e-12)
     assert np.allclose(np.hypot(p[:, 0], p[:, 1]), 0.02, atol=1e-12)
     assert np.allclose(p[:, 2], 0.0195, atol=1e-12)
 
 
+def test_cylinder_standing_on_box_multiccd():
+    """mjc_Convex (cylinder-box has no analytic collider): one MPR contact on
+    the cap, and with multiccd four more -- each perturbed run tips the cap
+    onto a rim point, pos within 1 mm of the rim, 2 r x 1e-3 rad deeper"""
+    n, p, fr, dist = contacts('<geom type="cylinder" size="0.02 0.03"/>', "0 0 0.049")
+    assert n == 1 and np.allclose(dist, -0.001, atol=2e-6)
+    # geom 1 is the cylinder (MuJoCo type 5 < box 6): the normal points into the floor
+    assert np.allclose(fr[0, :3], [0, 0, -1], atol=1e-6)
+    n, p, fr, dist = contacts('<geom type="cylinder" size="0.02 0.03"/>', "0 0 0.049", flag=MULTICCD)
+    assert n == 5
+    assert np.allclose(dist[0], -0.001, atol=2e-6)
+    assert np.allclose(dist[1:], -0.001 - 2 * 0.02 * 1e-3, atol=5e-6)
+    rad = np.hypot(p[1:, 0], p[1:, 1])
+    assert np.all(rad > 0.019) and np.all(rad < 0.0201)
+    assert np.allclose(fr[:, 2], -1.0, atol=1e-5)
+    assert np.all(np.abs(p[:, 2] - 0.0195) < 2e-4)      # libccd positions: within the overlap
+
+
 @pytest.mark.parametrize("spin", [0.0, 0.3, 0.7])
-def test_cylinder_lying_on_box_two_generator_contacts(spin):
+def test_cylinder_lying_on_box_r5_two_generator_contacts(spin):
     # axis along world x, turned about its own axis by `spin` (0.3 / 0.7 rad put
     # no vertex of an inscribed 16-gon at the bottom: a prism would rest up to
     # r (1 - cos(pi / 16)) = 0.38 mm higher), 0.4 mm into the floor: the exact
@@ -72,7 +96,7 @@ def test_cylinder_lying_on_box_two_generator_contacts(spin):
     R = Rotation.from_euler("y", np.pi / 2) * Rotation.from_euler("z", spin)
     x, y, z, w = R.as_quat()
     n, p, fr, dist = contacts(f'<geom type="cylinder" size="{r} {h}"/>', f"0 0.003 {0.02 + r - depth}",
-                              f"{w} {x} {y} {z}")
+                              f"{w} {x} {y} {z}", model="r5")
     assert n == 2
     # MPR's normal (mpr_tolerance 1e-6) carries into the feature heights, as
     # for the capsule (test_capsule_lying_on_box_two_contacts)
@@ -83,27 +107,129 @@ def test_cylinder_lying_on_box_two_generator_contacts(spin):
     assert np.allclose(p[:, 2], 0.02 - depth / 2, atol=1e-7)
 
 
+@pytest.mark.parametrize("spin", [0.0, 0.3, 0.7])
+def test_cylinder_lying_on_box_multiccd(spin):
+    """the exact cylinder along its bottom generator: MPR's contact, then
+    multiccd's tilts about the generator's axis find its two ends (the tilts
+    about the other tangent find the same line again: not distinct)"""
+    from scipy.spatial.transform import Rotation
+    r, h, depth = 0.02, 0.03, 0.0004
+    R = Rotation.from_euler("y", np.pi / 2) * Rotation.from_euler("z", spin)
+    x, y, z, w = R.as_quat()
+    n, p, fr, dist = contacts(f'<geom type="cylinder" size="{r} {h}"/>', f"0 0.003 {0.02 + r - depth}",
+                              f"{w} {x} {y} {z}", flag=MULTICCD)
+    assert n == 3
+    assert np.allclose(dist[0], -depth, atol=2e-6)
+    assert np.allclose(sorted(p[1:, 0]), [-h, h], atol=1e-3)
+    assert np.allclose(p[:, 1], 0.003, atol=1e-5)
+    assert np.allclose(fr[:, 2], -1.0, atol=1e-5)
+
+
 def test_cylinder_tilted_on_box_rim_contact():
     # axis tilted 0.4 rad about x and spun 0.2 rad: one rim point is lowest;
-    # exact depth and position (the point midway between it and the face)
+    # MPR's depth and normal are exact to the tolerance; libccd's position is
+    # the barycentre of the portal's witness points (within the cap's reach)
     from scipy.spatial.transform import Rotation
     r, h, depth = 0.02, 0.03, 0.0005
     R = Rotation.from_euler("x", 0.4) * Rotation.from_euler("z", 0.2)
-    low = R.apply([0.0, -r, -h])            # rim point on the low side: local (0, -r, -h)
-    # the lowest point of the tilted solid: rim point towards -y of the bottom cap
     zs = [R.apply([r * np.cos(a), r * np.sin(a), -h])[2] for a in np.linspace(0, 2 * np.pi, 20001)]
     zlow = min(zs)
-    assert abs(zlow - low[2]) < 1e-12 or zlow <= low[2]
     c = np.array([0.001, 0.002, 0.02 - zlow - depth])
     x, y, z, w = R.as_quat()
-    n, p, fr, dist = contacts(f'<geom type="cylinder" size="{r} {h}"/>', " ".join(map(str, c)), f"{w} {x} {y} {z}")
-    assert n == 1
-    assert np.allclose(dist, [-depth], atol=1e-8)
-    assert np.allclose(np.abs(fr[0, :3]), [0, 0, 1], atol=1e-6)
-    lowest = c + R.apply([0.0, -r, -h]) if abs(zlow - low[2]) < 1e-12 else None
-    assert np.allclose(p[0, 2], 0.02 - depth / 2, atol=1e-8)
-    if lowest is not None:
-        assert np.allclose(p[0, :2], lowest[:2], atol=1e-6)
+    for model in ("mujoco", "r5"):
+        n, p, fr, dist = contacts(f'<geom type="cylinder" size="{r} {h}"/>', " ".join(map(str, c)),
+                                  f"{w} {x} {y} {z}", model=model)
+        assert n == 1
+        assert np.allclose(dist, [-depth], atol=1e-6 if model == "mujoco" else 1e-8)
+        assert np.allclose(np.abs(fr[0, :3]), [0, 0, 1], atol=1e-6)
+        assert np.hypot(*(p[0, :2] - c[:2])) < r + 1e-9
+    assert np.allclose(p[0, 2], 0.02 - depth / 2, atol=1e-8)    # r5: midway between the surfaces
+
+
+def test_capsule_pair_analytic():
+    """mjc_CapsuleCapsule: crossed capsules touch at the closest points of their
+    segments (1 contact); parallel ones get a contact at each overlapping end"""
+    from mgs.core.mjcf import compile_xml, PAIR_CAPSULE_CAPSULE
+    from oracle import oracle as O
+    xml = """
+<mujoco><option gravity="0 0 0" cone="elliptic" integrator="implicitfast"/>
+<worldbody>
+  <body name="a" pos="0 0 0"><geom type="capsule" size="0.01 0.05" quat="{qa}"/></body>
+  <body name="b" pos="0.001 0.002 {z}"><freejoint name="fj"/><geom type="capsule" size="0.01 0.03" quat="{qb}"/></body>
+</worldbody></mujoco>"""
+    c, s_ = np.cos(np.pi / 4), np.sin(np.pi / 4)
+    along_x, along_y = f"{c} 0 {s_} 0", f"{c} {-s_} 0 0"
+    cm = compile_xml(xml.format(qa=along_x, qb=along_y, z=0.0197))
+    assert cm.pair_table(2)[2].tolist() == [PAIR_CAPSULE_CAPSULE]
+    om = O.OracleModel(cm)
+    n, p, fr, dist, g = om.contacts(cm.qpos0, np.zeros(3), np.array([1.0, 0, 0, 0]))
+    assert n == 1 and np.allclose(dist, [-0.0003], atol=1e-15)
+    assert np.allclose(p[0], [0.001, 0.0, 0.0197 / 2], atol=1e-15)
+    assert np.allclose(fr[0, :3], [0, 0, 1], atol=1e-15)
+    cm = compile_xml(xml.format(qa=along_x, qb=along_x, z=0.0197))
+    om = O.OracleModel(cm)
+    n, p, fr, dist, g = om.contacts(cm.qpos0, np.zeros(3), np.array([1.0, 0, 0, 0]))
+    assert n == 2 and np.allclose(dist, np.hypot(0.002, 0.0197) - 0.02, atol=1e-15)
+    assert np.allclose(sorted(p[:, 0]), [0.001 - 0.03, 0.001 + 0.03], atol=1e-15)
+
+
+def test_sphere_cylinder_analytic():
+    """mjc_SphereCylinder: the side, the cap and the rim edge"""
+    from mgs.core.mjcf import compile_xml, PAIR_SPHERE_CYLINDER
+    from oracle import oracle as O
+    xml = """
+<mujoco><option gravity="0 0 0" cone="elliptic" integrator="implicitfast"/>
+<worldbody>
+  <body name="c" pos="0 0 0"><geom type="cylinder" size="0.02 0.03"/></body>
+  <body name="s" pos="{pos}"><freejoint name="fj"/><geom type="sphere" size="0.005"/></body>
+</worldbody></mujoco>"""
+    for pos, depth, normal in [("0.0248 0 0.01", 0.0002, [-1, 0, 0]), ("0.003 0.004 0.0349", 0.0001, [0, 0, -1])]:
+        cm = compile_xml(xml.format(pos=pos))
+        assert cm.pair_table(2)[2].tolist() == [PAIR_SPHERE_CYLINDER]
+        n, p, fr, dist, g = O.OracleModel(cm).contacts(cm.qpos0, np.zeros(3), np.array([1.0, 0, 0, 0]))
+        assert n == 1 and np.allclose(dist, [-depth], atol=1e-12)
+        assert np.allclose(fr[0, :3], normal, atol=1e-12)       # sphere (geom 1) -> cylinder
+    # rim: the sphere centre beyond both the side and the cap, 45 deg
+    d = 0.005 - 0.0002
+    cm = compile_xml(xml.format(pos=f"{0.02 + d / np.sqrt(2)} 0 {0.03 + d / np.sqrt(2)}"))
+    n, p, fr, dist, g = O.OracleModel(cm).contacts(cm.qpos0, np.zeros(3), np.array([1.0, 0, 0, 0]))
+    assert n == 1 and np.allclose(dist, [-0.0002], atol=1e-12)
+    assert np.allclose(fr[0, :3], [-np.sqrt(0.5), 0, -np.sqrt(0.5)], atol=1e-12)
+
+
+def test_pair_table_follows_mujoco_types():
+    """mj_collideGeoms orders a pair by MuJoCo geom type (geom 1 the smaller);
+    the collider comes from the type pair (mjCOLLISIONFUNC)"""
+    from mgs.core import mjcf
+    from mgs.core.mjcf import compile_xml
+    kinds = {"sphere": {"sphere": mjcf.PAIR_SPHERE_SPHERE, "capsule": mjcf.PAIR_SPHERE_CAPSULE,
+                        "cylinder": mjcf.PAIR_SPHERE_CYLINDER, "box": mjcf.PAIR_SPHERE_BOX},
+             "capsule": {"capsule": mjcf.PAIR_CAPSULE_CAPSULE, "cylinder": mjcf.PAIR_CONVEX,
+                         "box": mjcf.PAIR_CAPSULE_BOX},
+             "cylinder": {"cylinder": mjcf.PAIR_CONVEX, "box": mjcf.PAIR_CONVEX},
+             "box": {"box": mjcf.PAIR_BOXBOX}}
+    size = {"sphere": "0.01", "capsule": "0.01 0.02", "cylinder": "0.01 0.02", "box": "0.01 0.01 0.01"}
+    for ta, row in kinds.items():
+        for tb, kind in row.items():
+            # the larger type first in the file: the table swaps it
+            xml = f"""<mujoco><option integrator="implicitfast" cone="elliptic"/><worldbody>
+  <body name="x"><geom type="{tb}" size="{size[tb]}"/></body>
+  <body name="y" pos="0 0 1"><freejoint/><geom type="{ta}" size="{size[ta]}"/></body>
+</worldbody></mujoco>"""
+            cm = compile_xml(xml)
+            g1, g2, k = cm.pair_table(1)
+            assert k.tolist() == [kind], (ta, tb)
+            assert mjcf.GEOM_TYPES[ta] <= mjcf.GEOM_TYPES[tb]
+            if ta != tb:
+                assert (g1[0], g2[0]) == (1, 0)
+            g1, g2, k = cm.pair_table(0)        # round 5: file order, convex / box-box
+            assert (g1[0], g2[0]) == (0, 1)
+            assert k.tolist() == [mjcf.PAIR_BOXBOX if ta == tb == "box" else mjcf.PAIR_CONVEX]
+    # a mesh pair with a sphere: MPR without multiccd
+    cm = compile_xml("""<mujoco><option integrator="implicitfast" cone="elliptic"/><asset><mesh name="m" vertex="0 0 0 1 0 0 0 1 0 0 0 1"/></asset><worldbody>
+  <body name="x"><geom type="mesh" mesh="m"/></body>
+  <body name="y" pos="0 0 1"><freejoint/><geom type="sphere" size="0.01"/></body></worldbody></mujoco>""")
+    assert cm.pair_table(1)[2].tolist() == [mjcf.PAIR_CONVEX_SMOOTH]
 
 
 def test_cylinder_support_is_exact():
@@ -133,7 +259,7 @@ def test_cylinder_support_is_exact():
 
 def test_rounded_aabb_includes_radius():
     from mgs.core.mjcf import compile_xml
-    cm = compile_xml(BASE.format(geom='<geom type="capsule" size="0.01 0.03"/>', pos="0 0 1", quat="1 0 0 0"))
+    cm = compile_xml(BASE.format(geom='<geom type="capsule" size="0.01 0.03"/>', pos="0 0 1", quat="1 0 0 0", flag=""))
     assert np.allclose(cm.geom_radius, [0.0, 0.01])
     assert np.allclose(cm.geom_aabb[1, 3:], [0.01, 0.01, 0.04])
 
@@ -143,10 +269,10 @@ def test_rounded_aabb_includes_radius():
 
 
 def test_box_pair_uses_box_collider():
-    from mgs.core.mjcf import compile_xml, PAIR_BOXBOX, PAIR_CONVEX
-    cm = compile_xml(BASE.format(geom='<geom type="box" size="0.01 0.01 0.01"/>', pos="0 0 1", quat="1 0 0 0"))
+    from mgs.core.mjcf import compile_xml, PAIR_BOXBOX, PAIR_CONVEX  # noqa: F401 (pair_kind: the compiled order's)
+    cm = compile_xml(BASE.format(geom='<geom type="box" size="0.01 0.01 0.01"/>', pos="0 0 1", quat="1 0 0 0", flag=""))
     assert list(cm.pair_kind) == [PAIR_BOXBOX]
-    cm = compile_xml(BASE.format(geom='<geom type="sphere" size="0.01"/>', pos="0 0 1", quat="1 0 0 0"))
+    cm = compile_xml(BASE.format(geom='<geom type="sphere" size="0.01"/>', pos="0 0 1", quat="1 0 0 0", flag=""))
     assert list(cm.pair_kind) == [PAIR_CONVEX]
 
 

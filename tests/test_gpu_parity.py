@@ -475,13 +475,41 @@ def test_contact_capacity_escalation(env):
     keep = np.setdiff1d(np.arange(len(idx)), ov)
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(res[k][keep], capped[k][keep]), k
-    ro = O.OracleModel(env.model, ncon_max=32, nefc_max=e16.engine_for(32).desc.nefc_max).rollout(
-        plan.subset(ov), nthreads=8)
-    _assert_same({k: res[k][ov] for k in ro}, ro, "escalated")
-    # the default capacity (20 contacts, auto rows) holds all of them
-    assert env.ncon_max == 20
-    r20 = env.rollout(plan.subset(ov))
-    assert not r20["stats"][:, 2].any()
+    # the escalation's stages (32, 64, 128 contacts) end where each one fits:
+    # equal to the oracle at full capacity
+    ro = O.OracleModel(env.model, ncon_max=128, nefc_max=256).rollout(plan.subset(ov), nthreads=8)
+    for k in ("label", "fail_step", "obj_qpos"):
+        assert np.array_equal(res[k][ov], ro[k]), k
+    assert not (res["stats"][ov, 2] & 3).any()
+
+
+def test_capped_contact_set_raises_never_labels(env):
+    """a call whose escalation cannot hold a candidate's contacts
+    (max_ncon below them) raises CapacityError -- no label from a capped
+    contact set -- and with the default escalation the same call returns the
+    full-capacity oracle's results"""
+    from conftest import plan_for
+    from mgs.env.gravityless_object_grasping import CapacityError, GravitylessObjectGrasping
+    from mgs.sampler.antipodal import robotiq_candidates
+    from mgs.util.geo.transforms import SE3Pose
+    from oracle import oracle as O
+    e4 = GravitylessObjectGrasping(env.gripper, env.obj, ncon_max=4)
+    H, J, _ = robotiq_candidates(env.obj, 2048, seed=0)
+    P = SE3Pose.from_mat(H)
+    q, mp, mq, _ = e4.initial_state(P, J)
+    idx = np.nonzero(e4.engine.collision_free(q, mp, mq))[0][:64]
+    plan = plan_for(e4, P[idx], J[idx])
+    ro = O.OracleModel(env.model, ncon_max=128, nefc_max=256).rollout(plan, nthreads=8)
+    over8 = np.nonzero(ro["stats"][:, 0] > 8)[0]
+    assert len(over8) > 0
+    with pytest.raises(CapacityError) as ei:
+        e4.rollout(plan, max_ncon=8)
+    assert set(ei.value.candidates.tolist()) <= set(range(len(idx)))
+    assert set(over8.tolist()) & set(ei.value.candidates.tolist())
+    res = e4.rollout(plan)            # 4 -> 8 -> ... -> 128
+    for k in ("label", "fail_step", "obj_qpos"):
+        assert np.array_equal(res[k], ro[k]), k
+    assert res["overflow"] == 0
 
 
 def test_resumed_escalation_equals_wide_run(env, candidates):
@@ -677,10 +705,10 @@ def test_time_slices_keep_capacity_flags(env, candidates):
     q, mp, mq, _ = e4.initial_state(poses, J)
     idx = np.nonzero(e4.engine.collision_free(q, mp, mq))[0][:96]
     plan = plan_for(e4, poses[idx], J[idx])
-    one = e4.rollout(plan, max_ncon=4, slices=1)
+    one = e4.rollout(plan, max_ncon=4, slices=1, on_capacity="capped")
     assert one["overflow"] > 0
     for k in (2, 3, 7):
-        r = e4.rollout(plan, max_ncon=4, slices=k)
+        r = e4.rollout(plan, max_ncon=4, slices=k, on_capacity="capped")
         _assert_same(r, one, f"{k} slices, capped")
         assert r["overflow"] == one["overflow"]
 
@@ -806,9 +834,20 @@ def test_queue_spans_device_clock(env, candidates):
     finally:
         eng.lib.mgs_rollout_queue(prev)
     s = eng.queue_spans()
-    assert len(s) == 1
+    assert len(s) == 1 and eng.spans_overwritten == 0
     assert 0.0 < s[0] <= r["kernel_ms"] * 1.05 + 0.05     # inside the HIP events around the launch
     assert eng.queue_spans() == []
+    # more than the ring's 64 launches between two calls: the lost ones are counted
+    sub = plan_for(env, poses[idx[:20]], J[idx[:20]], horizon="h200")
+    sub.nsteps = [2] * len(sub.nsteps)
+    prev = eng.lib.mgs_rollout_queue(4)
+    try:
+        for _ in range(70):
+            eng.rollout(sub)
+    finally:
+        eng.lib.mgs_rollout_queue(prev)
+    s = eng.queue_spans()
+    assert len(s) == 64 and eng.spans_overwritten == 6
 
 
 @pytest.mark.gpu

@@ -137,7 +137,7 @@ def test_panda_ycb_set_gpu_parity(obj_id):
     idx = np.nonzero(fg)[0][:96]
     assert len(idx) >= 8
     plan = plan_for(env, poses[idx], J[idx])
-    rg = env.rollout(plan, max_ncon=env.ncon_max)
+    rg = env.rollout(plan, max_ncon=env.ncon_max, on_capacity="capped")
     ro = om.rollout(plan, nthreads=8)
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(rg[k], ro[k]), k

@@ -97,8 +97,30 @@ def test_sliced_rollout_equals_one_uncapped_run(seed, slices):
     assert 1 <= len(main) <= slices and all(c["resumed"] for c in main[1:])
 
 
-def test_escalation_stops_at_max_ncon():
-    """a candidate still over the largest capacity runs on capped and flagged
+def test_escalation_past_max_ncon_raises():
+    """a candidate still over the largest capacity fails the
+    call (CapacityError naming it) instead of returning a label from a capped
+    contact set; the last stage stops it (no capped_continue)"""
+    from mgs.env.gravityless_object_grasping import CapacityError
+    need, fail_at, plan = _case(3)
+    need[5, 20] = 500
+    fail_at[5] = -1
+    engines = {}
+    log = []
+
+    def engine_for(c):
+        return engines.setdefault(c, FakeEngine(need, fail_at, c, log))
+    with pytest.raises(CapacityError) as ei:
+        sliced_rollout(plan, engine_for(10), engine_for, 10, 40, 1)
+    assert 5 in ei.value.candidates.tolist()
+    assert max(c["cap"] for c in log) == 40
+    # every candidate the escalation could hold is below 40: raising the cap resolves it
+    res = sliced_rollout(plan, engine_for(10), engine_for, 10, 640, 1)
+    assert res["overflow"] == 0 and not res["stats"][5, 2] & CAP
+
+
+def test_escalation_stops_at_max_ncon_when_capped_is_accepted():
+    """on_capacity="capped" (opt-in): the candidate runs on capped and flagged
     (capped_continue on the last stage), counted in res['overflow']"""
     need, fail_at, plan = _case(3)
     need[5, 20] = 500
@@ -108,7 +130,7 @@ def test_escalation_stops_at_max_ncon():
 
     def engine_for(c):
         return engines.setdefault(c, FakeEngine(need, fail_at, c, log))
-    res = sliced_rollout(plan, engine_for(10), engine_for, 10, 40, 1)
+    res = sliced_rollout(plan, engine_for(10), engine_for, 10, 40, 1, on_capacity="capped")
     assert res["overflow"] >= 1 and res["stats"][5, 2] & CAP
     assert res["label"][5] and res["fail_step"][5] == -1
     assert max(c["cap"] for c in log) == 40
@@ -120,9 +142,9 @@ def test_capped_slices_keep_capacity_flags(slices):
     max_ncon, capped_continue) with slices: a capped candidate that pauses keeps
     FLAG_CAPACITY through the relaunch, so res['overflow'] equals one launch's"""
     need, fail_at, plan = _case(4)
-    one = sliced_rollout(plan, FakeEngine(need, fail_at, 10, []), None, 10, 10, 1)
+    one = sliced_rollout(plan, FakeEngine(need, fail_at, 10, []), None, 10, 10, 1, on_capacity="capped")
     assert one["overflow"] > 0
-    res = sliced_rollout(plan, FakeEngine(need, fail_at, 10, []), None, 10, 10, slices)
+    res = sliced_rollout(plan, FakeEngine(need, fail_at, 10, []), None, 10, 10, slices, on_capacity="capped")
     assert res["overflow"] == one["overflow"]
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(res[k], one[k]), k

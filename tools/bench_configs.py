@@ -32,7 +32,7 @@ import numpy as np  # noqa: E402
 YIELD = None    # --yield: the envs' in-launch rotation (steps per slice; None = the env default)
 
 
-def gravityless(gripper_name, object_ids, n, horizon="h200"):
+def gravityless(gripper_name, object_ids, n, horizon="h200", cpu_sample=0, threads=16):
     from mgs.env.gravityless_object_grasping import GravitylessObjectGrasping, HORIZONS
     from mgs.gripper.selector import get_gripper
     from mgs.obj.selector import get_object
@@ -66,10 +66,41 @@ def gravityless(gripper_name, object_ids, n, horizon="h200"):
         per.append(dict(object=oid, candidates=n, collision_free=int(mask.sum()),
                         stable=int(res["label"].sum()) if res is not None else 0, seconds=dt,
                         kernel_ms=km + kr, static_layout_kernel=bool(env.engine.specialized())))
+        if cpu_sample:
+            per[-1]["cpu"] = gravityless_cpu(env, P, J, cpu_sample, h, threads)
         tot_n += n
         tot_t += dt
         tot_k += (km + kr) * 1e-3
-    return dict(value=tot_n / tot_t, kernel_only=tot_n / tot_k, objects=per)
+    out = dict(value=tot_n / tot_t, kernel_only=tot_n / tot_k, objects=per)
+    if cpu_sample:
+        cs = sum(o["cpu"]["candidates"] for o in per)
+        ct = sum(o["cpu"]["seconds"] for o in per)
+        out["cpu_baseline"] = dict(value=cs / ct, unit="grasp candidates/s", cores=threads, kind="port",
+                                   seconds=ct, sample=f"{cpu_sample} evenly spaced candidates per object "
+                                   f"({len(per)} objects): mask + the collision-free rollouts at {horizon}, the "
+                                   "C oracle (checker build) on the host cores, same run")
+        for o in per:
+            o.pop("cpu")
+    return out
+
+
+def gravityless_cpu(env, P, J, sample, h, threads):
+    """the C oracle over a bounded evenly spaced sample of the same candidates:
+    the collision mask, then the h-horizon rollouts of the collision-free ones
+    at the env's main capacity (the oracle flags what the GPU escalates)"""
+    from oracle import oracle as O
+    sel = np.linspace(0, len(P) - 1, sample).astype(int)
+    Ps, Js = P[sel], J[sel]
+    om = O.OracleModel(env.model, ncon_max=64, nefc_max=256)
+    t0 = time.perf_counter()
+    q, mp, mq, _ = env.initial_state(Ps, Js)
+    free = om.collision_free(q, mp, mq, nthreads=threads)
+    idx = np.nonzero(free)[0]
+    if len(idx):
+        om.rollout(env.rollout_plan(Ps[idx], Js[idx], nstep_lift=h["nstep_lift"], shake_steps=h["shake_steps"],
+                                    close_steps=h["close_steps"], lift_check_every=h["lift_check_every"]),
+                   nthreads=threads)
+    return dict(candidates=int(sample), seconds=time.perf_counter() - t0)
 
 
 def clutter(n_per_obj, steps, cpu_sample=0, threads=16):
@@ -229,6 +260,8 @@ def main():
     ap.add_argument("--c5-per-object", type=int, default=256)
     ap.add_argument("--c5-cpu-sample", type=int, default=0, help="candidates for the C5 CPU baseline (0: none)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=1024,
+                    help="candidates per object for the C3 / C4 CPU baselines (0: none)")
     ap.add_argument("--yield", dest="yield_every", type=int, default=None,
                     help="in-launch rotation of the envs' rollout launches, steps per slice (0 = off)")
     ap.add_argument("--scene-piles", type=int, default=256)
@@ -243,13 +276,16 @@ def main():
     ycb = ObjectYCB.all_object_ids()
     for c in a.configs:
         if c == "c3":
-            r = gravityless("PandaGripper", ycb, 16384)
-            out = dict(config="c3", workload=f"Franka Panda x {len(ycb)} synthetic YCB objects, 16384 candidates/object,"
-                                             " mask + h200 rollout", unit="candidates/s", **r)
+            r = gravityless("PandaGripper", ycb, 16384, cpu_sample=a.cpu_sample, threads=a.cpu_threads)
+            out = dict(config="c3", workload=f"Franka Panda x {len(ycb)} synthetic YCB stand-ins (the YCB set is not "
+                                             "shipped: 5 stand-in objects, not the full set), 16384 candidates/object,"
+                                             " mask + h200 rollout, 1 GPU", unit="candidates/s", **r)
         elif c == "c4":
-            r = gravityless("AllegroGripper", ["Synthetic_Mug_Body"], 32768)
-            out = dict(config="c4", workload="Allegro x GSO-format stand-in (Synthetic_Mug_Body), 32768 candidates on "
-                                             "one GPU, mask + h200 rollout", unit="candidates/s", **r)
+            r = gravityless("AllegroGripper", ["Synthetic_Mug_Body"], 32768, cpu_sample=a.cpu_sample,
+                            threads=a.cpu_threads)
+            out = dict(config="c4", workload="Allegro x GSO-format stand-in (Synthetic_Mug_Body), 32768 candidates, "
+                                             "measured on 1 GPU (BASELINE names 8 GPUs: the whole 8-GPU job on one; "
+                                             "per-GPU share 4096), mask + h200 rollout", unit="candidates/s", **r)
         elif c == "c5":
             r = clutter(a.c5_per_object, a.c5_steps, a.c5_cpu_sample, a.cpu_threads)
             out = dict(config="c5", workload=f"Shadow Hand x settled 5-object pile, {r['candidates']} candidates, "
