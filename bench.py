@@ -160,6 +160,43 @@ def host_info():
             "cgroup_cpu_quota": quota}
 
 
+# VALU issue peak of the chip (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs; a wave64
+# VALU instruction issues over 2 cycles on a SIMD-32 at f32, and f64 vector
+# arithmetic runs at half that lane rate -- 78.6 TF f64 vector = 256 x 4 x 16
+# lanes x 2 flops x 2.4 GHz -- so 4 cycles; the sustained clock under this load
+# is 2.39-2.40 GHz, profiles/r03_clock_probe.txt)
+CHIP_SIMDS = 256 * 4
+CLOCK_HZ = 2.4e9
+VALU_CYC_F64, VALU_CYC_OTHER = 4.0, 2.0
+
+
+def valu_roofline(candidate_steps_per_s):
+    """the rollout kernel against the chip's VALU issue peak: VALU wave-
+    instructions per candidate-step (the committed PMC pass) x this run's
+    candidate-steps/s / (CHIP_SIMDS x CLOCK_HZ / c), c the mix's mean issue
+    cycles per wave-instruction (f64 arithmetic 4, the rest 2)"""
+    j, label = pmc_record()
+    if j is None:
+        return None
+    sq, cs = j.get("sq", {}), j.get("executed_candidate_steps")
+    if not sq.get("SQ_INSTS_VALU") or not cs:
+        return None
+    valu = sq["SQ_INSTS_VALU"]
+    f64 = sum(sq.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                        "SQ_INSTS_VALU_TRANS_F64"))
+    share = f64 / valu
+    cyc = share * VALU_CYC_F64 + (1.0 - share) * VALU_CYC_OTHER
+    peak = CHIP_SIMDS * CLOCK_HZ / cyc
+    per_cs = valu / cs
+    achieved = per_cs * candidate_steps_per_s
+    return {"bound": "valu_issue", "achieved": achieved, "peak": peak, "unit": "wave-instructions/s",
+            "frac": achieved / peak, "valu_per_candidate_step": per_cs, "f64_share": share,
+            "mean_issue_cycles": cyc, "candidate_steps_per_s": candidate_steps_per_s,
+            "source": label,
+            "what": "VALU wave-instructions per candidate-step (PMC pass) x this run's executed candidate-steps/s "
+                    "(device level: all launches in flight) / the chip's VALU issue peak for this f64 / other mix"}
+
+
 def issue_summary():
     """latency / issue view of the rollout kernel from the committed PMC pass
     (profiles/pmc_rollout.json): instructions and wave cycles per executed
@@ -672,6 +709,7 @@ def main():
                      "launches_in_flight": len(pipes),
                      "achieved_device": achieved_device,
                      "frac_device": achieved_device / HBM_PEAK_GBS,
+                     "valu": valu_roofline(steps_exec * args.steps / dt),
                      "what": "achieved = SURVEY 8(d) bytes of one main rollout launch (its executed "
                              "candidate-steps) / launch_ms, the timed main launches' mean execution span on "
                              "the device clock (mgs_queue_spans: first candidate taken -> last workgroup out, "

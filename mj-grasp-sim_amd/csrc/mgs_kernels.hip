@@ -2603,6 +2603,16 @@ DEVI void ccd_find_pos(const SupPt& p0, const SupPt& p1, const SupPt& p2, const 
 // g1 / g2 the half's geoms, whose centres are their geom_xpos); dir is the
 // caller's array as in mpr_penetration (the certificate's direction on a miss)
 #define CCD_CERT(P) do { *cm = -dot3((P).v, dir); } while (0)
+// the MPR's interior point: the two geoms' centres (mjccd_center: geom_xpos,
+// or the perturbed centre of a multiccd run, which the context holds)
+DEVI void mpr_centres(const PairCtx& c, const Dat&, int, int, double* a, double* b) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) { a[k] = c.x1[k]; b[k] = c.x2[k]; }
+}
+DEVI void mpr_centres(const PairCtx2&, const Dat& d, int g1, int g2, double* a, double* b) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) { a[k] = d.geom_xpos[3 * g1 + k]; b[k] = d.geom_xpos[3 * g2 + k]; }
+}
 template <class Ctx>
 DEVI int ccd_mpr(const Mdl& md, const Dat& d, const Ctx& pc, int g1, int g2, double* n, double* depth, double* pos,
                  double* dir, double* cm) {
@@ -2611,8 +2621,7 @@ DEVI int ccd_mpr(const Mdl& md, const Dat& d, const Ctx& pc, int g1, int g2, dou
   const int maxit = md.m.ccd_iterations;
   SupPt p0, p1, p2, p3, p4;
   double dt;
-#pragma unroll
-  for (int k = 0; k < 3; k++) { p0.a[k] = d.geom_xpos[3 * g1 + k]; p0.b[k] = d.geom_xpos[3 * g2 + k]; }
+  mpr_centres(pc, d, g1, g2, p0.a, p0.b);
   sub3(p0.v, p0.a, p0.b);
   if (ccd_vzero(p0.v)) p0.v[0] = p0.v[0] + CCD_EPS * 10.0;
   dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
@@ -2713,7 +2722,7 @@ DEVI void multiccd(const Mdl& md, Dat& d, const PairCtx& pc, int pair, int g1, i
   double rb1 = rb[g1] + rr[g1], rb2 = rb[g2] + rr[g2];
   double tolr = MCCD_RELTOL * (rb1 < rb2 ? rb1 : rb2);
   const int ncmax = md.m.ncon_max;
-#pragma unroll
+#pragma unroll 1
   for (int q = 0; q < 4; q++) {
     const int ax = q >> 1, sg = q & 1;
     double axis[3] = {ax ? t2[0] : t1[0], ax ? t2[1] : t1[1], ax ? t2[2] : t1[2]};
@@ -2723,9 +2732,17 @@ DEVI void multiccd(const Mdl& md, Dat& d, const PairCtx& pc, int pair, int g1, i
     double M1[9], M2[9];
     quat2mat(M1, q1);
     quat2mat(M2, q2);
+    // mjc_rotateFrame about the first contact: x' = p + M (x - p), R' = M R
     PairCtx pp = pc;
+    double r[3], t[3];
     mulmm3(pp.R1, M1, pc.R1);
+    sub3(r, pc.x1, pos);
+    mulmv3(t, M1, r);
+    add3(pp.x1, t, pos);
     mulmm3(pp.R2, M2, pc.R2);
+    sub3(r, pc.x2, pos);
+    mulmv3(t, M2, r);
+    add3(pp.x2, t, pos);
     double nn[3], dd, ppos[3], dir[3], cmx;
     if (!ccd_mpr(md, d, pp, g1, g2, nn, &dd, ppos, dir, &cmx)) continue;
     int isnew = 1;
@@ -2748,6 +2765,182 @@ DEVI void multiccd(const Mdl& md, Dat& d, const PairCtx& pc, int pair, int g1, i
   wsync();
 }
 
+// multiccd's four perturbed MPRs of one pair at once (round 6): groups of
+// 2 x HW lanes each run one perturbation's MPR, HW lanes per hull (lane
+// HW * side + i of a group holds vertex i of geom 1 or 2), for pairs whose
+// two hulls have at most HW vertices: HW 8 -> four MPRs per pass, HW 16 ->
+// two.  Each group computes exactly what the whole wave computes for its
+// perturbation (the MPR's control flow depends only on values uniform within
+// a group), so the contacts are multiccd()'s, bit for bit.
+template <int HW>
+struct PairCtxQ {
+  int n;               // this lane's hull: its vertex count,
+  double R[9], x[3];   // its geom's pose (the group's perturbation about the first contact),
+  double cx1[3], cx2[3];   // the group's two perturbed centres (the MPR's interior point)
+  double c[3];         // the lane's vertex (lane % HW < n)
+  double r;            // and rounding radius
+  int P;               // reduction width: next_pow2 of the larger count (<= HW)
+};
+// the perturbation q = 2 ax + sg of a group (oracle collide_convex_mj's loop order)
+template <int HW>
+DEVI void pair_ctxq(const Mdl& md, const Dat& d, int g1, int g2, const double* t1, const double* t2,
+                    const double* pv, int q0, PairCtxQ<HW>& c) {
+  const int lane = lane_id(), grp = lane / (2 * HW), side = (lane / HW) & 1, li = lane % HW;
+  const int q = q0 + grp, ax = q >> 1, sg = q & 1;
+  const int g = side ? g2 : g1;
+  const int32_t *ghull = IA(md, geom_hullid), *hadr = IA(md, hull_vertadr), *hnum = IA(md, hull_vertnum);
+  const int h = ghull[g];
+  c.n = hnum[h];
+  const double* V = DA(md, hull_vert) + 3 * hadr[h];
+  const int i = li < c.n ? li : 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) c.c[k] = V[k * c.n + i];
+  c.r = DA(md, geom_radius)[g];
+  double axis[3] = {ax ? t2[0] : t1[0], ax ? t2[1] : t1[1], ax ? t2[2] : t1[2]};
+  double s = sg ? MCCD_S : -MCCD_S;
+  double qq[4];
+  qq[0] = MCCD_C;
+  if (side) { qq[1] = -(axis[0] * s); qq[2] = -(axis[1] * s); qq[3] = -(axis[2] * s); }
+  else { qq[1] = axis[0] * s; qq[2] = axis[1] * s; qq[3] = axis[2] * s; }
+  double M[9], Rg[9], xg[3], r[3], t[3];
+  quat2mat(M, qq);
+#pragma unroll
+  for (int k = 0; k < 9; k++) Rg[k] = d.geom_xmat[9 * g + k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) xg[k] = d.geom_xpos[3 * g + k];
+  // mjc_rotateFrame about the first contact pv (oracle collide_convex_mj)
+  mulmm3(c.R, M, Rg);
+  sub3(r, xg, pv);
+  mulmv3(t, M, r);
+  add3(c.x, t, pv);
+  // the group's centres: geom 1's from its first lane, geom 2's from lane HW
+  const int gb = lane - (lane % (2 * HW));
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    c.cx1[k] = shfl(c.x[k], gb);
+    c.cx2[k] = shfl(c.x[k], gb + HW);
+  }
+  const int n1 = hnum[ghull[g1]], n2 = hnum[ghull[g2]];
+  c.P = next_pow2(n1 > n2 ? n1 : n2);
+}
+template <int HW>
+DEVI void mpr_centres(const PairCtxQ<HW>& c, const Dat&, int, int, double* a, double* b) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) { a[k] = c.cx1[k]; b[k] = c.cx2[k]; }
+}
+template <int HW>
+DEVI void support_pairq(const PairCtxQ<HW>& c, const double* dir, double* out1, double* out2) {
+  const int lane = lane_id(), side = (lane / HW) & 1, li = lane % HW, hb = lane - li;
+  double sd[3] = {side ? -dir[0] : dir[0], side ? -dir[1] : dir[1], side ? -dir[2] : dir[2]};
+  double dl[3];
+  mulmtv3(dl, c.R, sd);
+  SupAcc a;
+  sup_init(a);
+  if (li < c.n) {
+    double sc = (c.c[0] * dl[0] + c.c[1] * dl[1]) + c.c[2] * dl[2];
+    if (sc > a.best) { a.best = sc; a.bi = li; a.vx = c.c[0]; a.vy = c.c[1]; a.vz = c.c[2]; }
+  }
+  const int P = c.P;
+  double m = a.best;
+  if (P > 1) m = max_f64(m, dpp_d(m, 0));
+  if (P > 2) m = max_f64(m, dpp_d(m, 1));
+  if (P > 4) m = max_f64(m, dpp_d(m, 2));
+  if (HW > 8 && P > 8) m = max_f64(m, dpp_d(m, 3));
+  // this lane's hull maximum: the reduced value of the hull's first lane
+  const double M = shfl(m, hb);
+  const unsigned long long tied = __ballot(a.bi != 0x7fffffff && a.best == M);
+  const unsigned tr = (unsigned)(tied >> hb) & ((1u << HW) - 1u);
+  const int src = hb + (tr ? __ffs(tr) - 1 : 0);
+  double v[3] = {shfl(a.vx, src), shfl(a.vy, src), shfl(a.vz, src)};
+  double t[3], wv[3];
+  mulmv3(t, c.R, v);
+  add3(wv, c.x, t);
+  if (c.r > 0.0) { wv[0] = wv[0] + c.r * sd[0]; wv[1] = wv[1] + c.r * sd[1]; wv[2] = wv[2] + c.r * sd[2]; }
+  const int s1 = lane - (lane % (2 * HW)), s2 = s1 + HW;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    out1[k] = shfl(wv[k], s1);
+    out2[k] = shfl(wv[k], s2);
+  }
+}
+template <int HW>
+DEVI void mink_support(const PairCtxQ<HW>& c, const double* dir, SupPt* p) {
+  PT(4);
+  PCNT(28, 1);
+  support_pairq<HW>(c, dir, p->a, p->b);
+  sub3(p->v, p->a, p->b);
+  PT(22);
+}
+// multiccd() with its four perturbed MPRs on groups of 2 x HW lanes (pairs
+// whose hulls have at most HW vertices and no cylinder): the same contacts in
+// the same order
+template <int HW>
+DEVI void multiccd_q(const Mdl& md, Dat& d, int pair, int g1, int g2, const double* n, const double* pos) {
+  constexpr int G = WAVE / (2 * HW);      // perturbations per pass
+  double t1[3], t2[3];
+  make_frame(n, t1, t2);
+  double cpx[5], cpy[5], cpz[5];
+  cpx[0] = pos[0]; cpy[0] = pos[1]; cpz[0] = pos[2];
+  int nc = 1;
+  const double* rb = DA(md, geom_rbound);
+  const double* rr = DA(md, geom_radius);
+  double rb1 = rb[g1] + rr[g1], rb2 = rb[g2] + rr[g2];
+  double tolr = MCCD_RELTOL * (rb1 < rb2 ? rb1 : rb2);
+  const int ncmax = md.m.ncon_max;
+#pragma unroll 1
+  for (int q0 = 0; q0 < 4; q0 += G) {
+    PairCtxQ<HW> pc;
+    pair_ctxq<HW>(md, d, g1, g2, t1, t2, pos, q0, pc);
+    double nn[3], dd, pp[3], dir[3], cmx;
+    int hit = ccd_mpr(md, d, pc, g1, g2, nn, &dd, pp, dir, &cmx);
+#pragma unroll 1
+    for (int k = 0; k < G; k++) {
+      const int src = 2 * HW * k;
+      if (!__builtin_amdgcn_readlane(hit, src)) continue;
+      double nk[3], pk[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        nk[i] = readlane_d(nn[i], src);
+        pk[i] = readlane_d(pp[i], src);
+      }
+      const double dk = readlane_d(dd, src);
+      int isnew = 1;
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        if (j < nc) {
+          double dx[3] = {pk[0] - cpx[j], pk[1] - cpy[j], pk[2] - cpz[j]};
+          if (sqrt(dot3(dx, dx)) < tolr) isnew = 0;
+        }
+      }
+      if (!isnew) continue;
+#pragma unroll
+      for (int j = 1; j < 5; j++)
+        if (j == nc) { cpx[j] = pk[0]; cpy[j] = pk[1]; cpz[j] = pk[2]; }
+      nc++;
+      double u1[3], u2[3];
+      make_frame(nk, u1, u2);
+      if (lane_id() == 0) add_contact(d, ncmax, pair, g1, g2, pk, nk, u1, u2, -dk);
+    }
+  }
+  wsync();
+}
+
+// multiccd on the widest grouping the pair's hulls allow
+DEVI void multiccd_any(const Mdl& md, Dat& d, int pair, int g1, int g2, const double* n, const double* pos) {
+  const int32_t *ghull = IA(md, geom_hullid), *hnum = IA(md, hull_vertnum);
+  const double* cy = DA(md, geom_cyl);
+  const int n1 = hnum[ghull[g1]], n2 = hnum[ghull[g2]];
+  const int nm = n1 > n2 ? n1 : n2;
+  const bool cyl = cy[2 * g1] > 0.0 || cy[2 * g2] > 0.0;
+  if (!cyl && nm <= 8) {
+    multiccd_q<8>(md, d, pair, g1, g2, n, pos);
+  } else {
+    PairCtx pc;
+    pair_ctx(md, d, g1, g2, pc);
+    multiccd(md, d, pc, pair, g1, g2, n, pos);
+  }
+}
+
 // one convex pair (ccd_mode 1 / 2): MPR, certificate, first contact, multiccd
 DEVI void collide_pair_mj(const Mdl& md, Dat& d, int pair, int multi) {
   int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
@@ -2763,7 +2956,7 @@ DEVI void collide_pair_mj(const Mdl& md, Dat& d, int pair, int multi) {
   make_frame(n, t1, t2);
   if (lane_id() == 0) add_contact(d, md.m.ncon_max, pair, g1, g2, pos, n, t1, t2, -depth);
   wsync();
-  if (multi) multiccd(md, d, pc, pair, g1, g2, n, pos);
+  if (multi) multiccd_any(md, d, pair, g1, g2, n, pos);
   PT(41);
 }
 
@@ -2779,7 +2972,7 @@ DEVI void collide_pair2_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
   double n[3], depth, pos[3], cd[3], cm;
   int hit = ccd_mpr(md, d, q, g1, g2, n, &depth, pos, cd, &cm);
   PT(4);
-#pragma unroll
+#pragma unroll 1
   for (int k = 0; k < 2; k++) {
     const int src = 32 * k, pair = k ? pairB : pairA, G1 = k ? gB1 : gA1, G2 = k ? gB2 : gA2;
     const int hk = __builtin_amdgcn_readlane(hit, src);
@@ -2798,11 +2991,8 @@ DEVI void collide_pair2_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
       make_frame(nk, t1, t2);
       if (lane == 0) add_contact(d, md.m.ncon_max, pair, G1, G2, pk, nk, t1, t2, -readlane_d(depth, src));
       wsync();
-      if (md.m.ccd_mode == MGS_CCD_MULTI && IA(md, pair_kind)[pair] == MGS_PAIR_CONVEX) {
-        PairCtx pc;
-        pair_ctx(md, d, G1, G2, pc);
-        multiccd(md, d, pc, pair, G1, G2, nk, pk);
-      }
+      if (md.m.ccd_mode == MGS_CCD_MULTI && IA(md, pair_kind)[pair] == MGS_PAIR_CONVEX)
+        multiccd_any(md, d, pair, G1, G2, nk, pk);
     }
   }
 }

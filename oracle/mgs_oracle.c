@@ -1460,10 +1460,12 @@ static void collide_boxbox(const Mdl* md, Dat* d, int pair) {
  * position as the tetrahedron barycentre of the origin (findPos).  With the
  * multiccd flag (both envs: gravityless_object_grasping.py:40,
  * clutter_table.py:48) and no sphere in the pair, four more MPR runs with the
- * geoms turned about their centres -- geom 1 by +-1e-3 rad and geom 2 by the
- * opposite angle about each tangent of the first contact's frame -- add every
- * contact farther than 1e-3 x the smaller bounding radius from the pair's
- * contacts so far (<= 5 per pair).  Box pairs keep collide_boxbox. */
+ * geoms turned about the first contact's point (mjc_rotateFrame) -- geom 1 by
+ * -+1e-3 rad and geom 2 by the opposite angle about each tangent of the first
+ * contact's frame -- add every contact farther than 1e-3 x the smaller
+ * bounding radius from the pair's contacts so far (<= 5 per pair).  A point or
+ * edge contact stays put under such a turn (its repeats are not distinct); a
+ * face contact tips onto the overlap's edges.  Box pairs keep collide_boxbox. */
 #define CCD_EPS 2.2204460492503131e-16   /* libccd CCD_EPS, double build (DBL_EPSILON) */
 #define MCCD_ANGLE 1e-3                  /* multiccd perturbation angle */
 #define MCCD_RELTOL 1e-3                 /* multiccd distinct-contact tolerance, x min rbound */
@@ -1716,12 +1718,19 @@ static void collide_convex_mj(const Mdl* md, Dat* d, int pair, int multi) {
       double s = sg ? MCCD_S : -MCCD_S;
       double q1[4] = {MCCD_C, axis[0] * s, axis[1] * s, axis[2] * s};
       double q2[4] = {MCCD_C, -(axis[0] * s), -(axis[1] * s), -(axis[2] * s)};
-      double M1[9], M2[9], R1p[9], R2p[9];
+      double M1[9], M2[9], R1p[9], R2p[9], x1p[3], x2p[3], r[3], t[3];
       quat2mat(M1, q1);
       quat2mat(M2, q2);
+      /* mjc_rotateFrame: x' = p + M (x - p), R' = M R about the first contact p */
       mulmm3(R1p, M1, R1);
+      sub3(r, x1, pos);
+      mulmv3(t, M1, r);
+      add3(x1p, t, pos);
       mulmm3(R2p, M2, R2);
-      CObj p1o = {g1, R1p, x1}, p2o = {g2, R2p, x2};
+      sub3(r, x2, pos);
+      mulmv3(t, M2, r);
+      add3(x2p, t, pos);
+      CObj p1o = {g1, R1p, x1p}, p2o = {g2, R2p, x2p};
       double nn[3], dd, pp[3], cdx[3], cmx;
       if (!ccd_mpr(md, &p1o, &p2o, nn, &dd, pp, cdx, &cmx)) continue;
       int isnew = 1;

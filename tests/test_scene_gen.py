@@ -221,7 +221,7 @@ def test_gen_scene_cli(tmp_path, monkeypatch):
     from mgs.util.const import ASSET_PATH
     fast = open(os.path.join(ASSET_PATH, "mj-objects", "fast_eta_objects.txt")).read().splitlines()
     for k, oid in enumerate(fast):
-        h, j, _ = robotiq_candidates(get_object(oid), 64, seed=k)
+        h, j, _ = robotiq_candidates(get_object(oid), 256, seed=k)
         d = tmp_path / "in" / "Robotiq2f85Gripper" / oid
         d.mkdir(parents=True)
         np.savez(d / "stable_grasps.npz", pose=np.asarray(h, np.float32), joints=j)
