@@ -1247,7 +1247,9 @@ struct PairCtx {
   double r1, r2;   // rounding radii (sphere / capsule: hull (+) ball), 0 for hulls
   double cy1[2], cy2[2];   // cylinder radius / half-height (exact solid), 0 0 for others
 };
-DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
+// the context with the geoms' poses read from R1 / x1 / R2 / x2 (LDS)
+DEVI void pair_ctx_pose(const Mdl& md, int g1, int g2, const double* R1, const double* x1, const double* R2,
+                        const double* x2, PairCtx& c) {
   int lane = lane_id();
   const int32_t *ghull = IA(md, geom_hullid), *hadr = IA(md, hull_vertadr), *hnum = IA(md, hull_vertnum);
   int h1 = ghull[g1], h2 = ghull[g2];
@@ -1255,8 +1257,8 @@ DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   c.n2 = hnum[h2];
   c.V1 = DA(md, hull_vert) + 3 * hadr[h1];
   c.V2 = DA(md, hull_vert) + 3 * hadr[h2];
-  for (int k = 0; k < 9; k++) { c.R1[k] = d.geom_xmat[9 * g1 + k]; c.R2[k] = d.geom_xmat[9 * g2 + k]; }
-  for (int k = 0; k < 3; k++) { c.x1[k] = d.geom_xpos[3 * g1 + k]; c.x2[k] = d.geom_xpos[3 * g2 + k]; }
+  for (int k = 0; k < 9; k++) { c.R1[k] = R1[k]; c.R2[k] = R2[k]; }
+  for (int k = 0; k < 3; k++) { c.x1[k] = x1[k]; c.x2[k] = x2[k]; }
   int i1 = (lane < c.n1) ? lane : 0, i2 = (lane < c.n2) ? lane : 0;
   for (int k = 0; k < 3; k++) { c.c1[k] = c.V1[k * c.n1 + i1]; c.c2[k] = c.V2[k * c.n2 + i2]; }
   c.r1 = DA(md, geom_radius)[g1];
@@ -1264,6 +1266,9 @@ DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
   const double* cy = DA(md, geom_cyl);
   c.cy1[0] = cy[2 * g1]; c.cy1[1] = cy[2 * g1 + 1];
   c.cy2[0] = cy[2 * g2]; c.cy2[1] = cy[2 * g2 + 1];
+}
+DEVI void pair_ctx(const Mdl& md, const Dat& d, int g1, int g2, PairCtx& c) {
+  pair_ctx_pose(md, g1, g2, d.geom_xmat + 9 * g1, d.geom_xpos + 3 * g1, d.geom_xmat + 9 * g2, d.geom_xpos + 3 * g2, c);
 }
 
 // exact cylinder support in the geom frame (oracle cyl_support; MuJoCo's ccd
@@ -2490,6 +2495,20 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
 // Primitive pairs: the analytic colliders.  Parity vs MuJoCo unpinned
 // (DESIGN.md §2); GPU == oracle bit for bit.
 #define CCD_EPS 2.2204460492503131e-16
+// multiccd's four perturbations on 16-lane groups at once (1) or one after
+// another on the whole wave (0).  Off in register-capped objects
+// (MGS_WAVES_PER_EU, the main engine's G-rows-in-HBM object): there the
+// compiler spills inside the groups' divergent MPR loops and the results left
+// the oracle's (round 6: tools/probe_ab_parity.py, the same source without the
+// cap or with the perturbations in sequence is bit-exact) -- the grouped MPR
+// needs registers the capped object does not have
+#ifndef MGS_MCCD_Q
+#ifdef MGS_WAVES_PER_EU
+#define MGS_MCCD_Q 0
+#else
+#define MGS_MCCD_Q 1
+#endif
+#endif
 #define MCCD_RELTOL 1e-3
 #define MCCD_C 0.9999998750000026       // cos(5e-4): half the perturbation angle
 #define MCCD_S 4.999999791666669e-04    // sin(5e-4)
@@ -2710,59 +2729,34 @@ DEVI int ccd_mpr(const Mdl& md, const Dat& d, const Ctx& pc, int g1, int g2, dou
 // and geom 2 by the opposite angle about the frame's tangents, each new
 // contact farther than MCCD_RELTOL x the smaller bounding radius from the
 // pair's contacts so far added (all lanes; lane 0 writes)
-DEVI void multiccd(const Mdl& md, Dat& d, const PairCtx& pc, int pair, int g1, int g2, const double* n,
-                   const double* pos) {
-  double t1[3], t2[3];
-  make_frame(n, t1, t2);
-  double cpx[5], cpy[5], cpz[5];
-  cpx[0] = pos[0]; cpy[0] = pos[1]; cpz[0] = pos[2];
-  int nc = 1;
+// the pair's contacts so far, for multiccd's distinctness test: in the
+// collision stage's polygon scratch (unused by the ccd_mode 1 / 2 colliders),
+// uniform addresses, lane 0 writes (registers here spilled the object)
+DEVI void mccd_list_init(Dat& d, const double* pos) {
+  double* cp = (double*)d.poly;
+  if (lane_id() == 0) { cp[0] = pos[0]; cp[1] = pos[1]; cp[2] = pos[2]; }
+  wsync();
+}
+DEVI int mccd_is_new(const Dat& d, int nc, const double* p, double tolr) {
+  const double* cp = (const double*)d.poly;
+  int isnew = 1;
+  for (int k = 0; k < nc; k++) {
+    double dx[3] = {p[0] - cp[3 * k], p[1] - cp[3 * k + 1], p[2] - cp[3 * k + 2]};
+    if (sqrt(dot3(dx, dx)) < tolr) isnew = 0;
+  }
+  return isnew;
+}
+DEVI void mccd_list_add(Dat& d, int nc, const double* p) {
+  double* cp = (double*)d.poly;
+  wsync();
+  if (lane_id() == 0) { cp[3 * nc] = p[0]; cp[3 * nc + 1] = p[1]; cp[3 * nc + 2] = p[2]; }
+  wsync();
+}
+DEVI double mccd_tol(const Mdl& md, int g1, int g2) {
   const double* rb = DA(md, geom_rbound);
   const double* rr = DA(md, geom_radius);
   double rb1 = rb[g1] + rr[g1], rb2 = rb[g2] + rr[g2];
-  double tolr = MCCD_RELTOL * (rb1 < rb2 ? rb1 : rb2);
-  const int ncmax = md.m.ncon_max;
-#pragma unroll 1
-  for (int q = 0; q < 4; q++) {
-    const int ax = q >> 1, sg = q & 1;
-    double axis[3] = {ax ? t2[0] : t1[0], ax ? t2[1] : t1[1], ax ? t2[2] : t1[2]};
-    double s = sg ? MCCD_S : -MCCD_S;
-    double q1[4] = {MCCD_C, axis[0] * s, axis[1] * s, axis[2] * s};
-    double q2[4] = {MCCD_C, -(axis[0] * s), -(axis[1] * s), -(axis[2] * s)};
-    double M1[9], M2[9];
-    quat2mat(M1, q1);
-    quat2mat(M2, q2);
-    // mjc_rotateFrame about the first contact: x' = p + M (x - p), R' = M R
-    PairCtx pp = pc;
-    double r[3], t[3];
-    mulmm3(pp.R1, M1, pc.R1);
-    sub3(r, pc.x1, pos);
-    mulmv3(t, M1, r);
-    add3(pp.x1, t, pos);
-    mulmm3(pp.R2, M2, pc.R2);
-    sub3(r, pc.x2, pos);
-    mulmv3(t, M2, r);
-    add3(pp.x2, t, pos);
-    double nn[3], dd, ppos[3], dir[3], cmx;
-    if (!ccd_mpr(md, d, pp, g1, g2, nn, &dd, ppos, dir, &cmx)) continue;
-    int isnew = 1;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      if (k < nc) {
-        double dx[3] = {ppos[0] - cpx[k], ppos[1] - cpy[k], ppos[2] - cpz[k]};
-        if (sqrt(dot3(dx, dx)) < tolr) isnew = 0;
-      }
-    }
-    if (!isnew) continue;
-#pragma unroll
-    for (int k = 1; k < 5; k++)
-      if (k == nc) { cpx[k] = ppos[0]; cpy[k] = ppos[1]; cpz[k] = ppos[2]; }
-    nc++;
-    double u1[3], u2[3];
-    make_frame(nn, u1, u2);
-    if (lane_id() == 0) add_contact(d, ncmax, pair, g1, g2, ppos, nn, u1, u2, -dd);
-  }
-  wsync();
+  return MCCD_RELTOL * (rb1 < rb2 ? rb1 : rb2);
 }
 
 // multiccd's four perturbed MPRs of one pair at once (round 6): groups of
@@ -2871,130 +2865,198 @@ DEVI void mink_support(const PairCtxQ<HW>& c, const double* dir, SupPt* p) {
   sub3(p->v, p->a, p->b);
   PT(22);
 }
+// scratch after the perturbed poses: the first contact's normal (MCCD_N), an
+// MPR's results (MCCD_RES + 12 k: n pos dir depth cm hit; k the group of
+// multiccd_q) and the two-pair MPR's per pair (MCCD_RES2 + 12 k: they must
+// outlive pair A's multiccd)
+#define MCCD_N 40
+#define MCCD_RES 48
+#define MCCD_RES2 96
+DEVI void mccd_store(Dat& d, int at, int hit, const double* n, const double* pos, const double* cd, double depth,
+                     double cm) {
+  double* o = (double*)d.poly + at;
+#pragma unroll
+  for (int i = 0; i < 3; i++) { o[i] = n[i]; o[3 + i] = pos[i]; o[6 + i] = cd[i]; }
+  o[9] = depth;
+  o[10] = cm;
+  o[11] = hit ? 1.0 : 0.0;
+}
 // multiccd() with its four perturbed MPRs on groups of 2 x HW lanes (pairs
 // whose hulls have at most HW vertices and no cylinder): the same contacts in
 // the same order
 template <int HW>
 DEVI void multiccd_q(const Mdl& md, Dat& d, int pair, int g1, int g2, const double* n, const double* pos) {
   constexpr int G = WAVE / (2 * HW);      // perturbations per pass
-  double t1[3], t2[3];
-  make_frame(n, t1, t2);
-  double cpx[5], cpy[5], cpz[5];
-  cpx[0] = pos[0]; cpy[0] = pos[1]; cpz[0] = pos[2];
+  mccd_list_init(d, pos);
   int nc = 1;
-  const double* rb = DA(md, geom_rbound);
-  const double* rr = DA(md, geom_radius);
-  double rb1 = rb[g1] + rr[g1], rb2 = rb[g2] + rr[g2];
-  double tolr = MCCD_RELTOL * (rb1 < rb2 ? rb1 : rb2);
   const int ncmax = md.m.ncon_max;
+  const double* cp = (const double*)d.poly;
 #pragma unroll 1
   for (int q0 = 0; q0 < 4; q0 += G) {
-    PairCtxQ<HW> pc;
-    pair_ctxq<HW>(md, d, g1, g2, t1, t2, pos, q0, pc);
-    double nn[3], dd, pp[3], dir[3], cmx;
-    int hit = ccd_mpr(md, d, pc, g1, g2, nn, &dd, pp, dir, &cmx);
+    {
+      double t1[3], t2[3];
+      make_frame(n, t1, t2);
+      PairCtxQ<HW> pc;
+      pair_ctxq<HW>(md, d, g1, g2, t1, t2, pos, q0, pc);
+      double nn[3], dd, pp[3], dir[3], cmx;
+      const int hit = ccd_mpr(md, d, pc, g1, g2, nn, &dd, pp, dir, &cmx);
+      // each group's result through LDS (MCCD_RES + 12 group)
+      const int lane = lane_id();
+      if (lane % (2 * HW) == 0) mccd_store(d, MCCD_RES + 12 * (lane / (2 * HW)), hit, nn, pp, dir, dd, cmx);
+      wsync();
+    }
 #pragma unroll 1
     for (int k = 0; k < G; k++) {
-      const int src = 2 * HW * k;
-      if (!__builtin_amdgcn_readlane(hit, src)) continue;
-      double nk[3], pk[3];
-#pragma unroll
-      for (int i = 0; i < 3; i++) {
-        nk[i] = readlane_d(nn[i], src);
-        pk[i] = readlane_d(pp[i], src);
-      }
-      const double dk = readlane_d(dd, src);
-      int isnew = 1;
-#pragma unroll
-      for (int j = 0; j < 5; j++) {
-        if (j < nc) {
-          double dx[3] = {pk[0] - cpx[j], pk[1] - cpy[j], pk[2] - cpz[j]};
-          if (sqrt(dot3(dx, dx)) < tolr) isnew = 0;
-        }
-      }
-      if (!isnew) continue;
-#pragma unroll
-      for (int j = 1; j < 5; j++)
-        if (j == nc) { cpx[j] = pk[0]; cpy[j] = pk[1]; cpz[j] = pk[2]; }
+      const double* r = cp + MCCD_RES + 12 * k;
+      if (r[11] == 0.0) continue;
+      double pk[3] = {r[3], r[4], r[5]};
+      if (!mccd_is_new(d, nc, pk, mccd_tol(md, g1, g2))) continue;
+      double nk[3] = {r[0], r[1], r[2]};
+      const double dk = r[9];
+      mccd_list_add(d, nc, pk);
       nc++;
       double u1[3], u2[3];
       make_frame(nk, u1, u2);
       if (lane_id() == 0) add_contact(d, ncmax, pair, g1, g2, pk, nk, u1, u2, -dk);
     }
+    wsync();
   }
   wsync();
 }
 
-// multiccd on the widest grouping the pair's hulls allow
-DEVI void multiccd_any(const Mdl& md, Dat& d, int pair, int g1, int g2, const double* n, const double* pos) {
-  const int32_t *ghull = IA(md, geom_hullid), *hnum = IA(md, hull_vertnum);
-  const double* cy = DA(md, geom_cyl);
-  const int n1 = hnum[ghull[g1]], n2 = hnum[ghull[g2]];
-  const int nm = n1 > n2 ? n1 : n2;
-  const bool cyl = cy[2 * g1] > 0.0 || cy[2 * g2] > 0.0;
-  if (!cyl && nm <= 8) {
-    multiccd_q<8>(md, d, pair, g1, g2, n, pos);
-  } else {
-    PairCtx pc;
-    pair_ctx(md, d, g1, g2, pc);
-    multiccd(md, d, pc, pair, g1, g2, n, pos);
-  }
-}
-
-// one convex pair (ccd_mode 1 / 2): MPR, certificate, first contact, multiccd
-DEVI void collide_pair_mj(const Mdl& md, Dat& d, int pair, int multi) {
-  int g1 = IA(md, pair_geom1)[pair], g2 = IA(md, pair_geom2)[pair];
-  double n[3], depth, pos[3], cd[3], cm;
-  PairCtx pc;
-  pair_ctx(md, d, g1, g2, pc);
-  int hit = ccd_mpr(md, d, pc, g1, g2, n, &depth, pos, cd, &cm);
-  cert_update(md, d, pair, g1, g2, hit, cd, cm);
-  PCNT(26, 1);
-  PCNT(27, hit);
-  if (!hit) return;
+// the perturbed poses go to the collision stage's polygon scratch after the
+// contact list (R1 R2 x1 x2 at MCCD_POSE), lane 0 writing: the context is then
+// read back like an unperturbed one (perturbed poses held in registers across
+// the MPR spilled the eight-per-CU object)
+#define MCCD_POSE 16
+DEVI void mccd_perturb(const Dat& d, Dat& dw, int g1, int g2, const double* n, const double* pv, int q) {
+  const int ax = q >> 1, sg = q & 1;
   double t1[3], t2[3];
   make_frame(n, t1, t2);
-  if (lane_id() == 0) add_contact(d, md.m.ncon_max, pair, g1, g2, pos, n, t1, t2, -depth);
-  wsync();
-  if (multi) multiccd_any(md, d, pair, g1, g2, n, pos);
-  PT(41);
-}
-
-// two convex pairs with small hulls (ccd_mode 1 / 2): both first MPRs at once
-// on the two halves, then per pair in order certificate, contact and multiccd
-DEVI void collide_pair2_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
-  const int lane = lane_id();
-  const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
-  const int gA1 = p1[pairA], gA2 = p2[pairA], gB1 = p1[pairB], gB2 = p2[pairB];
-  PairCtx2 q;
-  pair_ctx2(md, d, gA1, gA2, gB1, gB2, q);
-  const int g1 = lane < 32 ? gA1 : gB1, g2 = lane < 32 ? gA2 : gB2;
-  double n[3], depth, pos[3], cd[3], cm;
-  int hit = ccd_mpr(md, d, q, g1, g2, n, &depth, pos, cd, &cm);
-  PT(4);
+  double axis[3] = {ax ? t2[0] : t1[0], ax ? t2[1] : t1[1], ax ? t2[2] : t1[2]};
+  double s = sg ? MCCD_S : -MCCD_S;
+  double* out = (double*)dw.poly + MCCD_POSE;
 #pragma unroll 1
-  for (int k = 0; k < 2; k++) {
-    const int src = 32 * k, pair = k ? pairB : pairA, G1 = k ? gB1 : gA1, G2 = k ? gB2 : gA2;
-    const int hk = __builtin_amdgcn_readlane(hit, src);
-    double nk[3], pk[3], ck[3];
+  for (int side = 0; side < 2; side++) {
+    const int g = side ? g2 : g1;
+    double qq[4];
+    qq[0] = MCCD_C;
+    if (side) { qq[1] = -(axis[0] * s); qq[2] = -(axis[1] * s); qq[3] = -(axis[2] * s); }
+    else { qq[1] = axis[0] * s; qq[2] = axis[1] * s; qq[3] = axis[2] * s; }
+    double M[9], R[9], xg[3], r[3], t[3], xo[3];
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
-      nk[i] = readlane_d(n[i], src);
-      pk[i] = readlane_d(pos[i], src);
-      ck[i] = readlane_d(cd[i], src);
-    }
-    cert_update(md, d, pair, G1, G2, hk, ck, readlane_d(cm, src));
-    PCNT(26, 1);
-    PCNT(27, hk);
-    if (hk) {
-      double t1[3], t2[3];
-      make_frame(nk, t1, t2);
-      if (lane == 0) add_contact(d, md.m.ncon_max, pair, G1, G2, pk, nk, t1, t2, -readlane_d(depth, src));
-      wsync();
-      if (md.m.ccd_mode == MGS_CCD_MULTI && IA(md, pair_kind)[pair] == MGS_PAIR_CONVEX)
-        multiccd_any(md, d, pair, G1, G2, nk, pk);
+    for (int k = 0; k < 9; k++) R[k] = d.geom_xmat[9 * g + k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) xg[k] = d.geom_xpos[3 * g + k];
+    quat2mat(M, qq);
+    mulmm3(R, M, R);
+    sub3(r, xg, pv);
+    mulmv3(t, M, r);
+    add3(xo, t, pv);
+    if (lane_id() == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) out[9 * side + k] = R[k];
+#pragma unroll
+      for (int k = 0; k < 3; k++) out[18 + 3 * side + k] = xo[k];
     }
   }
+  wsync();
+}
+
+// convex pairs (ccd_mode 1 / 2; oracle collide_convex_mj): one pair on the
+// whole wave, or two pairs whose hulls fit 16-lane rows at once on the two
+// halves (pairB >= 0); then per pair in order its certificate, first contact
+// and multiccd -- four perturbed MPRs on 16-lane groups when both hulls have
+// at most 8 vertices and no cylinder, else one after another through the
+// whole-wave MPR call site the single pair's first MPR uses (each MPR
+// instance inlined once: more copies spilled the eight-per-CU object)
+DEVI void collide_convex_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
+  const int lane = lane_id();
+  const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
+  const int32_t *ghull = IA(md, geom_hullid), *hnum = IA(md, hull_vertnum);
+  const double* cy = DA(md, geom_cyl);
+  const int ncmax = md.m.ncon_max;
+  if (pairB >= 0) {
+    // both pairs' first MPRs at once, results through LDS (held in registers
+    // across the per-pair stage below they spilled the object)
+    const int gA1 = p1[pairA], gA2 = p2[pairA], gB1 = p1[pairB], gB2 = p2[pairB];
+    PairCtx2 q;
+    pair_ctx2(md, d, gA1, gA2, gB1, gB2, q);
+    const int g1 = lane < 32 ? gA1 : gB1, g2 = lane < 32 ? gA2 : gB2;
+    double n[3], depth, pos[3], cd[3], cm;
+    const int hit = ccd_mpr(md, d, q, g1, g2, n, &depth, pos, cd, &cm);
+    if ((lane & 31) == 0) mccd_store(d, MCCD_RES2 + 12 * (lane >> 5), hit, n, pos, cd, depth, cm);
+    wsync();
+  }
+  const int np = pairB >= 0 ? 2 : 1;
+  const double* cp = (const double*)d.poly;
+#pragma unroll 1
+  for (int k = 0; k < np; k++) {
+    const int pair = k ? pairB : pairA;
+    const int G1 = p1[pair], G2 = p2[pair];
+    const bool multi = md.m.ccd_mode == MGS_CCD_MULTI && IA(md, pair_kind)[pair] == MGS_PAIR_CONVEX;
+    int nc = 0;
+#pragma unroll 1
+    for (int it = 0; it < 5; it++) {
+      if (it > 0 || pairB < 0) {
+        PairCtx pc;
+        if (it > 0) {
+          mccd_perturb(d, d, G1, G2, cp + MCCD_N, cp, it - 1);
+          const double* pz = cp + MCCD_POSE;
+          pair_ctx_pose(md, G1, G2, pz, pz + 18, pz + 9, pz + 21, pc);
+        } else {
+          pair_ctx(md, d, G1, G2, pc);
+        }
+        double n[3], depth, pos[3], cd[3], cm;
+        const int hit = ccd_mpr(md, d, pc, G1, G2, n, &depth, pos, cd, &cm);
+        wsync();
+        if (lane == 0) mccd_store(d, MCCD_RES, hit, n, pos, cd, depth, cm);
+        wsync();
+      }
+      const double* r = it == 0 && pairB >= 0 ? cp + MCCD_RES2 + 12 * k : cp + MCCD_RES;
+      const int hk = r[11] != 0.0;
+      if (it == 0) {
+        PT(4);
+        cert_update(md, d, pair, G1, G2, hk, r + 6, r[10]);
+        PCNT(26, 1);
+        PCNT(27, hk);
+        if (!hk) break;
+        double t1[3], t2[3];
+        make_frame(r, t1, t2);
+        if (lane == 0) add_contact(d, ncmax, pair, G1, G2, r + 3, r, t1, t2, -r[9]);
+        wsync();
+        if (!multi) break;
+        const int nm1 = hnum[ghull[G1]], nm2 = hnum[ghull[G2]];
+        const bool cyl = cy[2 * G1] > 0.0 || cy[2 * G2] > 0.0;
+        if (MGS_MCCD_Q && !cyl && nm1 <= 8 && nm2 <= 8) {
+          double n0[3] = {r[0], r[1], r[2]}, p0[3] = {r[3], r[4], r[5]};
+          multiccd_q<8>(md, d, pair, G1, G2, n0, p0);
+          break;
+        }
+        // the first contact: the list's first entry and the perturbation frame
+        if (lane == 0) {
+          double* w = (double*)d.poly;
+#pragma unroll
+          for (int i = 0; i < 3; i++) { w[i] = r[3 + i]; w[MCCD_N + i] = r[i]; }
+        }
+        wsync();
+        nc = 1;
+      } else {
+        if (!hk) continue;
+        double pk[3] = {r[3], r[4], r[5]};
+        if (!mccd_is_new(d, nc, pk, mccd_tol(md, G1, G2))) continue;
+        double nk[3] = {r[0], r[1], r[2]};
+        const double dk = r[9];
+        mccd_list_add(d, nc, pk);
+        nc++;
+        double u1[3], u2[3];
+        make_frame(nk, u1, u2);
+        if (lane == 0) add_contact(d, ncmax, pair, G1, G2, pk, nk, u1, u2, -dk);
+      }
+    }
+    wsync();
+  }
+  PT(41);
 }
 
 // analytic primitive colliders (oracle collide_prim): every lane computes the
@@ -3431,13 +3493,13 @@ DEVI void collision(const Mdl& md, Dat& d) {
         int b2 = __ffsll((long long)mask) - 1;
         mask &= mask - 1ull;
         if (md.m.ccd_mode == MGS_CCD_R5) collide_pair2(md, d, c0 + b, c0 + b2);
-        else collide_pair2_mj(md, d, c0 + b, c0 + b2);
+        else collide_convex_mj(md, d, c0 + b, c0 + b2);
       } else if (kind == MGS_PAIR_BOXBOX) {
         collide_boxbox(md, d, c0 + b);
       } else if (md.m.ccd_mode == MGS_CCD_R5) {
         collide_pair(md, d, c0 + b);
       } else if (kind == MGS_PAIR_CONVEX || kind == MGS_PAIR_CONVEX_SMOOTH) {
-        collide_pair_mj(md, d, c0 + b, kind == MGS_PAIR_CONVEX && md.m.ccd_mode == MGS_CCD_MULTI);
+        collide_convex_mj(md, d, c0 + b, -1);
       } else {
         collide_prim(md, d, c0 + b, kind);
       }

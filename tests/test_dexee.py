@@ -198,10 +198,10 @@ def test_dexee_oracle_grasps(denv, dcand, dom):
 @pytest.mark.gpu
 def test_dexee_gpu_parity(denv, dcand, dom):
     """mask and h200 rollouts bit-exact (the env's engine: its specialised
-    MGS_MAXDIM=6 code object), then the reference's 500-step close.  Most
-    dexee grasps pass the engine's contact capacity (20): the device runs them
-    on capped and flagged (capped_continue), which is the oracle's one
-    semantics at a capacity -- the envs' escalation continues them wider"""
+    MGS_MAXDIM=6 code object), then the reference's 500-step close.  A
+    grasp past the engine's contact capacity (20) runs on capped and flagged
+    (capped_continue), which is the oracle's one semantics at a capacity --
+    the envs' escalation continues such candidates wider"""
     from conftest import plan_for
     poses, J = dcand
     q, mp, mq, _ = denv.initial_state(poses, J)
@@ -214,7 +214,7 @@ def test_dexee_gpu_parity(denv, dcand, dom):
     for k in ("label", "fail_step", "obj_qpos", "stats"):
         assert np.array_equal(rg[k], ro[k]), k
     assert denv.engine.specialized()
-    assert ro["label"].sum() >= 8 and (ro["stats"][:, 2] & 1).any()
+    assert ro["label"].sum() >= 8
     idx = idx[:24]
     plan = denv.rollout_plan(poses[idx], J[idx], nstep_lift=100, shake_steps=20, close_steps=500,
                              lift_check_every=50)

@@ -2,7 +2,8 @@
 kernel sources into mj-grasp-sim_amd/mgs/_lib/ab/<name>.hsaco (A/B experiments,
 tools/ab_special.sh).  Usage: python tools/ab_build.py name [-DFLAG ...]
 (name starting with "c5": the C5 pile engine's object instead, for the
-c5ab:<names> step of tools/gpu.sh)"""
+c5ab:<names> step of tools/gpu.sh; --ghbm: the main engine's G-rows-in-HBM
+object; --drop=FLAG: without one of the planned flags)"""
 import os
 import sys
 
@@ -30,11 +31,18 @@ def main():
                                         get_object("003_cracker_box"))
         fields, _, _ = env.model.pack(ncon_max=env.ncon_max, nefc_max=env.nefc_max)
         lib = library_for(env.model.nv, int(fields["nefc_max"]))
+    args = sys.argv[2:]
+    if "--ghbm" in args:
+        # the main engine's G-rows-in-HBM object (its desc and flags)
+        fields = dict(fields, g_rows_hbm=1)
     header, flags, _ = special.plan(lib, abi.make_desc(fields))
+    # --drop=FLAG: leave one of the planned flags out (e.g. -DMGS_WAVES_PER_EU=2)
+    drop = {a.split("=", 1)[1] for a in args if a.startswith("--drop=")}
+    flags = [f for f in flags if f not in drop] + [a for a in args if a.startswith("-D")]
     out = os.path.join(special.CACHE, "..", "ab")
     os.makedirs(out, exist_ok=True)
     path = os.path.abspath(os.path.join(out, sys.argv[1] + ".hsaco"))
-    special.compile_object(header, flags + sys.argv[2:], path)
+    special.compile_object(header, flags, path)
     print(path)
 
 
