@@ -2495,19 +2495,10 @@ DEVI void collide_boxbox(const Mdl& md, Dat& d, int pair) {
 // Primitive pairs: the analytic colliders.  Parity vs MuJoCo unpinned
 // (DESIGN.md §2); GPU == oracle bit for bit.
 #define CCD_EPS 2.2204460492503131e-16
-// multiccd's four perturbations on 16-lane groups at once (1) or one after
-// another on the whole wave (0).  Off in register-capped objects
-// (MGS_WAVES_PER_EU, the main engine's G-rows-in-HBM object): there the
-// compiler spills inside the groups' divergent MPR loops and the results left
-// the oracle's (round 6: tools/probe_ab_parity.py, the same source without the
-// cap or with the perturbations in sequence is bit-exact) -- the grouped MPR
-// needs registers the capped object does not have
+// multiccd's four perturbations on 16-lane groups at once (1, ccd_mpr_q) or
+// one after another on the whole wave (0: A/B builds)
 #ifndef MGS_MCCD_Q
-#ifdef MGS_WAVES_PER_EU
-#define MGS_MCCD_Q 0
-#else
 #define MGS_MCCD_Q 1
-#endif
 #endif
 #define MCCD_RELTOL 1e-3
 #define MCCD_C 0.9999998750000026       // cos(5e-4): half the perturbation angle
@@ -2865,6 +2856,140 @@ DEVI void mink_support(const PairCtxQ<HW>& c, const double* dir, SupPt* p) {
   sub3(p->v, p->a, p->b);
   PT(22);
 }
+// multiccd_q's MPR: ccd_mpr's arithmetic step for step, with every group in
+// lockstep -- one support call per pass for the whole wave, each group
+// advancing its own phase (first two supports, portal discovery, refinement,
+// penetration) with its own counter; a group that is done keeps its state and
+// the loop ends when no group is left.  (ccd_mpr's own loops diverge per group
+// here, and in the register-capped object the compiler spilled inside those
+// divergent loops: 39 of 41 parity rollouts left the oracle, round 6.)  The
+// normal, depth and position of a hit; no certificate (multiccd has none).
+#define MQ_P1 0
+#define MQ_P2 1
+#define MQ_DISC 2
+#define MQ_REF 3
+#define MQ_PEN 4
+#define MQ_FIN 5
+#define MQ_DONE 6
+template <int HW>
+DEVI int ccd_mpr_q(const Mdl& md, const Dat& d, const PairCtxQ<HW>& pc, double* n, double* depth, double* pos) {
+  const double tol = md.m.mpr_tolerance;
+  const int maxit = md.m.ccd_iterations;
+  SupPt p0, p1, p2, p3, ps;
+  double dir[3];
+  int ph = MQ_P1, it = 0, hit = 0;
+  mpr_centres(pc, d, 0, 0, p0.a, p0.b);
+  sub3(p0.v, p0.a, p0.b);
+  if (ccd_vzero(p0.v)) p0.v[0] = p0.v[0] + CCD_EPS * 10.0;
+  dir[0] = -p0.v[0]; dir[1] = -p0.v[1]; dir[2] = -p0.v[2];
+  ccd_normalize(dir);
+  p1 = p0; p2 = p0; p3 = p0;
+  for (;;) {
+    if (ph == MQ_REF || ph == MQ_PEN) {
+      ccd_portal_dir(dir, p1, p2, p3);
+      if (ph == MQ_REF) {
+        const double dt = dot3(dir, p1.v);
+        if (ccd_iszero(dt) || dt > 0.0) { ph = MQ_PEN; it = 0; }
+      }
+    }
+    if (!__ballot(ph < MQ_FIN)) break;
+    mink_support(pc, dir, &ps);
+    const double dt = dot3(ps.v, dir);
+    if (ph == MQ_P1) {
+      if (ccd_iszero(dt) || dt < 0.0) {
+        ph = MQ_DONE;
+      } else {
+        p1 = ps;
+        cross3(dir, p0.v, p1.v);
+        if (ccd_iszero(dot3(dir, dir))) {
+          if (!ccd_vzero(p1.v)) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) { n[k] = p1.v[k]; pos[k] = (p1.a[k] + p1.b[k]) * 0.5; }
+            *depth = sqrt(dot3(n, n));
+            ccd_normalize(n);
+            hit = 1;
+          }
+          ph = MQ_DONE;
+        } else {
+          ccd_normalize(dir);
+          ph = MQ_P2;
+        }
+      }
+    } else if (ph == MQ_P2) {
+      if (ccd_iszero(dt) || dt < 0.0) {
+        ph = MQ_DONE;
+      } else {
+        p2 = ps;
+        double e1[3], e2[3];
+        sub3(e1, p1.v, p0.v);
+        sub3(e2, p2.v, p0.v);
+        cross3(dir, e1, e2);
+        ccd_normalize(dir);
+        if (dot3(dir, p0.v) > 0.0) {
+          SupPt tmp = p1; p1 = p2; p2 = tmp;
+          dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+        }
+        ph = MQ_DISC;
+        it = 0;
+      }
+    } else if (ph == MQ_DISC) {
+      if (ccd_iszero(dt) || dt < 0.0) {
+        ph = MQ_DONE;
+      } else {
+        p3 = ps;
+        double c[3];
+        int cont = 0;
+        cross3(c, p1.v, p3.v);
+        double dc = dot3(c, p0.v);
+        if (dc < 0.0 && !ccd_iszero(dc)) { p2 = p3; cont = 1; }
+        if (!cont) {
+          cross3(c, p3.v, p2.v);
+          dc = dot3(c, p0.v);
+          if (dc < 0.0 && !ccd_iszero(dc)) { p1 = p3; cont = 1; }
+        }
+        if (!cont) {
+          ph = MQ_REF;
+          it = 0;
+        } else {
+          double e1[3], e2[3];
+          sub3(e1, p1.v, p0.v);
+          sub3(e2, p2.v, p0.v);
+          cross3(dir, e1, e2);
+          ccd_normalize(dir);
+          if (++it == CCD_MAXLOOP) ph = MQ_DONE;
+        }
+      }
+    } else if (ph == MQ_REF) {
+      if (!(ccd_iszero(dt) || dt > 0.0) || ccd_reach_tol(p1, p2, p3, ps, dir, tol)) {
+        ph = MQ_DONE;
+      } else {
+        PORTAL_EXPAND(p0, p1, p2, p3, ps);
+        if (++it == CCD_MAXLOOP) ph = MQ_DONE;
+      }
+    } else if (ph == MQ_PEN) {
+      if (ccd_reach_tol(p1, p2, p3, ps, dir, tol) || it > maxit) {
+        ph = MQ_FIN;
+      } else {
+        PORTAL_EXPAND(p0, p1, p2, p3, ps);
+        it++;
+      }
+    }
+  }
+  // the penetration's end (ccd_mpr's last block), every lane computing it; the
+  // groups that stopped there take it
+  double w[3], fp[3];
+  const double dep = sqrt(ccd_tri_dist2(p1.v, p2.v, p3.v, w));
+  ccd_normalize(w);
+  ccd_find_pos(p0, p1, p2, p3, fp);
+  if (ph == MQ_FIN && !ccd_iszero(dep)) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) { n[k] = w[k]; pos[k] = fp[k]; }
+    *depth = dep;
+    hit = 1;
+  }
+  return hit;
+}
+
 // scratch after the perturbed poses: the first contact's normal (MCCD_N), an
 // MPR's results (MCCD_RES + 12 k: n pos dir depth cm hit; k the group of
 // multiccd_q) and the two-pair MPR's per pair (MCCD_RES2 + 12 k: they must
@@ -2898,8 +3023,8 @@ DEVI void multiccd_q(const Mdl& md, Dat& d, int pair, int g1, int g2, const doub
       make_frame(n, t1, t2);
       PairCtxQ<HW> pc;
       pair_ctxq<HW>(md, d, g1, g2, t1, t2, pos, q0, pc);
-      double nn[3], dd, pp[3], dir[3], cmx;
-      const int hit = ccd_mpr(md, d, pc, g1, g2, nn, &dd, pp, dir, &cmx);
+      double nn[3], dd = 0.0, pp[3], dir[3] = {0.0, 0.0, 0.0}, cmx = -1.0;
+      const int hit = ccd_mpr_q<HW>(md, d, pc, nn, &dd, pp);
       // each group's result through LDS (MCCD_RES + 12 group)
       const int lane = lane_id();
       if (lane % (2 * HW) == 0) mccd_store(d, MCCD_RES + 12 * (lane / (2 * HW)), hit, nn, pp, dir, dd, cmx);

@@ -10,7 +10,7 @@ NAMES = ['loop/ctrl/checks', 'kinematics', 'com_pos', 'coll: certificate checks'
          'noslip', 'finalize', 'int: crb', 'int: qDeriv+M', 'int: ldl+solve+qpos', 'coll: small-hull support calls',
          'newton: H accumulate', 'newton: H to rows', 'newton: H factor',
          'con: equality rows', 'con: limit/friction rows', 'actuation', 'passive', 'rne',
-         'coll: big-hull support calls', 'coll: feature passes', 'coll: select4+add (lane 0)',
+         'coll: big-hull support calls', 'coll: feature passes', 'coll: select4+add / multiccd',
          'noslip/pgs block: residual', 'noslip/pgs block: qcqp', 'noslip/pgs block: update',
          'coll: sort+dedup', 'coll: hull chains', 'coll: clip+depth filter', 'coll: broadphase AABB',
          'coll: broadphase OBB']
