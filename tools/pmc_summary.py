@@ -40,10 +40,43 @@ def _commit():
         return None
 
 
+def main_launch_stats(trace_csv, out_path):
+    """per-kernel time of the traced command without the escalation objects'
+    *_esc launches (one-workgroup re-runs queued behind the persistent grids:
+    their trace durations are mostly dispatch wait), as
+    percentages of the remaining kernel time; the *_esc rows listed apart"""
+    with open(trace_csv) as f:
+        rr = list(csv.DictReader(f))
+    agg = {}
+    for r in rr:
+        k = r["Kernel_Name"].split("(")[0]
+        dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+        a = agg.setdefault(k, [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += dt
+        a[2] = max(a[2], dt)
+    main = {k: v for k, v in agg.items() if "_esc" not in k}
+    tot = sum(v[1] for v in main.values()) or 1.0
+    with open(out_path, "w") as f:
+        f.write("kernel time of the traced command without the escalation re-runs (*_esc), ms\n")
+        f.write("%-44s %7s %11s %10s %10s %7s\n" % ("kernel", "calls", "total", "mean", "max", "pct"))
+        for k, (n, t, mx) in sorted(main.items(), key=lambda kv: -kv[1][1]):
+            f.write("%-44s %7d %11.3f %10.3f %10.3f %6.1f%%\n" % (k[:44], n, t, t / n, mx, 100.0 * t / tot))
+        esc = {k: v for k, v in agg.items() if "_esc" in k}
+        if esc:
+            f.write("\nescalation re-runs (not in the percentages: trace span includes the wait for CUs)\n")
+            for k, (n, t, mx) in sorted(esc.items()):
+                f.write("%-44s %7d %11.3f %10.3f %10.3f\n" % (k[:44], n, t, t / n, mx))
+    print(open(out_path).read())
+
+
 def main(d, tag="r03"):
     tr = os.path.join(d, "trace", "bench_kernel_stats.csv")
     if os.path.isfile(tr):
         shutil.copy(tr, os.path.join(PROF, f"{tag}_rocprof_kernel_stats.csv"))
+    kt = os.path.join(d, "trace", "bench_kernel_trace.csv")
+    if os.path.isfile(kt):
+        main_launch_stats(kt, os.path.join(PROF, f"{tag}_rocprof_main_launches.txt"))
     out = {"source": "rocprofv3 --kernel-trace --pmc <counters> (separate passes) on `python3 bench.py --streams 1 "
                      "--steps 1 --warmup 0 --cpu-budget 0 --e2e-steps 0 --no-escalate --fused 0` (tools/gpu.sh pmc, "
                      f"{tag}); "
