@@ -2849,7 +2849,7 @@ DEVI void support_pairq(const PairCtxQ<HW>& c, const double* dir, double* out1, 
   }
 }
 template <int HW>
-DEVI void mink_support(const PairCtxQ<HW>& c, const double* dir, SupPt* p) {
+DEVI void mink_support(const PairCtxQ<HW>& c, const double* dir, SupPt* p, unsigned long long) {
   PT(4);
   PCNT(28, 1);
   support_pairq<HW>(c, dir, p->a, p->b);
@@ -2871,8 +2871,8 @@ DEVI void mink_support(const PairCtxQ<HW>& c, const double* dir, SupPt* p) {
 #define MQ_PEN 4
 #define MQ_FIN 5
 #define MQ_DONE 6
-template <int HW>
-DEVI int ccd_mpr_q(const Mdl& md, const Dat& d, const PairCtxQ<HW>& pc, double* n, double* depth, double* pos) {
+template <class QC>
+DEVI int ccd_mpr_q(const Mdl& md, const Dat& d, const QC& pc, double* n, double* depth, double* pos) {
   const double tol = md.m.mpr_tolerance;
   const int maxit = md.m.ccd_iterations;
   SupPt p0, p1, p2, p3, ps;
@@ -2892,8 +2892,9 @@ DEVI int ccd_mpr_q(const Mdl& md, const Dat& d, const PairCtxQ<HW>& pc, double* 
         if (ccd_iszero(dt) || dt > 0.0) { ph = MQ_PEN; it = 0; }
       }
     }
-    if (!__ballot(ph < MQ_FIN)) break;
-    mink_support(pc, dir, &ps);
+    const unsigned long long act = __ballot(ph < MQ_FIN);
+    if (!act) break;
+    mink_support(pc, dir, &ps, act);
     const double dt = dot3(ps.v, dir);
     if (ph == MQ_P1) {
       if (ccd_iszero(dt) || dt < 0.0) {
@@ -3006,6 +3007,27 @@ DEVI void mccd_store(Dat& d, int at, int hit, const double* n, const double* pos
   o[10] = cm;
   o[11] = hit ? 1.0 : 0.0;
 }
+// each group's MPR result (multiccd_q's and multiccd_w's, MCCD_RES + 12 group)
+// taken in perturbation order: distinct ones added to the pair's contacts
+DEVI void mccd_take_groups(const Mdl& md, Dat& d, int pair, int g1, int g2, int ngroups, int& nc) {
+  const double* cp = (const double*)d.poly;
+  const int ncmax = md.m.ncon_max;
+#pragma unroll 1
+  for (int k = 0; k < ngroups; k++) {
+    const double* r = cp + MCCD_RES + 12 * k;
+    if (r[11] == 0.0) continue;
+    double pk[3] = {r[3], r[4], r[5]};
+    if (!mccd_is_new(d, nc, pk, mccd_tol(md, g1, g2))) continue;
+    double nk[3] = {r[0], r[1], r[2]};
+    const double dk = r[9];
+    mccd_list_add(d, nc, pk);
+    nc++;
+    double u1[3], u2[3];
+    make_frame(nk, u1, u2);
+    if (lane_id() == 0) add_contact(d, ncmax, pair, g1, g2, pk, nk, u1, u2, -dk);
+  }
+  wsync();
+}
 // multiccd() with its four perturbed MPRs on groups of 2 x HW lanes (pairs
 // whose hulls have at most HW vertices and no cylinder): the same contacts in
 // the same order
@@ -3014,8 +3036,6 @@ DEVI void multiccd_q(const Mdl& md, Dat& d, int pair, int g1, int g2, const doub
   constexpr int G = WAVE / (2 * HW);      // perturbations per pass
   mccd_list_init(d, pos);
   int nc = 1;
-  const int ncmax = md.m.ncon_max;
-  const double* cp = (const double*)d.poly;
 #pragma unroll 1
   for (int q0 = 0; q0 < 4; q0 += G) {
     {
@@ -3024,27 +3044,13 @@ DEVI void multiccd_q(const Mdl& md, Dat& d, int pair, int g1, int g2, const doub
       PairCtxQ<HW> pc;
       pair_ctxq<HW>(md, d, g1, g2, t1, t2, pos, q0, pc);
       double nn[3], dd = 0.0, pp[3], dir[3] = {0.0, 0.0, 0.0}, cmx = -1.0;
-      const int hit = ccd_mpr_q<HW>(md, d, pc, nn, &dd, pp);
+      const int hit = ccd_mpr_q(md, d, pc, nn, &dd, pp);
       // each group's result through LDS (MCCD_RES + 12 group)
       const int lane = lane_id();
       if (lane % (2 * HW) == 0) mccd_store(d, MCCD_RES + 12 * (lane / (2 * HW)), hit, nn, pp, dir, dd, cmx);
       wsync();
     }
-#pragma unroll 1
-    for (int k = 0; k < G; k++) {
-      const double* r = cp + MCCD_RES + 12 * k;
-      if (r[11] == 0.0) continue;
-      double pk[3] = {r[3], r[4], r[5]};
-      if (!mccd_is_new(d, nc, pk, mccd_tol(md, g1, g2))) continue;
-      double nk[3] = {r[0], r[1], r[2]};
-      const double dk = r[9];
-      mccd_list_add(d, nc, pk);
-      nc++;
-      double u1[3], u2[3];
-      make_frame(nk, u1, u2);
-      if (lane_id() == 0) add_contact(d, ncmax, pair, g1, g2, pk, nk, u1, u2, -dk);
-    }
-    wsync();
+    mccd_take_groups(md, d, pair, g1, g2, G, nc);
   }
   wsync();
 }
@@ -3054,13 +3060,13 @@ DEVI void multiccd_q(const Mdl& md, Dat& d, int pair, int g1, int g2, const doub
 // read back like an unperturbed one (perturbed poses held in registers across
 // the MPR spilled the eight-per-CU object)
 #define MCCD_POSE 16
-DEVI void mccd_perturb(const Dat& d, Dat& dw, int g1, int g2, const double* n, const double* pv, int q) {
+DEVI void mccd_perturb(const Dat& d, Dat& dw, int g1, int g2, const double* n, const double* pv, int q, int at) {
   const int ax = q >> 1, sg = q & 1;
   double t1[3], t2[3];
   make_frame(n, t1, t2);
   double axis[3] = {ax ? t2[0] : t1[0], ax ? t2[1] : t1[1], ax ? t2[2] : t1[2]};
   double s = sg ? MCCD_S : -MCCD_S;
-  double* out = (double*)dw.poly + MCCD_POSE;
+  double* out = (double*)dw.poly + at;
 #pragma unroll 1
   for (int side = 0; side < 2; side++) {
     const int g = side ? g2 : g1;
@@ -3086,6 +3092,68 @@ DEVI void mccd_perturb(const Dat& d, Dat& dw, int g1, int g2, const double* n, c
     }
   }
   wsync();
+}
+
+// multiccd's four perturbed MPRs of a pair that multiccd_q cannot take (a hull
+// of more than 8 vertices, or a cylinder: the gripper's link meshes on the
+// object), in lockstep on four 16-lane groups as there (ccd_mpr_q), each
+// support of the four perturbations computed by the whole wave in turn
+// (support_pair over the pair's hulls, the group's perturbed poses from LDS,
+// only for the groups still running): four MPR scalar chains at once instead
+// of one after another, the same supports, the same contacts in the same order
+#ifndef MGS_MCCD_W
+#define MGS_MCCD_W 1   // 0: these perturbations one after another (A/B builds)
+#endif
+#define MCCD_POSEW 128   // the four perturbed poses (24 doubles each: R1 R2 x1 x2)
+struct PairCtxW {
+  PairCtx base;          // the pair's hulls, radii and cylinder sizes (its poses unused)
+  const double* pose;    // the four perturbed poses
+  double cx1[3], cx2[3];  // this lane's group's perturbed centres
+};
+DEVI void mpr_centres(const PairCtxW& c, const Dat&, int, int, double* a, double* b) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) { a[k] = c.cx1[k]; b[k] = c.cx2[k]; }
+}
+DEVI void mink_support(const PairCtxW& c, const double* dir, SupPt* p, unsigned long long act) {
+  const int grp = lane_id() >> 4;
+#pragma unroll 1
+  for (int g = 0; g < 4; g++) {
+    if (!((act >> (16 * g)) & 1ull)) continue;
+    double dg[3] = {readlane_d(dir[0], 16 * g), readlane_d(dir[1], 16 * g), readlane_d(dir[2], 16 * g)};
+    PairCtx q = c.base;
+    const double* P = c.pose + 24 * g;
+#pragma unroll
+    for (int k = 0; k < 9; k++) { q.R1[k] = P[k]; q.R2[k] = P[9 + k]; }
+#pragma unroll
+    for (int k = 0; k < 3; k++) { q.x1[k] = P[18 + k]; q.x2[k] = P[21 + k]; }
+    SupPt t;
+    mink_support(q, dg, &t);
+    if (grp == g) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) { p->a[k] = t.a[k]; p->b[k] = t.b[k]; }
+    }
+  }
+  sub3(p->v, p->a, p->b);
+}
+DEVI void multiccd_w(const Mdl& md, Dat& d, int pair, int g1, int g2, const double* n, const double* pos) {
+  mccd_list_init(d, pos);
+#pragma unroll 1
+  for (int q = 0; q < 4; q++) mccd_perturb(d, d, g1, g2, n, pos, q, MCCD_POSEW + 24 * q);
+  const int lane = lane_id(), grp = lane >> 4;
+  {
+    PairCtxW pc;
+    pair_ctx(md, d, g1, g2, pc.base);
+    pc.pose = (const double*)d.poly + MCCD_POSEW;
+    const double* P = pc.pose + 24 * grp;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { pc.cx1[k] = P[18 + k]; pc.cx2[k] = P[21 + k]; }
+    double nn[3], dd = 0.0, pp[3], dir[3] = {0.0, 0.0, 0.0};
+    const int hit = ccd_mpr_q(md, d, pc, nn, &dd, pp);
+    if ((lane & 15) == 0) mccd_store(d, MCCD_RES + 12 * grp, hit, nn, pp, dir, dd, -1.0);
+    wsync();
+  }
+  int nc = 1;
+  mccd_take_groups(md, d, pair, g1, g2, 4, nc);
 }
 
 // convex pairs (ccd_mode 1 / 2; oracle collide_convex_mj): one pair on the
@@ -3126,7 +3194,7 @@ DEVI void collide_convex_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
       if (it > 0 || pairB < 0) {
         PairCtx pc;
         if (it > 0) {
-          mccd_perturb(d, d, G1, G2, cp + MCCD_N, cp, it - 1);
+          mccd_perturb(d, d, G1, G2, cp + MCCD_N, cp, it - 1, MCCD_POSE);
           const double* pz = cp + MCCD_POSE;
           pair_ctx_pose(md, G1, G2, pz, pz + 18, pz + 9, pz + 21, pc);
         } else {
@@ -3156,6 +3224,11 @@ DEVI void collide_convex_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
         if (MGS_MCCD_Q && !cyl && nm1 <= 8 && nm2 <= 8) {
           double n0[3] = {r[0], r[1], r[2]}, p0[3] = {r[3], r[4], r[5]};
           multiccd_q<8>(md, d, pair, G1, G2, n0, p0);
+          break;
+        }
+        if (MGS_MCCD_W) {
+          double n0[3] = {r[0], r[1], r[2]}, p0[3] = {r[3], r[4], r[5]};
+          multiccd_w(md, d, pair, G1, G2, n0, p0);
           break;
         }
         // the first contact: the list's first entry and the perturbation frame
