@@ -3163,7 +3163,7 @@ DEVI void multiccd_w(const Mdl& md, Dat& d, int pair, int g1, int g2, const doub
 // at most 8 vertices and no cylinder, else one after another through the
 // whole-wave MPR call site the single pair's first MPR uses (each MPR
 // instance inlined once: more copies spilled the eight-per-CU object)
-DEVI void collide_convex_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
+DEVI void collide_convex_mj(const Mdl& md, Dat& d, int pairA, int pairB, int mccd) {
   const int lane = lane_id();
   const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
   const int32_t *ghull = IA(md, geom_hullid), *hnum = IA(md, hull_vertnum);
@@ -3187,7 +3187,7 @@ DEVI void collide_convex_mj(const Mdl& md, Dat& d, int pairA, int pairB) {
   for (int k = 0; k < np; k++) {
     const int pair = k ? pairB : pairA;
     const int G1 = p1[pair], G2 = p2[pair];
-    const bool multi = md.m.ccd_mode == MGS_CCD_MULTI && IA(md, pair_kind)[pair] == MGS_PAIR_CONVEX;
+    const bool multi = mccd && md.m.ccd_mode == MGS_CCD_MULTI && IA(md, pair_kind)[pair] == MGS_PAIR_CONVEX;
     int nc = 0;
 #pragma unroll 1
     for (int it = 0; it < 5; it++) {
@@ -3633,8 +3633,12 @@ DEVI unsigned long long obb_separated_wave(const Dat& d, unsigned long long am, 
   return sep;
 }
 
-// broadphase over all admissible pairs (lanes over pairs), then narrowphase in pair order
-DEVI void collision(const Mdl& md, Dat& d) {
+// broadphase over all admissible pairs (lanes over pairs), then narrowphase in
+// pair order.  mccd 0 (the collision masks: forward(full 0)): no multiccd --
+// its contacts repeat a pair that already has one, so no mask predicate can
+// change, and they cannot crowd a later pair's first contact out of the
+// capacity (oracle_collision_free, the same rule)
+DEVI void collision(const Mdl& md, Dat& d, int mccd = 1) {
   int lane = lane_id();
   const int32_t *p1 = IA(md, pair_geom1), *p2 = IA(md, pair_geom2);
   const double *aabb = DA(md, geom_aabb), *pm = DA(md, pair_margin);
@@ -3691,13 +3695,13 @@ DEVI void collision(const Mdl& md, Dat& d) {
         int b2 = __ffsll((long long)mask) - 1;
         mask &= mask - 1ull;
         if (md.m.ccd_mode == MGS_CCD_R5) collide_pair2(md, d, c0 + b, c0 + b2);
-        else collide_convex_mj(md, d, c0 + b, c0 + b2);
+        else collide_convex_mj(md, d, c0 + b, c0 + b2, mccd);
       } else if (kind == MGS_PAIR_BOXBOX) {
         collide_boxbox(md, d, c0 + b);
       } else if (md.m.ccd_mode == MGS_CCD_R5) {
         collide_pair(md, d, c0 + b);
       } else if (kind == MGS_PAIR_CONVEX || kind == MGS_PAIR_CONVEX_SMOOTH) {
-        collide_convex_mj(md, d, c0 + b, -1);
+        collide_convex_mj(md, d, c0 + b, -1, mccd);
       } else {
         collide_prim(md, d, c0 + b, kind);
       }
@@ -6094,7 +6098,7 @@ DEVI void forward(const Mdl& md, Dat& d, int full) {
   if (!full) {
     kinematics(md, d);
     com_pos(md, d);
-    collision(md, d);
+    collision(md, d, 0);
     return;
   }
   forward_rows<NV>(md, d);

@@ -92,6 +92,7 @@ typedef struct {
   double* cert;      /* O_CERT separation certificate slots */
   int overflow;
   int iters;
+  int mask_only;     /* collision without multiccd (oracle_collision_free) */
 } Dat;
 
 /* ------------------------------------------------------------------------ */
@@ -2081,7 +2082,7 @@ static void collision(const Mdl* md, Dat* d) {
       if (kind == MGS_PAIR_BOXBOX) collide_boxbox(md, d, p);
       else if (m->ccd_mode == MGS_CCD_R5) collide_pair(md, d, p);
       else if (kind == MGS_PAIR_CONVEX || kind == MGS_PAIR_CONVEX_SMOOTH)
-        collide_convex_mj(md, d, p, kind == MGS_PAIR_CONVEX && m->ccd_mode == MGS_CCD_MULTI);
+        collide_convex_mj(md, d, p, kind == MGS_PAIR_CONVEX && m->ccd_mode == MGS_CCD_MULTI && !d->mask_only);
       else collide_prim(md, d, p, kind);
       if (p < 256) g_pair_sup[p] += g_sup_calls - s0;
       if (p < 256 && d->ncon > n0) g_pair_hit[p]++;
@@ -3342,6 +3343,10 @@ int oracle_collision_free(const mgs_model_desc* desc, const int32_t* I, const do
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
   {
     Dat* d = dat_alloc(&md);
+    /* the masks skip multiccd (kernel collision(mccd 0)): its contacts repeat
+     * a pair that already has one, so no mask predicate changes, and they
+     * cannot crowd a later pair's first contact out of the capacity */
+    d->mask_only = 1;
 #pragma omp for schedule(dynamic, 4)
     for (int i = 0; i < n; i++) {
       reset(&md, d, qpos_init + (size_t)i * desc->nq, mocap_pos + 3 * i, mocap_quat + 4 * i);

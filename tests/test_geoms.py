@@ -344,3 +344,21 @@ def test_crossed_ridges_edge_edge_contact():
     assert np.allclose(fr[0, :3], [0, 0, 1], atol=1e-12)
     assert np.allclose(dist, [-depth], atol=1e-12)
     assert np.allclose(p[0], [0.0, 0.002, h - depth / 2], atol=1e-12)   # lower ridge x = 0, upper ridge y
+
+
+def test_mask_without_multiccd_keeps_the_predicate(env, candidates):
+    """The collision masks skip multiccd (oracle_collision_free and the
+    kernels' forward(full 0), round 6): its contacts repeat a pair that already
+    has one, so the any-contact predicate of the full contact set (with
+    multiccd, oracle_contacts) is unchanged on the headline's 256 candidates."""
+    from oracle import oracle as O
+    poses, J = candidates
+    q, mp, mq, _ = env.initial_state(poses, J)
+    om = O.OracleModel(env.model, ncon_max=128, nefc_max=256)
+    free = om.collision_free(q, mp, mq, nthreads=4).astype(bool)
+    full = np.array([om.contacts(q[i], mp[i], mq[i], maxc=128)[0] == 0 for i in range(len(q))])
+    assert np.array_equal(free, full)
+    assert 0 < free.sum() < len(free)
+    # and multiccd does add contacts on the colliding ones (the rule is exercised)
+    n_full = sum(om.contacts(q[i], mp[i], mq[i], maxc=128)[0] for i in np.nonzero(~free)[0][:32])
+    assert n_full > len(np.nonzero(~free)[0][:32])
