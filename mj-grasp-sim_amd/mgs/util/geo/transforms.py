@@ -43,6 +43,91 @@ def _drop_pool():
 os.register_at_fork(after_in_child=_drop_pool)
 
 
+# from_mat's fast path (round 6): scipy 1.15's Rotation.from_matrix takes the
+# nearest rotation of every non-orthogonal matrix with an SVD (U @ Vt) and
+# then Markley's method; a float32 pose product is never orthogonal to its
+# 1e-12 test, so the SVD ran on every pose (most of the drop-in API's host
+# time, profiles/r06p_api_breakdown.txt).  The same polar factor comes from
+# three Newton steps X <- (X + X^-T) / 2 (quadratic from the float32 matrix's
+# 1e-7 defect), followed by the same Markley formulas in the same operation
+# order; measured against scipy the float64 quaternions differ by <= 3e-15
+# (tests/test_model_and_host.py).  What SE3Pose keeps is their float32
+# rounding, so a row takes scipy's own path whenever that rounding or the
+# branch could depend on a difference that small: a component within
+# _FAST_TOL of a float32 rounding midpoint or below _FAST_SMALL in magnitude,
+# Markley's two largest decision values within _FAST_GAP, a matrix that scipy
+# would take as already orthogonal (no SVD), or any non-finite / det <= 0
+# input (scipy raises).  The result is scipy's, row for row.
+_FAST_MIN = 64
+_FAST_TOL = 1e-13
+_FAST_SMALL = 1e-5
+_FAST_GAP = 1e-9
+
+
+def _scipy_quat(R):
+    if R.ndim == 3 and len(R) >= _PAR_MIN:
+        # scipy orthogonalises every float32 matrix with an SVD; chunks are
+        # independent, so a thread pool over row blocks returns the identical
+        # quaternions
+        return np.concatenate(list(_pool().map(lambda c: Rotation.from_matrix(c).as_quat(canonical=False),
+                                               np.array_split(R, _PAR_CHUNKS))))
+    return Rotation.from_matrix(R).as_quat(canonical=False)
+
+
+def _fast_quat(R):
+    """(n, 3, 3) -> (n, 4) xyzw quaternions equal to scipy's from_matrix(R)
+    .as_quat(canonical=False) (see _FAST_* above)"""
+    m = np.ascontiguousarray(R.reshape(-1, 9).astype(np.float64).T)  # (9, n)
+    if not np.isfinite(m).all():
+        return _scipy_quat(R)
+    a, b, c, d, e, f, g, h, i = m
+    det0 = a * (e * i - f * h) + b * (f * g - d * i) + c * (d * h - e * g)
+    if not (det0 > 0).all():
+        return _scipy_quat(R)      # scipy's ValueError (or its own handling)
+    # scipy's orthogonality test skips the SVD when every Gram entry is within
+    # 1e-12 of the identity's: such rows (and near ones) go to scipy
+    gram_off = np.maximum.reduce([np.abs(a * d + b * e + c * f), np.abs(a * g + b * h + c * i),
+                                  np.abs(d * g + e * h + f * i)])
+    for _ in range(3):
+        c00, c01, c02 = e * i - f * h, f * g - d * i, d * h - e * g
+        c10, c11, c12 = c * h - b * i, a * i - c * g, b * g - a * h
+        c20, c21, c22 = b * f - c * e, c * d - a * f, a * e - b * d
+        s = 0.5 / (a * c00 + b * c01 + c * c02)
+        a, b, c = 0.5 * a + s * c00, 0.5 * b + s * c01, 0.5 * c + s * c02
+        d, e, f = 0.5 * d + s * c10, 0.5 * e + s * c11, 0.5 * f + s * c12
+        g, h, i = 0.5 * g + s * c20, 0.5 * h + s * c21, 0.5 * i + s * c22
+    M = (a, b, c, d, e, f, g, h, i)
+    dec = np.stack([a, e, i, a + e + i])
+    ch = np.argmax(dec, axis=0)
+    srt = np.sort(dec, axis=0)
+    q = np.empty((4, m.shape[1]))
+    q[0], q[1], q[2], q[3] = h - f, c - g, d - b, 1 + dec[3]
+    for k0 in range(3):
+        sel = ch == k0
+        if not sel.any():
+            continue
+        k1 = (k0 + 1) % 3
+        k2 = (k1 + 1) % 3
+
+        def mm(r, col):
+            return M[3 * r + col][sel]
+        q[k0, sel] = 1 - dec[3, sel] + 2 * mm(k0, k0)
+        q[k1, sel] = mm(k1, k0) + mm(k0, k1)
+        q[k2, sel] = mm(k2, k0) + mm(k0, k2)
+        q[3, sel] = mm(k2, k1) - mm(k1, k2)
+    q = q / np.sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3])
+    q32 = q.astype(np.float32)
+    lo = (q32.astype(np.float64) + np.nextafter(q32, np.float32(-np.inf)).astype(np.float64)) * 0.5
+    hi = (q32.astype(np.float64) + np.nextafter(q32, np.float32(np.inf)).astype(np.float64)) * 0.5
+    risky = ((np.minimum(np.abs(q - lo), np.abs(q - hi)) < _FAST_TOL) | (np.abs(q) < _FAST_SMALL)).any(axis=0)
+    risky |= (srt[3] - srt[2]) < _FAST_GAP
+    risky |= gram_off < 1e-10
+    q = np.ascontiguousarray(q.T)
+    if risky.any():
+        q[risky] = _scipy_quat(R[risky])
+    return q
+
+
 def _wxyz_to_xyzw(q):
     return np.concatenate([q[..., 1:], q[..., :1]], axis=-1)
 
@@ -93,14 +178,10 @@ class SE3Pose:
         if type != "wxyz":
             raise ValueError(type)
         R = mat[..., :3, :3]
-        if R.ndim == 3 and len(R) >= _PAR_MIN:
-            # scipy orthogonalises every float32 matrix with an SVD (most of the
-            # host time of a large batch); chunks are independent, so a thread
-            # pool over row blocks returns the identical quaternions
-            q = np.concatenate(list(_pool().map(lambda c: Rotation.from_matrix(c).as_quat(canonical=False),
-                                                 np.array_split(R, _PAR_CHUNKS))))
+        if R.ndim == 3 and len(R) >= _FAST_MIN:
+            q = _fast_quat(R)
         else:
-            q = Rotation.from_matrix(R).as_quat(canonical=False)
+            q = _scipy_quat(R)
         return cls(mat[..., :3, 3], _xyzw_to_wxyz(q), type)
 
     def __getitem__(self, idx) -> "SE3Pose":

@@ -119,6 +119,30 @@ def test_se3_pose_against_reference_golden():
     assert c.quat.dtype == g["self_quat"].dtype and np.array_equal(c.quat, g["self_quat"])
 
 
+def test_from_mat_fast_path_equals_scipy():
+    """SE3Pose.from_mat's batch path (Newton polar factor + Markley, rows at
+    risk handed to scipy) returns scipy's from_matrix(...).as_quat(canonical=
+    False) float32 rounding row for row: float32 pose products (the API's
+    `poses @ b2c`), float64 rotations (all rows at risk: scipy's own path),
+    identities and axis permutations (scipy skips its SVD)."""
+    from scipy.spatial.transform import Rotation
+    from mgs.util.geo import transforms as T
+    n = 40000
+    A = Rotation.random(n, random_state=11).as_matrix().astype(np.float32)
+    B = Rotation.random(n, random_state=12).as_matrix().astype(np.float32)
+    R32 = np.einsum("...ij,...jk->...ik", A, B)
+    R64 = Rotation.random(500, random_state=13).as_matrix()
+    Rax = Rotation.from_euler("zx", np.arange(400).reshape(200, 2) * 90, degrees=True).as_matrix().astype(np.float32)
+    for R in (R32, R64, Rax, np.concatenate([Rax, R32[:300]])):
+        want = Rotation.from_matrix(R).as_quat(canonical=False).astype(np.float32)
+        assert np.array_equal(T._fast_quat(R).astype(np.float32), want)
+    H = np.tile(np.eye(4, dtype=np.float32), (n, 1, 1))
+    H[:, :3, :3] = R32
+    assert np.array_equal(T.SE3Pose.from_mat(H).quat, T._xyzw_to_wxyz(T._scipy_quat(R32)).astype(np.float32))
+    with pytest.raises(ValueError):
+        T.SE3Pose.from_mat(-H)
+
+
 def test_eig3_mesh_frame():
     """mgs.core.mjcf.eig3 (MuJoCo's mju_eig3 restated, the mesh compiler's
     principal axes): eigenvalues in decreasing order, the quaternion's matrix
