@@ -116,16 +116,46 @@ def _fast_quat(R):
         q[k2, sel] = mm(k2, k0) + mm(k0, k2)
         q[3, sel] = mm(k2, k1) - mm(k1, k2)
     q = q / np.sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3])
-    q32 = q.astype(np.float32)
-    lo = (q32.astype(np.float64) + np.nextafter(q32, np.float32(-np.inf)).astype(np.float64)) * 0.5
-    hi = (q32.astype(np.float64) + np.nextafter(q32, np.float32(np.inf)).astype(np.float64)) * 0.5
-    risky = ((np.minimum(np.abs(q - lo), np.abs(q - hi)) < _FAST_TOL) | (np.abs(q) < _FAST_SMALL)).any(axis=0)
+    risky = _near_f32_midpoint(q).any(axis=0)
     risky |= (srt[3] - srt[2]) < _FAST_GAP
     risky |= gram_off < 1e-10
     q = np.ascontiguousarray(q.T)
     if risky.any():
         q[risky] = _scipy_quat(R[risky])
     return q
+
+
+def _near_f32_midpoint(x):
+    """x (float64) within _FAST_TOL of a float32 rounding midpoint, or small"""
+    # |x - float32(x)| (exact) against the half spacings on either side of
+    # float32(x): u / 2 above, u / 2 or u / 4 (at a power of two) below --
+    # both are tested, which only ever flags more rows
+    x32 = x.astype(np.float32)
+    err = np.abs(x - x32)
+    half = np.spacing(np.abs(x32)).astype(np.float64) * 0.5
+    return (np.abs(err - half) < _FAST_TOL) | (np.abs(err - 0.5 * half) < _FAST_TOL) | (np.abs(x) < _FAST_SMALL)
+
+
+def _fast_mat(q_xyzw):
+    """(n, 4) xyzw -> (n, 3, 3) float32 equal to scipy's Rotation.from_quat(q)
+    .as_matrix() cast to float32: scipy's normalisation and products in its
+    order (float64-identical on 300k random rotations), rows whose entries sit
+    near a float32 rounding midpoint (or are small) from scipy itself"""
+    q = np.ascontiguousarray(np.asarray(q_xyzw).reshape(-1, 4).astype(np.float64).T)
+    nrm = np.sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3])
+    if not (np.isfinite(nrm).all() and (nrm > 0).all()):
+        return Rotation.from_quat(np.copy(q_xyzw)).as_matrix().astype(np.float32)
+    x, y, z, w = q / nrm
+    x2, y2, z2, w2 = x * x, y * y, z * z, w * w
+    xy, zw, xz, yw, yz, xw = x * y, z * w, x * z, y * w, y * z, x * w
+    m = np.stack([x2 - y2 - z2 + w2, 2 * (xy - zw), 2 * (xz + yw),
+                  2 * (xy + zw), -x2 + y2 - z2 + w2, 2 * (yz - xw),
+                  2 * (xz - yw), 2 * (yz + xw), -x2 - y2 + z2 + w2])
+    risky = _near_f32_midpoint(m).any(axis=0)
+    out = np.ascontiguousarray(m.T).reshape(-1, 3, 3).astype(np.float32)
+    if risky.any():
+        out[risky] = Rotation.from_quat(np.copy(q_xyzw[risky])).as_matrix().astype(np.float32)
+    return out
 
 
 def _wxyz_to_xyzw(q):
@@ -197,7 +227,10 @@ class SE3Pose:
     def to_mat(self) -> np.ndarray:
         q = _wxyz_to_xyzw(self.quat) if self.type == "wxyz" else self.quat
         out = np.zeros((*self.quat.shape[:-1], 4, 4), dtype=np.float32)
-        out[..., :3, :3] = Rotation.from_quat(np.copy(q)).as_matrix()
+        if q.ndim == 2 and len(q) >= _FAST_MIN:
+            out[..., :3, :3] = _fast_mat(q)
+        else:
+            out[..., :3, :3] = Rotation.from_quat(np.copy(q)).as_matrix()
         out[..., :3, 3] = self.pos
         out[..., 3, 3] = 1.0
         return out

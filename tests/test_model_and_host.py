@@ -141,6 +141,13 @@ def test_from_mat_fast_path_equals_scipy():
     assert np.array_equal(T.SE3Pose.from_mat(H).quat, T._xyzw_to_wxyz(T._scipy_quat(R32)).astype(np.float32))
     with pytest.raises(ValueError):
         T.SE3Pose.from_mat(-H)
+    # to_mat's batch path (scipy's from_quat(...).as_matrix() products in its
+    # order) against scipy, random and axis-aligned quaternions
+    for R in (R32, Rax):
+        q = Rotation.from_matrix(R).as_quat(canonical=False).astype(np.float32)
+        want = Rotation.from_quat(np.copy(q)).as_matrix().astype(np.float32)
+        assert np.array_equal(T._fast_mat(q), want)
+        assert np.array_equal(T.SE3Pose(np.zeros((len(q), 3)), q, "xyzw").to_mat()[:, :3, :3], want)
 
 
 def test_eig3_mesh_frame():
